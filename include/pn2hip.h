@@ -1,0 +1,170 @@
+/*
+ * pn2hip.h — C ABI of the MI355X (gfx950) PointNet++ geometric hot path.
+ *
+ * This is the drop-in boundary. Each entry point replaces one TensorFlow custom op (or one
+ * inline TF graph fragment) of the reference and keeps its argument meaning:
+ *
+ *   reference op / fragment                                     → entry point here
+ *   FarthestPointSample  tf_sampling.cpp:94-123, .cu:105-170     → pn2_fps
+ *   GatherPoint          tf_sampling.cpp:125-148, .cu:172-181    → pn2_gather_point
+ *   GatherPointGrad      tf_sampling.cpp:150-178, .cu:183-192    → pn2_gather_point_grad
+ *   QueryBallPoint       tf_grouping.cpp:66-106, _g.cu:3-36      → pn2_ball_query
+ *   GroupPoint           tf_grouping.cpp:139-171, _g.cu:40-57    → pn2_group_point
+ *   GroupPointGrad       tf_grouping.cpp:174-208, _g.cu:61-78    → pn2_group_point_grad
+ *   ThreeNN              tf_interpolate.cpp:157-187, :60-103     → pn2_three_nn
+ *   ThreeInterpolate     tf_interpolate.cpp:191-222, :107-127    → pn2_three_interpolate
+ *   ThreeInterpolateGrad tf_interpolate.cpp:225-262, :131-153    → pn2_three_interpolate_grad
+ *   IDW weights          pointnet_util.py:219-222                → pn2_idw_weights
+ *   sample_and_group     pointnet_util.py:16-58 (SSG), :180-191  → pn2_sample_and_group,
+ *                                                                  pn2_group_concat
+ *   pointnet_fp_module   pointnet_util.py:218-226 (geometry)     → pn2_fp_fused
+ *   AttentionLayer.call  attention_layer.py:29-45 (reduction)    → pn2_attn_reduce
+ *   SA pooling           pointnet_util.py:130-145, :200          → pn2_group_pool
+ *
+ * (reference paths are under pointnet2_tensorflow/tf_ops/{sampling,grouping,interpolation_3d},
+ *  pointnet2_tensorflow/utils and attention_points/attention_scannet.)
+ *
+ * Conventions (all entry points):
+ *  - every buffer is a caller-owned DEVICE pointer, row-major, channel-last, contiguous;
+ *    float = IEEE fp32, indices int32 — the reference's tensor dtypes;
+ *  - every launch goes on `stream` (a hipStream_t; NULL = legacy default stream); nothing
+ *    synchronises, nothing allocates, so every call can be captured into a hipGraph;
+ *  - return 0 on success, PN2_EINVAL (-22) for a shape/attribute error (where the reference
+ *    raises InvalidArgument through OP_REQUIRES), or a positive hipError_t from the launch.
+ */
+#ifndef PN2HIP_H
+#define PN2HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* pn2_stream_t; /* hipStream_t */
+
+#define PN2_OK 0
+#define PN2_EINVAL (-22)
+
+/* flags of pn2_group_concat / pn2_sample_and_group */
+#define PN2_USE_XYZ 1  /* concat the centred xyz with the grouped features (use_xyz=True)      */
+#define PN2_XYZ_LAST 2 /* MSG order [points, xyz] (pointnet_util.py:191) instead of SSG
+                          [xyz, points] (pointnet_util.py:52)                                 */
+
+/* pn2_group_pool modes (pointnet_util.py:130-145) */
+#define PN2_POOL_MAX 0
+#define PN2_POOL_AVG 1
+#define PN2_POOL_WEIGHTED_AVG 2
+#define PN2_POOL_MAX_AND_AVG 3
+
+const char* pn2_version(void);
+const char* pn2_strerror(int status);
+
+/* ---------------------------------------------------------------- sampling -------------- */
+
+/* Farthest-point sampling. xyz (B,N,3) → idx (B,npoint). idx[b,0]=0; each next index is the
+ * argmax of the running min squared distance, ties broken exactly like the reference's
+ * 512-thread block reduction: smallest (k mod 512), then smallest (k div 512)
+ * (tf_sampling_g.cu:130-165). Distances are ((dx*dx+dy*dy)+dz*dz) in fp32 without FMA.
+ * npoint must be > 0 (tf_sampling.cpp:99). N <= pn2_fps_max_points() needs no workspace;
+ * larger N must use pn2_fps_ws. */
+int pn2_fps(const float* xyz, int B, int N, int npoint, int32_t* idx, pn2_stream_t stream);
+/* Same, also writing new_xyz (B,npoint,3) = gather_point(xyz, idx) (pointnet_util.py:34). */
+int pn2_fps_gather(const float* xyz, int B, int N, int npoint, int32_t* idx, float* new_xyz,
+                   pn2_stream_t stream);
+int pn2_fps_max_points(void);
+size_t pn2_fps_workspace_size(int B, int N);
+int pn2_fps_ws(const float* xyz, int B, int N, int npoint, int32_t* idx, float* new_xyz,
+               void* workspace, size_t workspace_bytes, pn2_stream_t stream);
+
+/* out (B,M,3) = inp[b, idx[b,j], :]; inp must have 3 channels (tf_sampling.cpp:131). */
+int pn2_gather_point(const float* inp, const int32_t* idx, int B, int N, int M, float* out,
+                     pn2_stream_t stream);
+/* inp_g (B,N,3) = scatter-add of out_g (B,M,3) at idx; zero-fills inp_g first
+ * (tf_sampling.cpp:174). Float atomics: summation order is not fixed. */
+int pn2_gather_point_grad(const float* out_g, const int32_t* idx, int B, int N, int M,
+                          float* inp_g, pn2_stream_t stream);
+
+/* ---------------------------------------------------------------- grouping -------------- */
+
+/* Ball query. For every query j: the first `nsample` points of xyz1 (in index order) with
+ * max(sqrtf(d2),1e-20f) < radius; remaining slots repeat the first hit; pts_cnt = number
+ * found (<= nsample) (tf_grouping_g.cu:3-36). A query with no hit gets idx 0 and pts_cnt 0
+ * (the reference leaves that row uninitialised). radius > 0, nsample > 0
+ * (tf_grouping.cpp:71,74). */
+int pn2_ball_query(const float* xyz1, const float* xyz2, int B, int N, int M, float radius,
+                   int nsample, int32_t* idx, int32_t* pts_cnt, pn2_stream_t stream);
+/* The float T with  d2 < T  <=>  max(sqrtf(d2),1e-20f) < radius  for every fp32 d2 >= 0.
+ * Host function (pure, no GPU). */
+float pn2_ball_threshold(float radius);
+
+/* out (B,M,nsample,C) = points[b, idx[b,j,k], :] (tf_grouping_g.cu:40-57). */
+int pn2_group_point(const float* points, const int32_t* idx, int B, int N, int C, int M,
+                    int nsample, float* out, pn2_stream_t stream);
+/* grad_points (B,N,C) = scatter-add of grad_out (B,M,nsample,C); zero-fills first
+ * (tf_grouping.cpp:204, tf_grouping_g.cu:61-78). Float atomics. */
+int pn2_group_point_grad(const float* grad_out, const int32_t* idx, int B, int N, int C, int M,
+                         int nsample, float* grad_points, pn2_stream_t stream);
+
+/* Fused group + centre + concat (pointnet_util.py:39-56 SSG, :186-193 MSG):
+ *   grouped_xyz (B,M,nsample,3) = xyz[idx] - new_xyz[j]            (optional, may be NULL)
+ *   new_points  (B,M,nsample,Cout):
+ *     points == NULL          → Cout = 3,      grouped_xyz
+ *     !(flags & PN2_USE_XYZ)  → Cout = C,      points[idx]
+ *     flags & PN2_XYZ_LAST    → Cout = C + 3,  [points[idx], grouped_xyz]   (MSG)
+ *     otherwise               → Cout = 3 + C,  [grouped_xyz, points[idx]]   (SSG) */
+int pn2_group_concat(const float* xyz, const float* points, const float* new_xyz,
+                     const int32_t* idx, int B, int N, int C, int M, int nsample, int flags,
+                     float* grouped_xyz, float* new_points, pn2_stream_t stream);
+/* sample_and_group (pointnet_util.py:16-58, knn=False): FPS + gather + ball query + fused
+ * group/centre/concat, four launches on `stream`. Outputs as in the reference:
+ * fps_idx (B,npoint), new_xyz (B,npoint,3), idx (B,npoint,nsample), pts_cnt (B,npoint),
+ * grouped_xyz (B,npoint,nsample,3) (may be NULL), new_points (B,npoint,nsample,Cout). */
+int pn2_sample_and_group(const float* xyz, const float* points, int B, int N, int C,
+                         int npoint, float radius, int nsample, int flags, int32_t* fps_idx,
+                         float* new_xyz, int32_t* idx, int32_t* pts_cnt, float* grouped_xyz,
+                         float* new_points, pn2_stream_t stream);
+
+/* ---------------------------------------------------------------- interpolation --------- */
+
+/* Three nearest known points (xyz2, (B,m,3)) of every unknown point (xyz1, (B,n,3)):
+ * SQUARED distances ascending, ties keep the lower index, m<3 leaves idx 0 / dist +inf
+ * (tf_interpolate.cpp:60-103). */
+int pn2_three_nn(const float* xyz1, const float* xyz2, int B, int n, int m, float* dist,
+                 int32_t* idx, pn2_stream_t stream);
+/* out (B,n,C) = ((p[i1]*w1) + (p[i2]*w2)) + (p[i3]*w3)  (tf_interpolate.cpp:107-127). */
+int pn2_three_interpolate(const float* points, const int32_t* idx, const float* weight, int B,
+                          int m, int C, int n, float* out, pn2_stream_t stream);
+/* grad_points (B,m,C) scatter-add (tf_interpolate.cpp:131-153); zero-fills first. */
+int pn2_three_interpolate_grad(const float* grad_out, const int32_t* idx, const float* weight,
+                               int B, int n, int C, int m, float* grad_points,
+                               pn2_stream_t stream);
+/* weight = (1/d)/sum(1/d), d = max(dist,1e-10)  (pointnet_util.py:219-222). */
+int pn2_idw_weights(const float* dist, int B, int n, float* weight, pn2_stream_t stream);
+/* pointnet_fp_module geometry (pointnet_util.py:218-226): three_nn + IDW weights +
+ * three_interpolate + concat [interp (C2), points1 (C1)] → out (B,n,C2+C1).
+ * points1 may be NULL (C1 must then be 0). */
+int pn2_fp_fused(const float* xyz1, const float* xyz2, const float* points1, int C1,
+                 const float* points2, int C2, int B, int n, int m, float* out,
+                 pn2_stream_t stream);
+
+/* ---------------------------------------------------------------- attention / pooling --- */
+
+/* AttentionLayer reduction core (attention_layer.py:35-42) with key_dim = output_dim = 4,
+ * heads H = C/4. Q (B,M,C), K,V (B,M,ns,C) → out (B,M,C). Head h reads the CONTIGUOUS
+ * block [4*ns*h, 4*ns*(h+1)) of each group's flattened ns*C K/V values as ns rows of 4
+ * (the reference's tf.reshape reinterpretation), s = (K_h·q_h)/2, a = softmax(s),
+ * out[4h:4h+4] = aᵀ V_h. C must be a multiple of 4. */
+int pn2_attn_reduce(const float* Q, const float* K, const float* V, int B, int M, int ns,
+                    int C, float* out, pn2_stream_t stream);
+/* Per-group pooling over nsample (pointnet_util.py:130-145): x (B,M,ns,C) → out (B,M,C),
+ * or (B,M,2C) = [avg, max] for PN2_POOL_MAX_AND_AVG. grouped_xyz (B,M,ns,3) is read only
+ * by PN2_POOL_WEIGHTED_AVG (w = exp(-5|xyz|)/sum). */
+int pn2_group_pool(const float* x, const float* grouped_xyz, int B, int M, int ns, int C,
+                   int mode, float* out, pn2_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PN2HIP_H */

@@ -1,0 +1,349 @@
+"""Python front of the oracle — TEST INFRASTRUCTURE ONLY.
+
+Loads
+  oracle/liboracle.so          our C restatement (pn2_oracle.c), numpy in / numpy out
+  oracle/_ref/libref_cpu.so    the reference's own CPU code (query_ball_point.cpp,
+                               interpolate.cpp, tf_interpolate.cpp:57-103), compiled unchanged
+  oracle/_ref/libref_gpu.so    the reference's own CUDA kernels (tf_sampling_g.cu,
+                               tf_grouping_g.cu) compiled unchanged for gfx950 (GPU box only)
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this module, and
+only as the checker / CPU baseline. The product never does.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ORACLE_SO = os.path.join(HERE, "liboracle.so")
+REF_CPU_SO = os.path.join(HERE, "_ref", "libref_cpu.so")
+REF_GPU_SO = os.path.join(HERE, "_ref", "libref_gpu.so")
+
+_P, _I, _F = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
+
+_ORACLE_SIGS = {
+    "pn2o_set_threads": [_I],
+    "pn2o_fps": [_P, _I, _I, _I, _P],
+    "pn2o_gather_point": [_P, _P, _I, _I, _I, _P],
+    "pn2o_gather_point_grad": [_P, _P, _I, _I, _I, _P],
+    "pn2o_ball_query": [_P, _P, _I, _I, _I, _F, _I, _P, _P],
+    "pn2o_group_point": [_P, _P, _I, _I, _I, _I, _I, _P],
+    "pn2o_group_point_grad": [_P, _P, _I, _I, _I, _I, _I, _P],
+    "pn2o_group_concat": [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P],
+    "pn2o_three_nn": [_P, _P, _I, _I, _I, _P, _P],
+    "pn2o_three_interpolate": [_P, _P, _P, _I, _I, _I, _I, _P],
+    "pn2o_three_interpolate_grad": [_P, _P, _P, _I, _I, _I, _I, _P],
+    "pn2o_idw_weights": [_P, _I, _I, _P],
+    "pn2o_fp_fused": [_P, _P, _P, _I, _P, _I, _I, _I, _I, _P],
+    "pn2o_attn_reduce": [_P, _P, _P, _I, _I, _I, _I, _P],
+    "pn2o_group_pool": [_P, _P, _I, _I, _I, _I, _I, _P],
+}
+_REF_CPU_SIGS = {
+    "pn2ref_query_ball_point": [_I, _I, _I, _F, _I, _P, _P, _P],
+    "pn2ref_group_point": [_I, _I, _I, _I, _I, _P, _P, _P],
+    "pn2ref_group_point_grad": [_I, _I, _I, _I, _I, _P, _P, _P],
+    "pn2ref_three_nn": [_I, _I, _I, _P, _P, _P, _P],
+    "pn2ref_three_interpolate": [_I, _I, _I, _I, _P, _P, _P, _P],
+    "pn2ref_three_interpolate_grad": [_I, _I, _I, _I, _P, _P, _P, _P],
+}
+_REF_GPU_SIGS = {
+    "pn2ref_fps": [_P, _I, _I, _I, _P],
+    "pn2ref_gather_point": [_P, _P, _I, _I, _I, _P],
+    "pn2ref_query_ball_point": [_P, _P, _I, _I, _I, _F, _I, _P, _P],
+    "pn2ref_group_point": [_P, _P, _I, _I, _I, _I, _I, _P],
+}
+
+_cache = {}
+
+
+def build(ref=False):
+    """make -C oracle (and the _ref targets when /root/reference is present and ref=True)."""
+    targets = ["all"]
+    if ref and os.path.isdir("/root/reference"):
+        targets.append("ref")
+    subprocess.run(["make", "-s", "-C", HERE] + targets, check=True)
+
+
+def _load(path, sigs, restype=None):
+    if path not in _cache:
+        if not os.path.exists(path):
+            if path == ORACLE_SO:
+                build()
+            else:
+                raise FileNotFoundError(f"{path} not built (make -C oracle ref, needs /root/reference)")
+        lib = ctypes.CDLL(path)
+        for name, args in sigs.items():
+            fn = getattr(lib, name)
+            fn.argtypes = args
+            fn.restype = restype
+        _cache[path] = lib
+    return _cache[path]
+
+
+def olib():
+    return _load(ORACLE_SO, _ORACLE_SIGS)
+
+
+def ref_cpu():
+    return _load(REF_CPU_SO, _REF_CPU_SIGS)
+
+
+def ref_gpu():
+    return _load(REF_GPU_SO, _REF_GPU_SIGS, restype=_I)
+
+
+def have_ref_cpu():
+    return os.path.exists(REF_CPU_SO)
+
+
+def have_ref_gpu():
+    return os.path.exists(REF_GPU_SO)
+
+
+def _f32(a):
+    return np.ascontiguousarray(a, dtype=np.float32)
+
+
+def _i32(a):
+    return np.ascontiguousarray(a, dtype=np.int32)
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data
+
+
+def set_threads(n):
+    olib().pn2o_set_threads(int(n))
+
+
+# ---------------------------------------------------------------- restatement (numpy API)
+
+def fps(xyz, npoint):
+    xyz = _f32(xyz)
+    B, N = xyz.shape[:2]
+    idx = np.zeros((B, npoint), np.int32)
+    olib().pn2o_fps(_p(xyz), B, N, npoint, _p(idx))
+    return idx
+
+
+def gather_point(inp, idx):
+    inp, idx = _f32(inp), _i32(idx)
+    B, N = inp.shape[:2]
+    M = idx.shape[1]
+    out = np.zeros((B, M, 3), np.float32)
+    olib().pn2o_gather_point(_p(inp), _p(idx), B, N, M, _p(out))
+    return out
+
+
+def gather_point_grad(N, idx, out_g):
+    idx, out_g = _i32(idx), _f32(out_g)
+    B, M = idx.shape
+    g = np.zeros((B, N, 3), np.float32)
+    olib().pn2o_gather_point_grad(_p(out_g), _p(idx), B, N, M, _p(g))
+    return g
+
+
+def ball_query(xyz1, xyz2, radius, nsample):
+    xyz1, xyz2 = _f32(xyz1), _f32(xyz2)
+    B, N = xyz1.shape[:2]
+    M = xyz2.shape[1]
+    idx = np.zeros((B, M, nsample), np.int32)
+    cnt = np.zeros((B, M), np.int32)
+    olib().pn2o_ball_query(_p(xyz1), _p(xyz2), B, N, M, float(radius), nsample, _p(idx), _p(cnt))
+    return idx, cnt
+
+
+def group_point(points, idx):
+    points, idx = _f32(points), _i32(idx)
+    B, N, C = points.shape
+    M, ns = idx.shape[1:]
+    out = np.zeros((B, M, ns, C), np.float32)
+    olib().pn2o_group_point(_p(points), _p(idx), B, N, C, M, ns, _p(out))
+    return out
+
+
+def group_point_grad(N, idx, grad_out):
+    idx, grad_out = _i32(idx), _f32(grad_out)
+    B, M, ns, C = grad_out.shape
+    g = np.zeros((B, N, C), np.float32)
+    olib().pn2o_group_point_grad(_p(grad_out), _p(idx), B, N, C, M, ns, _p(g))
+    return g
+
+
+def group_concat(xyz, points, new_xyz, idx, use_xyz=True, xyz_last=False):
+    xyz, new_xyz, idx = _f32(xyz), _f32(new_xyz), _i32(idx)
+    B, N = xyz.shape[:2]
+    M, ns = idx.shape[1:]
+    if points is None:
+        C, Cout = 0, 3
+    else:
+        points = _f32(points)
+        C = points.shape[2]
+        Cout = C + 3 if use_xyz else C
+    gx = np.zeros((B, M, ns, 3), np.float32)
+    out = np.zeros((B, M, ns, Cout), np.float32)
+    flags = (1 if use_xyz else 0) | (2 if xyz_last else 0)
+    olib().pn2o_group_concat(_p(xyz), _p(points), _p(new_xyz), _p(idx), B, N, C, M, ns, flags,
+                             _p(gx), _p(out))
+    return out, gx
+
+
+def three_nn(xyz1, xyz2):
+    xyz1, xyz2 = _f32(xyz1), _f32(xyz2)
+    B, n = xyz1.shape[:2]
+    m = xyz2.shape[1]
+    dist = np.zeros((B, n, 3), np.float32)
+    idx = np.zeros((B, n, 3), np.int32)
+    olib().pn2o_three_nn(_p(xyz1), _p(xyz2), B, n, m, _p(dist), _p(idx))
+    return dist, idx
+
+
+def three_interpolate(points, idx, weight):
+    points, idx, weight = _f32(points), _i32(idx), _f32(weight)
+    B, m, C = points.shape
+    n = idx.shape[1]
+    out = np.zeros((B, n, C), np.float32)
+    olib().pn2o_three_interpolate(_p(points), _p(idx), _p(weight), B, m, C, n, _p(out))
+    return out
+
+
+def three_interpolate_grad(m, idx, weight, grad_out):
+    idx, weight, grad_out = _i32(idx), _f32(weight), _f32(grad_out)
+    B, n, C = grad_out.shape
+    g = np.zeros((B, m, C), np.float32)
+    olib().pn2o_three_interpolate_grad(_p(grad_out), _p(idx), _p(weight), B, n, C, m, _p(g))
+    return g
+
+
+def idw_weights(dist):
+    dist = _f32(dist)
+    B, n = dist.shape[:2]
+    w = np.zeros_like(dist)
+    olib().pn2o_idw_weights(_p(dist), B, n, _p(w))
+    return w
+
+
+def fp_fused(xyz1, xyz2, points1, points2):
+    xyz1, xyz2, points2 = _f32(xyz1), _f32(xyz2), _f32(points2)
+    B, n = xyz1.shape[:2]
+    m, C2 = xyz2.shape[1], points2.shape[2]
+    C1 = 0 if points1 is None else points1.shape[2]
+    if points1 is not None:
+        points1 = _f32(points1)
+    out = np.zeros((B, n, C1 + C2), np.float32)
+    olib().pn2o_fp_fused(_p(xyz1), _p(xyz2), _p(points1), C1, _p(points2), C2, B, n, m, _p(out))
+    return out
+
+
+def attn_reduce(Q, K, V):
+    Q, K, V = _f32(Q), _f32(K), _f32(V)
+    B, M, ns, C = K.shape
+    out = np.zeros((B, M, C), np.float32)
+    olib().pn2o_attn_reduce(_p(Q), _p(K), _p(V), B, M, ns, C, _p(out))
+    return out
+
+
+def group_pool(x, grouped_xyz, mode):
+    modes = {"max": 0, "avg": 1, "weighted_avg": 2, "max_and_avg": 3}
+    x = _f32(x)
+    B, M, ns, C = x.shape
+    g = _f32(grouped_xyz) if grouped_xyz is not None else None
+    Cout = 2 * C if mode == "max_and_avg" else C
+    out = np.zeros((B, M, 1, Cout), np.float32)
+    olib().pn2o_group_pool(_p(x), _p(g), B, M, ns, C, modes[mode], _p(out))
+    return out
+
+
+# ---------------------------------------------------------------- reference CPU code
+
+def ref_ball_query(xyz1, xyz2, radius, nsample, fill=-1):
+    """query_ball_point_cpu (query_ball_point.cpp:19-47). idx rows of queries with no hit keep
+    `fill` (the reference leaves them uninitialised)."""
+    xyz1, xyz2 = _f32(xyz1), _f32(xyz2)
+    B, N = xyz1.shape[:2]
+    M = xyz2.shape[1]
+    idx = np.full((B, M, nsample), fill, np.int32)
+    ref_cpu().pn2ref_query_ball_point(B, N, M, float(radius), nsample, _p(xyz1), _p(xyz2), _p(idx))
+    return idx
+
+
+def ref_group_point(points, idx):
+    points, idx = _f32(points), _i32(idx)
+    B, N, C = points.shape
+    M, ns = idx.shape[1:]
+    out = np.zeros((B, M, ns, C), np.float32)
+    ref_cpu().pn2ref_group_point(B, N, C, M, ns, _p(points), _p(idx), _p(out))
+    return out
+
+
+def ref_group_point_grad(N, idx, grad_out):
+    idx, grad_out = _i32(idx), _f32(grad_out)
+    B, M, ns, C = grad_out.shape
+    g = np.zeros((B, N, C), np.float32)  # the CPU twin accumulates into caller memory
+    ref_cpu().pn2ref_group_point_grad(B, N, C, M, ns, _p(grad_out), _p(idx), _p(g))
+    return g
+
+
+def ref_three_nn(xyz1, xyz2):
+    xyz1, xyz2 = _f32(xyz1), _f32(xyz2)
+    B, n = xyz1.shape[:2]
+    m = xyz2.shape[1]
+    dist = np.zeros((B, n, 3), np.float32)
+    idx = np.zeros((B, n, 3), np.int32)
+    ref_cpu().pn2ref_three_nn(B, n, m, _p(xyz1), _p(xyz2), _p(dist), _p(idx))
+    return dist, idx
+
+
+def ref_three_interpolate(points, idx, weight):
+    points, idx, weight = _f32(points), _i32(idx), _f32(weight)
+    B, m, C = points.shape
+    n = idx.shape[1]
+    out = np.zeros((B, n, C), np.float32)
+    ref_cpu().pn2ref_three_interpolate(B, m, C, n, _p(points), _p(idx), _p(weight), _p(out))
+    return out
+
+
+def ref_three_interpolate_grad(m, idx, weight, grad_out):
+    idx, weight, grad_out = _i32(idx), _f32(weight), _f32(grad_out)
+    B, n, C = grad_out.shape
+    g = np.zeros((B, m, C), np.float32)
+    ref_cpu().pn2ref_three_interpolate_grad(B, n, C, m, _p(grad_out), _p(idx), _p(weight), _p(g))
+    return g
+
+
+# ---------------------------------------------------------------- the geometric stack on CPU
+
+def run_stack_cpu(inp_np, config):
+    """The same step as stack.run(), on the CPU restatement (numpy inputs)."""
+    import importlib
+    stack = importlib.import_module("pointcloud-segmentation-attention_amd.stack")
+    kind = stack.CONFIGS[config][1]
+    outs = []
+    if kind == "ssg":
+        xyz, points = [inp_np["xyz"]], [inp_np["feats"]]
+        for i, (npoint, radius, nsample, _) in enumerate(stack.SSG_SA):
+            idx = fps(xyz[-1], npoint)
+            new_xyz = gather_point(xyz[-1], idx)
+            gidx, _ = ball_query(xyz[-1], new_xyz, radius, nsample)
+            new_points, _ = group_concat(xyz[-1], points[-1], new_xyz, gidx)
+            outs.append(new_points)
+            if "attn" in inp_np:
+                outs.append(attn_reduce(*inp_np["attn"][i]))
+            xyz.append(new_xyz)
+            points.append(inp_np["sa_out"][i])
+        feat = inp_np["sa_out"][3]
+        for k in range(4):
+            lvl = 3 - k
+            outs.append(fp_fused(xyz[lvl], xyz[lvl + 1], points[lvl], feat))
+            feat = inp_np["fp_out"][k] if k < 3 else None
+    else:
+        xyz, points = inp_np["xyz"], None
+        for i, (npoint, radii, nsamples, _) in enumerate(stack.MSG_SA):
+            idx = fps(xyz, npoint)
+            new_xyz = gather_point(xyz, idx)
+            for radius, nsample in zip(radii, nsamples):
+                gidx, _ = ball_query(xyz, new_xyz, radius, nsample)
+                outs.append(group_concat(xyz, points, new_xyz, gidx, xyz_last=True)[0])
+            xyz, points = new_xyz, inp_np["sa_out"][0]
+    return outs

@@ -1,0 +1,108 @@
+"""ctypes binding of libpn2hip.so — the C ABI declared in include/pn2hip.h.
+
+The product path is the HIP library: if it is missing, every op raises; there is no CPU
+fallback. `torch` is imported first on purpose: torch ships its own libamdhip64.so (SONAME
+libamdhip64.so.7) and libpn2hip.so links the same SONAME, so loading it after torch binds it
+to torch's HIP runtime — one runtime per process, torch's streams and allocations are valid
+inside the library.
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libpn2hip.so")
+
+PN2_EINVAL = -22
+PN2_USE_XYZ = 1
+PN2_XYZ_LAST = 2
+POOL_MODES = {"max": 0, "avg": 1, "weighted_avg": 2, "max_and_avg": 3}
+
+
+class InvalidArgumentError(ValueError):
+    """Raised where the reference's OP_REQUIRES raises tf.errors.InvalidArgumentError."""
+
+
+class Pn2RuntimeError(RuntimeError):
+    """A HIP launch error reported by the C ABI."""
+
+
+_P, _I, _F, _S = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_size_t
+
+# name -> (restype, argtypes); mirrors include/pn2hip.h (tests/test_capi.py checks the header)
+SIGNATURES = {
+    "pn2_version": (ctypes.c_char_p, []),
+    "pn2_strerror": (ctypes.c_char_p, [_I]),
+    "pn2_fps": (_I, [_P, _I, _I, _I, _P, _P]),
+    "pn2_fps_gather": (_I, [_P, _I, _I, _I, _P, _P, _P]),
+    "pn2_fps_max_points": (_I, []),
+    "pn2_fps_workspace_size": (_S, [_I, _I]),
+    "pn2_fps_ws": (_I, [_P, _I, _I, _I, _P, _P, _P, _S, _P]),
+    "pn2_gather_point": (_I, [_P, _P, _I, _I, _I, _P, _P]),
+    "pn2_gather_point_grad": (_I, [_P, _P, _I, _I, _I, _P, _P]),
+    "pn2_ball_query": (_I, [_P, _P, _I, _I, _I, _F, _I, _P, _P, _P]),
+    "pn2_ball_threshold": (_F, [_F]),
+    "pn2_group_point": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _P]),
+    "pn2_group_point_grad": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _P]),
+    "pn2_group_concat": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P]),
+    "pn2_sample_and_group": (_I, [_P, _P, _I, _I, _I, _I, _F, _I, _I, _P, _P, _P, _P, _P, _P,
+                                  _P]),
+    "pn2_three_nn": (_I, [_P, _P, _I, _I, _I, _P, _P, _P]),
+    "pn2_three_interpolate": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P]),
+    "pn2_three_interpolate_grad": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P]),
+    "pn2_idw_weights": (_I, [_P, _I, _I, _P, _P]),
+    "pn2_fp_fused": (_I, [_P, _P, _P, _I, _P, _I, _I, _I, _I, _P, _P]),
+    "pn2_attn_reduce": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P]),
+    "pn2_group_pool": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _P]),
+}
+
+_lib = None
+
+
+def lib():
+    """The loaded libpn2hip.so (raises if it was not built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; "
+                "g.build()'` (make -C pointcloud-segmentation-attention_amd/csrc). "
+                "pn2hip has no CPU fallback.")
+        handle = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(handle, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = handle
+    return _lib
+
+
+def check(rc, op):
+    if rc == 0:
+        return
+    if rc == PN2_EINVAL:
+        raise InvalidArgumentError(f"{op}: invalid argument")
+    msg = lib().pn2_strerror(rc)
+    raise Pn2RuntimeError(f"{op}: HIP error {rc}: {msg.decode() if msg else '?'}")
+
+
+def stream_of(t):
+    """hipStream_t handle of torch's current stream on t's device."""
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def device_tensor(t, name, dtype):
+    """Validate an op input: a GPU tensor of the reference dtype, made contiguous."""
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name} must be a torch.Tensor, got {type(t).__name__}")
+    if t.device.type != "cuda":
+        raise RuntimeError(
+            f"{name} is on {t.device}: pn2hip ops run on the MI355X only (no CPU fallback)")
+    if t.dtype != dtype:
+        raise TypeError(f"{name} must be {dtype}, got {t.dtype}")
+    return t.contiguous()

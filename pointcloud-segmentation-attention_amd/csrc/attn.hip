@@ -1,0 +1,240 @@
+// Per-group attention reduction and SA pooling for gfx950.
+//
+// Replaces the reduction core of AttentionLayer.call
+// (attention_points/attention_scannet/attention_layer.py:35-42; instantiated with
+// key_dim = output_dim = 4, num_heads = C/4 at :256-258 and :313-315) — six TF ops per SA
+// layer (reshape, matmul, div, softmax, matmul, reshape) on 1x4 by 4xns heads — and the
+// pooling variants of pointnet_util.py:130-145 (max / avg / weighted_avg / max_and_avg).
+//
+// The reshape quirk is reproduced, not fixed: tf.reshape of K and V from (B,M,ns,4H) to
+// (B,M,H,ns,4) is a row-major reinterpretation, so head h reads the CONTIGUOUS block
+// [4*ns*h, 4*ns*(h+1)) of the group's flattened ns*C values as ns pseudo-keys of width 4.
+// That makes every head a 16*ns-byte contiguous slab: a lane loads one pseudo-key as one
+// float4 (ns lanes per head, 64/ns heads per wave instruction = 1 KiB fully coalesced), the
+// softmax max/sum and the four weighted sums are lane-segment reductions in registers, and
+// one lane per head stores the head's 4 outputs as one float4. K and V are read exactly once.
+#include <math.h>
+
+#include "common.h"
+
+namespace pn2 {
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kWavesPerBlock = kBlock / kWave;
+
+PN2_DEV float dot4(float4 q, float4 k) {  // (1x4)·(4x1) of tf.matmul, summed left to right
+  float s = q.x * k.x;
+  s = s + q.y * k.y;
+  s = s + q.z * k.z;
+  s = s + q.w * k.w;
+  return s;
+}
+
+// NS = nsample (power of two). LPH lanes per head, KPL pseudo-keys per lane.
+template <int NS>
+__global__ __launch_bounds__(kBlock) void attn_reduce_kernel(const float* __restrict__ Q,
+                                                             const float* __restrict__ K,
+                                                             const float* __restrict__ V, int G,
+                                                             int C, int steps, FastDiv div_steps,
+                                                             float* __restrict__ out) {
+  constexpr int LPH = NS < kWave ? NS : kWave;
+  constexpr int KPL = NS / LPH;
+  constexpr int HPW = kWave / LPH;  // heads per wave step
+  const int lane = lane_id();
+  const int hl = lane / LPH, sl = lane % LPH;
+  const int H = C / 4;
+  const long long tasks = (long long)G * steps;
+  const long long nwaves = (long long)gridDim.x * kWavesPerBlock;
+  for (long long task = (long long)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave; task < tasks;
+       task += nwaves) {
+    const uint32_t g = fdiv((uint32_t)task, div_steps);
+    const int step = (int)((uint32_t)task - g * (uint32_t)steps);
+    const int h = step * HPW + hl;
+    const bool valid = h < H;
+    const int hh = valid ? h : 0;
+    const float4 q = *reinterpret_cast<const float4*>(Q + (size_t)g * C + 4 * hh);
+    const float* Kh = K + (size_t)g * NS * C + (size_t)hh * 4 * NS;  // reshape quirk (:35-36)
+    const float* Vh = V + (size_t)g * NS * C + (size_t)hh * 4 * NS;
+    float4 v[KPL];
+    float sc[KPL];
+    float mx = -__builtin_inff();
+#pragma unroll
+    for (int kk = 0; kk < KPL; ++kk) {
+      const int s = sl + kk * LPH;
+      const float4 k = *reinterpret_cast<const float4*>(Kh + 4 * s);
+      v[kk] = *reinterpret_cast<const float4*>(Vh + 4 * s);
+      sc[kk] = dot4(q, k) / 2.0f;  // / tf.sqrt(key_dim = 4)  (:38)
+      mx = fmaxf(mx, sc[kk]);
+    }
+    mx = seg_max<LPH>(mx);  // softmax over the ns pseudo-keys (:39)
+    float sum = 0.0f;
+#pragma unroll
+    for (int kk = 0; kk < KPL; ++kk) {
+      sc[kk] = expf(sc[kk] - mx);
+      sum = sum + sc[kk];
+    }
+    sum = seg_sum<LPH>(sum);
+    float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int kk = 0; kk < KPL; ++kk) {
+      const float a = sc[kk] / sum;
+      o.x = o.x + a * v[kk].x;  // aᵀ·V_h (:40)
+      o.y = o.y + a * v[kk].y;
+      o.z = o.z + a * v[kk].z;
+      o.w = o.w + a * v[kk].w;
+    }
+    o.x = seg_sum<LPH>(o.x);
+    o.y = seg_sum<LPH>(o.y);
+    o.z = seg_sum<LPH>(o.z);
+    o.w = seg_sum<LPH>(o.w);
+    if (sl == 0 && valid) *reinterpret_cast<float4*>(out + (size_t)g * C + 4 * h) = o;  // (:42)
+  }
+}
+
+// Any nsample: one wave per (group, head), lanes stride over the pseudo-keys, running
+// (max, sum, weighted sum) per lane merged across the wave.
+__global__ __launch_bounds__(kBlock) void attn_reduce_generic_kernel(
+    const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V, int G,
+    int ns, int C, float* __restrict__ out) {
+  const int lane = lane_id();
+  const int H = C / 4;
+  const long long tasks = (long long)G * H;
+  const long long nwaves = (long long)gridDim.x * kWavesPerBlock;
+  for (long long task = (long long)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave; task < tasks;
+       task += nwaves) {
+    const long long g = task / H;
+    const int h = (int)(task - g * H);
+    const float4 q = *reinterpret_cast<const float4*>(Q + g * C + 4 * h);
+    const float* Kh = K + g * (long long)ns * C + (long long)h * 4 * ns;
+    const float* Vh = V + g * (long long)ns * C + (long long)h * 4 * ns;
+    float mx = -__builtin_inff();
+    for (int s = lane; s < ns; s += kWave)
+      mx = fmaxf(mx, dot4(q, *reinterpret_cast<const float4*>(Kh + 4 * s)) / 2.0f);
+    mx = seg_max<kWave>(mx);
+    float sum = 0.f;
+    float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int s = lane; s < ns; s += kWave) {
+      const float e = expf(dot4(q, *reinterpret_cast<const float4*>(Kh + 4 * s)) / 2.0f - mx);
+      const float4 v = *reinterpret_cast<const float4*>(Vh + 4 * s);
+      sum = sum + e;
+      o.x = o.x + e * v.x;
+      o.y = o.y + e * v.y;
+      o.z = o.z + e * v.z;
+      o.w = o.w + e * v.w;
+    }
+    sum = seg_sum<kWave>(sum);
+    o.x = seg_sum<kWave>(o.x) / sum;
+    o.y = seg_sum<kWave>(o.y) / sum;
+    o.z = seg_sum<kWave>(o.z) / sum;
+    o.w = seg_sum<kWave>(o.w) / sum;
+    if (lane == 0) *reinterpret_cast<float4*>(out + g * C + 4 * h) = o;
+  }
+}
+
+// One wave per group, lanes over channels (pointnet_util.py:130-145).
+__global__ __launch_bounds__(kBlock) void group_pool_kernel(const float* __restrict__ x,
+                                                            const float* __restrict__ gxyz, int G,
+                                                            int ns, int C, int mode,
+                                                            float* __restrict__ out) {
+  __shared__ float s_w[kWavesPerBlock][256];
+  const int lane = lane_id(), w = threadIdx.x / kWave;
+  for (long long g = (long long)blockIdx.x * kWavesPerBlock + w; g < G;
+       g += (long long)gridDim.x * kWavesPerBlock) {
+    const float* X = x + g * (long long)ns * C;
+    if (mode == PN2_POOL_WEIGHTED_AVG) {
+      // dists = |grouped_xyz| (:136), exp(-5 d) (:137), normalised over ns (:138-139)
+      float part = 0.f;
+      for (int k = lane; k < ns; k += kWave) {
+        const float* p = gxyz + (g * ns + k) * 3;
+        const float d = sqrtf((p[0] * p[0] + p[1] * p[1]) + p[2] * p[2]);
+        const float e = expf(-d * 5.0f);
+        s_w[w][k] = e;
+        part = part + e;
+      }
+      const float tot = seg_sum<kWave>(part);
+      for (int k = lane; k < ns; k += kWave) s_w[w][k] = s_w[w][k] / tot;
+    }
+    for (int c = lane; c < C; c += kWave) {
+      float mx = -__builtin_inff(), sum = 0.f;
+      for (int k = 0; k < ns; ++k) {
+        const float v = X[(size_t)k * C + c];
+        mx = fmaxf(mx, v);
+        sum = (mode == PN2_POOL_WEIGHTED_AVG) ? sum + v * s_w[w][k] : sum + v;
+      }
+      const float avg = sum / (float)ns;
+      if (mode == PN2_POOL_MAX) out[g * C + c] = mx;
+      else if (mode == PN2_POOL_AVG) out[g * C + c] = avg;
+      else if (mode == PN2_POOL_WEIGHTED_AVG) out[g * C + c] = sum;
+      else { out[g * 2 * C + c] = avg; out[g * 2 * C + C + c] = mx; }  // [avg, max] (:145)
+    }
+  }
+}
+
+unsigned grid_for(long long waves) {
+  long long blocks = (waves + kWavesPerBlock - 1) / kWavesPerBlock;
+  if (blocks > 256 * 16) blocks = 256 * 16;  // grid-stride beyond ~16 blocks per CU
+  return (unsigned)(blocks > 0 ? blocks : 1);
+}
+
+template <int NS>
+void launch_attn(const float* Q, const float* K, const float* V, int G, int C, float* out,
+                 hipStream_t s) {
+  constexpr int LPH = NS < kWave ? NS : kWave;
+  constexpr int HPW = kWave / LPH;
+  const int H = C / 4;
+  const int steps = (H + HPW - 1) / HPW;
+  hipLaunchKernelGGL((attn_reduce_kernel<NS>), dim3(grid_for((long long)G * steps)),
+                     dim3(kBlock), 0, s, Q, K, V, G, C, steps, make_fastdiv((uint32_t)steps),
+                     out);
+}
+
+}  // namespace
+}  // namespace pn2
+
+extern "C" {
+
+int pn2_attn_reduce(const float* Q, const float* K, const float* V, int B, int M, int ns, int C,
+                    float* out, pn2_stream_t stream) {
+  if (B < 0 || M < 0 || ns <= 0 || C < 0 || (C % 4) != 0) return PN2_EINVAL;
+  const long long G = (long long)B * M;
+  if (G == 0 || C == 0) return PN2_OK;
+  if (!Q || !K || !V || !out || G > INT32_MAX) return PN2_EINVAL;
+  if ((((uintptr_t)Q | (uintptr_t)K | (uintptr_t)V | (uintptr_t)out) & 15) != 0) return PN2_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  const long long steps_max = (long long)C / 4;  // worst case HPW = 1
+  const bool small_tasks = G * steps_max * steps_max < (1LL << 32);  // FastDiv exactness
+  if (small_tasks && ns == 8) pn2::launch_attn<8>(Q, K, V, (int)G, C, out, s);
+  else if (small_tasks && ns == 16) pn2::launch_attn<16>(Q, K, V, (int)G, C, out, s);
+  else if (small_tasks && ns == 32) pn2::launch_attn<32>(Q, K, V, (int)G, C, out, s);
+  else if (small_tasks && ns == 64) pn2::launch_attn<64>(Q, K, V, (int)G, C, out, s);
+  else if (small_tasks && ns == 128) pn2::launch_attn<128>(Q, K, V, (int)G, C, out, s);
+  else
+    hipLaunchKernelGGL(pn2::attn_reduce_generic_kernel,
+                       dim3(pn2::grid_for(G * (C / 4))), dim3(pn2::kBlock), 0, s, Q, K, V,
+                       (int)G, ns, C, out);
+  PN2_RETURN_LAUNCH();
+}
+
+int pn2_group_pool(const float* x, const float* grouped_xyz, int B, int M, int ns, int C,
+                   int mode, float* out, pn2_stream_t stream) {
+  if (B < 0 || M < 0 || ns <= 0 || C < 0 || mode < PN2_POOL_MAX || mode > PN2_POOL_MAX_AND_AVG)
+    return PN2_EINVAL;
+  if (mode == PN2_POOL_WEIGHTED_AVG && (ns > 256 || !grouped_xyz)) return PN2_EINVAL;
+  const long long G = (long long)B * M;
+  if (G == 0 || C == 0) return PN2_OK;
+  if (!x || !out || G > INT32_MAX) return PN2_EINVAL;
+  hipLaunchKernelGGL(pn2::group_pool_kernel, dim3(pn2::grid_for(G)), dim3(pn2::kBlock), 0,
+                     (hipStream_t)stream, x, grouped_xyz, (int)G, ns, C, mode, out);
+  PN2_RETURN_LAUNCH();
+}
+
+const char* pn2_version(void) { return "pn2hip 0.1 (gfx950)"; }
+
+const char* pn2_strerror(int status) {
+  if (status == PN2_OK) return "ok";
+  if (status == PN2_EINVAL) return "invalid argument (shape, attribute or null pointer)";
+  return hipGetErrorString((hipError_t)status);
+}
+
+}  // extern "C"

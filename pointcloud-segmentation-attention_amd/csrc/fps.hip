@@ -1,0 +1,308 @@
+// Farthest-point sampling + gather_point for gfx950.
+//
+// Replaces FarthestPointSampleGpuOp / farthestpointsamplingKernel
+// (pointnet2_tensorflow/tf_ops/sampling/tf_sampling.cpp:94-123, tf_sampling_g.cu:105-170) and
+// GatherPoint(+Grad) (tf_sampling.cpp:125-178, tf_sampling_g.cu:172-192).
+//
+// Design (MI355X-first, not a translation of the reference's <<<32,512>>> kernel):
+//  * one workgroup per cloud; the cloud's xyz and the running min-distance live in VGPRs
+//    (PPT points per thread), so the N-point sweep of every iteration touches no memory;
+//  * the per-iteration argmax is ONE u64 max: key = (fp32 bits of d) << 32 | ~tiekey, with
+//    tiekey = (k mod 512) << 20 | (k div 512). Since d >= 0 its bits order like the float,
+//    so the max picks the largest distance and, among equal distances, the smallest
+//    (k mod 512, k div 512) — exactly the winner of the reference's per-thread strict '>'
+//    scan (tf_sampling_g.cu:146) followed by its left-biased tree (tf_sampling_g.cu:158);
+//  * wave reduce in registers (DPP + v_permlane16/32_swap), one LDS slot per wave,
+//    double-buffered by iteration parity so ONE barrier per iteration is race-free (the
+//    reference's single dists_i buffer has a write-after-read race, :151-152 vs :165);
+//  * the winner's coordinates come from an LDS copy of the cloud (uniform-address
+//    broadcast read) when it fits, otherwise from global memory (scalar load);
+//  * thread 0 also writes new_xyz, fusing gather_point into the sampler (pointnet_util.py:34).
+#include "common.h"
+
+namespace pn2 {
+namespace {
+
+constexpr float kInitTemp = 1e38f;  // tf_sampling_g.cu:118
+
+// Low word of the argmax key: larger = earlier in the reference's tie order.
+PN2_DEV uint32_t tie_low(int k) {
+  const uint32_t tk = (((uint32_t)k & 511u) << 20) | ((uint32_t)k >> 9);
+  return 0xFFFFFFFFu - tk;
+}
+PN2_DEV int tie_decode(uint32_t low) {
+  const uint32_t tk = 0xFFFFFFFFu - low;
+  return (int)((tk >> 20) + ((tk & 0xFFFFFu) << 9));
+}
+
+// Thread t owns points t + slot_off(i), i = 0..PPT-1. Slots are ordered so that, within one
+// thread, ascending slot = ascending (k mod 512, k div 512); then a strict '>' scan over the
+// slots keeps the reference's tie winner inside the thread.
+template <int BLOCK, int PPT>
+PN2_DEV constexpr int slot_off(int i) {
+  if constexpr (BLOCK >= 512) {
+    return BLOCK * i;  // k mod 512 is the same for every slot of the thread
+  } else {
+    constexpr int R = 512 / BLOCK;  // slots per residue class
+    if constexpr (PPT <= R) {
+      return BLOCK * i;  // all slots < 512: k mod 512 == k
+    } else {
+      constexpr int Q = PPT / R;  // slots that share one residue
+      return BLOCK * ((i % Q) * R + i / Q);
+    }
+  }
+}
+
+template <int BLOCK, int PPT, bool XYZ_LDS>
+__global__ __launch_bounds__(BLOCK) void fps_reg_kernel(const float* __restrict__ xyz, int N,
+                                                        int M, int32_t* __restrict__ idx,
+                                                        float* __restrict__ new_xyz) {
+  constexpr int NW = BLOCK / kWave;
+  static_assert(NW <= 16, "the cross-wave step reduces one 16-lane DPP row");
+  __shared__ uint64_t red[2][16];
+  __shared__ float sxyz[XYZ_LDS ? 3 * BLOCK * PPT : 1];
+
+  const int b = blockIdx.x;
+  const int t = threadIdx.x;
+  const int lane = t & (kWave - 1);
+  const int w = t / kWave;
+  const float* __restrict__ P = xyz + (size_t)b * N * 3;
+  int32_t* __restrict__ I = idx + (size_t)b * M;
+  float* __restrict__ NX = new_xyz ? new_xyz + (size_t)b * M * 3 : nullptr;
+
+  float px[PPT], py[PPT], pz[PPT], tm[PPT];
+#pragma unroll
+  for (int i = 0; i < PPT; ++i) {
+    const int k = t + slot_off<BLOCK, PPT>(i);
+    if (k < N) {
+      px[i] = P[3 * k + 0];
+      py[i] = P[3 * k + 1];
+      pz[i] = P[3 * k + 2];
+      tm[i] = kInitTemp;
+    } else {  // padding slot: min(d, -1) stays -1 and never wins
+      px[i] = py[i] = pz[i] = 0.0f;
+      tm[i] = -1.0f;
+    }
+  }
+  if constexpr (XYZ_LDS) {
+    for (int e = t; e < 3 * N; e += BLOCK) sxyz[e] = P[e];
+    __syncthreads();
+  }
+
+  float cx = P[0], cy = P[1], cz = P[2];  // old = 0 (tf_sampling_g.cu:114-116)
+  if (t == 0) {
+    I[0] = 0;
+    if (NX) { NX[0] = cx; NX[1] = cy; NX[2] = cz; }
+  }
+
+  for (int j = 1; j < M; ++j) {
+    float bd = -1.0f;
+    int bi = 0;
+#pragma unroll
+    for (int i = 0; i < PPT; ++i) {
+      const float d = sqdist(px[i], py[i], pz[i], cx, cy, cz);
+      const float v = fminf(d, tm[i]);  // tf_sampling_g.cu:143
+      tm[i] = v;
+      if (v > bd) { bd = v; bi = i; }   // tf_sampling_g.cu:146-149
+    }
+    // runtime slot -> point index (same mapping as slot_off, shifts and masks only)
+    int off;
+    if constexpr (BLOCK >= 512 || PPT <= 512 / BLOCK) {
+      off = BLOCK * bi;
+    } else {
+      constexpr int R = 512 / BLOCK, Q = PPT / R;
+      off = BLOCK * ((bi % Q) * R + bi / Q);
+    }
+    uint64_t key = bd < 0.0f ? 0ull : pack64(tie_low(t + off), __float_as_uint(bd));
+    key = wave_max_u64(key);
+    if constexpr (NW > 1) {
+      if (lane == 0) red[j & 1][w] = key;
+      __syncthreads();
+      key = row16_max_u64(lane < NW ? red[j & 1][lane] : 0ull);
+    }
+    const int old = tie_decode(uniform_u32((uint32_t)key));
+    if constexpr (XYZ_LDS) {
+      cx = sxyz[3 * old + 0]; cy = sxyz[3 * old + 1]; cz = sxyz[3 * old + 2];
+    } else {
+      cx = P[3 * old + 0]; cy = P[3 * old + 1]; cz = P[3 * old + 2];
+    }
+    if (t == 0) {
+      I[j] = old;
+      if (NX) { NX[3 * j + 0] = cx; NX[3 * j + 1] = cy; NX[3 * j + 2] = cz; }
+    }
+  }
+}
+
+// Large clouds (N beyond the register path): running min-distance in a global workspace,
+// 1024 threads, point k on thread k mod 1024 (ascending slot order = reference tie order).
+__global__ __launch_bounds__(1024) void fps_ws_kernel(const float* __restrict__ xyz, int N, int M,
+                                                      float* __restrict__ ws,
+                                                      int32_t* __restrict__ idx,
+                                                      float* __restrict__ new_xyz) {
+  constexpr int BLOCK = 1024, NW = BLOCK / kWave;
+  __shared__ uint64_t red[2][16];
+  const int b = blockIdx.x, t = threadIdx.x, lane = t & (kWave - 1), w = t / kWave;
+  const float* __restrict__ P = xyz + (size_t)b * N * 3;
+  float* __restrict__ T = ws + (size_t)b * N;
+  int32_t* __restrict__ I = idx + (size_t)b * M;
+  float* __restrict__ NX = new_xyz ? new_xyz + (size_t)b * M * 3 : nullptr;
+  for (int k = t; k < N; k += BLOCK) T[k] = kInitTemp;
+  float cx = P[0], cy = P[1], cz = P[2];
+  if (t == 0) {
+    I[0] = 0;
+    if (NX) { NX[0] = cx; NX[1] = cy; NX[2] = cz; }
+  }
+  for (int j = 1; j < M; ++j) {
+    float bd = -1.0f;
+    int bk = 0;
+    for (int k = t; k < N; k += BLOCK) {
+      const float d = sqdist(P[3 * k], P[3 * k + 1], P[3 * k + 2], cx, cy, cz);
+      const float v = fminf(d, T[k]);
+      T[k] = v;
+      if (v > bd) { bd = v; bk = k; }
+    }
+    uint64_t key = bd < 0.0f ? 0ull : pack64(tie_low(bk), __float_as_uint(bd));
+    key = wave_max_u64(key);
+    if (lane == 0) red[j & 1][w] = key;
+    __syncthreads();
+    key = row16_max_u64(lane < NW ? red[j & 1][lane] : 0ull);
+    const int old = tie_decode(uniform_u32((uint32_t)key));
+    cx = P[3 * old + 0]; cy = P[3 * old + 1]; cz = P[3 * old + 2];
+    if (t == 0) {
+      I[j] = old;
+      if (NX) { NX[3 * j + 0] = cx; NX[3 * j + 1] = cy; NX[3 * j + 2] = cz; }
+    }
+  }
+}
+
+// N == 0: the reference still emits idx 0 everywhere (tf_sampling_g.cu:125-167 with no point
+// scanned leaves besti = 0); new_xyz has nothing to gather and is zero-filled.
+__global__ void fps_empty_kernel(int total, int32_t* idx, float* new_xyz) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < total) {
+    idx[i] = 0;
+    if (new_xyz) { new_xyz[3 * i] = 0.f; new_xyz[3 * i + 1] = 0.f; new_xyz[3 * i + 2] = 0.f; }
+  }
+}
+
+__global__ void gather_point_kernel(const float* __restrict__ inp, const int32_t* __restrict__ idx,
+                                    int N, int M, int total, float* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;  // i = b*M + j
+  if (i >= total) return;
+  const int b = i / M;
+  const int a = idx[i];
+  const float* src = inp + ((size_t)b * N + a) * 3;
+  out[3 * (size_t)i + 0] = src[0];
+  out[3 * (size_t)i + 1] = src[1];
+  out[3 * (size_t)i + 2] = src[2];
+}
+
+__global__ void gather_point_grad_kernel(const float* __restrict__ out_g,
+                                         const int32_t* __restrict__ idx, int N, int M,
+                                         int total, float* __restrict__ inp_g) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int b = i / M;
+  const int a = idx[i];
+  float* dst = inp_g + ((size_t)b * N + a) * 3;
+  atomicAdd(dst + 0, out_g[3 * (size_t)i + 0]);
+  atomicAdd(dst + 1, out_g[3 * (size_t)i + 1]);
+  atomicAdd(dst + 2, out_g[3 * (size_t)i + 2]);
+}
+
+constexpr int kMaxRegPoints = 1024 * 16;
+
+// The LDS copy of the cloud (12 B per point) is used whenever it fits next to the key slots
+// in the 160 KiB of one CU; otherwise the winner's xyz is re-read from global memory.
+template <int BLOCK, int PPT>
+void launch_reg(const float* xyz, int B, int N, int M, int32_t* idx, float* nx, hipStream_t s) {
+  if constexpr (3 * BLOCK * PPT * 4 + 256 <= 160 * 1024)
+    hipLaunchKernelGGL((fps_reg_kernel<BLOCK, PPT, true>), dim3(B), dim3(BLOCK), 0, s, xyz, N, M,
+                       idx, nx);
+  else
+    hipLaunchKernelGGL((fps_reg_kernel<BLOCK, PPT, false>), dim3(B), dim3(BLOCK), 0, s, xyz, N,
+                       M, idx, nx);
+}
+
+int fps_impl(const float* xyz, int B, int N, int M, int32_t* idx, float* nx, void* ws,
+             size_t ws_bytes, hipStream_t s) {
+  if (B < 0 || N < 0 || M <= 0 || (B > 0 && (!xyz || !idx))) return PN2_EINVAL;
+  if (B == 0) return PN2_OK;
+  if (N == 0) {
+    const int total = B * M;
+    hipLaunchKernelGGL(fps_empty_kernel, dim3((total + 255) / 256), dim3(256), 0, s, total, idx,
+                       nx);
+    PN2_RETURN_LAUNCH();
+  }
+  if (N <= 64) launch_reg<64, 1>(xyz, B, N, M, idx, nx, s);
+  else if (N <= 128) launch_reg<64, 2>(xyz, B, N, M, idx, nx, s);
+  else if (N <= 256) launch_reg<64, 4>(xyz, B, N, M, idx, nx, s);
+  else if (N <= 512) launch_reg<128, 4>(xyz, B, N, M, idx, nx, s);
+  else if (N <= 1024) launch_reg<256, 4>(xyz, B, N, M, idx, nx, s);
+  else if (N <= 2048) launch_reg<256, 8>(xyz, B, N, M, idx, nx, s);
+  else if (N <= 4096) launch_reg<512, 8>(xyz, B, N, M, idx, nx, s);
+  else if (N <= 8192) launch_reg<1024, 8>(xyz, B, N, M, idx, nx, s);
+  else if (N <= kMaxRegPoints) launch_reg<1024, 16>(xyz, B, N, M, idx, nx, s);
+  else {
+    if (!ws || ws_bytes < (size_t)B * N * sizeof(float)) return PN2_EINVAL;
+    hipLaunchKernelGGL(fps_ws_kernel, dim3(B), dim3(1024), 0, s, xyz, N, M, (float*)ws, idx, nx);
+  }
+  PN2_RETURN_LAUNCH();
+}
+
+}  // namespace
+}  // namespace pn2
+
+extern "C" {
+
+int pn2_fps_max_points(void) { return pn2::kMaxRegPoints; }
+
+size_t pn2_fps_workspace_size(int B, int N) {
+  if (B <= 0 || N <= pn2::kMaxRegPoints) return 0;
+  return (size_t)B * (size_t)N * sizeof(float);
+}
+
+int pn2_fps(const float* xyz, int B, int N, int npoint, int32_t* idx, pn2_stream_t stream) {
+  return pn2::fps_impl(xyz, B, N, npoint, idx, nullptr, nullptr, 0, (hipStream_t)stream);
+}
+
+int pn2_fps_gather(const float* xyz, int B, int N, int npoint, int32_t* idx, float* new_xyz,
+                   pn2_stream_t stream) {
+  return pn2::fps_impl(xyz, B, N, npoint, idx, new_xyz, nullptr, 0, (hipStream_t)stream);
+}
+
+int pn2_fps_ws(const float* xyz, int B, int N, int npoint, int32_t* idx, float* new_xyz,
+               void* workspace, size_t workspace_bytes, pn2_stream_t stream) {
+  return pn2::fps_impl(xyz, B, N, npoint, idx, new_xyz, workspace, workspace_bytes,
+                       (hipStream_t)stream);
+}
+
+int pn2_gather_point(const float* inp, const int32_t* idx, int B, int N, int M, float* out,
+                     pn2_stream_t stream) {
+  if (B < 0 || N < 0 || M < 0) return PN2_EINVAL;
+  const long long total = (long long)B * M;
+  if (total == 0) return PN2_OK;
+  if (total > INT32_MAX || !inp || !idx || !out) return PN2_EINVAL;
+  hipLaunchKernelGGL(pn2::gather_point_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256),
+                     0, (hipStream_t)stream, inp, idx, N, M, (int)total, out);
+  PN2_RETURN_LAUNCH();
+}
+
+int pn2_gather_point_grad(const float* out_g, const int32_t* idx, int B, int N, int M,
+                          float* inp_g, pn2_stream_t stream) {
+  if (B < 0 || N < 0 || M < 0) return PN2_EINVAL;
+  const size_t bytes = (size_t)B * N * 3 * sizeof(float);
+  if (bytes) {
+    if (!inp_g) return PN2_EINVAL;
+    hipError_t e = hipMemsetAsync(inp_g, 0, bytes, (hipStream_t)stream);
+    if (e != hipSuccess) return (int)e;
+  }
+  const long long total = (long long)B * M;
+  if (total == 0) return PN2_OK;
+  if (total > INT32_MAX || !out_g || !idx) return PN2_EINVAL;
+  hipLaunchKernelGGL(pn2::gather_point_grad_kernel, dim3((unsigned)((total + 255) / 256)),
+                     dim3(256), 0, (hipStream_t)stream, out_g, idx, N, M, (int)total, inp_g);
+  PN2_RETURN_LAUNCH();
+}
+
+}  // extern "C"

@@ -1,0 +1,305 @@
+// Feature propagation for gfx950: three_nn, IDW weights, three_interpolate (+grad), and the
+// fused pointnet_fp_module geometry.
+//
+// Replaces ThreeNNOp / threenn_cpu (tf_interpolate.cpp:157-187, :60-103), ThreeInterpolateOp /
+// threeinterpolate_cpu (:191-222, :107-127), ThreeInterpolateGradOp (:225-262, :131-153) and
+// the TF graph ops of pointnet_util.py:218-226. In the reference these run on the HOST CPU
+// (DEVICE_CPU kernels only, tf_interpolate.cpp:187,222,262), so every FP layer of a GPU
+// training step pays a device→host→device round trip; here they stay in HBM.
+//
+// three_nn semantics kept bit-exact: d2 = ((dx*dx+dy*dy)+dz*dz) in fp32 (:73, stored to a
+// double without changing its value), strict '<' insertion into best1..3 (:74-89) so equal
+// distances keep the lower known index, unfilled slots stay idx 0 / dist +inf (= (float)1e40).
+// three_interpolate: ((p1*w1)+(p2*w2))+(p3*w3) in fp32 without FMA (:119).
+//
+// Design: one lane per unknown point; the known cloud is staged in LDS as float4 tiles and
+// every lane reads the same element (a broadcast), keeping best1..3 in registers with a
+// branch-free insertion. The fused FP kernel then parks each row's (idx, weight) triple in
+// LDS and writes the [interp, points1] rows of the whole workgroup as one coalesced stream.
+#include "common.h"
+
+namespace pn2 {
+namespace {
+
+constexpr int kNNBlock = 256;
+constexpr int kNNTile = 2048;  // known points per LDS tile (32 KiB of float4)
+
+struct Best3 {
+  float d1, d2, d3;
+  int i1, i2, i3;
+};
+
+PN2_DEV void best3_init(Best3& b) {
+  b.d1 = b.d2 = b.d3 = __builtin_inff();
+  b.i1 = b.i2 = b.i3 = 0;
+}
+
+// tf_interpolate.cpp:74-89 as selects (same result: the if/else-if chain is a stable insert)
+PN2_DEV void best3_insert(Best3& b, float d, int k) {
+  const bool c1 = d < b.d1, c2 = d < b.d2, c3 = d < b.d3;
+  b.d3 = c2 ? b.d2 : (c3 ? d : b.d3);
+  b.i3 = c2 ? b.i2 : (c3 ? k : b.i3);
+  b.d2 = c1 ? b.d1 : (c2 ? d : b.d2);
+  b.i2 = c1 ? b.i1 : (c2 ? k : b.i2);
+  b.d1 = c1 ? d : b.d1;
+  b.i1 = c1 ? k : b.i1;
+}
+
+// Scans all m known points of cloud b for the unknown point (x1,y1,z1). Every thread of the
+// block must call it (it stages tiles with barriers).
+PN2_DEV void scan_known(const float* __restrict__ K, int m, float x1, float y1, float z1,
+                        float4* sk, Best3& best) {
+  for (int t0 = 0; t0 < m; t0 += kNNTile) {
+    const int cnt = min(kNNTile, m - t0);
+    __syncthreads();  // previous tile fully consumed
+    for (int e = threadIdx.x; e < cnt; e += kNNBlock) {
+      const float* p = K + 3 * (size_t)(t0 + e);
+      sk[e] = make_float4(p[0], p[1], p[2], 0.0f);
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int e = 0; e < cnt; ++e) {
+      const float4 p = sk[e];
+      best3_insert(best, sqdist(p.x, p.y, p.z, x1, y1, z1), t0 + e);  // (x2-x1), x2 known
+    }
+  }
+}
+
+// weight = (1/d)/sum(1/d), d = max(dist, 1e-10)  (pointnet_util.py:219-222)
+PN2_DEV void idw(float d1, float d2, float d3, float& w1, float& w2, float& w3) {
+  const float r1 = 1.0f / fmaxf(d1, 1e-10f);
+  const float r2 = 1.0f / fmaxf(d2, 1e-10f);
+  const float r3 = 1.0f / fmaxf(d3, 1e-10f);
+  const float norm = (r1 + r2) + r3;
+  w1 = r1 / norm;
+  w2 = r2 / norm;
+  w3 = r3 / norm;
+}
+
+__global__ __launch_bounds__(kNNBlock) void three_nn_kernel(const float* __restrict__ xyz1,
+                                                            const float* __restrict__ xyz2, int n,
+                                                            int m, float* __restrict__ dist,
+                                                            int32_t* __restrict__ idx) {
+  __shared__ float4 sk[kNNTile];
+  const int b = blockIdx.y;
+  const int j = blockIdx.x * kNNBlock + threadIdx.x;
+  const bool valid = j < n;
+  const float* U = xyz1 + ((size_t)b * n + (valid ? j : 0)) * 3;
+  Best3 best;
+  best3_init(best);
+  scan_known(xyz2 + (size_t)b * m * 3, m, U[0], U[1], U[2], sk, best);
+  if (valid) {
+    float* D = dist + ((size_t)b * n + j) * 3;
+    int32_t* I = idx + ((size_t)b * n + j) * 3;
+    D[0] = best.d1; D[1] = best.d2; D[2] = best.d3;
+    I[0] = best.i1; I[1] = best.i2; I[2] = best.i3;
+  }
+}
+
+__global__ void idw_kernel(const float* __restrict__ dist, int total, float* __restrict__ weight) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const float* d = dist + 3 * (size_t)i;
+  float w1, w2, w3;
+  idw(d[0], d[1], d[2], w1, w2, w3);
+  weight[3 * (size_t)i + 0] = w1;
+  weight[3 * (size_t)i + 1] = w2;
+  weight[3 * (size_t)i + 2] = w3;
+}
+
+constexpr int kBlock = 256;
+constexpr int kTileElems = 2048;
+
+// out (B,n,C): flat coalesced stream, `rows` rows per workgroup
+__global__ __launch_bounds__(kBlock) void three_interp_kernel(
+    const float* __restrict__ points, const int32_t* __restrict__ idx,
+    const float* __restrict__ weight, int m, int C, int n, int rows, FastDiv div_c,
+    FastDiv div_n, uint32_t total_rows, float* __restrict__ out) {
+  const uint32_t r0 = blockIdx.x * (uint32_t)rows;
+  const int nrows = (int)min((uint32_t)rows, total_rows - r0);
+  const int elems = nrows * C;
+  for (int e = threadIdx.x; e < elems; e += kBlock) {
+    const uint32_t rl = fdiv((uint32_t)e, div_c);
+    const int c = e - (int)rl * C;
+    const uint32_t r = r0 + rl;  // r = b*n + j
+    const uint32_t b = fdiv(r, div_n);
+    const int32_t* I = idx + 3 * (size_t)r;
+    const float* W = weight + 3 * (size_t)r;
+    const float* P = points + (size_t)b * m * C + c;
+    float v = P[(size_t)I[0] * C] * W[0];
+    v = v + P[(size_t)I[1] * C] * W[1];
+    v = v + P[(size_t)I[2] * C] * W[2];
+    out[(size_t)r * C + c] = v;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void three_interp_grad_kernel(
+    const float* __restrict__ grad_out, const int32_t* __restrict__ idx,
+    const float* __restrict__ weight, int m, int C, int rows, FastDiv div_c, FastDiv div_n,
+    uint32_t total_rows, float* __restrict__ grad_points) {
+  const uint32_t r0 = blockIdx.x * (uint32_t)rows;
+  const int nrows = (int)min((uint32_t)rows, total_rows - r0);
+  const int elems = nrows * C;
+  for (int e = threadIdx.x; e < elems; e += kBlock) {
+    const uint32_t rl = fdiv((uint32_t)e, div_c);
+    const int c = e - (int)rl * C;
+    const uint32_t r = r0 + rl;
+    const uint32_t b = fdiv(r, div_n);
+    const int32_t* I = idx + 3 * (size_t)r;
+    const float* W = weight + 3 * (size_t)r;
+    float* G = grad_points + (size_t)b * m * C + c;
+    const float g = grad_out[(size_t)r * C + c];
+    atomicAdd(G + (size_t)I[0] * C, g * W[0]);  // tf_interpolate.cpp:143-145
+    atomicAdd(G + (size_t)I[1] * C, g * W[1]);
+    atomicAdd(G + (size_t)I[2] * C, g * W[2]);
+  }
+}
+
+// pointnet_fp_module geometry, one workgroup = 256 unknown points of one cloud.
+__global__ __launch_bounds__(kNNBlock) void fp_fused_kernel(
+    const float* __restrict__ xyz1, const float* __restrict__ xyz2,
+    const float* __restrict__ points1, int C1, const float* __restrict__ points2, int C2, int n,
+    int m, FastDiv div_cout, float* __restrict__ out) {
+  __shared__ float4 sk[kNNTile];
+  __shared__ int4 s_idx[kNNBlock];
+  __shared__ float4 s_w[kNNBlock];
+  const int b = blockIdx.y;
+  const int j0 = blockIdx.x * kNNBlock;
+  const int j = j0 + threadIdx.x;
+  const bool valid = j < n;
+  const float* U = xyz1 + ((size_t)b * n + (valid ? j : 0)) * 3;
+  Best3 best;
+  best3_init(best);
+  scan_known(xyz2 + (size_t)b * m * 3, m, U[0], U[1], U[2], sk, best);
+  float w1, w2, w3;
+  idw(best.d1, best.d2, best.d3, w1, w2, w3);
+  s_idx[threadIdx.x] = make_int4(best.i1, best.i2, best.i3, 0);
+  s_w[threadIdx.x] = make_float4(w1, w2, w3, 0.0f);
+  __syncthreads();
+  const int Cout = C2 + C1;
+  const int nrows = min(kNNBlock, n - j0);
+  const int elems = nrows * Cout;
+  const float* P2 = points2 + (size_t)b * m * C2;
+  float* O = out + ((size_t)b * n + j0) * Cout;
+  for (int e = threadIdx.x; e < elems; e += kNNBlock) {
+    const int rl = (int)fdiv((uint32_t)e, div_cout);
+    const int c = e - rl * Cout;
+    float v;
+    if (c < C2) {  // three_interpolate (tf_interpolate.cpp:119)
+      const int4 I = s_idx[rl];
+      const float4 W = s_w[rl];
+      v = P2[(size_t)I.x * C2 + c] * W.x;
+      v = v + P2[(size_t)I.y * C2 + c] * W.y;
+      v = v + P2[(size_t)I.z * C2 + c] * W.z;
+    } else {       // concat [interpolated, points1] (pointnet_util.py:226)
+      v = points1[((size_t)b * n + j0 + rl) * C1 + (c - C2)];
+    }
+    O[(size_t)e] = v;
+  }
+}
+
+// Largest batch chunk whose 32-bit row arithmetic stays exact (rows*n < 2^32, see FastDiv).
+int batch_chunk(int B, int n, int C, int rows) {
+  if ((long long)rows * C * C >= (1LL << 32)) return 0;
+  long long per_b = (long long)n * n;  // rows of one cloud times the divisor n
+  if (per_b >= (1LL << 32)) return 0;
+  long long ch = ((1LL << 32) - 1) / (per_b > 0 ? per_b : 1);
+  if ((long long)n * ch >= (1LL << 31)) ch = ((1LL << 31) - 1) / (n > 0 ? n : 1);
+  return (int)(ch < B ? ch : B);
+}
+
+}  // namespace
+}  // namespace pn2
+
+extern "C" {
+
+int pn2_three_nn(const float* xyz1, const float* xyz2, int B, int n, int m, float* dist,
+                 int32_t* idx, pn2_stream_t stream) {
+  if (B < 0 || n < 0 || m < 0 || B > 65535) return PN2_EINVAL;
+  if ((long long)B * n == 0) return PN2_OK;
+  if (!xyz1 || !dist || !idx || (m > 0 && !xyz2)) return PN2_EINVAL;
+  hipLaunchKernelGGL(pn2::three_nn_kernel, dim3((n + pn2::kNNBlock - 1) / pn2::kNNBlock, B),
+                     dim3(pn2::kNNBlock), 0, (hipStream_t)stream, xyz1, xyz2, n, m, dist, idx);
+  PN2_RETURN_LAUNCH();
+}
+
+int pn2_idw_weights(const float* dist, int B, int n, float* weight, pn2_stream_t stream) {
+  if (B < 0 || n < 0) return PN2_EINVAL;
+  const long long total = (long long)B * n;
+  if (total == 0) return PN2_OK;
+  if (total > INT32_MAX || !dist || !weight) return PN2_EINVAL;
+  hipLaunchKernelGGL(pn2::idw_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, dist, (int)total, weight);
+  PN2_RETURN_LAUNCH();
+}
+
+int pn2_three_interpolate(const float* points, const int32_t* idx, const float* weight, int B,
+                          int m, int C, int n, float* out, pn2_stream_t stream) {
+  if (B < 0 || m < 0 || C < 0 || n < 0) return PN2_EINVAL;
+  if ((long long)B * n == 0 || C == 0) return PN2_OK;
+  if (!points || !idx || !weight || !out) return PN2_EINVAL;
+  const int rows = C >= pn2::kTileElems ? 1 : pn2::kTileElems / C;
+  const int chunk = pn2::batch_chunk(B, n, C, rows);
+  if (chunk <= 0) return PN2_EINVAL;
+  for (int b0 = 0; b0 < B; b0 += chunk) {
+    const int nb = B - b0 < chunk ? B - b0 : chunk;
+    const long long total_rows = (long long)nb * n;
+    const long long tiles = (total_rows + rows - 1) / rows;
+    hipLaunchKernelGGL(pn2::three_interp_kernel, dim3((unsigned)tiles), dim3(pn2::kBlock), 0,
+                       (hipStream_t)stream, points + (size_t)b0 * m * C, idx + (size_t)b0 * n * 3,
+                       weight + (size_t)b0 * n * 3, m, C, n, rows, pn2::make_fastdiv((uint32_t)C),
+                       pn2::make_fastdiv((uint32_t)n), (uint32_t)total_rows,
+                       out + (size_t)b0 * n * C);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return (int)e;
+  }
+  return PN2_OK;
+}
+
+int pn2_three_interpolate_grad(const float* grad_out, const int32_t* idx, const float* weight,
+                               int B, int n, int C, int m, float* grad_points,
+                               pn2_stream_t stream) {
+  if (B < 0 || m < 0 || C < 0 || n < 0) return PN2_EINVAL;
+  const size_t bytes = (size_t)B * m * C * sizeof(float);
+  if (bytes) {
+    if (!grad_points) return PN2_EINVAL;
+    hipError_t e = hipMemsetAsync(grad_points, 0, bytes, (hipStream_t)stream);
+    if (e != hipSuccess) return (int)e;
+  }
+  if ((long long)B * n == 0 || C == 0) return PN2_OK;
+  if (!grad_out || !idx || !weight) return PN2_EINVAL;
+  const int rows = C >= pn2::kTileElems ? 1 : pn2::kTileElems / C;
+  const int chunk = pn2::batch_chunk(B, n, C, rows);
+  if (chunk <= 0) return PN2_EINVAL;
+  for (int b0 = 0; b0 < B; b0 += chunk) {
+    const int nb = B - b0 < chunk ? B - b0 : chunk;
+    const long long total_rows = (long long)nb * n;
+    const long long tiles = (total_rows + rows - 1) / rows;
+    hipLaunchKernelGGL(pn2::three_interp_grad_kernel, dim3((unsigned)tiles), dim3(pn2::kBlock), 0,
+                       (hipStream_t)stream, grad_out + (size_t)b0 * n * C,
+                       idx + (size_t)b0 * n * 3, weight + (size_t)b0 * n * 3, m, C, rows,
+                       pn2::make_fastdiv((uint32_t)C), pn2::make_fastdiv((uint32_t)n),
+                       (uint32_t)total_rows, grad_points + (size_t)b0 * m * C);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return (int)e;
+  }
+  return PN2_OK;
+}
+
+int pn2_fp_fused(const float* xyz1, const float* xyz2, const float* points1, int C1,
+                 const float* points2, int C2, int B, int n, int m, float* out,
+                 pn2_stream_t stream) {
+  if (B < 0 || n < 0 || m < 0 || C1 < 0 || C2 < 0 || B > 65535) return PN2_EINVAL;
+  if (!points1 && C1 != 0) return PN2_EINVAL;
+  if ((long long)B * n == 0 || C1 + C2 == 0) return PN2_OK;
+  if (!xyz1 || !out || (m > 0 && !xyz2) || (C2 > 0 && !points2)) return PN2_EINVAL;
+  if (m == 0 && C2 > 0) return PN2_EINVAL;  // nothing to interpolate from
+  const int Cout = C1 + C2;
+  if ((long long)pn2::kNNBlock * Cout * Cout >= (1LL << 32)) return PN2_EINVAL;
+  hipLaunchKernelGGL(pn2::fp_fused_kernel, dim3((n + pn2::kNNBlock - 1) / pn2::kNNBlock, B),
+                     dim3(pn2::kNNBlock), 0, (hipStream_t)stream, xyz1, xyz2, points1, C1,
+                     points2, C2, n, m, pn2::make_fastdiv((uint32_t)Cout), out);
+  PN2_RETURN_LAUNCH();
+}
+
+}  // extern "C"

@@ -1,0 +1,165 @@
+"""The hot-path geometry of pointnet2_tensorflow/utils/pointnet_util.py on gfx950.
+
+sample_and_group / sample_and_group_all keep the reference signatures and return values; the
+dense MLP / BN parts of pointnet_sa_module / pointnet_fp_module are out of scope (torch
+provides them), so this module exposes the geometric halves of those layers:
+
+  sample_and_group          pointnet_util.py:16-58    FPS + gather + ball query + fused group
+  sample_and_group_all      pointnet_util.py:61-87
+  sample_and_group_msg      pointnet_util.py:180-193  one FPS, several (radius, nsample) scales
+  group_pool                pointnet_util.py:130-145  max / avg / weighted_avg / max_and_avg
+  fp_interpolate            pointnet_util.py:218-228  three_nn + IDW + interpolate + concat
+
+Without autograd the fused kernels run (fewest launches, one pass over HBM); when a gradient
+is required, the composition of differentiable ops (gather_point, group_point,
+three_interpolate) is used instead so that backward reaches xyz and points like the
+reference's registered gradients.
+"""
+import torch
+
+from . import tf_grouping, tf_interpolate, tf_sampling
+from ._lib import (POOL_MODES, PN2_USE_XYZ, PN2_XYZ_LAST, InvalidArgumentError, check,
+                   device_tensor, lib, ptr, stream_of)
+
+
+def _is_empty_points(points):
+    # pointnet_util.py:41: points with the shape of tf.zeros([0]) mean "no features"
+    return points is None or (points.dim() == 1 and points.shape[0] == 0)
+
+
+def _needs_grad(*ts):
+    return torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in ts)
+
+
+def group_concat(xyz, points, new_xyz, idx, use_xyz=True, xyz_last=False, want_grouped_xyz=True):
+    """Fused group_point(xyz) - new_xyz, group_point(points) and concat
+    (pointnet_util.py:39-56 SSG order [xyz, points]; xyz_last=True gives the MSG order
+    [points, xyz] of :191). Returns (new_points, grouped_xyz or None)."""
+    B, N = int(xyz.shape[0]), int(xyz.shape[1])
+    M, ns = int(idx.shape[1]), int(idx.shape[2])
+    if _is_empty_points(points):
+        points, C, Cout = None, 0, 3
+    else:
+        points = device_tensor(points, "points", torch.float32)
+        C = int(points.shape[2])
+        Cout = C + 3 if use_xyz else C
+    if _needs_grad(xyz, points, new_xyz):
+        grouped_xyz = tf_grouping.group_point(xyz, idx) - new_xyz.unsqueeze(2)
+        if points is None:
+            return grouped_xyz, grouped_xyz
+        gp = tf_grouping.group_point(points, idx)
+        if not use_xyz:
+            return gp, grouped_xyz
+        parts = [gp, grouped_xyz] if xyz_last else [grouped_xyz, gp]
+        return torch.cat(parts, dim=-1), grouped_xyz
+    flags = (PN2_USE_XYZ if use_xyz else 0) | (PN2_XYZ_LAST if xyz_last else 0)
+    new_points = torch.empty((B, M, ns, Cout), dtype=torch.float32, device=xyz.device)
+    grouped_xyz = torch.empty((B, M, ns, 3), dtype=torch.float32, device=xyz.device) \
+        if (want_grouped_xyz and points is not None) else None
+    check(lib().pn2_group_concat(ptr(xyz), ptr(points), ptr(new_xyz), ptr(idx), B, N, C, M, ns,
+                                 flags, ptr(grouped_xyz), ptr(new_points), stream_of(xyz)),
+          "group_concat")
+    if points is None and want_grouped_xyz:
+        grouped_xyz = new_points  # identical values (pointnet_util.py:56)
+    return new_points, grouped_xyz
+
+
+def sample_and_group(npoint, radius, nsample, xyz, points, knn=False, use_xyz=True):
+    """pointnet_util.py:16-58.
+
+    Output:
+        new_xyz: (batch_size, npoint, 3)
+        new_points: (batch_size, npoint, nsample, 3+channel)
+        idx: (batch_size, npoint, nsample) int32
+        grouped_xyz: (batch_size, npoint, nsample, 3), centred on new_xyz
+    """
+    if knn:
+        raise NotImplementedError(
+            "sample_and_group(knn=True) needs knn_point/select_top_k (SURVEY §8(f) row 2)")
+    xyz = device_tensor(xyz, "xyz", torch.float32)
+    if _needs_grad(xyz):
+        fps_idx = tf_sampling.farthest_point_sample(npoint, xyz)
+        new_xyz = tf_sampling.gather_point(xyz, fps_idx)
+    else:
+        _, new_xyz = tf_sampling.farthest_point_sample_and_gather(npoint, xyz)
+    idx, _ = tf_grouping.query_ball_point(radius, nsample, xyz, new_xyz.detach())
+    new_points, grouped_xyz = group_concat(xyz, points, new_xyz, idx, use_xyz=use_xyz)
+    return new_xyz, new_points, idx, grouped_xyz
+
+
+def sample_and_group_all(xyz, points, use_xyz=True):
+    """pointnet_util.py:61-87: one group per cloud holding every point, centroid (0,0,0)."""
+    xyz = device_tensor(xyz, "xyz", torch.float32)
+    B, N = int(xyz.shape[0]), int(xyz.shape[1])
+    new_xyz = torch.zeros((B, 1, 3), dtype=torch.float32, device=xyz.device)
+    idx = torch.arange(N, dtype=torch.int32, device=xyz.device).reshape(1, 1, N).expand(
+        B, 1, N).contiguous()
+    grouped_xyz = xyz.reshape(B, 1, N, 3)
+    if _is_empty_points(points):
+        return new_xyz, grouped_xyz, idx, grouped_xyz
+    new_points = torch.cat([xyz, points], dim=2) if use_xyz else points
+    return new_xyz, new_points.unsqueeze(1), idx, grouped_xyz
+
+
+def sample_and_group_msg(npoint, radius_list, nsample_list, xyz, points, use_xyz=True):
+    """Grouping half of pointnet_sa_module_msg (pointnet_util.py:180-193): one FPS, then per
+    scale a ball query and the fused group with the MSG concat order [points, xyz].
+    Returns (new_xyz, [grouped_points per scale])."""
+    xyz = device_tensor(xyz, "xyz", torch.float32)
+    if _needs_grad(xyz):
+        new_xyz = tf_sampling.gather_point(xyz, tf_sampling.farthest_point_sample(npoint, xyz))
+    else:
+        _, new_xyz = tf_sampling.farthest_point_sample_and_gather(npoint, xyz)
+    out = []
+    for radius, nsample in zip(radius_list, nsample_list):
+        idx, _ = tf_grouping.query_ball_point(radius, nsample, xyz, new_xyz.detach())
+        gp, _ = group_concat(xyz, points, new_xyz, idx, use_xyz=use_xyz, xyz_last=True,
+                             want_grouped_xyz=False)
+        out.append(gp)
+    return new_xyz, out
+
+
+def group_pool(new_points, pooling="max", grouped_xyz=None):
+    """Per-region pooling of pointnet_sa_module (pointnet_util.py:130-145), keep_dims=True:
+    (B, M, ns, C) -> (B, M, 1, C), or (B, M, 1, 2C) = [avg, max] for 'max_and_avg'."""
+    if pooling not in POOL_MODES:
+        raise InvalidArgumentError(f"unknown pooling {pooling!r}")
+    if new_points.dim() != 4:
+        raise InvalidArgumentError("group_pool expects (batch_size, npoint, nsample, channel)")
+    x = device_tensor(new_points, "new_points", torch.float32)
+    B, M, ns, C = (int(s) for s in x.shape)
+    g = None
+    if pooling == "weighted_avg":
+        if grouped_xyz is None or tuple(grouped_xyz.shape) != (B, M, ns, 3):
+            raise InvalidArgumentError("weighted_avg pooling needs grouped_xyz (B, M, ns, 3)")
+        g = device_tensor(grouped_xyz, "grouped_xyz", torch.float32)
+    Cout = 2 * C if pooling == "max_and_avg" else C
+    out = torch.empty((B, M, 1, Cout), dtype=torch.float32, device=x.device)
+    check(lib().pn2_group_pool(ptr(x), ptr(g), B, M, ns, C, POOL_MODES[pooling], ptr(out),
+                               stream_of(x)), "group_pool")
+    return out
+
+
+def fp_interpolate(xyz1, xyz2, points1, points2):
+    """Geometry of pointnet_fp_module (pointnet_util.py:218-228), before its MLP:
+    three_nn, IDW weights, three_interpolate and concat [interpolated, points1].
+    Returns (B, n, C2 + C1)."""
+    xyz1 = device_tensor(xyz1, "xyz1", torch.float32)
+    xyz2 = device_tensor(xyz2, "xyz2", torch.float32)
+    points2 = device_tensor(points2, "points2", torch.float32)
+    if _needs_grad(points1, points2):
+        dist, idx = tf_interpolate.three_nn(xyz1, xyz2)
+        weight = tf_interpolate.idw_weights(dist)
+        interp = tf_interpolate.three_interpolate(points2, idx, weight)
+        return interp if points1 is None else torch.cat([interp, points1], dim=2)
+    B, n, m = int(xyz1.shape[0]), int(xyz1.shape[1]), int(xyz2.shape[1])
+    C2 = int(points2.shape[2])
+    if points1 is not None:
+        points1 = device_tensor(points1, "points1", torch.float32)
+        C1 = int(points1.shape[2])
+    else:
+        C1 = 0
+    out = torch.empty((B, n, C2 + C1), dtype=torch.float32, device=xyz1.device)
+    check(lib().pn2_fp_fused(ptr(xyz1), ptr(xyz2), ptr(points1), C1, ptr(points2), C2, B, n, m,
+                             ptr(out), stream_of(xyz1)), "fp_interpolate")
+    return out

@@ -1,0 +1,107 @@
+"""Ball-query grouping and group_point — drop-in for
+pointnet2_tensorflow/tf_ops/grouping/tf_grouping.py (same names, argument order, shapes,
+dtypes and error messages), running the gfx950 kernels of libpn2hip.so.
+
+select_top_k / knn_point (tf_grouping.py:22-31,48-73) are the §8(f) "next" row: only the
+knn=True path of sample_and_group uses them, and no attention model sets it.
+"""
+import torch
+
+from ._lib import InvalidArgumentError, check, device_tensor, lib, ptr, stream_of
+
+
+def query_ball_point(radius, nsample, xyz1, xyz2):
+    """tf_grouping.py:8-20.
+
+    Input:
+        radius: float32, ball search radius
+        nsample: int32, number of points selected in each ball region
+        xyz1: (batch_size, ndataset, 3) float32 array, input points
+        xyz2: (batch_size, npoint, 3) float32 array, query points
+    Output:
+        idx: (batch_size, npoint, nsample) int32 array, indices to input points
+        pts_cnt: (batch_size, npoint) int32 array, number of unique points in each local region
+    """
+    if not radius > 0:  # tf_grouping.cpp:71
+        raise InvalidArgumentError("QueryBallPoint expects positive radius")
+    if int(nsample) <= 0:  # tf_grouping.cpp:74
+        raise InvalidArgumentError("QueryBallPoint expects positive nsample")
+    if xyz1.dim() != 3 or xyz1.shape[2] != 3:  # tf_grouping.cpp:79
+        raise InvalidArgumentError("QueryBallPoint expects (batch_size, ndataset, 3) xyz1 shape.")
+    if xyz2.dim() != 3 or xyz2.shape[2] != 3:  # tf_grouping.cpp:84
+        raise InvalidArgumentError("QueryBallPoint expects (batch_size, npoint, 3) xyz2 shape.")
+    xyz1 = device_tensor(xyz1, "xyz1", torch.float32)
+    xyz2 = device_tensor(xyz2, "xyz2", torch.float32)
+    B, N = int(xyz1.shape[0]), int(xyz1.shape[1])
+    M, ns = int(xyz2.shape[1]), int(nsample)
+    idx = torch.empty((B, M, ns), dtype=torch.int32, device=xyz1.device)
+    pts_cnt = torch.empty((B, M), dtype=torch.int32, device=xyz1.device)
+    check(lib().pn2_ball_query(ptr(xyz1), ptr(xyz2), B, N, M, float(radius), ns, ptr(idx),
+                               ptr(pts_cnt), stream_of(xyz1)), "QueryBallPoint")
+    return idx, pts_cnt
+
+
+def _check_group(points, idx, name="GroupPoint"):
+    if points.dim() != 3:  # tf_grouping.cpp:149
+        raise InvalidArgumentError(f"{name} expects (batch_size, num_points, channel) points shape")
+    if idx.dim() != 3 or idx.shape[0] != points.shape[0]:  # tf_grouping.cpp:155
+        raise InvalidArgumentError(f"{name} expects (batch_size, npoints, nsample) idx shape")
+
+
+def _group_fwd(points, idx):
+    B, N, C = (int(s) for s in points.shape)
+    M, ns = int(idx.shape[1]), int(idx.shape[2])
+    out = torch.empty((B, M, ns, C), dtype=torch.float32, device=points.device)
+    check(lib().pn2_group_point(ptr(points), ptr(idx), B, N, C, M, ns, ptr(out),
+                                stream_of(points)), "GroupPoint")
+    return out
+
+
+def _group_grad(B, N, C, idx, grad_out):
+    M, ns = int(idx.shape[1]), int(idx.shape[2])
+    grad_out = device_tensor(grad_out, "grad_out", torch.float32)
+    gp = torch.empty((B, N, C), dtype=torch.float32, device=grad_out.device)
+    check(lib().pn2_group_point_grad(ptr(grad_out), ptr(idx), B, N, C, M, ns, ptr(gp),
+                                     stream_of(grad_out)), "GroupPointGrad")
+    return gp
+
+
+def group_point_grad(points, idx, grad_out):
+    """GroupPointGrad (tf_grouping.cpp:174-208)."""
+    _check_group(points, idx, "GroupPointGrad")
+    B, N, C = (int(s) for s in points.shape)
+    M, ns = int(idx.shape[1]), int(idx.shape[2])
+    if tuple(grad_out.shape) != (B, M, ns, C):  # tf_grouping.cpp:191
+        raise InvalidArgumentError(
+            "GroupPointGrad expects (batch_size, npoints, nsample, channel) grad_out shape")
+    return _group_grad(B, N, C, device_tensor(idx, "idx", torch.int32), grad_out)
+
+
+class _GroupPoint(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, points, idx):
+        ctx.save_for_backward(idx)
+        ctx.bnc = tuple(int(s) for s in points.shape)
+        return _group_fwd(points, idx)
+
+    @staticmethod
+    def backward(ctx, grad_out):  # tf_grouping.py:42-46 (no gradient for idx)
+        (idx,) = ctx.saved_tensors
+        return _group_grad(*ctx.bnc, idx, grad_out), None
+
+
+def group_point(points, idx):
+    """tf_grouping.py:33-41.
+
+    Input:
+        points: (batch_size, ndataset, channel) float32 array, points to sample from
+        idx: (batch_size, npoint, nsample) int32 array, indices to points
+    Output:
+        out: (batch_size, npoint, nsample, channel) float32 array — differentiable w.r.t. points
+    """
+    _check_group(points, idx)
+    points = device_tensor(points, "points", torch.float32)
+    idx = device_tensor(idx, "idx", torch.int32)
+    if torch.is_grad_enabled() and points.requires_grad:
+        return _GroupPoint.apply(points, idx)
+    return _group_fwd(points, idx)

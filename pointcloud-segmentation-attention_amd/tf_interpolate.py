@@ -1,0 +1,114 @@
+"""three_nn / three_interpolate — drop-in for
+pointnet2_tensorflow/tf_ops/interpolation_3d/tf_interpolate.py (same names, argument order,
+shapes, dtypes and error messages). The reference registers these ops for DEVICE_CPU only
+(tf_interpolate.cpp:187,222,262); here they are gfx950 kernels and the data never leaves HBM.
+"""
+import torch
+
+from ._lib import InvalidArgumentError, check, device_tensor, lib, ptr, stream_of
+
+
+def three_nn(xyz1, xyz2):
+    """tf_interpolate.py:8-17.
+
+    Input:
+        xyz1: (b,n,3) float32 array, unknown points
+        xyz2: (b,m,3) float32 array, known points
+    Output:
+        dist: (b,n,3) float32 array, (squared) distances to known points
+        idx: (b,n,3) int32 array, indices to known points
+    """
+    if xyz1.dim() != 3 or xyz1.shape[2] != 3:  # tf_interpolate.cpp:163
+        raise InvalidArgumentError("ThreeNN expects (b,n,3) xyz1 shape.")
+    if xyz2.dim() != 3 or xyz2.shape[2] != 3:  # tf_interpolate.cpp:168
+        raise InvalidArgumentError("ThreeNN expects (b,m,3) xyz2 shape.")
+    xyz1 = device_tensor(xyz1, "xyz1", torch.float32)
+    xyz2 = device_tensor(xyz2, "xyz2", torch.float32)
+    B, n, m = int(xyz1.shape[0]), int(xyz1.shape[1]), int(xyz2.shape[1])
+    dist = torch.empty((B, n, 3), dtype=torch.float32, device=xyz1.device)
+    idx = torch.empty((B, n, 3), dtype=torch.int32, device=xyz1.device)
+    check(lib().pn2_three_nn(ptr(xyz1), ptr(xyz2), B, n, m, ptr(dist), ptr(idx),
+                             stream_of(xyz1)), "ThreeNN")
+    return dist, idx
+
+
+def _check_interp(points, idx, weight, name="ThreeInterpolate"):
+    if points.dim() != 3:  # tf_interpolate.cpp:197
+        raise InvalidArgumentError(f"{name} expects (b,m,c) points shape")
+    b = points.shape[0]
+    if idx.dim() != 3 or idx.shape[0] != b or idx.shape[2] != 3:  # :203
+        raise InvalidArgumentError(f"{name} expects (b,n,3) idx shape")
+    if weight.dim() != 3 or tuple(weight.shape) != (b, idx.shape[1], 3):  # :206
+        raise InvalidArgumentError(f"{name} expects (b,n,3) weight shape")
+
+
+def _interp_fwd(points, idx, weight):
+    B, m, C = (int(s) for s in points.shape)
+    n = int(idx.shape[1])
+    out = torch.empty((B, n, C), dtype=torch.float32, device=points.device)
+    check(lib().pn2_three_interpolate(ptr(points), ptr(idx), ptr(weight), B, m, C, n, ptr(out),
+                                      stream_of(points)), "ThreeInterpolate")
+    return out
+
+
+def _interp_grad(B, m, C, idx, weight, grad_out):
+    n = int(idx.shape[1])
+    grad_out = device_tensor(grad_out, "grad_out", torch.float32)
+    gp = torch.empty((B, m, C), dtype=torch.float32, device=grad_out.device)
+    check(lib().pn2_three_interpolate_grad(ptr(grad_out), ptr(idx), ptr(weight), B, n, C, m,
+                                           ptr(gp), stream_of(grad_out)), "ThreeInterpolateGrad")
+    return gp
+
+
+def three_interpolate_grad(points, idx, weight, grad_out):
+    """ThreeInterpolateGrad (tf_interpolate.cpp:225-262)."""
+    _check_interp(points, idx, weight, "ThreeInterpolateGrad")
+    B, m, C = (int(s) for s in points.shape)
+    if tuple(grad_out.shape) != (B, idx.shape[1], C):  # :243
+        raise InvalidArgumentError("ThreeInterpolateGrad expects (b,n,c) grad_out shape")
+    return _interp_grad(B, m, C, device_tensor(idx, "idx", torch.int32),
+                        device_tensor(weight, "weight", torch.float32), grad_out)
+
+
+class _ThreeInterpolate(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, points, idx, weight):
+        ctx.save_for_backward(idx, weight)
+        ctx.bmc = tuple(int(s) for s in points.shape)
+        return _interp_fwd(points, idx, weight)
+
+    @staticmethod
+    def backward(ctx, grad_out):  # tf_interpolate.py:29-34 (points only)
+        idx, weight = ctx.saved_tensors
+        return _interp_grad(*ctx.bmc, idx, weight, grad_out), None, None
+
+
+def three_interpolate(points, idx, weight):
+    """tf_interpolate.py:19-28.
+
+    Input:
+        points: (b,m,c) float32 array, known points
+        idx: (b,n,3) int32 array, indices to known points
+        weight: (b,n,3) float32 array, weights on known points
+    Output:
+        out: (b,n,c) float32 array, interpolated point values — differentiable w.r.t. points
+    """
+    _check_interp(points, idx, weight)
+    points = device_tensor(points, "points", torch.float32)
+    idx = device_tensor(idx, "idx", torch.int32)
+    weight = device_tensor(weight, "weight", torch.float32)
+    if torch.is_grad_enabled() and points.requires_grad:
+        return _ThreeInterpolate.apply(points, idx, weight)
+    return _interp_fwd(points, idx, weight)
+
+
+def idw_weights(dist):
+    """The inverse-distance weights of pointnet_fp_module (pointnet_util.py:219-222):
+    d = max(dist, 1e-10); weight = (1/d) / sum_3(1/d)."""
+    if dist.dim() != 3 or dist.shape[2] != 3:
+        raise InvalidArgumentError("idw_weights expects (b,n,3) dist shape")
+    dist = device_tensor(dist, "dist", torch.float32)
+    B, n = int(dist.shape[0]), int(dist.shape[1])
+    w = torch.empty_like(dist)
+    check(lib().pn2_idw_weights(ptr(dist), B, n, ptr(w), stream_of(dist)), "idw_weights")
+    return w

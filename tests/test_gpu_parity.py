@@ -1,0 +1,352 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracle on identical inputs.
+
+Bars (BASELINE.json north_star): indices (FPS, ball query, three_nn idx, gather, group) and
+copies are BIT-EXACT; three_nn distances and three_interpolate are bit-exact too (same fp32
+expression order, no FMA); IDW weights, attention and pooling are within 1e-5 (rtol=atol=1e-5,
+written in each assert). Float-atomic gradients are within 1e-5 as well (order not fixed).
+The oracle is pinned to the reference's own code in test_oracle_golden.py and, on this box,
+against the reference's own CUDA kernels compiled for gfx950 (the *_vs_reference tests).
+"""
+import importlib
+
+import numpy as np
+import pytest
+
+from conftest import PKG_NAME, gpu_available
+
+pytestmark = [pytest.mark.gpu,
+              pytest.mark.skipif(not gpu_available(), reason="needs an MI355X")]
+
+TOL = dict(rtol=1e-5, atol=1e-5)
+
+
+@pytest.fixture(scope="module")
+def env():
+    import torch
+
+    from oracle import oracle as O
+    O.set_threads(16)
+    pkg = importlib.import_module(PKG_NAME)
+    return pkg, O, torch, torch.device("cuda:0")
+
+
+def _bits(a):
+    return np.ascontiguousarray(a, np.float32).view(np.int32)
+
+
+def _cloud(pkg, kind, B, N, seed=0):
+    if kind == "scannet":
+        return pkg.synth.batch(range(seed, seed + B), N, "scannet")[0]
+    if kind == "uniform":
+        return pkg.synth.batch(range(seed, seed + B), N, "uniform")[0]
+    if kind == "dup":  # every point the same: all distances tie
+        x = np.tile(np.array([[0.25, 0.5, 0.75]], np.float32), (B, N, 1))
+        return x.reshape(B, N, 3)
+    if kind == "grid":  # integer lattice: massive exact ties
+        g = np.stack(np.meshgrid(*[np.arange(16)] * 3, indexing="ij"), -1).reshape(-1, 3)
+        rng = np.random.default_rng(seed)
+        return np.stack([g[rng.integers(0, len(g), N)] for _ in range(B)]).astype(np.float32)
+    raise ValueError(kind)
+
+
+FPS_CASES = [
+    ("uniform", 1, 1024, 256),   # cfg1
+    ("scannet", 2, 8192, 1024),  # SSG SA1 (duplicates)
+    ("scannet", 2, 1024, 256),   # SA2
+    ("scannet", 3, 256, 64),     # SA3
+    ("scannet", 3, 64, 16),      # SA4
+    ("scannet", 2, 16384, 512),  # MSG SA1 (global-coordinate path)
+    ("scannet", 2, 3000, 300),
+    ("uniform", 2, 100, 37),
+    ("uniform", 1, 1, 5),        # N = 1
+    ("uniform", 2, 50, 80),      # npoint > N
+    ("dup", 2, 700, 40),         # all-duplicate cloud
+    ("grid", 2, 4096, 512),      # tie-heavy lattice
+    ("grid", 2, 600, 100),
+    ("scannet", 1, 20000, 64),   # workspace path (N > 16384)
+]
+
+
+@pytest.mark.parametrize("kind,B,N,M", FPS_CASES)
+def test_fps_vs_oracle(env, kind, B, N, M):
+    pkg, O, torch, dev = env
+    x = _cloud(pkg, kind, B, N)
+    idx, new_xyz = pkg.tf_sampling.farthest_point_sample_and_gather(M, torch.from_numpy(x).to(dev))
+    ref = O.fps(x, M)
+    got = idx.cpu().numpy()
+    assert np.array_equal(got, ref), f"{(got != ref).sum()} FPS indices differ"
+    assert np.array_equal(_bits(new_xyz.cpu().numpy()), _bits(O.gather_point(x, ref)))
+    only = pkg.tf_sampling.farthest_point_sample(M, torch.from_numpy(x).to(dev))
+    assert np.array_equal(only.cpu().numpy(), ref)
+
+
+@pytest.mark.parametrize("kind,B,N,M", [c for c in FPS_CASES if c[2] <= 16384])
+def test_fps_vs_reference_kernel(env, kind, B, N, M):
+    """The reference's own farthestpointsamplingKernel (tf_sampling_g.cu:105-170) run on this
+    GPU pins the oracle and the HIP sampler to the reference's behaviour, ties included."""
+    pkg, O, torch, dev = env
+    if not O.have_ref_gpu():
+        pytest.skip("oracle/_ref/libref_gpu.so not built")
+    x = _cloud(pkg, kind, B, N)
+    xt = torch.from_numpy(x).to(dev)
+    ref_out = torch.zeros((B, M), dtype=torch.int32, device=dev)
+    assert O.ref_gpu().pn2ref_fps(xt.data_ptr(), B, N, M, ref_out.data_ptr()) == 0
+    ref = ref_out.cpu().numpy()
+    assert np.array_equal(O.fps(x, M), ref), "oracle FPS differs from the reference kernel"
+    got = pkg.tf_sampling.farthest_point_sample(M, xt).cpu().numpy()
+    assert np.array_equal(got, ref), f"{(got != ref).sum()} FPS indices differ from reference"
+
+
+def test_gather_point(env):
+    pkg, O, torch, dev = env
+    x = _cloud(pkg, "scannet", 3, 2048)
+    idx = np.random.default_rng(1).integers(0, 2048, (3, 300)).astype(np.int32)
+    got = pkg.tf_sampling.gather_point(torch.from_numpy(x).to(dev), torch.from_numpy(idx).to(dev))
+    assert np.array_equal(_bits(got.cpu().numpy()), _bits(O.gather_point(x, idx)))
+    if O.have_ref_gpu():
+        out = torch.zeros((3, 300, 3), device=dev)
+        xt, it = torch.from_numpy(x).to(dev), torch.from_numpy(idx).to(dev)
+        assert O.ref_gpu().pn2ref_gather_point(xt.data_ptr(), it.data_ptr(), 3, 2048, 300,
+                                               out.data_ptr()) == 0
+        assert np.array_equal(_bits(out.cpu().numpy()), _bits(got.cpu().numpy()))
+
+
+BQ_CASES = [
+    ("uniform", 1, 1024, 256, 0.2, 32),   # cfg1
+    ("scannet", 2, 8192, 1024, 0.1, 32),  # SA1
+    ("scannet", 2, 1024, 256, 0.2, 32),   # SA2
+    ("scannet", 2, 256, 64, 0.4, 32),     # SA3
+    ("scannet", 2, 64, 16, 0.8, 32),      # SA4
+    ("scannet", 1, 16384, 512, 0.4, 128),  # MSG, global path
+    ("scannet", 1, 16384, 512, 0.1, 16),
+    ("scannet", 2, 4096, 512, 0.2, 64),
+    ("grid", 2, 2000, 100, 1.0, 16),      # exact lattice distances at the radius
+    ("uniform", 2, 300, 50, 0.05, 8),     # sparse: many cnt < ns
+]
+
+
+@pytest.mark.parametrize("kind,B,N,M,r,ns", BQ_CASES)
+def test_ball_query_vs_oracle(env, kind, B, N, M, r, ns):
+    pkg, O, torch, dev = env
+    x = _cloud(pkg, kind, B, N)
+    q = O.gather_point(x, O.fps(x, M)) if kind != "grid" else x[:, :M].copy()
+    idx, cnt = pkg.tf_grouping.query_ball_point(r, ns, torch.from_numpy(x).to(dev),
+                                                torch.from_numpy(q).to(dev))
+    ridx, rcnt = O.ball_query(x, q, r, ns)
+    assert np.array_equal(cnt.cpu().numpy(), rcnt)
+    assert np.array_equal(idx.cpu().numpy(), ridx)
+
+
+def test_ball_query_no_hit_and_boundary(env):
+    """Queries far from every point (reference leaves idx uninitialised; defined as 0 here,
+    pts_cnt 0) and points whose sqrt rounds exactly onto the radius."""
+    pkg, O, torch, dev = env
+    r = np.float32(0.3)
+    xs = (r * (1.0 + np.arange(-40, 41, dtype=np.float64) * 2e-8)).astype(np.float32)
+    pts = np.zeros((1, len(xs), 3), np.float32)
+    pts[0, :, 0] = xs
+    q = np.array([[[0, 0, 0], [100, 100, 100], [0.0, 1e-7, 0]]], np.float32)
+    idx, cnt = pkg.tf_grouping.query_ball_point(float(r), 64, torch.from_numpy(pts).to(dev),
+                                                torch.from_numpy(q).to(dev))
+    ridx, rcnt = O.ball_query(pts, q, float(r), 64)
+    assert np.array_equal(cnt.cpu().numpy(), rcnt)
+    assert np.array_equal(idx.cpu().numpy(), ridx)
+    assert rcnt[0, 1] == 0 and (idx.cpu().numpy()[0, 1] == 0).all()
+    assert 0 < rcnt[0, 0] < len(xs)
+
+
+@pytest.mark.parametrize("kind,B,N,M,r,ns", BQ_CASES[:6])
+def test_ball_query_vs_reference_kernel(env, kind, B, N, M, r, ns):
+    """query_ball_point_gpu (tf_grouping_g.cu:3-36) itself, on this GPU."""
+    pkg, O, torch, dev = env
+    if not O.have_ref_gpu():
+        pytest.skip("oracle/_ref/libref_gpu.so not built")
+    x = _cloud(pkg, kind, B, N)
+    q = O.gather_point(x, O.fps(x, M))
+    xt, qt = torch.from_numpy(x).to(dev), torch.from_numpy(q).to(dev)
+    ri = torch.zeros((B, M, ns), dtype=torch.int32, device=dev)
+    rc = torch.zeros((B, M), dtype=torch.int32, device=dev)
+    assert O.ref_gpu().pn2ref_query_ball_point(xt.data_ptr(), qt.data_ptr(), B, N, M, r, ns,
+                                               ri.data_ptr(), rc.data_ptr()) == 0
+    idx, cnt = pkg.tf_grouping.query_ball_point(r, ns, xt, qt)
+    assert np.array_equal(cnt.cpu().numpy(), rc.cpu().numpy())
+    assert np.array_equal(idx.cpu().numpy(), ri.cpu().numpy())
+
+
+@pytest.mark.parametrize("C", [1, 3, 16, 64, 259])
+def test_group_point(env, C):
+    pkg, O, torch, dev = env
+    rng = np.random.default_rng(C)
+    pts = rng.standard_normal((2, 500, C)).astype(np.float32)
+    idx = rng.integers(0, 500, (2, 70, 32)).astype(np.int32)
+    got = pkg.tf_grouping.group_point(torch.from_numpy(pts).to(dev), torch.from_numpy(idx).to(dev))
+    assert np.array_equal(_bits(got.cpu().numpy()), _bits(O.group_point(pts, idx)))
+
+
+@pytest.mark.parametrize("C,use_xyz,xyz_last", [(0, True, False), (6, True, False),
+                                                (64, True, False), (64, False, False),
+                                                (320, True, True), (5, True, True)])
+def test_group_concat(env, C, use_xyz, xyz_last):
+    pkg, O, torch, dev = env
+    x = _cloud(pkg, "scannet", 2, 2048)
+    q = O.gather_point(x, O.fps(x, 128))
+    idx, _ = O.ball_query(x, q, 0.2, 32)
+    pts = pkg.synth.features_uniform(C + 1, (2, 2048, C)) if C else None
+    t = lambda a: None if a is None else torch.from_numpy(a).to(dev)
+    got, gx = pkg.pointnet_util.group_concat(t(x), t(pts), t(q), t(idx), use_xyz=use_xyz,
+                                             xyz_last=xyz_last)
+    ref, rgx = O.group_concat(x, pts, q, idx, use_xyz=use_xyz, xyz_last=xyz_last)
+    assert np.array_equal(_bits(got.cpu().numpy()), _bits(ref))
+    assert np.array_equal(_bits(gx.cpu().numpy()), _bits(rgx))
+
+
+def test_sample_and_group_api(env):
+    pkg, O, torch, dev = env
+    x, f = pkg.synth.batch([3, 4], 4096, "scannet", with_features=True)
+    new_xyz, new_points, idx, gxyz = pkg.pointnet_util.sample_and_group(
+        512, 0.2, 32, torch.from_numpy(x).to(dev), torch.from_numpy(f).to(dev))
+    nx = O.gather_point(x, O.fps(x, 512))
+    bi, _ = O.ball_query(x, nx, 0.2, 32)
+    npts, gx = O.group_concat(x, f, nx, bi)
+    assert np.array_equal(_bits(new_xyz.cpu().numpy()), _bits(nx))
+    assert np.array_equal(idx.cpu().numpy(), bi)
+    assert np.array_equal(_bits(new_points.cpu().numpy()), _bits(npts))
+    assert np.array_equal(_bits(gxyz.cpu().numpy()), _bits(gx))
+
+
+NN_CASES = [(2, 512, 128), (2, 8192, 1024), (2, 64, 16), (1, 100, 3), (1, 100, 2), (1, 7, 1),
+            (2, 1024, 4097)]
+
+
+@pytest.mark.parametrize("B,n,m", NN_CASES)
+def test_three_nn(env, B, n, m):
+    pkg, O, torch, dev = env
+    x1 = _cloud(pkg, "scannet", B, n, seed=5)
+    x2 = _cloud(pkg, "scannet", B, m, seed=9)
+    d, i = pkg.tf_interpolate.three_nn(torch.from_numpy(x1).to(dev), torch.from_numpy(x2).to(dev))
+    rd, ri = O.three_nn(x1, x2)
+    assert np.array_equal(i.cpu().numpy(), ri)
+    assert np.array_equal(_bits(d.cpu().numpy()), _bits(rd))
+
+
+def test_three_nn_ties(env):
+    pkg, O, torch, dev = env
+    x2 = _cloud(pkg, "grid", 2, 300)
+    x1 = _cloud(pkg, "grid", 2, 500, seed=3) + np.float32(0.5)
+    d, i = pkg.tf_interpolate.three_nn(torch.from_numpy(x1).to(dev), torch.from_numpy(x2).to(dev))
+    rd, ri = O.three_nn(x1, x2)
+    assert np.array_equal(i.cpu().numpy(), ri)
+    assert np.array_equal(_bits(d.cpu().numpy()), _bits(rd))
+
+
+@pytest.mark.parametrize("C", [1, 16, 128, 512])
+def test_three_interpolate_and_idw(env, C):
+    pkg, O, torch, dev = env
+    x1 = _cloud(pkg, "scannet", 2, 1024, seed=2)
+    x2 = _cloud(pkg, "scannet", 2, 256, seed=7)
+    rd, ri = O.three_nn(x1, x2)
+    w = pkg.tf_interpolate.idw_weights(torch.from_numpy(rd).to(dev)).cpu().numpy()
+    rw = O.idw_weights(rd)
+    np.testing.assert_allclose(w, rw, **TOL)
+    pts = pkg.synth.features_uniform(C, (2, 256, C))
+    got = pkg.tf_interpolate.three_interpolate(torch.from_numpy(pts).to(dev),
+                                               torch.from_numpy(ri).to(dev),
+                                               torch.from_numpy(rw).to(dev))
+    assert np.array_equal(_bits(got.cpu().numpy()), _bits(O.three_interpolate(pts, ri, rw)))
+
+
+@pytest.mark.parametrize("n,m,C1,C2", [(64, 16, 256, 512), (256, 64, 128, 256),
+                                       (1024, 256, 64, 256), (8192, 1024, 0, 128),
+                                       (8192, 1024, 6, 128), (300, 5, 3, 7)])
+def test_fp_fused(env, n, m, C1, C2):
+    pkg, O, torch, dev = env
+    x1 = _cloud(pkg, "scannet", 2, n, seed=11)
+    x2 = O.gather_point(x1, O.fps(x1, m))
+    p1 = pkg.synth.features_uniform(1, (2, n, C1)) if C1 else None
+    p2 = pkg.synth.features_uniform(2, (2, m, C2))
+    t = lambda a: None if a is None else torch.from_numpy(a).to(dev)
+    got = pkg.pointnet_util.fp_interpolate(t(x1), t(x2), t(p1), t(p2)).cpu().numpy()
+    ref = O.fp_fused(x1, x2, p1, p2)
+    np.testing.assert_allclose(got, ref, **TOL)
+    if C1:
+        assert np.array_equal(_bits(got[..., C2:]), _bits(p1))  # the concat is a copy
+
+
+@pytest.mark.parametrize("ns,C", [(32, 64), (32, 128), (32, 512), (16, 64), (64, 256),
+                                  (128, 128), (8, 32), (24, 64), (100, 8)])
+def test_attention_reduce(env, ns, C):
+    pkg, O, torch, dev = env
+    rng = np.random.default_rng(ns * 1000 + C)
+    B, M = 2, 37
+    Q = rng.uniform(-1, 1, (B, M, C)).astype(np.float32)
+    K = rng.uniform(-1, 1, (B, M, ns, C)).astype(np.float32)
+    V = rng.uniform(-1, 1, (B, M, ns, C)).astype(np.float32)
+    t = lambda a: torch.from_numpy(a).to(dev)
+    got = pkg.attention_layer.attention_reduce(t(Q), t(K), t(V)).cpu().numpy()
+    np.testing.assert_allclose(got, O.attn_reduce(Q, K, V), **TOL)
+
+
+@pytest.mark.parametrize("mode", ["max", "avg", "weighted_avg", "max_and_avg"])
+def test_group_pool(env, mode):
+    pkg, O, torch, dev = env
+    rng = np.random.default_rng(4)
+    x = rng.uniform(-1, 1, (2, 50, 32, 64)).astype(np.float32)
+    g = rng.uniform(-0.2, 0.2, (2, 50, 32, 3)).astype(np.float32)
+    got = pkg.pointnet_util.group_pool(torch.from_numpy(x).to(dev), mode,
+                                       torch.from_numpy(g).to(dev)).cpu().numpy()
+    np.testing.assert_allclose(got, O.group_pool(x, g, mode), **TOL)
+
+
+def test_gradients(env):
+    pkg, O, torch, dev = env
+    rng = np.random.default_rng(8)
+    x = _cloud(pkg, "scannet", 2, 1024)
+    idx = rng.integers(0, 1024, (2, 200)).astype(np.int32)
+    og = rng.standard_normal((2, 200, 3)).astype(np.float32)
+    g = pkg.tf_sampling.gather_point_grad(torch.from_numpy(x).to(dev),
+                                          torch.from_numpy(idx).to(dev), torch.from_numpy(og).to(dev))
+    np.testing.assert_allclose(g.cpu().numpy(), O.gather_point_grad(1024, idx, og), **TOL)
+    pts = rng.standard_normal((2, 1024, 16)).astype(np.float32)
+    gi = rng.integers(0, 1024, (2, 64, 32)).astype(np.int32)
+    go = rng.standard_normal((2, 64, 32, 16)).astype(np.float32)
+    g = pkg.tf_grouping.group_point_grad(torch.from_numpy(pts).to(dev),
+                                         torch.from_numpy(gi).to(dev), torch.from_numpy(go).to(dev))
+    np.testing.assert_allclose(g.cpu().numpy(), O.group_point_grad(1024, gi, go), **TOL)
+    d, i = O.three_nn(_cloud(pkg, "scannet", 2, 512, 3), _cloud(pkg, "scannet", 2, 128, 4))
+    w = O.idw_weights(d)
+    go = rng.standard_normal((2, 512, 16)).astype(np.float32)
+    g = pkg.tf_interpolate.three_interpolate_grad(torch.zeros((2, 128, 16), device=dev),
+                                                  torch.from_numpy(i).to(dev),
+                                                  torch.from_numpy(w).to(dev),
+                                                  torch.from_numpy(go).to(dev))
+    np.testing.assert_allclose(g.cpu().numpy(), O.three_interpolate_grad(128, i, w, go), **TOL)
+    # autograd wiring: d/dpoints of sum(group_point(points, idx)) = occurrence counts
+    p = torch.from_numpy(pts).to(dev).requires_grad_(True)
+    pkg.tf_grouping.group_point(p, torch.from_numpy(gi).to(dev)).sum().backward()
+    counts = np.zeros((2, 1024), np.float32)
+    for b in range(2):
+        np.add.at(counts[b], gi[b].ravel(), 1.0)
+    np.testing.assert_allclose(p.grad.cpu().numpy(), np.repeat(counts[..., None], 16, -1), **TOL)
+
+
+@pytest.mark.parametrize("config,B", [("cfg2", 16), ("cfg3", 4), ("cfg5", 2)])
+def test_stack_full_size(env, config, B):
+    """The benchmark step at full size, every output against the CPU restatement."""
+    pkg, O, torch, dev = env
+    inp = pkg.stack.make_inputs(config, list(range(B)), dev)
+    outs = pkg.stack.run(inp)
+    torch.cuda.synchronize()
+    np_inp = {k: v for k, v in inp.items()}
+    for k in ("xyz", "feats"):
+        np_inp[k] = None if inp[k] is None else inp[k].cpu().numpy()
+    for k in ("sa_out", "fp_out"):
+        if k in inp:
+            np_inp[k] = [t.cpu().numpy() for t in inp[k]]
+    if "attn" in inp:
+        np_inp["attn"] = [tuple(t.cpu().numpy() for t in qkv) for qkv in inp["attn"]]
+    ref = O.run_stack_cpu(np_inp, config)
+    assert len(ref) == len(outs)
+    for k, (g, r) in enumerate(zip(outs, ref)):
+        g = g.cpu().numpy()
+        assert g.shape == r.shape, (k, g.shape, r.shape)
+        np.testing.assert_allclose(g, r, err_msg=f"output {k}", **TOL)
