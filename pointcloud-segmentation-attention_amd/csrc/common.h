@@ -83,6 +83,33 @@ PN2_DEV uint64_t wave_max_u64(uint64_t v) {
   return v;
 }
 
+// 32-bit max over the 16 lanes of each DPP row / over the wave. The DPP moves fold into
+// v_max_u32_dpp (one instruction per step).
+template <int CTRL>
+PN2_DEV uint32_t max_dpp_u32(uint32_t v) {
+  const uint32_t o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
+  return o > v ? o : v;
+}
+PN2_DEV uint32_t row16_max_u32(uint32_t v) {
+  v = max_dpp_u32<kDppXor1>(v);
+  v = max_dpp_u32<kDppXor2>(v);
+  v = max_dpp_u32<kDppHalfMirror>(v);
+  v = max_dpp_u32<kDppMirror>(v);
+  return v;
+}
+PN2_DEV uint32_t wave_max_u32(uint32_t v) {
+  v = row16_max_u32(v);
+  {
+    auto x = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+    v = x[0] > x[1] ? x[0] : x[1];
+  }
+  {
+    auto x = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    v = x[0] > x[1] ? x[0] : x[1];
+  }
+  return v;
+}
+
 PN2_DEV uint32_t uniform_u32(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 PN2_DEV uint64_t uniform_u64(uint64_t v) {
   return pack64(uniform_u32((uint32_t)v), uniform_u32((uint32_t)(v >> 32)));

@@ -12,17 +12,27 @@
 // distances keep the lower known index, unfilled slots stay idx 0 / dist +inf (= (float)1e40).
 // three_interpolate: ((p1*w1)+(p2*w2))+(p3*w3) in fp32 without FMA (:119).
 //
-// Design: one lane per unknown point; the known cloud is staged in LDS as float4 tiles and
-// every lane reads the same element (a broadcast), keeping best1..3 in registers with a
-// branch-free insertion. The fused FP kernel then parks each row's (idx, weight) triple in
-// LDS and writes the [interp, points1] rows of the whole workgroup as one coalesced stream.
+// Design: a workgroup owns 64 unknown points of one cloud; the known cloud is staged in LDS
+// as float4 tiles. Each unknown point is searched by a QUAD of lanes (lane q of the quad scans
+// known points k = q mod 4: 4 distinct broadcast addresses per ds_read_b128, conflict-free),
+// so a 256-thread workgroup keeps 4 waves busy per 64 points and FP4 (8192 unknowns per cloud)
+// runs 8 waves per SIMD. Each lane keeps its best three sorted by (d2, k) — which is exactly
+// the order the reference's stable strict-'<' insertion produces — and the quad merges its four
+// lists with two xor-shuffle steps. The fused FP kernel then parks each row's (idx, weight)
+// triple in LDS and writes the [interp, points1] rows; for short layers (FP1-FP3) the channel
+// range is split over extra workgroups (grid.z) so that the chip is full, and the copy is
+// float4-vectorised when the channel counts allow.
+#include <type_traits>
+
 #include "common.h"
 
 namespace pn2 {
 namespace {
 
 constexpr int kNNBlock = 256;
-constexpr int kNNTile = 2048;  // known points per LDS tile (32 KiB of float4)
+constexpr int kNNGroup = 4;                       // lanes per unknown point (a quad)
+constexpr int kNNRows = kNNBlock / kNNGroup;      // unknown points per workgroup
+constexpr int kNNTile = 2048;                     // known points per LDS tile (32 KiB float4)
 
 struct Best3 {
   float d1, d2, d3;
@@ -45,10 +55,35 @@ PN2_DEV void best3_insert(Best3& b, float d, int k) {
   b.i1 = c1 ? k : b.i1;
 }
 
-// Scans all m known points of cloud b for the unknown point (x1,y1,z1). Every thread of the
-// block must call it (it stages tiles with barriers).
+// (d, k) lexicographic insert: merging two lists that are each sorted by (d, k)
+PN2_DEV bool lex_lt(float d, int k, float bd, int bk) { return d < bd || (d == bd && k < bk); }
+PN2_DEV void best3_insert_lex(Best3& b, float d, int k) {
+  const bool c1 = lex_lt(d, k, b.d1, b.i1), c2 = lex_lt(d, k, b.d2, b.i2),
+             c3 = lex_lt(d, k, b.d3, b.i3);
+  b.d3 = c2 ? b.d2 : (c3 ? d : b.d3);
+  b.i3 = c2 ? b.i2 : (c3 ? k : b.i3);
+  b.d2 = c1 ? b.d1 : (c2 ? d : b.d2);
+  b.i2 = c1 ? b.i1 : (c2 ? k : b.i2);
+  b.d1 = c1 ? d : b.d1;
+  b.i1 = c1 ? k : b.i1;
+}
+
+PN2_DEV void best3_merge_xor(Best3& b, int mask) {
+  const float d1 = __shfl_xor(b.d1, mask, kWave), d2 = __shfl_xor(b.d2, mask, kWave),
+              d3 = __shfl_xor(b.d3, mask, kWave);
+  const int i1 = __shfl_xor(b.i1, mask, kWave), i2 = __shfl_xor(b.i2, mask, kWave),
+            i3 = __shfl_xor(b.i3, mask, kWave);
+  best3_insert_lex(b, d1, i1);
+  best3_insert_lex(b, d2, i2);
+  best3_insert_lex(b, d3, i3);
+}
+
+// Top-3 search of one unknown point (x1,y1,z1) by the 4 lanes of a quad over the m known
+// points of one cloud. Every thread of the block must call it (tiles are staged with
+// barriers). On return every lane of the quad holds the quad's result.
 PN2_DEV void scan_known(const float* __restrict__ K, int m, float x1, float y1, float z1,
                         float4* sk, Best3& best) {
+  const int q = threadIdx.x & (kNNGroup - 1);
   for (int t0 = 0; t0 < m; t0 += kNNTile) {
     const int cnt = min(kNNTile, m - t0);
     __syncthreads();  // previous tile fully consumed
@@ -57,12 +92,14 @@ PN2_DEV void scan_known(const float* __restrict__ K, int m, float x1, float y1, 
       sk[e] = make_float4(p[0], p[1], p[2], 0.0f);
     }
     __syncthreads();
-#pragma unroll 4
-    for (int e = 0; e < cnt; ++e) {
+#pragma unroll 8
+    for (int e = q; e < cnt; e += kNNGroup) {
       const float4 p = sk[e];
       best3_insert(best, sqdist(p.x, p.y, p.z, x1, y1, z1), t0 + e);  // (x2-x1), x2 known
     }
   }
+  best3_merge_xor(best, 1);
+  best3_merge_xor(best, 2);
 }
 
 // weight = (1/d)/sum(1/d), d = max(dist, 1e-10)  (pointnet_util.py:219-222)
@@ -82,13 +119,13 @@ __global__ __launch_bounds__(kNNBlock) void three_nn_kernel(const float* __restr
                                                             int32_t* __restrict__ idx) {
   __shared__ float4 sk[kNNTile];
   const int b = blockIdx.y;
-  const int j = blockIdx.x * kNNBlock + threadIdx.x;
+  const int j = blockIdx.x * kNNRows + threadIdx.x / kNNGroup;
   const bool valid = j < n;
   const float* U = xyz1 + ((size_t)b * n + (valid ? j : 0)) * 3;
   Best3 best;
   best3_init(best);
   scan_known(xyz2 + (size_t)b * m * 3, m, U[0], U[1], U[2], sk, best);
-  if (valid) {
+  if (valid && (threadIdx.x & (kNNGroup - 1)) == 0) {
     float* D = dist + ((size_t)b * n + j) * 3;
     int32_t* I = idx + ((size_t)b * n + j) * 3;
     D[0] = best.d1; D[1] = best.d2; D[2] = best.d3;
@@ -155,46 +192,66 @@ __global__ __launch_bounds__(kBlock) void three_interp_grad_kernel(
   }
 }
 
-// pointnet_fp_module geometry, one workgroup = 256 unknown points of one cloud.
+// pointnet_fp_module geometry. Workgroup (x, b, z): unknown points [64x, 64x+64) of cloud b,
+// output channels [z*cw, (z+1)*cw) of the Cout = C2 + C1 concat row (in units of VEC floats).
+template <int VEC>
 __global__ __launch_bounds__(kNNBlock) void fp_fused_kernel(
     const float* __restrict__ xyz1, const float* __restrict__ xyz2,
     const float* __restrict__ points1, int C1, const float* __restrict__ points2, int C2, int n,
-    int m, FastDiv div_cout, float* __restrict__ out) {
+    int m, int cw, FastDiv div_cw, float* __restrict__ out) {
+  using VecT = typename std::conditional<VEC == 4, float4, float>::type;
   __shared__ float4 sk[kNNTile];
-  __shared__ int4 s_idx[kNNBlock];
-  __shared__ float4 s_w[kNNBlock];
+  __shared__ int4 s_idx[kNNRows];
+  __shared__ float4 s_w[kNNRows];
   const int b = blockIdx.y;
-  const int j0 = blockIdx.x * kNNBlock;
-  const int j = j0 + threadIdx.x;
+  const int j0 = blockIdx.x * kNNRows;
+  const int jl = threadIdx.x / kNNGroup;
+  const int j = j0 + jl;
   const bool valid = j < n;
   const float* U = xyz1 + ((size_t)b * n + (valid ? j : 0)) * 3;
   Best3 best;
   best3_init(best);
   scan_known(xyz2 + (size_t)b * m * 3, m, U[0], U[1], U[2], sk, best);
-  float w1, w2, w3;
-  idw(best.d1, best.d2, best.d3, w1, w2, w3);
-  s_idx[threadIdx.x] = make_int4(best.i1, best.i2, best.i3, 0);
-  s_w[threadIdx.x] = make_float4(w1, w2, w3, 0.0f);
+  if ((threadIdx.x & (kNNGroup - 1)) == 0) {
+    float w1, w2, w3;
+    idw(best.d1, best.d2, best.d3, w1, w2, w3);
+    s_idx[jl] = make_int4(best.i1, best.i2, best.i3, 0);
+    s_w[jl] = make_float4(w1, w2, w3, 0.0f);
+  }
   __syncthreads();
-  const int Cout = C2 + C1;
-  const int nrows = min(kNNBlock, n - j0);
-  const int elems = nrows * Cout;
-  const float* P2 = points2 + (size_t)b * m * C2;
-  float* O = out + ((size_t)b * n + j0) * Cout;
+  const int Cout = C2 + C1;             // floats
+  const int c2v = C2 / VEC, coutv = Cout / VEC;
+  const int cb = blockIdx.z * cw;       // first vector column of this workgroup
+  const int ce = min(coutv, cb + cw);
+  const int width = ce - cb;
+  if (width <= 0) return;
+  const int nrows = min(kNNRows, n - j0);
+  const int elems = nrows * width;
+  const VecT* P2 = reinterpret_cast<const VecT*>(points2 + (size_t)b * m * C2);
+  const VecT* P1 = reinterpret_cast<const VecT*>(points1 + (size_t)b * n * C1);
+  VecT* O = reinterpret_cast<VecT*>(out + (size_t)b * n * Cout);
   for (int e = threadIdx.x; e < elems; e += kNNBlock) {
-    const int rl = (int)fdiv((uint32_t)e, div_cout);
-    const int c = e - rl * Cout;
-    float v;
-    if (c < C2) {  // three_interpolate (tf_interpolate.cpp:119)
+    const int rl = (int)fdiv((uint32_t)e, div_cw);
+    const int c = cb + (e - rl * width);
+    const int r = j0 + rl;
+    VecT v;
+    if (c < c2v) {  // three_interpolate (tf_interpolate.cpp:119): ((p1*w1)+(p2*w2))+(p3*w3)
       const int4 I = s_idx[rl];
       const float4 W = s_w[rl];
-      v = P2[(size_t)I.x * C2 + c] * W.x;
-      v = v + P2[(size_t)I.y * C2 + c] * W.y;
-      v = v + P2[(size_t)I.z * C2 + c] * W.z;
-    } else {       // concat [interpolated, points1] (pointnet_util.py:226)
-      v = points1[((size_t)b * n + j0 + rl) * C1 + (c - C2)];
+      const VecT a = P2[(size_t)I.x * c2v + c], bb = P2[(size_t)I.y * c2v + c],
+                 cc = P2[(size_t)I.z * c2v + c];
+      if constexpr (VEC == 4) {
+        v.x = (a.x * W.x + bb.x * W.y) + cc.x * W.z;
+        v.y = (a.y * W.x + bb.y * W.y) + cc.y * W.z;
+        v.z = (a.z * W.x + bb.z * W.y) + cc.z * W.z;
+        v.w = (a.w * W.x + bb.w * W.y) + cc.w * W.z;
+      } else {
+        v = (a * W.x + bb * W.y) + cc * W.z;
+      }
+    } else {        // concat [interpolated, points1] (pointnet_util.py:226)
+      v = P1[(size_t)r * (C1 / VEC) + (c - c2v)];
     }
-    O[(size_t)e] = v;
+    O[(size_t)r * coutv + c] = v;
   }
 }
 
@@ -218,7 +275,7 @@ int pn2_three_nn(const float* xyz1, const float* xyz2, int B, int n, int m, floa
   if (B < 0 || n < 0 || m < 0 || B > 65535) return PN2_EINVAL;
   if ((long long)B * n == 0) return PN2_OK;
   if (!xyz1 || !dist || !idx || (m > 0 && !xyz2)) return PN2_EINVAL;
-  hipLaunchKernelGGL(pn2::three_nn_kernel, dim3((n + pn2::kNNBlock - 1) / pn2::kNNBlock, B),
+  hipLaunchKernelGGL(pn2::three_nn_kernel, dim3((n + pn2::kNNRows - 1) / pn2::kNNRows, B),
                      dim3(pn2::kNNBlock), 0, (hipStream_t)stream, xyz1, xyz2, n, m, dist, idx);
   PN2_RETURN_LAUNCH();
 }
@@ -295,10 +352,28 @@ int pn2_fp_fused(const float* xyz1, const float* xyz2, const float* points1, int
   if (!xyz1 || !out || (m > 0 && !xyz2) || (C2 > 0 && !points2)) return PN2_EINVAL;
   if (m == 0 && C2 > 0) return PN2_EINVAL;  // nothing to interpolate from
   const int Cout = C1 + C2;
-  if ((long long)pn2::kNNBlock * Cout * Cout >= (1LL << 32)) return PN2_EINVAL;
-  hipLaunchKernelGGL(pn2::fp_fused_kernel, dim3((n + pn2::kNNBlock - 1) / pn2::kNNBlock, B),
-                     dim3(pn2::kNNBlock), 0, (hipStream_t)stream, xyz1, xyz2, points1, C1,
-                     points2, C2, n, m, pn2::make_fastdiv((uint32_t)Cout), out);
+  const bool vec4 = (C1 % 4 == 0) && (C2 % 4 == 0) &&
+                    ((((uintptr_t)points1 | (uintptr_t)points2 | (uintptr_t)out) & 15) == 0);
+  const int VEC = vec4 ? 4 : 1;
+  const int coutv = Cout / VEC;
+  const int row_blocks = (n + pn2::kNNRows - 1) / pn2::kNNRows;
+  // split the channels over grid.z until ~2 workgroups per CU, keeping >= 64 vector columns
+  // per workgroup and not re-running a long known-point scan too often
+  int zsplit = 1;
+  while ((long long)row_blocks * B * zsplit < 512 && coutv / (zsplit * 2) >= 16 &&
+         (long long)m * zsplit * 2 <= 4096)
+    zsplit *= 2;
+  const int cw = (coutv + zsplit - 1) / zsplit;
+  if ((long long)pn2::kNNRows * cw * cw >= (1LL << 32)) return PN2_EINVAL;
+  const dim3 grid(row_blocks, B, zsplit);
+  if (vec4)
+    hipLaunchKernelGGL(pn2::fp_fused_kernel<4>, grid, dim3(pn2::kNNBlock), 0, (hipStream_t)stream,
+                       xyz1, xyz2, points1, C1, points2, C2, n, m, cw,
+                       pn2::make_fastdiv((uint32_t)cw), out);
+  else
+    hipLaunchKernelGGL(pn2::fp_fused_kernel<1>, grid, dim3(pn2::kNNBlock), 0, (hipStream_t)stream,
+                       xyz1, xyz2, points1, C1, points2, C2, n, m, cw,
+                       pn2::make_fastdiv((uint32_t)cw), out);
   PN2_RETURN_LAUNCH();
 }
 

@@ -1,0 +1,96 @@
+#!/usr/bin/env python3
+"""Sweep the FPS launch table on the GPU: every (variant, block, points-per-thread) of
+pn2_fps_tune for the SA layer sizes, interleaved rounds in ONE process (methodology rule 24),
+each result checked index-exact against the production entry point. Prints one JSON line per
+(N, config) with the median and min kernel time (HIP events, B clouds per launch)."""
+import ctypes
+import importlib
+import json
+import os
+import statistics
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    import torch
+    pkg = importlib.import_module("pointcloud-segmentation-attention_amd")
+    L = pkg.lib()
+    L.pn2_fps_tune.restype = ctypes.c_int
+    L.pn2_fps_tune.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                               ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                               ctypes.c_int, ctypes.c_void_p]
+    dev = torch.device("cuda:0")
+    B = int(os.environ.get("TUNE_B", "16"))
+    rounds = int(os.environ.get("TUNE_ROUNDS", "5"))
+    sizes = [(64, 16), (256, 64), (1024, 256), (4096, 512), (8192, 1024), (16384, 512)]
+    cfgs = [(64, 1), (64, 2), (64, 4), (64, 8), (64, 16), (128, 4), (128, 8), (128, 16), (256, 1),
+            (256, 2), (256, 4), (256, 8), (256, 16), (512, 2), (512, 4), (512, 8), (512, 16),
+            (1024, 1), (1024, 2), (1024, 4), (1024, 8), (1024, 16)]
+    stream = torch.cuda.current_stream().cuda_stream
+    CULL = [(256, 4, 1), (256, 4, 2), (256, 4, 4), (512, 8, 2), (512, 8, 4), (512, 16, 2),
+            (512, 16, 4), (512, 16, 8), (1024, 8, 2), (1024, 8, 4), (256, 32, 4), (256, 32, 8),
+            (1024, 16, 4), (1024, 16, 8)]
+    CULL5 = CULL + [(64, 16, 4), (128, 8, 4), (128, 16, 4), (256, 16, 4), (256, 8, 4),
+                    (1024, 4, 4)]
+    CULL6 = [(256, 4, 1), (256, 4, 2), (256, 4, 4), (512, 8, 2), (512, 8, 4), (512, 16, 2),
+             (512, 16, 4), (512, 16, 8), (1024, 8, 2), (1024, 8, 4), (256, 32, 4), (256, 32, 8),
+             (1024, 16, 4), (1024, 16, 8), (128, 8, 2), (128, 8, 4), (256, 8, 2), (256, 16, 4),
+             (64, 16, 4), (512, 32, 8), (256, 32, 16)]
+    V8 = [(256, 4), (256, 8), (512, 8), (512, 16), (1024, 8), (1024, 16), (256, 16), (256, 32),
+          (512, 32), (1024, 4), (128, 8), (128, 16), (64, 16), (512, 4)]
+    # exactness of every config on tie-heavy inputs first (grid lattice, duplicates, uniform)
+    rng = np.random.default_rng(0)
+    g = np.stack(np.meshgrid(*[np.arange(16)] * 3, indexing="ij"), -1).reshape(-1, 3)
+    for N, M in sizes:
+        tests = [np.stack([g[rng.integers(0, len(g), N)] for _ in range(4)]).astype(np.float32),
+                 pkg.synth.batch(range(4), N, "uniform")[0],
+                 np.repeat(pkg.synth.batch(range(4), N // 3 + 1, "scannet")[0], 3, axis=1)[:, :N]]
+        for x in tests:
+            x = np.ascontiguousarray(x)
+            xt = torch.from_numpy(x).to(dev)
+            ref = pkg.tf_sampling.farthest_point_sample(M, xt)
+            out = torch.empty((4, M), dtype=torch.int32, device=dev)
+            checks = [(8, bl, pp) for bl, pp in V8 if N <= bl * pp <= 4 * max(N, 64)]
+            for v, bl, pp in checks:
+                assert L.pn2_fps_tune(xt.data_ptr(), 4, N, M, out.data_ptr(), None, v, bl, pp,
+                                      stream) == 0, (v, bl, pp)
+                torch.cuda.synchronize()
+                assert torch.equal(out, ref), f"variant {(v, bl, pp)} differs at N={N}"
+    print(json.dumps({"exactness": "all culled configs index-exact on grid/uniform/dup inputs"}),
+          flush=True)
+    for N, M in sizes:
+        xyz = torch.from_numpy(pkg.synth.batch(range(B), N, "scannet")[0]).to(dev)
+        ref = pkg.tf_sampling.farthest_point_sample(M, xyz)
+        cand = [(v, bl, pp) for v in (2,) for bl, pp in cfgs if N <= bl * pp <= max(4 * N, 64)]
+        cand += [(8, bl, pp) for bl, pp in V8 if N <= bl * pp <= max(2 * N, 64)]
+        times = {c: [] for c in cand}
+        out = torch.empty((B, M), dtype=torch.int32, device=dev)
+        nx = torch.empty((B, M, 3), dtype=torch.float32, device=dev)
+        for c in cand:  # warm + verify
+            rc = L.pn2_fps_tune(xyz.data_ptr(), B, N, M, out.data_ptr(), nx.data_ptr(), *c, stream)
+            assert rc == 0, (c, rc)
+            torch.cuda.synchronize()
+            assert torch.equal(out, ref), f"config {c} differs at N={N}"
+        for _ in range(rounds):
+            for c in cand:
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record()
+                L.pn2_fps_tune(xyz.data_ptr(), B, N, M, out.data_ptr(), nx.data_ptr(), *c, stream)
+                b.record()
+                b.synchronize()
+                times[c].append(a.elapsed_time(b) * 1e3)
+        best = min(cand, key=lambda c: statistics.median(times[c]))
+        for c in cand:
+            print(json.dumps({"N": N, "M": M, "B": B, "variant": c[0], "block": c[1], "ppt": c[2],
+                              "median_us": statistics.median(times[c]), "min_us": min(times[c]),
+                              "us_per_iter": statistics.median(times[c]) / (M - 1),
+                              "best": c == best}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
