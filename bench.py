@@ -77,6 +77,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--eager", action="store_true",
+                    help="launch every op from Python instead of replaying the captured hipGraphs")
     args = ap.parse_args()
 
     import torch
@@ -94,12 +96,25 @@ def main():
         dist.init_process_group("nccl", device_id=dev)  # RCCL over xGMI
 
     B = args.batch or (8 if args.config == "cfg5" else 16)
-    ids = list(range(rank * B, rank * B + B))  # contiguous batch split
+    ids = pkg.shard.shard_ids(rank, world, B)  # contiguous batch split
     inp = pkg.stack.make_inputs(args.config, ids, dev)
     torch.cuda.synchronize()
 
+    step = pkg.stack.Step(inp)
+    graph = None if args.eager else pkg.stack.GraphStep(inp)
+
+    def run_step(events=None):
+        if graph is not None:
+            return graph.replay(events)
+        if events is not None:
+            events[0].record()
+        step.sampler()
+        if events is not None:
+            events[1].record()
+        return step.rest()
+
     for _ in range(args.warmup):
-        pkg.stack.run(inp)
+        run_step()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(args.steps)]
 
@@ -111,23 +126,14 @@ def main():
     barrier()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        outs = pkg.stack.run(inp, fps_events=ev[k])
+        outs = run_step(ev[k])
     torch.cuda.synchronize()
     barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = pkg.shard.max_over_ranks(time.perf_counter() - t0, dev)
 
     fps_ms = sum(a.elapsed_time(b) for a, b in ev) / len(ev)  # SA1 sampler, per launch
     # per-cloud output checksums, gathered (outside the timed region) so ranks can be compared
-    sums = torch.stack([torch.stack([o[b].double().sum() for o in outs]).sum()
-                        for b in range(B)])
-    if world > 1:
-        allsums = [torch.zeros_like(sums) for _ in range(world)]
-        dist.all_gather(allsums, sums)
-        sums = torch.cat(allsums)
+    sums = pkg.shard.gather_checksums(pkg.shard.cloud_checksums(outs, B))
 
     if rank == 0:
         clouds = world * B * args.steps
@@ -147,7 +153,8 @@ def main():
                     "12k surface points); U[-1,1) stand-ins for the MLP outputs",
             "config": {"workload": WORKLOADS[args.config], "config": args.config,
                        "clouds_per_gpu": B, "global_batch": world * B, "points": N,
-                       "parallelism": f"dp{world} (batch split)"},
+                       "parallelism": f"dp{world} (batch split)",
+                       "launch": "eager" if args.eager else "hipGraph replay"},
             "roofline": {"kernel": "fps_reg_kernel (SA1 farthest-point sampling + gather)",
                          "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": None,

@@ -30,8 +30,16 @@ CONFIGS = {
 }
 
 
-def _rand(gen, shape, device):
-    return (torch.rand(shape, generator=gen, device=device, dtype=torch.float32) * 2.0 - 1.0)
+def _rand_per_cloud(cloud_ids, shape, device, seed, slot):
+    """U[-1,1) stand-in tensor (B, *shape) whose row b depends only on the GLOBAL cloud id
+    cloud_ids[b] (and the tensor's slot), so a rank's shard of a global batch gets exactly the
+    values the same clouds get in a single-process run."""
+    rows = []
+    for cid in cloud_ids:
+        gen = torch.Generator(device=device)
+        gen.manual_seed(seed * 1_000_003 + int(cid) * 1009 + slot)
+        rows.append(torch.rand(shape, generator=gen, device=device, dtype=torch.float32))
+    return torch.stack(rows) * 2.0 - 1.0
 
 
 def make_inputs(config, cloud_ids, device, seed=1234):
@@ -39,76 +47,122 @@ def make_inputs(config, cloud_ids, device, seed=1234):
     N, kind, with_feat, attn = CONFIGS[config]
     B = len(cloud_ids)
     xyz, feats = synth.batch(cloud_ids, N, "scannet", with_features=with_feat)
-    gen = torch.Generator(device=device)
-    gen.manual_seed(seed + int(cloud_ids[0]))
     inp = {"config": config, "B": B, "N": N,
            "xyz": torch.from_numpy(xyz).to(device),
            "feats": torch.from_numpy(feats).to(device) if feats is not None else None}
+    r = lambda shape, slot: _rand_per_cloud(cloud_ids, shape, device, seed, slot)  # noqa: E731
     if kind == "ssg":
-        inp["sa_out"] = [_rand(gen, (B, npt, c), device) for (npt, _, _, c) in SSG_SA]
+        inp["sa_out"] = [r((npt, c), i) for i, (npt, _, _, c) in enumerate(SSG_SA)]
         n_fp = [SSG_SA[2][0], SSG_SA[1][0], SSG_SA[0][0]]  # FP1..3 output point counts
-        inp["fp_out"] = [_rand(gen, (B, n, c), device) for n, c in zip(n_fp, SSG_FP_OUT[:3])]
+        inp["fp_out"] = [r((n, c), 10 + i) for i, (n, c) in enumerate(zip(n_fp, SSG_FP_OUT[:3]))]
         if attn:
-            inp["attn"] = [(_rand(gen, (B, npt, c), device), _rand(gen, (B, npt, ns, c), device),
-                            _rand(gen, (B, npt, ns, c), device)) for (npt, _, ns, c) in SSG_SA]
+            inp["attn"] = [(r((npt, c), 20 + 3 * i), r((npt, ns, c), 21 + 3 * i),
+                            r((npt, ns, c), 22 + 3 * i)) for i, (npt, _, ns, c) in enumerate(SSG_SA)]
     else:
-        inp["sa_out"] = [_rand(gen, (B, MSG_SA[0][0], sum(MSG_SA[0][3])), device)]
+        inp["sa_out"] = [r((MSG_SA[0][0], sum(MSG_SA[0][3])), 0)]
     return inp
 
 
-def run_ssg(inp, fps_events=None):
-    """One step of the SSG SA x4 + FP x4 geometry. fps_events = (start, end) CUDA events
-    recorded around the SA1 sampler (the dominant kernel) when given."""
-    xyz = [inp["xyz"]]
-    points = [inp["feats"]]  # l0_points: None (cfg2) or rgb+normals (cfg3)
-    outs = []
-    for i, (npoint, radius, nsample, _) in enumerate(SSG_SA):
-        if i == 0 and fps_events is not None:
-            fps_events[0].record()
-        _, new_xyz = tf_sampling.farthest_point_sample_and_gather(npoint, xyz[-1])
-        if i == 0 and fps_events is not None:
-            fps_events[1].record()
-        idx, _ = tf_grouping.query_ball_point(radius, nsample, xyz[-1], new_xyz)
-        new_points, _ = pointnet_util.group_concat(xyz[-1], points[-1], new_xyz, idx,
+class Step:
+    """One benchmark step, split in two phases so that the dominant kernel (the SA1 sampler)
+    can be timed on its own: sampler() runs FPS + gather of the first SA layer, rest() runs
+    everything after it and returns the step's outputs. __call__ runs both."""
+
+    def __init__(self, inp):
+        self.inp = inp
+        self.kind = CONFIGS[inp["config"]][1]
+        self.new_xyz1 = None
+
+    def sampler(self):
+        npoint = SSG_SA[0][0] if self.kind == "ssg" else MSG_SA[0][0]
+        _, self.new_xyz1 = tf_sampling.farthest_point_sample_and_gather(npoint, self.inp["xyz"])
+        return self.new_xyz1
+
+    def rest(self):
+        return self._rest_ssg() if self.kind == "ssg" else self._rest_msg()
+
+    def __call__(self):
+        self.sampler()
+        return self.rest()
+
+    def _rest_ssg(self):
+        inp = self.inp
+        xyz = [inp["xyz"]]
+        points = [inp["feats"]]  # l0_points: None (cfg2) or rgb+normals (cfg3)
+        outs = []
+        for i, (npoint, radius, nsample, _) in enumerate(SSG_SA):
+            if i == 0:
+                new_xyz = self.new_xyz1
+            else:
+                _, new_xyz = tf_sampling.farthest_point_sample_and_gather(npoint, xyz[-1])
+            idx, _ = tf_grouping.query_ball_point(radius, nsample, xyz[-1], new_xyz)
+            new_points, _ = pointnet_util.group_concat(xyz[-1], points[-1], new_xyz, idx,
+                                                       want_grouped_xyz=False)
+            outs.append(new_points)
+            if "attn" in inp:  # attention instead of pooling (attention_layer.py:256-261)
+                Q, K, V = inp["attn"][i]
+                outs.append(attention_layer.attention_reduce(Q, K, V))
+            xyz.append(new_xyz)
+            points.append(inp["sa_out"][i])  # stand-in for the SA MLP output (l{i+1}_points)
+        # FP layers (pointnet2_sem_seg_attention.py:46-53)
+        feat = inp["sa_out"][3]  # l4_points
+        for k in range(4):
+            lvl = 3 - k  # interpolate level lvl+1 -> lvl
+            out = pointnet_util.fp_interpolate(xyz[lvl], xyz[lvl + 1], points[lvl], feat)
+            outs.append(out)
+            feat = inp["fp_out"][k] if k < 3 else None  # stand-in for the FP MLP output
+        return outs
+
+    def _rest_msg(self):
+        inp = self.inp
+        xyz, points, new_xyz = inp["xyz"], None, self.new_xyz1
+        outs = []
+        for i, (npoint, radii, nsamples, _) in enumerate(MSG_SA):
+            if i > 0:
+                _, new_xyz = tf_sampling.farthest_point_sample_and_gather(npoint, xyz)
+            for radius, nsample in zip(radii, nsamples):
+                idx, _ = tf_grouping.query_ball_point(radius, nsample, xyz, new_xyz)
+                gp, _ = pointnet_util.group_concat(xyz, points, new_xyz, idx, xyz_last=True,
                                                    want_grouped_xyz=False)
-        outs.append(new_points)
-        if "attn" in inp:  # attention instead of pooling (attention_layer.py:256-261)
-            Q, K, V = inp["attn"][i]
-            outs.append(attention_layer.attention_reduce(Q, K, V))
-        xyz.append(new_xyz)
-        points.append(inp["sa_out"][i])  # stand-in for the SA MLP output (l{i+1}_points)
-    # FP layers (pointnet2_sem_seg_attention.py:46-53)
-    feat = inp["sa_out"][3]  # l4_points
-    for k in range(4):
-        lvl = 3 - k  # interpolate level lvl+1 -> lvl
-        out = pointnet_util.fp_interpolate(xyz[lvl], xyz[lvl + 1], points[lvl], feat)
-        outs.append(out)
-        feat = inp["fp_out"][k] if k < 3 else None  # stand-in for the FP MLP output
-    return outs
+                outs.append(gp)
+            xyz, points = new_xyz, inp["sa_out"][0]
+        return outs
 
 
-def run_msg(inp, fps_events=None):
-    """One step of the MSG SA1 + SA2 grouping geometry (cfg5)."""
-    xyz, points = inp["xyz"], None
-    outs = []
-    for i, (npoint, radii, nsamples, _) in enumerate(MSG_SA):
-        if i == 0 and fps_events is not None:
-            fps_events[0].record()
-        _, new_xyz = tf_sampling.farthest_point_sample_and_gather(npoint, xyz)
-        if i == 0 and fps_events is not None:
-            fps_events[1].record()
-        for radius, nsample in zip(radii, nsamples):
-            idx, _ = tf_grouping.query_ball_point(radius, nsample, xyz, new_xyz)
-            gp, _ = pointnet_util.group_concat(xyz, points, new_xyz, idx, xyz_last=True,
-                                               want_grouped_xyz=False)
-            outs.append(gp)
-        xyz, points = new_xyz, inp["sa_out"][0]
-    return outs
+def run(inp):
+    """One step of the configured SA + FP geometry (eager)."""
+    return Step(inp)()
 
 
-def run(inp, fps_events=None):
-    kind = CONFIGS[inp["config"]][1]
-    return run_ssg(inp, fps_events) if kind == "ssg" else run_msg(inp, fps_events)
+class GraphStep:
+    """The step captured as two hipGraphs (sampler, rest) sharing one memory pool; replay()
+    launches both on the current stream. Inputs stay resident, outputs are overwritten in
+    place at every replay."""
+
+    def __init__(self, inp, warmup=2):
+        import torch
+        self.step = Step(inp)
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(warmup):
+                self.step()
+        torch.cuda.current_stream().wait_stream(side)
+        self.g_sampler = torch.cuda.CUDAGraph()
+        self.g_rest = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.g_sampler):
+            self.step.sampler()
+        with torch.cuda.graph(self.g_rest, pool=self.g_sampler.pool()):
+            self.outs = self.step.rest()
+
+    def replay(self, sampler_events=None):
+        if sampler_events is not None:
+            sampler_events[0].record()
+        self.g_sampler.replay()
+        if sampler_events is not None:
+            sampler_events[1].record()
+        self.g_rest.replay()
+        return self.outs
 
 
 def sa_fp_bytes(config, B):

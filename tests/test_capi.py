@@ -1,0 +1,95 @@
+"""CPU: the C-ABI library builds, loads and exports every entry point include/pn2hip.h declares.
+No kernel is launched here (no GPU in the build container): only host functions and argument
+checks that return before any HIP call."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "pn2hip.h")
+
+
+def header_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(pn2_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_header_declares_the_boundary():
+    names = header_functions()
+    for need in ("pn2_fps", "pn2_gather_point", "pn2_ball_query", "pn2_group_point",
+                 "pn2_three_nn", "pn2_three_interpolate", "pn2_attn_reduce", "pn2_fp_fused",
+                 "pn2_sample_and_group", "pn2_group_pool"):
+        assert need in names
+
+
+def test_library_exports_every_declared_symbol(pn2):
+    lib = pn2.lib()
+    so = pn2.LIB_PATH
+    exported = subprocess.run(["nm", "-D", "--defined-only", so], capture_output=True, text=True,
+                              check=True).stdout
+    for name in header_functions():
+        assert re.search(rf"\bT {name}$", exported, re.M), f"{name} not exported by {so}"
+        assert getattr(lib, name) is not None
+
+
+def test_ctypes_signatures_match_header(pn2):
+    from importlib import import_module
+    _lib = import_module("pointcloud-segmentation-attention_amd._lib")
+    assert sorted(_lib.SIGNATURES) == header_functions()
+
+
+def test_library_is_gfx950_code_object(pn2):
+    """The fat binary embedded in libpn2hip.so carries gfx950 code objects (and nothing else)."""
+    data = open(pn2.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in data
+    assert b"amdgcn-amd-amdhsa--gfx942" not in data
+
+
+def test_version_and_errors(pn2):
+    lib = pn2.lib()
+    assert b"gfx950" in lib.pn2_version()
+    assert b"invalid" in lib.pn2_strerror(-22)
+    assert lib.pn2_strerror(0) == b"ok"
+
+
+def test_argument_checks_return_einval_without_launching(pn2):
+    lib = pn2.lib()
+    E = -22
+    assert lib.pn2_fps(None, 1, 100, 0, None, None) == E          # npoint <= 0 (tf_sampling.cpp:99)
+    assert lib.pn2_fps(None, -1, 100, 4, None, None) == E
+    assert lib.pn2_fps(None, 2, 100, 4, None, None) == E          # null buffers
+    assert lib.pn2_ball_query(None, None, 1, 10, 10, 0.0, 8, None, None, None) == E  # radius
+    assert lib.pn2_ball_query(None, None, 1, 10, 10, 0.1, 0, None, None, None) == E  # nsample
+    assert lib.pn2_attn_reduce(None, None, None, 1, 1, 32, 6, None, None) == E  # C % 4
+    assert lib.pn2_group_pool(None, None, 1, 1, 4, 8, 7, None, None) == E       # mode
+    assert lib.pn2_fp_fused(None, None, None, 3, None, 4, 1, 4, 4, None, None) == E  # C1 w/o points1
+    # empty work is a no-op, not an error (nothing is launched)
+    assert lib.pn2_gather_point(None, None, 0, 10, 10, None, None) == 0
+    assert lib.pn2_three_nn(None, None, 0, 10, 10, None, None, None) == 0
+
+
+def test_fps_workspace_contract(pn2):
+    lib = pn2.lib()
+    cap = lib.pn2_fps_max_points()
+    assert cap >= 16384
+    assert lib.pn2_fps_workspace_size(16, 8192) == 0
+    assert lib.pn2_fps_workspace_size(2, cap + 1) == 2 * (cap + 1) * 4
+
+
+@pytest.mark.parametrize("r", [0.1, 0.2, 0.4, 0.8, 0.3, 1.0, 1e-3, 7.5, 1e-19])
+def test_ball_threshold_equals_sqrt_predicate(pn2, r):
+    """d2 < T  <=>  max(sqrtf(d2), 1e-20f) < r  (tf_grouping_g.cu:24-25), checked on the fp32
+    neighbourhood of T with numpy's correctly rounded float32 sqrt."""
+    lib = pn2.lib()
+    r32 = np.float32(r)
+    T = np.float32(lib.pn2_ball_threshold(float(r32)))
+    bits = T.view(np.int32)
+    cand = np.arange(max(int(bits) - 64, 0), int(bits) + 64, dtype=np.int32).view(np.float32)
+    s = np.maximum(np.sqrt(cand), np.float32(1e-20))
+    assert np.array_equal(cand < T, s < r32)
+    assert lib.pn2_ball_threshold(0.0) == 0.0

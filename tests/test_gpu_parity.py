@@ -350,3 +350,18 @@ def test_stack_full_size(env, config, B):
         g = g.cpu().numpy()
         assert g.shape == r.shape, (k, g.shape, r.shape)
         np.testing.assert_allclose(g, r, err_msg=f"output {k}", **TOL)
+
+
+@pytest.mark.parametrize("config,B", [("cfg2", 4), ("cfg3", 2), ("cfg5", 2)])
+def test_graph_replay_matches_eager(env, config, B):
+    """The hipGraph-captured step (what bench.py times) reproduces the eager step exactly."""
+    pkg, O, torch, dev = env
+    inp = pkg.stack.make_inputs(config, list(range(10, 10 + B)), dev)
+    eager = [o.clone() for o in pkg.stack.run(inp)]
+    g = pkg.stack.GraphStep(inp)
+    for _ in range(3):
+        outs = g.replay()
+    torch.cuda.synchronize()
+    assert len(outs) == len(eager)
+    for a, b in zip(outs, eager):
+        assert torch.equal(a, b)
