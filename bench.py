@@ -67,6 +67,28 @@ def cpu_baseline(config, B_per_step, seconds, threads):
                       f"{el:.1f} s on {threads} host threads; C restatement oracle/pn2_oracle.c"}
 
 
+def pmc_traffic(config, B):
+    """HBM bytes per launch of the SA1 sampler from the committed rocprofv3 --pmc summary
+    (profiles/<round>/pmc_traffic_<config>_B<B>.json, written by tools/pmc_summary.py from
+    separate FETCH_SIZE and WRITE_SIZE passes of this bench). Counters cannot be read inside
+    this (unprofiled) process, so the figure is the profiled run's, for the same workload."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", f"pmc_traffic_{config}_B{B}.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    ks = [k for k in d["kernels"] if k.startswith("fps_v")]
+    if not ks:
+        return None, None
+    k = max(ks, key=lambda k: d["kernels"][k]["fetch_bytes"] or 0)  # SA1 = largest sampler
+    e = d["kernels"][k]
+    # FETCH_SIZE x2: the gfx950 correction of MI355X_MICROARCH.md (HBM section); for this
+    # kernel it lands within 6 % of the algorithmic read bytes, and WRITE_SIZE equals the
+    # idx + new_xyz bytes exactly.
+    return e["fetch_bytes_x2"] + e["write_bytes"], os.path.relpath(files[-1], ROOT) + f" [{k}]"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -79,6 +101,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--eager", action="store_true",
                     help="launch every op from Python instead of replaying the captured hipGraphs")
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="run the whole step on one stream (no side stream beside the sampler chain)")
     args = ap.parse_args()
 
     import torch
@@ -100,8 +124,9 @@ def main():
     inp = pkg.stack.make_inputs(args.config, ids, dev)
     torch.cuda.synchronize()
 
-    step = pkg.stack.Step(inp)
-    graph = None if args.eager else pkg.stack.GraphStep(inp)
+    overlap = not args.no_overlap
+    step = pkg.stack.Step(inp, overlap=overlap)
+    graph = None if args.eager else pkg.stack.GraphStep(inp, overlap=overlap)
 
     def run_step(events=None):
         if graph is not None:
@@ -144,6 +169,7 @@ def main():
         M1 = pkg.stack.SSG_SA[0][0] if args.config != "cfg5" else pkg.stack.MSG_SA[0][0]
         fps_bytes = B * (N * 12 + M1 * 4)  # algorithmic bytes of one SA1 sampler launch
         achieved = fps_bytes / (fps_ms * 1e-3) / 1e9
+        traffic, traffic_src = pmc_traffic(args.config, B)
         result = {
             "metric": METRIC, "value": value, "unit": "clouds/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
@@ -154,12 +180,16 @@ def main():
             "config": {"workload": WORKLOADS[args.config], "config": args.config,
                        "clouds_per_gpu": B, "global_batch": world * B, "points": N,
                        "parallelism": f"dp{world} (batch split)",
-                       "launch": "eager" if args.eager else "hipGraph replay"},
-            "roofline": {"kernel": "fps_reg_kernel (SA1 farthest-point sampling + gather)",
+                       "launch": "eager" if args.eager else "hipGraph replay",
+                       "streams": "sampler chain + side stream" if overlap else "one stream"},
+            "roofline": {"kernel": f"SA1 sampler (FPS + gather fused): {B} clouds x {N} pts "
+                                   f"-> {M1}, one workgroup per cloud",
                          "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS,
+                         "traffic": traffic, "traffic_source": traffic_src,
                          "avg_launch_ms": fps_ms, "algorithmic_bytes_per_launch": fps_bytes,
-                         "note": "latency-bound serial argmax; HBM fraction is structurally low"},
+                         "note": "latency-bound serial argmax (M-1 dependent block-wide "
+                                 "reductions); the HBM fraction is structurally low"},
             "step_hbm": {"algorithmic_bytes": step_bytes,
                          "achieved_GBps": step_bytes * world / (elapsed / args.steps) / 1e9,
                          "frac": step_bytes * world / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBPS},

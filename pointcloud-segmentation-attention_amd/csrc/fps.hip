@@ -18,1269 +18,10 @@
 //  * the winner's coordinates come from an LDS copy of the cloud (uniform-address
 //    broadcast read) when it fits, otherwise from global memory (scalar load);
 //  * thread 0 also writes new_xyz, fusing gather_point into the sampler (pointnet_util.py:34).
-#include "common.h"
+#include "fps_kernels.h"
 
 namespace pn2 {
 namespace {
-
-constexpr float kInitTemp = 1e38f;  // tf_sampling_g.cu:118
-
-// Low word of the argmax key: larger = earlier in the reference's tie order.
-PN2_DEV uint32_t tie_low(int k) {
-  const uint32_t tk = (((uint32_t)k & 511u) << 20) | ((uint32_t)k >> 9);
-  return 0xFFFFFFFFu - tk;
-}
-PN2_DEV int tie_decode(uint32_t low) {
-  const uint32_t tk = 0xFFFFFFFFu - low;
-  return (int)((tk >> 20) + ((tk & 0xFFFFFu) << 9));
-}
-
-// Thread t owns points t + slot_off(i), i = 0..PPT-1. Slots are ordered so that, within one
-// thread, ascending slot = ascending (k mod 512, k div 512); then a strict '>' scan over the
-// slots keeps the reference's tie winner inside the thread.
-template <int BLOCK, int PPT>
-PN2_DEV constexpr int slot_off(int i) {
-  if constexpr (BLOCK >= 512) {
-    return BLOCK * i;  // k mod 512 is the same for every slot of the thread
-  } else {
-    constexpr int R = 512 / BLOCK;  // slots per residue class
-    if constexpr (PPT <= R) {
-      return BLOCK * i;  // all slots < 512: k mod 512 == k
-    } else {
-      constexpr int Q = PPT / R;  // slots that share one residue
-      return BLOCK * ((i % Q) * R + i / Q);
-    }
-  }
-}
-
-template <int BLOCK, int PPT, bool XYZ_LDS>
-__global__ __launch_bounds__(BLOCK) void fps_reg_kernel(const float* __restrict__ xyz, int N,
-                                                        int M, int32_t* __restrict__ idx,
-                                                        float* __restrict__ new_xyz) {
-  constexpr int NW = BLOCK / kWave;
-  static_assert(NW <= 16, "the cross-wave step reduces one 16-lane DPP row");
-  __shared__ uint64_t red[2][16];
-  __shared__ float sxyz[XYZ_LDS ? 3 * BLOCK * PPT : 1];
-
-  const int b = blockIdx.x;
-  const int t = threadIdx.x;
-  const int lane = t & (kWave - 1);
-  const int w = t / kWave;
-  const float* __restrict__ P = xyz + (size_t)b * N * 3;
-  int32_t* __restrict__ I = idx + (size_t)b * M;
-  float* __restrict__ NX = new_xyz ? new_xyz + (size_t)b * M * 3 : nullptr;
-
-  float px[PPT], py[PPT], pz[PPT], tm[PPT];
-#pragma unroll
-  for (int i = 0; i < PPT; ++i) {
-    const int k = t + slot_off<BLOCK, PPT>(i);
-    if (k < N) {
-      px[i] = P[3 * k + 0];
-      py[i] = P[3 * k + 1];
-      pz[i] = P[3 * k + 2];
-      tm[i] = kInitTemp;
-    } else {  // padding slot: min(d, -1) stays -1 and never wins
-      px[i] = py[i] = pz[i] = 0.0f;
-      tm[i] = -1.0f;
-    }
-  }
-  if constexpr (XYZ_LDS) {
-    for (int e = t; e < 3 * N; e += BLOCK) sxyz[e] = P[e];
-    __syncthreads();
-  }
-
-  float cx = P[0], cy = P[1], cz = P[2];  // old = 0 (tf_sampling_g.cu:114-116)
-  if (t == 0) {
-    I[0] = 0;
-    if (NX) { NX[0] = cx; NX[1] = cy; NX[2] = cz; }
-  }
-
-  for (int j = 1; j < M; ++j) {
-    float bd = -1.0f;
-    int bi = 0;
-#pragma unroll
-    for (int i = 0; i < PPT; ++i) {
-      const float d = sqdist(px[i], py[i], pz[i], cx, cy, cz);
-      const float v = fminf(d, tm[i]);  // tf_sampling_g.cu:143
-      tm[i] = v;
-      if (v > bd) { bd = v; bi = i; }   // tf_sampling_g.cu:146-149
-    }
-    // runtime slot -> point index (same mapping as slot_off, shifts and masks only)
-    int off;
-    if constexpr (BLOCK >= 512 || PPT <= 512 / BLOCK) {
-      off = BLOCK * bi;
-    } else {
-      constexpr int R = 512 / BLOCK, Q = PPT / R;
-      off = BLOCK * ((bi % Q) * R + bi / Q);
-    }
-    uint64_t key = bd < 0.0f ? 0ull : pack64(tie_low(t + off), __float_as_uint(bd));
-    key = wave_max_u64(key);
-    if constexpr (NW > 1) {
-      if (lane == 0) red[j & 1][w] = key;
-      __syncthreads();
-      key = row16_max_u64(lane < NW ? red[j & 1][lane] : 0ull);
-    }
-    const int old = tie_decode(uniform_u32((uint32_t)key));
-    if constexpr (XYZ_LDS) {
-      cx = sxyz[3 * old + 0]; cy = sxyz[3 * old + 1]; cz = sxyz[3 * old + 2];
-    } else {
-      cx = P[3 * old + 0]; cy = P[3 * old + 1]; cz = P[3 * old + 2];
-    }
-    if (t == 0) {
-      I[j] = old;
-      if (NX) { NX[3 * j + 0] = cx; NX[3 * j + 1] = cy; NX[3 * j + 2] = cz; }
-    }
-  }
-}
-
-// Variant 2 of the register sampler: the same selection, cheaper arithmetic.
-//  * the running min-distance is kept as int32 bit patterns: for d >= 0 (or NaN) and
-//    temp in {-1} U [0, 1e38] a signed-int min of the bits is exactly fminf (no IEEE-mode
-//    canonicalisation before every v_min_f32); padding slots hold -1 and never win;
-//  * the argmax is two 32-bit max-reductions (distance, then ~tiekey among the lanes that hold
-//    the maximum distance) whose DPP moves fold into v_max_u32_dpp, instead of one 64-bit
-//    reduction; the cross-wave step is the same pair over the per-wave results.
-// Diagnostic stamps (STAMP builds only; never in a timed production kernel): s_memtime
-// deltas per phase accumulated in SGPRs, lane 0 of each wave writes them to g_stamp.
-__device__ unsigned long long g_stamp[16 * 16 * 8];
-__device__ unsigned long long g_iter[4096];  // STAMP builds: s_memtime at each iteration start
-#define PN2_STAMP(ph)                                                              \
-  if constexpr (STAMP) {                                                           \
-    __builtin_amdgcn_sched_barrier(0);                                             \
-    unsigned long long tt__;                                                       \
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(tt__)::"memory");  \
-    __builtin_amdgcn_sched_barrier(0);                                             \
-    st_acc[ph] += tt__ - st_prev;                                                  \
-    st_prev = tt__;                                                                \
-  }
-
-template <int BLOCK, int PPT, bool XYZ_LDS, bool STAMP = false>
-__global__ __launch_bounds__(BLOCK) void fps_v2_kernel(const float* __restrict__ xyz, int N,
-                                                       int M, int32_t* __restrict__ idx,
-                                                       float* __restrict__ new_xyz) {
-  unsigned long long st_acc[6] = {0, 0, 0, 0, 0, 0}, st_prev = 0;
-  constexpr int NW = BLOCK / kWave;
-  static_assert(NW <= 16, "the cross-wave step reduces one 16-lane DPP row");
-  __shared__ uint2 red[2][16];
-  __shared__ float sxyz[XYZ_LDS ? 3 * BLOCK * PPT : 1];
-
-  const int b = blockIdx.x;
-  const int t = threadIdx.x;
-  const int lane = t & (kWave - 1);
-  const int w = t / kWave;
-  const float* __restrict__ P = xyz + (size_t)b * N * 3;
-  int32_t* __restrict__ I = idx + (size_t)b * M;
-  float* __restrict__ NX = new_xyz ? new_xyz + (size_t)b * M * 3 : nullptr;
-
-  float px[PPT], py[PPT], pz[PPT];
-  int tb[PPT];
-#pragma unroll
-  for (int i = 0; i < PPT; ++i) {
-    const int k = t + slot_off<BLOCK, PPT>(i);
-    if (k < N) {
-      px[i] = P[3 * k + 0];
-      py[i] = P[3 * k + 1];
-      pz[i] = P[3 * k + 2];
-      tb[i] = __float_as_int(kInitTemp);
-    } else {
-      px[i] = py[i] = pz[i] = 0.0f;
-      tb[i] = -1;
-    }
-  }
-  if constexpr (XYZ_LDS) {
-    for (int e = t; e < 3 * N; e += BLOCK) sxyz[e] = P[e];
-    __syncthreads();
-  }
-
-  float cx = P[0], cy = P[1], cz = P[2];
-  if (t == 0) {
-    I[0] = 0;
-    if (NX) { NX[0] = cx; NX[1] = cy; NX[2] = cz; }
-  }
-
-  if constexpr (STAMP) {
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_prev)::"memory");
-  }
-  for (int j = 1; j < M; ++j) {
-    int bd = -1, bi = 0;
-#pragma unroll
-    for (int i = 0; i < PPT; ++i) {
-      const int v = min(__float_as_int(sqdist(px[i], py[i], pz[i], cx, cy, cz)), tb[i]);
-      tb[i] = v;
-      if (v > bd) { bd = v; bi = i; }
-    }
-    int off;
-    if constexpr (BLOCK >= 512 || PPT <= 512 / BLOCK) {
-      off = BLOCK * bi;
-    } else {
-      constexpr int R = 512 / BLOCK, Q = PPT / R;
-      off = BLOCK * ((bi % Q) * R + bi / Q);
-    }
-    const uint32_t hi = bd < 0 ? 0u : (uint32_t)bd + 1u;
-    const uint32_t lo = bd < 0 ? 0u : tie_low(t + off);
-    PN2_STAMP(0)
-    uint32_t km = wave_max_u32(hi);
-    uint32_t kl = wave_max_u32(hi == km ? lo : 0u);
-    PN2_STAMP(1)
-    if constexpr (NW > 1) {
-      if (lane == 0) red[j & 1][w] = make_uint2(km, kl);
-      __syncthreads();
-      PN2_STAMP(2)
-      const uint2 r = lane < NW ? red[j & 1][lane] : make_uint2(0u, 0u);
-      km = row16_max_u32(r.x);
-      kl = row16_max_u32(r.x == km ? r.y : 0u);
-    }
-    const int old = tie_decode(uniform_u32(kl));
-    PN2_STAMP(3)
-    if constexpr (XYZ_LDS) {
-      cx = sxyz[3 * old + 0]; cy = sxyz[3 * old + 1]; cz = sxyz[3 * old + 2];
-    } else {
-      cx = P[3 * old + 0]; cy = P[3 * old + 1]; cz = P[3 * old + 2];
-    }
-    PN2_STAMP(4)
-    if (t == 0) {
-      I[j] = old;
-      if (NX) { NX[3 * j + 0] = cx; NX[3 * j + 1] = cy; NX[3 * j + 2] = cz; }
-    }
-    PN2_STAMP(5)
-  }
-  if constexpr (STAMP) {
-    if (lane == 0 && blockIdx.x < 16)
-      for (int ph = 0; ph < 6; ++ph) g_stamp[(blockIdx.x * 16 + w) * 8 + ph] = st_acc[ph];
-  }
-}
-
-// Variant 7: v2's scan with a short tail.
-//  * wave: ONE 32-bit max of the distance word (folded DPP + permlane swaps);
-//  * the lane(s) holding it issue ds_max_u64 of the packed (distance, tie word) key into one
-//    LDS word — the LDS atomic resolves equal distances across lanes and waves exactly (max of
-//    ~tiekey) and replaces the cross-wave reduction: after the barrier every wave reads one
-//    word. The word is triple-buffered by iteration (j mod 3); wave 0 zeroes word (j+2) mod 3
-//    right after barrier j, when every wave has finished reading it (iteration j-1) and before
-//    anyone can add to it (iteration j+2, after barrier j+1);
-//  * idx / new_xyz gathered in registers of wave 0 and stored 64 at a time.
-template <int BLOCK, int PPT, bool STAMP = false>
-__global__ __launch_bounds__(BLOCK) void fps_v7_kernel(const float* __restrict__ xyz, int N,
-                                                       int M, int32_t* __restrict__ idx,
-                                                       float* __restrict__ new_xyz) {
-  constexpr int NW = BLOCK / kWave;
-  constexpr bool XYZ_LDS = 12 * BLOCK * PPT + 64 <= 160 * 1024;
-  unsigned long long st_acc[6] = {0, 0, 0, 0, 0, 0}, st_prev = 0;
-  __shared__ unsigned long long s_key[3];
-  __shared__ float sxyz[XYZ_LDS ? 3 * BLOCK * PPT : 1];
-
-  const int b = blockIdx.x;
-  const int t = threadIdx.x;
-  const int lane = t & (kWave - 1);
-  const int w = t / kWave;
-  const float* __restrict__ P = xyz + (size_t)b * N * 3;
-  int32_t* __restrict__ I = idx + (size_t)b * M;
-  float* __restrict__ NX = new_xyz ? new_xyz + (size_t)b * M * 3 : nullptr;
-
-  float px[PPT], py[PPT], pz[PPT];
-  int tb[PPT];
-#pragma unroll
-  for (int i = 0; i < PPT; ++i) {
-    const int k = t + slot_off<BLOCK, PPT>(i);
-    if (k < N) {
-      px[i] = P[3 * k + 0];
-      py[i] = P[3 * k + 1];
-      pz[i] = P[3 * k + 2];
-      tb[i] = __float_as_int(kInitTemp);
-    } else {
-      px[i] = py[i] = pz[i] = 0.0f;
-      tb[i] = -1;
-    }
-  }
-  if constexpr (XYZ_LDS) {
-    for (int e = t; e < 3 * N; e += BLOCK) sxyz[e] = P[e];
-  }
-  if (t < 3) s_key[t] = 0ull;
-  __syncthreads();
-
-  float cx = P[0], cy = P[1], cz = P[2];
-  int ring_i = 0;
-  float ring_x = cx, ring_y = cy, ring_z = cz;
-  if constexpr (STAMP) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_prev)::"memory");
-  for (int j = 1; j < M; ++j) {
-    int bd = -1, bi = 0;
-#pragma unroll
-    for (int i = 0; i < PPT; ++i) {
-      const int v = min(__float_as_int(sqdist(px[i], py[i], pz[i], cx, cy, cz)), tb[i]);
-      tb[i] = v;
-      if (v > bd) { bd = v; bi = i; }
-    }
-    int off;
-    if constexpr (BLOCK >= 512 || PPT <= 512 / BLOCK) {
-      off = BLOCK * bi;
-    } else {
-      constexpr int R = 512 / BLOCK, Q = PPT / R;
-      off = BLOCK * ((bi % Q) * R + bi / Q);
-    }
-    const uint32_t hi = bd < 0 ? 0u : (uint32_t)bd + 1u;
-    PN2_STAMP(0)
-    const uint32_t wm = wave_max_u32(hi);
-    PN2_STAMP(1)
-    uint32_t kl;
-    if constexpr (NW > 1) {
-      if (hi == wm) atomicMax(&s_key[j % 3], pack64(tie_low(t + off), hi));
-      __syncthreads();
-      PN2_STAMP(2)
-      if (w == 0 && lane == 0) s_key[(j + 2) % 3] = 0ull;
-      kl = (uint32_t)s_key[j % 3];
-    } else {
-      const uint64_t ball = __ballot(hi == wm);
-      const uint32_t lo = tie_low(t + off);
-      if (__popcll(ball) == 1)
-        kl = (uint32_t)__builtin_amdgcn_readlane((int)lo, __ffsll((unsigned long long)ball) - 1);
-      else
-        kl = uniform_u32(wave_max_u32(hi == wm ? lo : 0u));
-    }
-    const int old = tie_decode(uniform_u32(kl));
-    PN2_STAMP(3)
-    if constexpr (XYZ_LDS) {
-      cx = sxyz[3 * old + 0]; cy = sxyz[3 * old + 1]; cz = sxyz[3 * old + 2];
-    } else {
-      cx = P[3 * old + 0]; cy = P[3 * old + 1]; cz = P[3 * old + 2];
-    }
-    PN2_STAMP(4)
-    if (w == 0) {
-      const int sl = j & (kWave - 1);
-      const bool mine = lane == sl;
-      ring_i = mine ? old : ring_i;
-      ring_x = mine ? cx : ring_x;
-      ring_y = mine ? cy : ring_y;
-      ring_z = mine ? cz : ring_z;
-      if (sl == kWave - 1 || j == M - 1) {
-        const int jj = (j & ~(kWave - 1)) + lane;
-        if (lane <= sl) {
-          I[jj] = ring_i;
-          if (NX) { NX[3 * jj] = ring_x; NX[3 * jj + 1] = ring_y; NX[3 * jj + 2] = ring_z; }
-        }
-      }
-    }
-    PN2_STAMP(5)
-  }
-  if (M == 1 && t == 0) {
-    I[0] = 0;
-    if (NX) { NX[0] = cx; NX[1] = cy; NX[2] = cz; }
-  }
-  if constexpr (STAMP) {
-    if (lane == 0 && blockIdx.x < 16)
-      for (int ph = 0; ph < 6; ++ph) g_stamp[(blockIdx.x * 16 + w) * 8 + ph] = st_acc[ph];
-  }
-}
-
-// Variant 3: spatially culled sampler (exact).
-// At setup the cloud is counting-sorted by a 12-bit Morton cell code (16^3 grid over its
-// bounding box) in LDS, and thread slots are filled in that order, so every "cell" = SUB
-// slots x 64 lanes of one wave holds 64*SUB spatially adjacent points. Each cell keeps, in
-// SGPRs, its bounding box, its best key (max running distance km, tie word kl) and therefore
-// U = max running distance inside it. When the new centre c is so far from the cell's box that
-// even the smallest possible fp32 squared distance exceeds U (lb*(1-2^-16) > U, lb from the
-// box; the margin covers fp32 rounding of both sides), no min(d, temp) of the
-// cell can change: the cell's scan, its reductions and its key are skipped. The result is
-// identical to the unculled sampler; only the work per iteration shrinks as sampling refines.
-// Ties are broken by each point's ORIGINAL index (the per-point tie word tl), so the spatial
-// reordering does not change the reference's choice.
-constexpr int kCellBits = 4;                       // 16 cells per axis
-constexpr int kNumCodes = 1 << (3 * kCellBits);    // 4096
-
-PN2_DEV uint32_t spread3(uint32_t v) {  // 4 bits -> every third bit
-  v &= 0xF;
-  v = (v | (v << 4)) & 0x0C3;
-  v = (v | (v << 2)) & 0x249;
-  return v;
-}
-
-PN2_DEV float wave_min_f(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, kWave));
-  return v;
-}
-PN2_DEV float wave_max_f(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, kWave));
-  return v;
-}
-PN2_DEV float uniform_f(float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); }
-
-template <int BLOCK, int PPT, int SUB, bool XYZ_LDS>
-__global__ __launch_bounds__(BLOCK) void fps_cull_kernel(const float* __restrict__ xyz, int N,
-                                                         int M, int32_t* __restrict__ idx,
-                                                         float* __restrict__ new_xyz) {
-  constexpr int NW = BLOCK / kWave;
-  constexpr int CAP = BLOCK * PPT;
-  constexpr int NCELL = PPT / SUB;
-  static_assert(NW <= 16 && PPT % SUB == 0, "config");
-  // LDS: [A] setup: cell code (u16) + sorted index (u16) per point; later: xyz copy (fp32)
-  //      [H] histogram / offsets of the 4096 Morton cells
-  constexpr int A_BYTES = XYZ_LDS ? 12 * CAP : 4 * CAP;
-  __shared__ __attribute__((aligned(16))) unsigned char smem_a[A_BYTES];
-  __shared__ uint32_t hist[kNumCodes];
-  __shared__ uint2 red[2][16];
-  __shared__ float bbox_red[16][6];
-  uint16_t* s_code = reinterpret_cast<uint16_t*>(smem_a);
-  uint16_t* s_sorted = s_code + CAP;
-  float* sxyz = reinterpret_cast<float*>(smem_a);
-
-  const int b = blockIdx.x;
-  const int t = threadIdx.x;
-  const int lane = t & (kWave - 1);
-  const int w = t / kWave;
-  const float* __restrict__ P = xyz + (size_t)b * N * 3;
-  int32_t* __restrict__ I = idx + (size_t)b * M;
-  float* __restrict__ NX = new_xyz ? new_xyz + (size_t)b * M * 3 : nullptr;
-
-  // ---- setup 1: bounding box of the cloud
-  float lo[3] = {__builtin_inff(), __builtin_inff(), __builtin_inff()};
-  float hi[3] = {-__builtin_inff(), -__builtin_inff(), -__builtin_inff()};
-  for (int k = t; k < N; k += BLOCK)
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-      const float v = P[3 * k + a];
-      lo[a] = fminf(lo[a], v);
-      hi[a] = fmaxf(hi[a], v);
-    }
-#pragma unroll
-  for (int a = 0; a < 3; ++a) { lo[a] = wave_min_f(lo[a]); hi[a] = wave_max_f(hi[a]); }
-  if (lane == 0)
-#pragma unroll
-    for (int a = 0; a < 3; ++a) { bbox_red[w][a] = lo[a]; bbox_red[w][3 + a] = hi[a]; }
-  for (int e = t; e < kNumCodes; e += BLOCK) hist[e] = 0;
-  __syncthreads();
-  float scale[3];
-#pragma unroll
-  for (int a = 0; a < 3; ++a) {
-    float l = bbox_red[0][a], h = bbox_red[0][3 + a];
-    for (int q = 1; q < NW; ++q) { l = fminf(l, bbox_red[q][a]); h = fmaxf(h, bbox_red[q][3 + a]); }
-    lo[a] = l;
-    scale[a] = h > l ? (float)(1 << kCellBits) / (h - l) : 0.0f;
-  }
-  // ---- setup 2: counting sort by Morton cell (any order inside a cell: ties use original k)
-  for (int k = t; k < N; k += BLOCK) {
-    uint32_t q[3];
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-      const int c = (int)((P[3 * k + a] - lo[a]) * scale[a]);
-      q[a] = (uint32_t)min(max(c, 0), (1 << kCellBits) - 1);
-    }
-    const uint32_t code = spread3(q[0]) | (spread3(q[1]) << 1) | (spread3(q[2]) << 2);
-    s_code[k] = (uint16_t)code;
-    atomicAdd(&hist[code], 1u);
-  }
-  __syncthreads();
-  {  // exclusive scan of hist[4096]: each thread owns kNumCodes/BLOCK consecutive entries
-    constexpr int PER = kNumCodes / BLOCK;
-    uint32_t loc[PER];
-    uint32_t sum = 0;
-#pragma unroll
-    for (int e = 0; e < PER; ++e) { loc[e] = hist[t * PER + e]; sum += loc[e]; }
-    uint32_t incl = sum;  // inclusive scan over the wave
-#pragma unroll
-    for (int o = 1; o < kWave; o <<= 1) {
-      const uint32_t y = __shfl_up(incl, o, kWave);
-      if (lane >= o) incl += y;
-    }
-    if (lane == kWave - 1) red[0][w].x = incl;
-    __syncthreads();
-    uint32_t base = 0;
-    for (int q = 0; q < w; ++q) base += red[0][q].x;
-    uint32_t run = base + incl - sum;
-#pragma unroll
-    for (int e = 0; e < PER; ++e) { hist[t * PER + e] = run; run += loc[e]; }
-  }
-  __syncthreads();
-  for (int k = t; k < N; k += BLOCK) s_sorted[atomicAdd(&hist[s_code[k]], 1u)] = (uint16_t)k;
-  __syncthreads();
-
-  // ---- setup 3: per-slot points in sorted order; per-cell boxes
-  float px[PPT], py[PPT], pz[PPT];
-  int tb[PPT];
-  uint32_t tl[PPT];
-#pragma unroll
-  for (int i = 0; i < PPT; ++i) {
-    const int pos = w * (kWave * PPT) + i * kWave + lane;
-    if (pos < N) {
-      const int k = s_sorted[pos];
-      px[i] = P[3 * k + 0];
-      py[i] = P[3 * k + 1];
-      pz[i] = P[3 * k + 2];
-      tb[i] = __float_as_int(kInitTemp);
-      tl[i] = tie_low(k);
-    } else {  // padding: key (0, 0) never wins, min(d, 0) stays 0
-      px[i] = py[i] = pz[i] = 0.0f;
-      tb[i] = 0;
-      tl[i] = 0u;
-    }
-  }
-  float clo[NCELL][3], chi[NCELL][3];
-  uint32_t ckm[NCELL], ckl[NCELL];
-#pragma unroll
-  for (int c = 0; c < NCELL; ++c) {
-    float l0 = __builtin_inff(), l1 = l0, l2 = l0, h0 = -l0, h1 = -l0, h2 = -l0;
-#pragma unroll
-    for (int i = c * SUB; i < (c + 1) * SUB; ++i)
-      if (tl[i] != 0u) {
-        l0 = fminf(l0, px[i]); h0 = fmaxf(h0, px[i]);
-        l1 = fminf(l1, py[i]); h1 = fmaxf(h1, py[i]);
-        l2 = fminf(l2, pz[i]); h2 = fmaxf(h2, pz[i]);
-      }
-    clo[c][0] = uniform_f(wave_min_f(l0)); chi[c][0] = uniform_f(wave_max_f(h0));
-    clo[c][1] = uniform_f(wave_min_f(l1)); chi[c][1] = uniform_f(wave_max_f(h1));
-    clo[c][2] = uniform_f(wave_min_f(l2)); chi[c][2] = uniform_f(wave_max_f(h2));
-    ckm[c] = 0u;
-    ckl[c] = 0u;
-  }
-  __syncthreads();  // s_sorted is dead; smem_a becomes the xyz copy
-  if constexpr (XYZ_LDS) {
-    for (int e = t; e < 3 * N; e += BLOCK) sxyz[e] = P[e];
-    __syncthreads();
-  }
-
-  float cx = P[0], cy = P[1], cz = P[2];
-  if (t == 0) {
-    I[0] = 0;
-    if (NX) { NX[0] = cx; NX[1] = cy; NX[2] = cz; }
-  }
-  bool first = true;
-  for (int j = 1; j < M; ++j) {
-    uint32_t wkm = 0u, wkl = 0u;
-#pragma unroll
-    for (int c = 0; c < NCELL; ++c) {
-      // lower bound of the squared distance from c to the cell's box
-      const float dx = fmaxf(fmaxf(clo[c][0] - cx, cx - chi[c][0]), 0.0f);
-      const float dy = fmaxf(fmaxf(clo[c][1] - cy, cy - chi[c][1]), 0.0f);
-      const float dz = fmaxf(fmaxf(clo[c][2] - cz, cz - chi[c][2]), 0.0f);
-      const float lb = (dx * dx + dy * dy) + dz * dz;
-      const float U = __uint_as_float(ckm[c]);
-      const bool skip = !first && lb > 1e-30f && lb * 0.99998f > U;
-      if (!skip) {
-        uint32_t bh = 0u, bl = 0u;
-#pragma unroll
-        for (int i = c * SUB; i < (c + 1) * SUB; ++i) {
-          const int v = min(__float_as_int(sqdist(px[i], py[i], pz[i], cx, cy, cz)), tb[i]);
-          tb[i] = v;
-          const uint64_t kv = pack64(tl[i], (uint32_t)v), kb = pack64(bl, bh);
-          if (kv > kb) { bh = (uint32_t)v; bl = tl[i]; }
-        }
-        const uint32_t km = uniform_u32(wave_max_u32(bh));
-        ckm[c] = km;
-        ckl[c] = uniform_u32(wave_max_u32(bh == km ? bl : 0u));
-      }
-      if (ckm[c] > wkm || (ckm[c] == wkm && ckl[c] > wkl)) { wkm = ckm[c]; wkl = ckl[c]; }
-    }
-    first = false;
-    uint32_t kl = wkl;
-    if constexpr (NW > 1) {
-      if (lane == 0) red[j & 1][w] = make_uint2(wkm, wkl);
-      __syncthreads();
-      const uint2 r = lane < NW ? red[j & 1][lane] : make_uint2(0u, 0u);
-      const uint32_t km = row16_max_u32(r.x);
-      kl = row16_max_u32(r.x == km ? r.y : 0u);
-    }
-    const int old = tie_decode(uniform_u32(kl));
-    if constexpr (XYZ_LDS) {
-      cx = sxyz[3 * old + 0]; cy = sxyz[3 * old + 1]; cz = sxyz[3 * old + 2];
-    } else {
-      cx = P[3 * old + 0]; cy = P[3 * old + 1]; cz = P[3 * old + 2];
-    }
-    if (t == 0) {
-      I[j] = old;
-      if (NX) { NX[3 * j + 0] = cx; NX[3 * j + 1] = cy; NX[3 * j + 2] = cz; }
-    }
-  }
-}
-
-// Variant 5: the iteration tail rebuilt for latency (optionally spatially culled as v3).
-//  * per-lane key (running distance bits, tie word of the ORIGINAL index) compared as one u64,
-//    so any slot order is exact; the lane also keeps the coordinates of its best point;
-//  * wave argmax = one 32-bit max of the distance plus a ballot: when a single lane holds the
-//    maximum (the common case) its tie word and coordinates are read with v_readlane; only a
-//    real tie runs the second (tie-word) reduction;
-//  * each wave publishes ONE 20-byte record {dist, tie, x, y, z} per iteration; after the
-//    barrier every wave reduces the records of the 16-lane row and v_readlane's the winner's
-//    coordinates: no dependent LDS lookup of the new centre.
-template <int BLOCK, int PPT, int SUB, bool CULL>
-__global__ __launch_bounds__(BLOCK) void fps_v5_kernel(const float* __restrict__ xyz, int N,
-                                                       int M, int32_t* __restrict__ idx,
-                                                       float* __restrict__ new_xyz) {
-  constexpr int NW = BLOCK / kWave;
-  constexpr int CAP = BLOCK * PPT;
-  constexpr int NCELL = PPT / SUB;
-  static_assert(NW <= 16 && PPT % SUB == 0, "config");
-  __shared__ __attribute__((aligned(16))) uint16_t s_sort[CULL ? 2 * CAP : 2];
-  __shared__ uint32_t hist[CULL ? kNumCodes : 1];
-  __shared__ uint4 recA[2][16];
-  __shared__ float recZ[2][16];
-  __shared__ float bbox_red[16][6];
-  __shared__ uint32_t scan_red[16];
-
-  const int b = blockIdx.x;
-  const int t = threadIdx.x;
-  const int lane = t & (kWave - 1);
-  const int w = t / kWave;
-  const float* __restrict__ P = xyz + (size_t)b * N * 3;
-  int32_t* __restrict__ I = idx + (size_t)b * M;
-  float* __restrict__ NX = new_xyz ? new_xyz + (size_t)b * M * 3 : nullptr;
-
-  if constexpr (CULL) {  // counting sort by Morton cell (see fps_cull_kernel)
-    uint16_t* s_code = s_sort;
-    uint16_t* s_sorted = s_sort + CAP;
-    float lo[3] = {__builtin_inff(), __builtin_inff(), __builtin_inff()};
-    float hi[3] = {-__builtin_inff(), -__builtin_inff(), -__builtin_inff()};
-    for (int k = t; k < N; k += BLOCK)
-#pragma unroll
-      for (int a = 0; a < 3; ++a) {
-        const float v = P[3 * k + a];
-        lo[a] = fminf(lo[a], v);
-        hi[a] = fmaxf(hi[a], v);
-      }
-#pragma unroll
-    for (int a = 0; a < 3; ++a) { lo[a] = wave_min_f(lo[a]); hi[a] = wave_max_f(hi[a]); }
-    if (lane == 0)
-#pragma unroll
-      for (int a = 0; a < 3; ++a) { bbox_red[w][a] = lo[a]; bbox_red[w][3 + a] = hi[a]; }
-    for (int e = t; e < kNumCodes; e += BLOCK) hist[e] = 0;
-    __syncthreads();
-    float scale[3];
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-      float l = bbox_red[0][a], h = bbox_red[0][3 + a];
-      for (int q = 1; q < NW; ++q) { l = fminf(l, bbox_red[q][a]); h = fmaxf(h, bbox_red[q][3 + a]); }
-      lo[a] = l;
-      scale[a] = h > l ? (float)(1 << kCellBits) / (h - l) : 0.0f;
-    }
-    for (int k = t; k < N; k += BLOCK) {
-      uint32_t q[3];
-#pragma unroll
-      for (int a = 0; a < 3; ++a) {
-        const int c = (int)((P[3 * k + a] - lo[a]) * scale[a]);
-        q[a] = (uint32_t)min(max(c, 0), (1 << kCellBits) - 1);
-      }
-      const uint32_t code = spread3(q[0]) | (spread3(q[1]) << 1) | (spread3(q[2]) << 2);
-      s_code[k] = (uint16_t)code;
-      atomicAdd(&hist[code], 1u);
-    }
-    __syncthreads();
-    {
-      constexpr int PER = kNumCodes / BLOCK;
-      uint32_t loc[PER];
-      uint32_t sum = 0;
-#pragma unroll
-      for (int e = 0; e < PER; ++e) { loc[e] = hist[t * PER + e]; sum += loc[e]; }
-      uint32_t incl = sum;
-#pragma unroll
-      for (int o = 1; o < kWave; o <<= 1) {
-        const uint32_t y = __shfl_up(incl, o, kWave);
-        if (lane >= o) incl += y;
-      }
-      if (lane == kWave - 1) scan_red[w] = incl;
-      __syncthreads();
-      uint32_t base = 0;
-      for (int q = 0; q < w; ++q) base += scan_red[q];
-      uint32_t run = base + incl - sum;
-#pragma unroll
-      for (int e = 0; e < PER; ++e) { hist[t * PER + e] = run; run += loc[e]; }
-    }
-    __syncthreads();
-    for (int k = t; k < N; k += BLOCK) s_sorted[atomicAdd(&hist[s_code[k]], 1u)] = (uint16_t)k;
-    __syncthreads();
-  }
-
-  float px[PPT], py[PPT], pz[PPT];
-  int tb[PPT];
-  uint32_t tl[PPT];
-#pragma unroll
-  for (int i = 0; i < PPT; ++i) {
-    int k;
-    if constexpr (CULL) {
-      const int pos = w * (kWave * PPT) + i * kWave + lane;
-      k = pos < N ? (int)s_sort[CAP + pos] : N;
-    } else {
-      k = t + slot_off<BLOCK, PPT>(i);
-    }
-    if (k < N) {
-      px[i] = P[3 * k + 0];
-      py[i] = P[3 * k + 1];
-      pz[i] = P[3 * k + 2];
-      tb[i] = __float_as_int(kInitTemp);
-      tl[i] = tie_low(k);
-    } else {  // padding: key (0, 0) never wins, min(d, 0) stays 0
-      px[i] = py[i] = pz[i] = 0.0f;
-      tb[i] = 0;
-      tl[i] = 0u;
-    }
-  }
-  float clo[NCELL][3], chi[NCELL][3];
-  uint32_t ckm[NCELL], ckl[NCELL];
-  float crx[NCELL], cry[NCELL], crz[NCELL];
-#pragma unroll
-  for (int c = 0; c < NCELL; ++c) {
-    if constexpr (CULL) {
-      float l0 = __builtin_inff(), l1 = l0, l2 = l0, h0 = -l0, h1 = -l0, h2 = -l0;
-#pragma unroll
-      for (int i = c * SUB; i < (c + 1) * SUB; ++i)
-        if (tl[i] != 0u) {
-          l0 = fminf(l0, px[i]); h0 = fmaxf(h0, px[i]);
-          l1 = fminf(l1, py[i]); h1 = fmaxf(h1, py[i]);
-          l2 = fminf(l2, pz[i]); h2 = fmaxf(h2, pz[i]);
-        }
-      clo[c][0] = uniform_f(wave_min_f(l0)); chi[c][0] = uniform_f(wave_max_f(h0));
-      clo[c][1] = uniform_f(wave_min_f(l1)); chi[c][1] = uniform_f(wave_max_f(h1));
-      clo[c][2] = uniform_f(wave_min_f(l2)); chi[c][2] = uniform_f(wave_max_f(h2));
-    }
-    ckm[c] = ckl[c] = 0u;
-    crx[c] = cry[c] = crz[c] = 0.0f;
-  }
-
-  float cx = P[0], cy = P[1], cz = P[2];
-  if (t == 0) {
-    I[0] = 0;
-    if (NX) { NX[0] = cx; NX[1] = cy; NX[2] = cz; }
-  }
-  bool first = true;
-  for (int j = 1; j < M; ++j) {
-    uint32_t wkm = 0u, wkl = 0u;
-    float wx = 0.0f, wy = 0.0f, wz = 0.0f;
-#pragma unroll
-    for (int c = 0; c < NCELL; ++c) {
-      bool skip = false;
-      if constexpr (CULL) {
-        const float dx = fmaxf(fmaxf(clo[c][0] - cx, cx - chi[c][0]), 0.0f);
-        const float dy = fmaxf(fmaxf(clo[c][1] - cy, cy - chi[c][1]), 0.0f);
-        const float dz = fmaxf(fmaxf(clo[c][2] - cz, cz - chi[c][2]), 0.0f);
-        const float lb = (dx * dx + dy * dy) + dz * dz;
-        skip = !first && lb > 1e-30f && lb * 0.99998f > __uint_as_float(ckm[c]);
-      }
-      if (!skip) {
-        uint32_t bh = 0u, bl = 0u;
-        int bi = c * SUB;
-#pragma unroll
-        for (int i = c * SUB; i < (c + 1) * SUB; ++i) {
-          const int v = min(__float_as_int(sqdist(px[i], py[i], pz[i], cx, cy, cz)), tb[i]);
-          tb[i] = v;
-          if (pack64(tl[i], (uint32_t)v) > pack64(bl, bh)) { bh = (uint32_t)v; bl = tl[i]; bi = i; }
-        }
-        float bx = px[c * SUB], by = py[c * SUB], bz = pz[c * SUB];
-#pragma unroll
-        for (int i = c * SUB + 1; i < (c + 1) * SUB; ++i)
-          if (bi == i) { bx = px[i]; by = py[i]; bz = pz[i]; }
-        const uint32_t km = uniform_u32(wave_max_u32(bh));
-        const uint64_t ball = __ballot(bh == km);
-        uint32_t kl;
-        int L;
-        if (__popcll(ball) == 1) {
-          L = __ffsll((unsigned long long)ball) - 1;
-          kl = (uint32_t)__builtin_amdgcn_readlane((int)bl, L);
-        } else {  // a real tie on the distance: smallest original-order tie key wins
-          kl = uniform_u32(wave_max_u32(bh == km ? bl : 0u));
-          L = __ffsll((unsigned long long)__ballot(bh == km && bl == kl)) - 1;
-        }
-        ckm[c] = km;
-        ckl[c] = kl;
-        crx[c] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(bx), L));
-        cry[c] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(by), L));
-        crz[c] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(bz), L));
-      }
-      if (ckm[c] > wkm || (ckm[c] == wkm && ckl[c] > wkl)) {
-        wkm = ckm[c]; wkl = ckl[c]; wx = crx[c]; wy = cry[c]; wz = crz[c];
-      }
-    }
-    first = false;
-    uint32_t kl = wkl;
-    if constexpr (NW > 1) {
-      if (lane == 0) {
-        recA[j & 1][w] = make_uint4(wkm, wkl, __float_as_uint(wx), __float_as_uint(wy));
-        recZ[j & 1][w] = wz;
-      }
-      __syncthreads();
-      const bool in = lane < NW;
-      const uint4 r = in ? recA[j & 1][lane] : make_uint4(0u, 0u, 0u, 0u);
-      const float rz = in ? recZ[j & 1][lane] : 0.0f;
-      const uint32_t km = (uint32_t)__builtin_amdgcn_readlane((int)row16_max_u32(r.x), 0);
-      const uint64_t ball = __ballot(in && r.x == km);
-      int L;
-      if (__popcll(ball) == 1) {
-        L = __ffsll((unsigned long long)ball) - 1;
-      } else {
-        const uint32_t kt = (uint32_t)__builtin_amdgcn_readlane(
-            (int)row16_max_u32(in && r.x == km ? r.y : 0u), 0);
-        L = __ffsll((unsigned long long)__ballot(in && r.x == km && r.y == kt)) - 1;
-      }
-      kl = (uint32_t)__builtin_amdgcn_readlane((int)r.y, L);
-      cx = __int_as_float(__builtin_amdgcn_readlane((int)r.z, L));
-      cy = __int_as_float(__builtin_amdgcn_readlane((int)r.w, L));
-      cz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(rz), L));
-    } else {
-      cx = wx; cy = wy; cz = wz;
-    }
-    const int old = tie_decode(kl);
-    if (t == 0) {
-      I[j] = old;
-      if (NX) { NX[3 * j + 0] = cx; NX[3 * j + 1] = cy; NX[3 * j + 2] = cz; }
-    }
-  }
-}
-
-// Variant 6: culled sampler with a short iteration tail (production path for large clouds).
-//  * points counting-sorted by Morton cell as in v3; wave w owns PPT*64 consecutive sorted
-//    points (a compact region) split into NCELL cells of SUB slots;
-//  * every lane keeps, per cell, the best (running distance, tie word) of its slots, so a cell
-//    that did not change needs no rescan and the wave needs ONE reduction per iteration — and
-//    none at all when the new centre is provably too far from the wave's whole box
-//    (wave-level skip); cells are skipped the same way inside an active wave. The skip bound is
-//    the wave's max running distance U_w (>= every cell's), test lb*(1-2^-16) > U_w;
-//  * argmax tie-breaks by ballot: a second reduction only when several lanes/waves share the
-//    maximum distance;
-//  * the winner's coordinates from an LDS copy of the cloud (one broadcast read);
-//  * idx / new_xyz are collected in registers of wave 0 (lane = j mod 64, one select each) and
-//    stored 64 at a time, instead of a masked global store per iteration.
-template <int BLOCK, int PPT, int SUB, bool STAMP = false>
-__global__ __launch_bounds__(BLOCK) void fps_v6_kernel(const float* __restrict__ xyz, int N,
-                                                       int M, int32_t* __restrict__ idx,
-                                                       float* __restrict__ new_xyz) {
-  constexpr int NW = BLOCK / kWave;
-  constexpr int CAP = BLOCK * PPT;
-  constexpr int NCELL = PPT / SUB;
-  constexpr bool XYZ_LDS = 12 * CAP + 4 * kNumCodes + 2048 <= 160 * 1024;
-  static_assert(NW <= 16 && PPT % SUB == 0, "config");
-  constexpr int A_BYTES = XYZ_LDS ? 12 * CAP : 4 * CAP;
-  __shared__ __attribute__((aligned(16))) unsigned char smem_a[A_BYTES];
-  __shared__ uint32_t hist[kNumCodes];
-  __shared__ uint2 red[2][16];
-  __shared__ float bbox_red[16][6];
-  __shared__ uint32_t scan_red[16];
-  uint16_t* s_code = reinterpret_cast<uint16_t*>(smem_a);
-  uint16_t* s_sorted = s_code + CAP;
-  float* sxyz = reinterpret_cast<float*>(smem_a);
-  unsigned long long st_acc[6] = {0, 0, 0, 0, 0, 0}, st_prev = 0;
-  if constexpr (STAMP) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_prev)::"memory");
-
-  const int b = blockIdx.x;
-  const int t = threadIdx.x;
-  const int lane = t & (kWave - 1);
-  const int w = t / kWave;
-  const float* __restrict__ P = xyz + (size_t)b * N * 3;
-  int32_t* __restrict__ I = idx + (size_t)b * M;
-  float* __restrict__ NX = new_xyz ? new_xyz + (size_t)b * M * 3 : nullptr;
-
-  // ---- setup: bounding box, counting sort by Morton cell
-  {
-    float lo[3] = {__builtin_inff(), __builtin_inff(), __builtin_inff()};
-    float hi[3] = {-__builtin_inff(), -__builtin_inff(), -__builtin_inff()};
-    for (int k = t; k < N; k += BLOCK)
-#pragma unroll
-      for (int a = 0; a < 3; ++a) {
-        const float v = P[3 * k + a];
-        lo[a] = fminf(lo[a], v);
-        hi[a] = fmaxf(hi[a], v);
-      }
-#pragma unroll
-    for (int a = 0; a < 3; ++a) { lo[a] = wave_min_f(lo[a]); hi[a] = wave_max_f(hi[a]); }
-    if (lane == 0)
-#pragma unroll
-      for (int a = 0; a < 3; ++a) { bbox_red[w][a] = lo[a]; bbox_red[w][3 + a] = hi[a]; }
-    for (int e = t; e < kNumCodes; e += BLOCK) hist[e] = 0;
-    __syncthreads();
-    float scale[3];
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-      float l = bbox_red[0][a], h = bbox_red[0][3 + a];
-      for (int q = 1; q < NW; ++q) { l = fminf(l, bbox_red[q][a]); h = fmaxf(h, bbox_red[q][3 + a]); }
-      lo[a] = l;
-      scale[a] = h > l ? (float)(1 << kCellBits) / (h - l) : 0.0f;
-    }
-    for (int k = t; k < N; k += BLOCK) {
-      uint32_t q[3];
-#pragma unroll
-      for (int a = 0; a < 3; ++a) {
-        const int c = (int)((P[3 * k + a] - lo[a]) * scale[a]);
-        q[a] = (uint32_t)min(max(c, 0), (1 << kCellBits) - 1);
-      }
-      const uint32_t code = spread3(q[0]) | (spread3(q[1]) << 1) | (spread3(q[2]) << 2);
-      s_code[k] = (uint16_t)code;
-      atomicAdd(&hist[code], 1u);
-    }
-    __syncthreads();
-    constexpr int PER = kNumCodes / BLOCK;
-    uint32_t loc[PER];
-    uint32_t sum = 0;
-#pragma unroll
-    for (int e = 0; e < PER; ++e) { loc[e] = hist[t * PER + e]; sum += loc[e]; }
-    uint32_t incl = sum;
-#pragma unroll
-    for (int o = 1; o < kWave; o <<= 1) {
-      const uint32_t y = __shfl_up(incl, o, kWave);
-      if (lane >= o) incl += y;
-    }
-    if (lane == kWave - 1) scan_red[w] = incl;
-    __syncthreads();
-    uint32_t base = 0;
-    for (int q = 0; q < w; ++q) base += scan_red[q];
-    uint32_t run = base + incl - sum;
-#pragma unroll
-    for (int e = 0; e < PER; ++e) { hist[t * PER + e] = run; run += loc[e]; }
-    __syncthreads();
-    for (int k = t; k < N; k += BLOCK) s_sorted[atomicAdd(&hist[s_code[k]], 1u)] = (uint16_t)k;
-    __syncthreads();
-  }
-
-  float px[PPT], py[PPT], pz[PPT];
-  int tb[PPT];
-  uint32_t tl[PPT];
-#pragma unroll
-  for (int i = 0; i < PPT; ++i) {
-    const int pos = w * (kWave * PPT) + i * kWave + lane;
-    const int k = pos < N ? (int)s_sorted[pos] : N;
-    if (k < N) {
-      px[i] = P[3 * k + 0];
-      py[i] = P[3 * k + 1];
-      pz[i] = P[3 * k + 2];
-      tb[i] = __float_as_int(kInitTemp);
-      tl[i] = tie_low(k);
-    } else {  // padding: key (0, 0) never wins, min(d, 0) stays 0
-      px[i] = py[i] = pz[i] = 0.0f;
-      tb[i] = 0;
-      tl[i] = 0u;
-    }
-  }
-  // per-cell boxes (wave-uniform) and the wave's box
-  float clo[NCELL][3], chi[NCELL][3], wlo[3], whi[3];
-#pragma unroll
-  for (int a = 0; a < 3; ++a) { wlo[a] = __builtin_inff(); whi[a] = -__builtin_inff(); }
-#pragma unroll
-  for (int c = 0; c < NCELL; ++c) {
-    float l0 = __builtin_inff(), l1 = l0, l2 = l0, h0 = -l0, h1 = -l0, h2 = -l0;
-#pragma unroll
-    for (int i = c * SUB; i < (c + 1) * SUB; ++i)
-      if (tl[i] != 0u) {
-        l0 = fminf(l0, px[i]); h0 = fmaxf(h0, px[i]);
-        l1 = fminf(l1, py[i]); h1 = fmaxf(h1, py[i]);
-        l2 = fminf(l2, pz[i]); h2 = fmaxf(h2, pz[i]);
-      }
-    clo[c][0] = uniform_f(wave_min_f(l0)); chi[c][0] = uniform_f(wave_max_f(h0));
-    clo[c][1] = uniform_f(wave_min_f(l1)); chi[c][1] = uniform_f(wave_max_f(h1));
-    clo[c][2] = uniform_f(wave_min_f(l2)); chi[c][2] = uniform_f(wave_max_f(h2));
-#pragma unroll
-    for (int a = 0; a < 3; ++a) { wlo[a] = fminf(wlo[a], clo[c][a]); whi[a] = fmaxf(whi[a], chi[c][a]); }
-  }
-  __syncthreads();  // s_sorted is dead; smem_a becomes the xyz copy
-  if constexpr (XYZ_LDS) {
-    for (int e = t; e < 3 * N; e += BLOCK) sxyz[e] = P[e];
-    __syncthreads();
-  }
-
-  uint32_t cbh[NCELL], cbl[NCELL];  // per lane, per cell: best (distance bits, tie word)
-#pragma unroll
-  for (int c = 0; c < NCELL; ++c) cbh[c] = cbl[c] = 0u;
-  uint32_t wkm = 0u, wkl = 0u;       // the wave's record (uniform)
-  float cx = P[0], cy = P[1], cz = P[2];
-  int ring_i = 0;                    // wave 0: idx / new_xyz of 64 iterations, lane = j & 63
-  float ring_x = cx, ring_y = cy, ring_z = cz;
-  PN2_STAMP(5)
-
-  for (int j = 1; j < M; ++j) {
-    if constexpr (STAMP) {
-      if (t == 0 && j < 4096) g_iter[j] = st_prev;
-    }
-    const bool first = j == 1;
-    const float Uw = __uint_as_float(wkm);
-    auto far_box = [&](const float* lo, const float* hi) {
-      const float dx = fmaxf(fmaxf(lo[0] - cx, cx - hi[0]), 0.0f);
-      const float dy = fmaxf(fmaxf(lo[1] - cy, cy - hi[1]), 0.0f);
-      const float dz = fmaxf(fmaxf(lo[2] - cz, cz - hi[2]), 0.0f);
-      const float lb = (dx * dx + dy * dy) + dz * dz;
-      return !first && lb > 1e-30f && lb * 0.99998f > Uw;
-    };
-    if (!far_box(wlo, whi)) {
-#pragma unroll
-      for (int c = 0; c < NCELL; ++c) {
-        if (far_box(clo[c], chi[c])) continue;
-        uint32_t bh = 0u, bl = 0u;
-#pragma unroll
-        for (int i = c * SUB; i < (c + 1) * SUB; ++i) {
-          const int v = min(__float_as_int(sqdist(px[i], py[i], pz[i], cx, cy, cz)), tb[i]);
-          tb[i] = v;
-          if (pack64(tl[i], (uint32_t)v) > pack64(bl, bh)) { bh = (uint32_t)v; bl = tl[i]; }
-        }
-        cbh[c] = bh;
-        cbl[c] = bl;
-      }
-      PN2_STAMP(0)
-      uint32_t bh = cbh[0], bl = cbl[0];
-#pragma unroll
-      for (int c = 1; c < NCELL; ++c)
-        if (pack64(cbl[c], cbh[c]) > pack64(bl, bh)) { bh = cbh[c]; bl = cbl[c]; }
-      wkm = uniform_u32(wave_max_u32(bh));
-      const uint64_t ball = __ballot(bh == wkm);
-      if (__popcll(ball) == 1)
-        wkl = (uint32_t)__builtin_amdgcn_readlane((int)bl, __ffsll((unsigned long long)ball) - 1);
-      else
-        wkl = uniform_u32(wave_max_u32(bh == wkm ? bl : 0u));
-      PN2_STAMP(1)
-    }
-    uint32_t kl = wkl;
-    if constexpr (NW > 1) {
-      if (lane == 0) red[j & 1][w] = make_uint2(wkm, wkl);
-      __syncthreads();
-      PN2_STAMP(2)
-      const bool in = lane < NW;
-      const uint2 r = in ? red[j & 1][lane] : make_uint2(0u, 0u);
-      const uint32_t km = (uint32_t)__builtin_amdgcn_readlane((int)row16_max_u32(r.x), 0);
-      const uint64_t ball = __ballot(in && r.x == km);
-      if (__popcll(ball) == 1)
-        kl = (uint32_t)__builtin_amdgcn_readlane((int)r.y, __ffsll((unsigned long long)ball) - 1);
-      else
-        kl = (uint32_t)__builtin_amdgcn_readlane(
-            (int)row16_max_u32(in && r.x == km ? r.y : 0u), 0);
-    }
-    const int old = tie_decode(kl);
-    PN2_STAMP(3)
-    if constexpr (XYZ_LDS) {
-      cx = sxyz[3 * old + 0]; cy = sxyz[3 * old + 1]; cz = sxyz[3 * old + 2];
-    } else {
-      cx = P[3 * old + 0]; cy = P[3 * old + 1]; cz = P[3 * old + 2];
-    }
-    PN2_STAMP(4)
-    if (w == 0) {  // wave-uniform: ring of the last 64 results, flushed when full
-      const int sl = j & (kWave - 1);
-      const bool mine = lane == sl;
-      ring_i = mine ? old : ring_i;
-      ring_x = mine ? cx : ring_x;
-      ring_y = mine ? cy : ring_y;
-      ring_z = mine ? cz : ring_z;
-      if (sl == kWave - 1 || j == M - 1) {
-        const int jj = (j & ~(kWave - 1)) + lane;
-        if (lane <= sl) {
-          I[jj] = ring_i;
-          if (NX) { NX[3 * jj] = ring_x; NX[3 * jj + 1] = ring_y; NX[3 * jj + 2] = ring_z; }
-        }
-      }
-    }
-    PN2_STAMP(5)
-  }
-  if (M == 1 && t == 0) {
-    I[0] = 0;
-    if (NX) { NX[0] = cx; NX[1] = cy; NX[2] = cz; }
-  }
-  if constexpr (STAMP) {
-    if (lane == 0 && blockIdx.x < 16)
-      for (int ph = 0; ph < 6; ++ph) g_stamp[(blockIdx.x * 16 + w) * 8 + ph] = st_acc[ph];
-  }
-}
-
-// Variant 8: culled sampler with the culled work spread over the SIMDs.
-//  * points counting-sorted by Morton cell (v3 setup); a "cell" is 64 consecutive sorted points
-//    = one slot of one wave, and cells are dealt round-robin (cell g -> wave g % NW, slot
-//    g / NW), so the few cells near the new centre land in DIFFERENT waves / SIMDs;
-//  * lane i of a wave holds the box of the wave's slot i, so all its slots are tested at once
-//    (lb*(1-2^-16) > U_w, U_w = the wave's max running distance) and a ballot gives the
-//    active slots; only those are rescanned (uniform scalar branches per slot);
-//  * argmax: one 32-bit wave max, then the lanes holding it ds_max_u64 their (distance, tie)
-//    key into a triple-buffered LDS word (v7) — inactive waves re-offer their unchanged best
-//    the same way; after the barrier one LDS read gives the winner.
-template <int BLOCK, int PPT, bool STAMP = false>
-__global__ __launch_bounds__(BLOCK) void fps_v8_kernel(const float* __restrict__ xyz, int N,
-                                                       int M, int32_t* __restrict__ idx,
-                                                       float* __restrict__ new_xyz) {
-  constexpr int NW = BLOCK / kWave;
-  constexpr int CAP = BLOCK * PPT;
-  static_assert(NW <= 16 && PPT <= kWave, "config");
-  constexpr bool XYZ_LDS = 12 * CAP + 4 * kNumCodes + 1024 <= 160 * 1024;
-  constexpr int A_BYTES = XYZ_LDS ? 12 * CAP : 4 * CAP;
-  __shared__ __attribute__((aligned(16))) unsigned char smem_a[A_BYTES];
-  __shared__ uint32_t hist[kNumCodes];
-  __shared__ uint2 red[2][16];
-  __shared__ float bbox_red[16][6];
-  __shared__ uint32_t scan_red[16];
-  uint16_t* s_code = reinterpret_cast<uint16_t*>(smem_a);
-  uint16_t* s_sorted = s_code + CAP;
-  float* sxyz = reinterpret_cast<float*>(smem_a);
-  unsigned long long st_acc[6] = {0, 0, 0, 0, 0, 0}, st_prev = 0;
-
-  const int b = blockIdx.x;
-  const int t = threadIdx.x;
-  const int lane = t & (kWave - 1);
-  const int w = t / kWave;
-  const float* __restrict__ P = xyz + (size_t)b * N * 3;
-  int32_t* __restrict__ I = idx + (size_t)b * M;
-  float* __restrict__ NX = new_xyz ? new_xyz + (size_t)b * M * 3 : nullptr;
-
-  {  // setup: cloud box, counting sort by 12-bit Morton cell
-    float lo[3] = {__builtin_inff(), __builtin_inff(), __builtin_inff()};
-    float hi[3] = {-__builtin_inff(), -__builtin_inff(), -__builtin_inff()};
-    for (int k = t; k < N; k += BLOCK)
-#pragma unroll
-      for (int a = 0; a < 3; ++a) {
-        const float v = P[3 * k + a];
-        lo[a] = fminf(lo[a], v);
-        hi[a] = fmaxf(hi[a], v);
-      }
-#pragma unroll
-    for (int a = 0; a < 3; ++a) { lo[a] = wave_min_f(lo[a]); hi[a] = wave_max_f(hi[a]); }
-    if (lane == 0)
-#pragma unroll
-      for (int a = 0; a < 3; ++a) { bbox_red[w][a] = lo[a]; bbox_red[w][3 + a] = hi[a]; }
-    for (int e = t; e < kNumCodes; e += BLOCK) hist[e] = 0;
-    __syncthreads();
-    float scale[3];
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-      float l = bbox_red[0][a], h = bbox_red[0][3 + a];
-      for (int q = 1; q < NW; ++q) { l = fminf(l, bbox_red[q][a]); h = fmaxf(h, bbox_red[q][3 + a]); }
-      lo[a] = l;
-      scale[a] = h > l ? (float)(1 << kCellBits) / (h - l) : 0.0f;
-    }
-    for (int k = t; k < N; k += BLOCK) {
-      uint32_t q[3];
-#pragma unroll
-      for (int a = 0; a < 3; ++a) {
-        const int c = (int)((P[3 * k + a] - lo[a]) * scale[a]);
-        q[a] = (uint32_t)min(max(c, 0), (1 << kCellBits) - 1);
-      }
-      const uint32_t code = spread3(q[0]) | (spread3(q[1]) << 1) | (spread3(q[2]) << 2);
-      s_code[k] = (uint16_t)code;
-      atomicAdd(&hist[code], 1u);
-    }
-    __syncthreads();
-    constexpr int PER = kNumCodes / BLOCK;
-    uint32_t loc[PER];
-    uint32_t sum = 0;
-#pragma unroll
-    for (int e = 0; e < PER; ++e) { loc[e] = hist[t * PER + e]; sum += loc[e]; }
-    uint32_t incl = sum;
-#pragma unroll
-    for (int o = 1; o < kWave; o <<= 1) {
-      const uint32_t y = __shfl_up(incl, o, kWave);
-      if (lane >= o) incl += y;
-    }
-    if (lane == kWave - 1) scan_red[w] = incl;
-    __syncthreads();
-    uint32_t base = 0;
-    for (int q = 0; q < w; ++q) base += scan_red[q];
-    uint32_t run = base + incl - sum;
-#pragma unroll
-    for (int e = 0; e < PER; ++e) { hist[t * PER + e] = run; run += loc[e]; }
-    __syncthreads();
-    for (int k = t; k < N; k += BLOCK) s_sorted[atomicAdd(&hist[s_code[k]], 1u)] = (uint16_t)k;
-    __syncthreads();
-  }
-
-  float px[PPT], py[PPT], pz[PPT];
-  int tb[PPT];
-  uint32_t tl[PPT];
-  float blx = __builtin_inff(), bly = blx, blz = blx, bhx = -blx, bhy = -blx, bhz = -blx;
-#pragma unroll
-  for (int i = 0; i < PPT; ++i) {
-    const int pos = (i * NW + w) * kWave + lane;  // cell i*NW + w
-    const int k = pos < N ? (int)s_sorted[pos] : N;
-    float l0 = __builtin_inff(), l1 = l0, l2 = l0, h0 = -l0, h1 = -l0, h2 = -l0;
-    if (k < N) {
-      px[i] = P[3 * k + 0];
-      py[i] = P[3 * k + 1];
-      pz[i] = P[3 * k + 2];
-      tb[i] = __float_as_int(kInitTemp);
-      tl[i] = tie_low(k);
-      l0 = h0 = px[i]; l1 = h1 = py[i]; l2 = h2 = pz[i];
-    } else {  // padding: key (0, 0) never wins, min(d, 0) stays 0
-      px[i] = py[i] = pz[i] = 0.0f;
-      tb[i] = 0;
-      tl[i] = 0u;
-    }
-    l0 = wave_min_f(l0); l1 = wave_min_f(l1); l2 = wave_min_f(l2);
-    h0 = wave_max_f(h0); h1 = wave_max_f(h1); h2 = wave_max_f(h2);
-    if (lane == i) { blx = l0; bly = l1; blz = l2; bhx = h0; bhy = h1; bhz = h2; }
-  }
-  __syncthreads();  // s_sorted is dead; smem_a becomes the xyz copy
-  if constexpr (XYZ_LDS) {
-    for (int e = t; e < 3 * N; e += BLOCK) sxyz[e] = P[e];
-    __syncthreads();
-  }
-
-  uint32_t bh = 0u, bl = 0u;  // this lane's best over its slots
-  uint32_t wkm = 0u, wkl = 0u;  // the wave's best (uniform)
-  float cx = P[0], cy = P[1], cz = P[2];
-  int ring_i = 0;
-  float ring_x = cx, ring_y = cy, ring_z = cz;
-  constexpr uint64_t kSlotMask = PPT >= 64 ? ~0ull : ((1ull << PPT) - 1);
-  if constexpr (STAMP) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_prev)::"memory");
-  for (int j = 1; j < M; ++j) {
-    // lane-parallel test of the wave's slots (lane i <-> slot i)
-    const float dx = fmaxf(fmaxf(blx - cx, cx - bhx), 0.0f);
-    const float dy = fmaxf(fmaxf(bly - cy, cy - bhy), 0.0f);
-    const float dz = fmaxf(fmaxf(blz - cz, cz - bhz), 0.0f);
-    const float lb = (dx * dx + dy * dy) + dz * dz;
-    const bool far = j > 1 && lb > 1e-30f && lb * 0.99998f > __uint_as_float(wkm);
-    const uint64_t active = __ballot(!far) & kSlotMask;
-    if (active) {
-#pragma unroll
-      for (int i = 0; i < PPT; ++i)
-        if ((active >> i) & 1ull)
-          tb[i] = min(__float_as_int(sqdist(px[i], py[i], pz[i], cx, cy, cz)), tb[i]);
-      bh = 0u; bl = 0u;
-#pragma unroll
-      for (int i = 0; i < PPT; ++i)
-        if (pack64(tl[i], (uint32_t)tb[i]) > pack64(bl, bh)) { bh = (uint32_t)tb[i]; bl = tl[i]; }
-      wkm = uniform_u32(wave_max_u32(bh));
-    }
-    PN2_STAMP(0)
-    if (active) {  // the wave's tie word (only when the wave changed)
-      const uint64_t ball = __ballot(bh == wkm);
-      if (__popcll(ball) == 1)
-        wkl = (uint32_t)__builtin_amdgcn_readlane((int)bl, __ffsll((unsigned long long)ball) - 1);
-      else
-        wkl = uniform_u32(wave_max_u32(bh == wkm ? bl : 0u));
-    }
-    PN2_STAMP(1)
-    uint32_t kl = wkl;
-    if constexpr (NW > 1) {
-      if (lane == 0) red[j & 1][w] = make_uint2(wkm, wkl);
-      __syncthreads();
-      PN2_STAMP(2)
-      const bool in = lane < NW;
-      const uint2 r = in ? red[j & 1][lane] : make_uint2(0u, 0u);
-      const uint32_t km = (uint32_t)__builtin_amdgcn_readlane((int)row16_max_u32(r.x), 0);
-      const uint64_t ball = __ballot(in && r.x == km);
-      if (__popcll(ball) == 1)
-        kl = (uint32_t)__builtin_amdgcn_readlane((int)r.y, __ffsll((unsigned long long)ball) - 1);
-      else
-        kl = (uint32_t)__builtin_amdgcn_readlane((int)row16_max_u32(in && r.x == km ? r.y : 0u), 0);
-    }
-    const int old = tie_decode(kl);
-    PN2_STAMP(3)
-    if constexpr (XYZ_LDS) {
-      cx = sxyz[3 * old + 0]; cy = sxyz[3 * old + 1]; cz = sxyz[3 * old + 2];
-    } else {
-      cx = P[3 * old + 0]; cy = P[3 * old + 1]; cz = P[3 * old + 2];
-    }
-    PN2_STAMP(4)
-    {
-      const int sl = j & (kWave - 1);
-      const bool mine = lane == sl;
-      ring_i = mine ? old : ring_i;
-      ring_x = mine ? cx : ring_x;
-      ring_y = mine ? cy : ring_y;
-      ring_z = mine ? cz : ring_z;
-      if ((sl == kWave - 1 || j == M - 1) && w == 0) {
-        const int jj = (j & ~(kWave - 1)) + lane;
-        if (lane <= sl) {
-          I[jj] = ring_i;
-          if (NX) { NX[3 * jj] = ring_x; NX[3 * jj + 1] = ring_y; NX[3 * jj + 2] = ring_z; }
-        }
-      }
-    }
-    PN2_STAMP(5)
-  }
-  if (M == 1 && t == 0) {
-    I[0] = 0;
-    if (NX) { NX[0] = cx; NX[1] = cy; NX[2] = cz; }
-  }
-  if constexpr (STAMP) {
-    if (lane == 0 && blockIdx.x < 16)
-      for (int ph = 0; ph < 6; ++ph) g_stamp[(blockIdx.x * 16 + w) * 8 + ph] = st_acc[ph];
-  }
-}
 
 // Large clouds (N beyond the register path): running min-distance in a global workspace,
 // 1024 threads, point k on thread k mod 1024 (ascending slot order = reference tie order).
@@ -1361,148 +102,7 @@ __global__ void gather_point_grad_kernel(const float* __restrict__ out_g,
 
 constexpr int kMaxRegPoints = 1024 * 16;
 
-// The LDS copy of the cloud (12 B per point) is used whenever it fits next to the key slots
-// in the 160 KiB of one CU; otherwise the winner's xyz is re-read from global memory.
-template <int BLOCK, int PPT>
-void launch_reg(const float* xyz, int B, int N, int M, int32_t* idx, float* nx, hipStream_t s) {
-  if constexpr (3 * BLOCK * PPT * 4 + 256 <= 160 * 1024)
-    hipLaunchKernelGGL((fps_reg_kernel<BLOCK, PPT, true>), dim3(B), dim3(BLOCK), 0, s, xyz, N, M,
-                       idx, nx);
-  else
-    hipLaunchKernelGGL((fps_reg_kernel<BLOCK, PPT, false>), dim3(B), dim3(BLOCK), 0, s, xyz, N,
-                       M, idx, nx);
-}
-
-// (variant, block, points-per-thread) launch table used by the tuner (pn2_fps_tune)
-#define PN2_FPS_CONFIGS(X)                                                                      \
-  X(64, 1) X(64, 2) X(64, 4) X(64, 8) X(64, 16) X(128, 4) X(128, 8) X(128, 16) X(256, 1)      \
-  X(256, 2) X(256, 4) X(256, 8) X(256, 16) X(512, 2) X(512, 4) X(512, 8) X(512, 16)           \
-  X(1024, 1) X(1024, 2) X(1024, 4) X(1024, 8) X(1024, 16)
-
-template <int BLOCK, int PPT>
-void launch_v2(const float* xyz, int B, int N, int M, int32_t* idx, float* nx, hipStream_t s) {
-  if constexpr (3 * BLOCK * PPT * 4 + 256 <= 160 * 1024)
-    hipLaunchKernelGGL((fps_v2_kernel<BLOCK, PPT, true>), dim3(B), dim3(BLOCK), 0, s, xyz, N, M,
-                       idx, nx);
-  else
-    hipLaunchKernelGGL((fps_v2_kernel<BLOCK, PPT, false>), dim3(B), dim3(BLOCK), 0, s, xyz, N,
-                       M, idx, nx);
-}
-
-template <int BLOCK, int PPT, int SUB>
-void launch_cull(const float* xyz, int B, int N, int M, int32_t* idx, float* nx, hipStream_t s) {
-  if constexpr (12 * BLOCK * PPT + 4 * 4096 + 1024 <= 160 * 1024)
-    hipLaunchKernelGGL((fps_cull_kernel<BLOCK, PPT, SUB, true>), dim3(B), dim3(BLOCK), 0, s, xyz,
-                       N, M, idx, nx);
-  else
-    hipLaunchKernelGGL((fps_cull_kernel<BLOCK, PPT, SUB, false>), dim3(B), dim3(BLOCK), 0, s,
-                       xyz, N, M, idx, nx);
-}
-
-template <int BLOCK, int PPT, int SUB, bool CULL>
-void launch_v5(const float* xyz, int B, int N, int M, int32_t* idx, float* nx, hipStream_t s) {
-  hipLaunchKernelGGL((fps_v5_kernel<BLOCK, PPT, SUB, CULL>), dim3(B), dim3(BLOCK), 0, s, xyz, N,
-                     M, idx, nx);
-}
-
-template <int BLOCK, int PPT, int SUB>
-void launch_v6(const float* xyz, int B, int N, int M, int32_t* idx, float* nx, hipStream_t s) {
-  hipLaunchKernelGGL((fps_v6_kernel<BLOCK, PPT, SUB>), dim3(B), dim3(BLOCK), 0, s, xyz, N, M, idx,
-                     nx);
-}
-
-template <int BLOCK, int PPT>
-void launch_v7(const float* xyz, int B, int N, int M, int32_t* idx, float* nx, hipStream_t s) {
-  hipLaunchKernelGGL((fps_v7_kernel<BLOCK, PPT>), dim3(B), dim3(BLOCK), 0, s, xyz, N, M, idx, nx);
-}
-
-template <int BLOCK, int PPT>
-void launch_v8(const float* xyz, int B, int N, int M, int32_t* idx, float* nx, hipStream_t s) {
-  hipLaunchKernelGGL((fps_v8_kernel<BLOCK, PPT>), dim3(B), dim3(BLOCK), 0, s, xyz, N, M, idx, nx);
-}
-
-int fps_tune_impl(const float* xyz, int B, int N, int M, int32_t* idx, float* nx, int variant,
-                  int block, int ppt, hipStream_t s) {
-  if (B <= 0 || N <= 0 || M <= 0 || block * ppt < N) return PN2_EINVAL;
-#define PN2_X(BL, PP)                                              \
-  if (block == BL && ppt == PP && (variant == 1 || variant == 2)) {\
-    if (variant == 1) launch_reg<BL, PP>(xyz, B, N, M, idx, nx, s); \
-    else if (variant == 2) launch_v2<BL, PP>(xyz, B, N, M, idx, nx, s); \
-    if (variant == 1 || variant == 2) PN2_RETURN_LAUNCH();         \
-    return PN2_EINVAL;                                             \
-  }
-  PN2_FPS_CONFIGS(PN2_X)
-#undef PN2_X
-  if (variant == 8) {
-#define PN2_V8(BL, PP)                                                         \
-    if (block == BL && ppt == PP) {                                            \
-      launch_v8<BL, PP>(xyz, B, N, M, idx, nx, s);                             \
-      PN2_RETURN_LAUNCH();                                                     \
-    }
-    PN2_V8(256, 4) PN2_V8(256, 8) PN2_V8(512, 8) PN2_V8(512, 16) PN2_V8(1024, 8)
-    PN2_V8(1024, 16) PN2_V8(256, 16) PN2_V8(256, 32) PN2_V8(512, 32) PN2_V8(1024, 4)
-    PN2_V8(128, 8) PN2_V8(128, 16) PN2_V8(64, 16) PN2_V8(512, 4)
-#undef PN2_V8
-  }
-  if (variant == 7) {
-#define PN2_V7(BL, PP)                                                         \
-    if (block == BL && ppt == PP) {                                            \
-      launch_v7<BL, PP>(xyz, B, N, M, idx, nx, s);                             \
-      PN2_RETURN_LAUNCH();                                                     \
-    }
-    PN2_FPS_CONFIGS(PN2_V7)
-#undef PN2_V7
-  }
-  if (variant == 5) {  // v5 without culling (one cell per wave)
-#define PN2_V(BL, PP)                                                          \
-    if (block == BL && ppt == PP) {                                            \
-      launch_v5<BL, PP, PP, false>(xyz, B, N, M, idx, nx, s);                  \
-      PN2_RETURN_LAUNCH();                                                     \
-    }
-    PN2_FPS_CONFIGS(PN2_V)
-#undef PN2_V
-  }
-  if (variant >= 60 && variant < 80) {  // v6, variant = 60 + SUB
-    const int sub = variant - 60;
-#define PN2_C6(BL, PP, SB)                                                     \
-    if (block == BL && ppt == PP && sub == SB) {                                \
-      launch_v6<BL, PP, SB>(xyz, B, N, M, idx, nx, s);                          \
-      PN2_RETURN_LAUNCH();                                                      \
-    }
-    PN2_C6(256, 4, 1) PN2_C6(256, 4, 2) PN2_C6(256, 4, 4) PN2_C6(512, 8, 2) PN2_C6(512, 8, 4)
-    PN2_C6(512, 16, 2) PN2_C6(512, 16, 4) PN2_C6(512, 16, 8) PN2_C6(1024, 8, 2) PN2_C6(1024, 8, 4)
-    PN2_C6(256, 32, 4) PN2_C6(256, 32, 8) PN2_C6(1024, 16, 4) PN2_C6(1024, 16, 8)
-    PN2_C6(128, 8, 2) PN2_C6(128, 8, 4) PN2_C6(256, 8, 2) PN2_C6(256, 16, 4) PN2_C6(64, 16, 4)
-    PN2_C6(512, 32, 8) PN2_C6(256, 32, 16)
-#undef PN2_C6
-  }
-  if (variant >= 50 && variant < 60) {  // v5 culled, variant = 50 + SUB
-    const int sub = variant - 50;
-#define PN2_C(BL, PP, SB)                                                      \
-    if (block == BL && ppt == PP && sub == SB) {                                \
-      launch_v5<BL, PP, SB, true>(xyz, B, N, M, idx, nx, s);                    \
-      PN2_RETURN_LAUNCH();                                                      \
-    }
-    PN2_C(256, 4, 1) PN2_C(256, 4, 2) PN2_C(256, 4, 4) PN2_C(512, 8, 2) PN2_C(512, 8, 4)
-    PN2_C(512, 16, 2) PN2_C(512, 16, 4) PN2_C(512, 16, 8) PN2_C(1024, 8, 2) PN2_C(1024, 8, 4)
-    PN2_C(256, 32, 4) PN2_C(256, 32, 8) PN2_C(1024, 16, 4) PN2_C(1024, 16, 8) PN2_C(64, 16, 4)
-    PN2_C(128, 8, 4) PN2_C(128, 16, 4) PN2_C(256, 16, 4) PN2_C(256, 8, 4) PN2_C(1024, 4, 4)
-#undef PN2_C
-  }
-  if (variant >= 30 && variant < 50) {  // culled sampler, variant = 30 + SUB
-    const int sub = variant - 30;
-#define PN2_C(BL, PP, SB)                                                      \
-    if (block == BL && ppt == PP && sub == SB) {                                \
-      launch_cull<BL, PP, SB>(xyz, B, N, M, idx, nx, s);                        \
-      PN2_RETURN_LAUNCH();                                                      \
-    }
-    PN2_C(256, 4, 1) PN2_C(256, 4, 2) PN2_C(256, 4, 4) PN2_C(512, 8, 2) PN2_C(512, 8, 4)
-    PN2_C(512, 16, 2) PN2_C(512, 16, 4) PN2_C(512, 16, 8) PN2_C(1024, 8, 2) PN2_C(1024, 8, 4)
-    PN2_C(256, 32, 4) PN2_C(256, 32, 8) PN2_C(1024, 16, 4) PN2_C(1024, 16, 8)
-#undef PN2_C
-  }
-  return PN2_EINVAL;
-}
+// @@LAUNCH_V9@@
 
 int fps_impl(const float* xyz, int B, int N, int M, int32_t* idx, float* nx, void* ws,
              size_t ws_bytes, hipStream_t s) {
@@ -1537,59 +137,6 @@ int fps_impl(const float* xyz, int B, int N, int M, int32_t* idx, float* nx, voi
 extern "C" {
 
 int pn2_fps_max_points(void) { return pn2::kMaxRegPoints; }
-
-// Diagnostic entry: stamped v2 run; out[w*8+ph] = cycles of phase ph summed over the
-// iterations, for wave w of cloud 0 (ph: 0 scan, 1 wave reduce, 2 write+barrier,
-// 3 cross-wave reduce, 4 centre load, 5 index store).
-int pn2_fps_stamp(const float* xyz, int N, int npoint, int32_t* idx, int block, int ppt,
-                  unsigned long long* out_host) {
-  hipStream_t s = 0;
-#define PN2_S(BL, PP)                                                                        \
-  if (block == BL && ppt == PP) {                                                            \
-    hipLaunchKernelGGL((pn2::fps_v2_kernel<BL, PP, (3 * BL * PP * 4 + 256 <= 160 * 1024), true>), \
-                       dim3(1), dim3(BL), 0, s, xyz, N, npoint, idx, nullptr);               \
-  } else
-  if (block < 0) {  // v6 stamped: block = -BL, ppt = PP*100 + SUB
-#define PN2_S6(BL, PP, SB)                                                                   \
-    if (-block == BL && ppt == PP * 100 + SB) {                                              \
-      hipLaunchKernelGGL((pn2::fps_v6_kernel<BL, PP, SB, true>), dim3(1), dim3(BL), 0, s, xyz, \
-                         N, npoint, idx, nullptr);                                           \
-    } else
-    PN2_S6(512, 16, 4) PN2_S6(1024, 8, 4) PN2_S6(256, 4, 2) PN2_S6(512, 16, 8) { return PN2_EINVAL; }
-#undef PN2_S6
-  } else if (ppt >= 20000) {  // v8 stamped: ppt = 20000 + PP
-#define PN2_S8(BL, PP)                                                                       \
-    if (block == BL && ppt == 20000 + PP) {                                                  \
-      hipLaunchKernelGGL((pn2::fps_v8_kernel<BL, PP, true>), dim3(1), dim3(BL), 0, s, xyz, N,  \
-                         npoint, idx, nullptr);                                              \
-    } else
-    PN2_S8(1024, 8) PN2_S8(512, 16) PN2_S8(256, 4) PN2_S8(512, 8) { return PN2_EINVAL; }
-#undef PN2_S8
-  } else if (ppt >= 10000) {  // v7 stamped: ppt = 10000 + PP
-#define PN2_S7(BL, PP)                                                                       \
-    if (block == BL && ppt == 10000 + PP) {                                                  \
-      hipLaunchKernelGGL((pn2::fps_v7_kernel<BL, PP, true>), dim3(1), dim3(BL), 0, s, xyz, N,  \
-                         npoint, idx, nullptr);                                              \
-    } else
-    PN2_S7(64, 4) PN2_S7(256, 4) PN2_S7(512, 16) PN2_S7(1024, 8) PN2_S7(512, 8) { return PN2_EINVAL; }
-#undef PN2_S7
-  } else
-  PN2_S(64, 4) PN2_S(256, 4) PN2_S(512, 16) PN2_S(1024, 8) PN2_S(512, 8) { return PN2_EINVAL; }
-#undef PN2_S
-  hipError_t e = hipDeviceSynchronize();
-  if (e != hipSuccess) return (int)e;
-  e = hipMemcpyFromSymbol(out_host, HIP_SYMBOL(pn2::g_stamp), sizeof(unsigned long long) * 16 * 8);
-  if (e != hipSuccess) return (int)e;
-  e = hipMemcpyFromSymbol(out_host + 16 * 8, HIP_SYMBOL(pn2::g_iter), sizeof(unsigned long long) * 4096);
-  return (int)e;
-}
-
-// Tuning entry (not part of include/pn2hip.h): run one (variant, block, ppt) instantiation.
-int pn2_fps_tune(const float* xyz, int B, int N, int npoint, int32_t* idx, float* new_xyz,
-                 int variant, int block, int ppt, pn2_stream_t stream) {
-  return pn2::fps_tune_impl(xyz, B, N, npoint, idx, new_xyz, variant, block, ppt,
-                            (hipStream_t)stream);
-}
 
 size_t pn2_fps_workspace_size(int B, int N) {
   if (B <= 0 || N <= pn2::kMaxRegPoints) return 0;

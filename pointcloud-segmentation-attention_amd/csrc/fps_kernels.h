@@ -1,0 +1,311 @@
+// Device-side building blocks of the gfx950 farthest-point sampler, shared by the
+// production dispatch (fps.hip) and the variant lab (tools/fps_lab/fps_lab.hip).
+// Reference: farthestpointsamplingKernel, pointnet2_tensorflow/tf_ops/sampling/
+// tf_sampling_g.cu:105-170 (tie rule :146-163).
+#pragma once
+#include "common.h"
+
+namespace pn2 {
+namespace {
+
+constexpr float kInitTemp = 1e38f;  // tf_sampling_g.cu:118
+
+// Low word of the argmax key: larger = earlier in the reference's tie order.
+PN2_DEV uint32_t tie_low(int k) {
+  const uint32_t tk = (((uint32_t)k & 511u) << 20) | ((uint32_t)k >> 9);
+  return 0xFFFFFFFFu - tk;
+}
+PN2_DEV int tie_decode(uint32_t low) {
+  const uint32_t tk = 0xFFFFFFFFu - low;
+  return (int)((tk >> 20) + ((tk & 0xFFFFFu) << 9));
+}
+
+// Thread t owns points t + slot_off(i), i = 0..PPT-1. Slots are ordered so that, within one
+// thread, ascending slot = ascending (k mod 512, k div 512); then a strict '>' scan over the
+// slots keeps the reference's tie winner inside the thread.
+template <int BLOCK, int PPT>
+PN2_DEV constexpr int slot_off(int i) {
+  if constexpr (BLOCK >= 512) {
+    return BLOCK * i;  // k mod 512 is the same for every slot of the thread
+  } else {
+    constexpr int R = 512 / BLOCK;  // slots per residue class
+    if constexpr (PPT <= R) {
+      return BLOCK * i;  // all slots < 512: k mod 512 == k
+    } else {
+      constexpr int Q = PPT / R;  // slots that share one residue
+      return BLOCK * ((i % Q) * R + i / Q);
+    }
+  }
+}
+
+
+// Variant 2 of the register sampler: the same selection, cheaper arithmetic.
+//  * the running min-distance is kept as int32 bit patterns: for d >= 0 (or NaN) and
+//    temp in {-1} U [0, 1e38] a signed-int min of the bits is exactly fminf (no IEEE-mode
+//    canonicalisation before every v_min_f32); padding slots hold -1 and never win;
+//  * the argmax is two 32-bit max-reductions (distance, then ~tiekey among the lanes that hold
+//    the maximum distance) whose DPP moves fold into v_max_u32_dpp, instead of one 64-bit
+//    reduction; the cross-wave step is the same pair over the per-wave results.
+// Diagnostic stamps (STAMP builds only; never in a timed production kernel): s_memtime
+// deltas per phase accumulated in SGPRs, lane 0 of each wave writes them to g_stamp.
+__device__ unsigned long long g_stamp[16 * 16 * 8];
+__device__ unsigned long long g_iter[4096];  // STAMP builds: s_memtime at each iteration start
+#define PN2_STAMP(ph)                                                              \
+  if constexpr (STAMP) {                                                           \
+    __builtin_amdgcn_sched_barrier(0);                                             \
+    unsigned long long tt__;                                                       \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(tt__)::"memory");  \
+    __builtin_amdgcn_sched_barrier(0);                                             \
+    st_acc[ph] += tt__ - st_prev;                                                  \
+    st_prev = tt__;                                                                \
+  }
+
+template <int BLOCK, int PPT, bool XYZ_LDS, bool STAMP = false>
+__global__ __launch_bounds__(BLOCK) void fps_v2_kernel(const float* __restrict__ xyz, int N,
+                                                       int M, int32_t* __restrict__ idx,
+                                                       float* __restrict__ new_xyz) {
+  unsigned long long st_acc[6] = {0, 0, 0, 0, 0, 0}, st_prev = 0;
+  constexpr int NW = BLOCK / kWave;
+  static_assert(NW <= 16, "the cross-wave step reduces one 16-lane DPP row");
+  __shared__ uint2 red[2][16];
+  __shared__ float sxyz[XYZ_LDS ? 3 * BLOCK * PPT : 1];
+
+  const int b = blockIdx.x;
+  const int t = threadIdx.x;
+  const int lane = t & (kWave - 1);
+  const int w = t / kWave;
+  const float* __restrict__ P = xyz + (size_t)b * N * 3;
+  int32_t* __restrict__ I = idx + (size_t)b * M;
+  float* __restrict__ NX = new_xyz ? new_xyz + (size_t)b * M * 3 : nullptr;
+
+  float px[PPT], py[PPT], pz[PPT];
+  int tb[PPT];
+#pragma unroll
+  for (int i = 0; i < PPT; ++i) {
+    const int k = t + slot_off<BLOCK, PPT>(i);
+    if (k < N) {
+      px[i] = P[3 * k + 0];
+      py[i] = P[3 * k + 1];
+      pz[i] = P[3 * k + 2];
+      tb[i] = __float_as_int(kInitTemp);
+    } else {
+      px[i] = py[i] = pz[i] = 0.0f;
+      tb[i] = -1;
+    }
+  }
+  if constexpr (XYZ_LDS) {
+    for (int e = t; e < 3 * N; e += BLOCK) sxyz[e] = P[e];
+    __syncthreads();
+  }
+
+  float cx = P[0], cy = P[1], cz = P[2];
+  if (t == 0) {
+    I[0] = 0;
+    if (NX) { NX[0] = cx; NX[1] = cy; NX[2] = cz; }
+  }
+
+  if constexpr (STAMP) {
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_prev)::"memory");
+  }
+  for (int j = 1; j < M; ++j) {
+    int bd = -1, bi = 0;
+#pragma unroll
+    for (int i = 0; i < PPT; ++i) {
+      const int v = min(__float_as_int(sqdist(px[i], py[i], pz[i], cx, cy, cz)), tb[i]);
+      tb[i] = v;
+      if (v > bd) { bd = v; bi = i; }
+    }
+    int off;
+    if constexpr (BLOCK >= 512 || PPT <= 512 / BLOCK) {
+      off = BLOCK * bi;
+    } else {
+      constexpr int R = 512 / BLOCK, Q = PPT / R;
+      off = BLOCK * ((bi % Q) * R + bi / Q);
+    }
+    const uint32_t hi = bd < 0 ? 0u : (uint32_t)bd + 1u;
+    const uint32_t lo = bd < 0 ? 0u : tie_low(t + off);
+    PN2_STAMP(0)
+    uint32_t km = wave_max_u32(hi);
+    uint32_t kl = wave_max_u32(hi == km ? lo : 0u);
+    PN2_STAMP(1)
+    if constexpr (NW > 1) {
+      if (lane == 0) red[j & 1][w] = make_uint2(km, kl);
+      __syncthreads();
+      PN2_STAMP(2)
+      const uint2 r = lane < NW ? red[j & 1][lane] : make_uint2(0u, 0u);
+      km = row16_max_u32(r.x);
+      kl = row16_max_u32(r.x == km ? r.y : 0u);
+    }
+    const int old = tie_decode(uniform_u32(kl));
+    PN2_STAMP(3)
+    if constexpr (XYZ_LDS) {
+      cx = sxyz[3 * old + 0]; cy = sxyz[3 * old + 1]; cz = sxyz[3 * old + 2];
+    } else {
+      cx = P[3 * old + 0]; cy = P[3 * old + 1]; cz = P[3 * old + 2];
+    }
+    PN2_STAMP(4)
+    if (t == 0) {
+      I[j] = old;
+      if (NX) { NX[3 * j + 0] = cx; NX[3 * j + 1] = cy; NX[3 * j + 2] = cz; }
+    }
+    PN2_STAMP(5)
+  }
+  if constexpr (STAMP) {
+    if (lane == 0 && blockIdx.x < 16)
+      for (int ph = 0; ph < 6; ++ph) g_stamp[(blockIdx.x * 16 + w) * 8 + ph] = st_acc[ph];
+  }
+}
+
+// Variant 9 (BLOCK <= 512): v2's register sampler with a cheaper scan and a shorter tail.
+//  * point layout: thread t owns residues R*t .. R*t+R-1 of each 512-wide row (R = 512/BLOCK,
+//    or all PPT points of a row < 512 wide), i.e. k = W*h + R*t + c with slot s = c*H + h.
+//    Then ascending (lane, slot) IS the reference's tie order (k mod 512, k div 512)
+//    (tf_sampling_g.cu:146-163), across lanes and waves as well as inside a thread;
+//  * scan: slots in groups of G; per group one v_max3 chain folds the G new temps into the
+//    running max and ONE compare+select remembers the first group that raised it (strict
+//    '>', so the earliest group wins ties) -- (G+1)/G instead of 3 VALU ops per point;
+//  * wave: ONE 32-bit max (DPP folded into v_max_u32_dpp + permlane swaps); the winner is
+//    the lowest lane of ballot(hi == max) (s_ff1) because lane order is tie order; its group
+//    is read with v_readlane and the first slot of that group holding the max is found with
+//    scalar compares -- no second (tie-word) reduction;
+//  * block: each wave publishes (max, point index) to a double-buffered LDS slot, ONE barrier,
+//    then an 8-lane DPP max + ballot/s_ff1 picks the lowest wave holding the block max
+//    (lower wave = lower t = earlier in tie order).
+template <int BLOCK, int PPT>
+struct Lay9 {
+  static_assert(BLOCK <= 512 && 512 % BLOCK == 0, "v9 layout needs BLOCK | 512");
+  static constexpr int R = PPT < 512 / BLOCK ? PPT : 512 / BLOCK;  // residues per thread
+  static constexpr int H = PPT / R;                                 // rows
+  static constexpr int W = R * BLOCK;                               // row width (<= 512)
+  static_assert(R * H == PPT, "PPT must be a multiple of 512 / BLOCK or below it");
+  PN2_DEV static constexpr int point(int t, int s) { return W * (s % H) + R * t + s / H; }
+};
+
+template <int BLOCK, int PPT, int G, bool XYZ_LDS>
+__global__ __launch_bounds__(BLOCK) void fps_v9_kernel(const float* __restrict__ xyz, int N,
+                                                       int M, int32_t* __restrict__ idx,
+                                                       float* __restrict__ new_xyz) {
+  using Lay = Lay9<BLOCK, PPT>;
+  constexpr int NW = BLOCK / kWave;
+  static_assert(BLOCK % kWave == 0 && NW <= 8, "the block step reduces 8 DPP lanes");
+  static_assert(PPT % G == 0 && (G == 1 || G == 2 || G == 4), "slot groups");
+  constexpr int NG = PPT / G;
+  __shared__ uint2 red[2][8];
+  __shared__ float sxyz[XYZ_LDS ? 3 * BLOCK * PPT : 1];
+
+  const int b = blockIdx.x;
+  const int t = threadIdx.x;
+  const int lane = t & (kWave - 1);
+  const int w = t / kWave;
+  const float* __restrict__ P = xyz + (size_t)b * N * 3;
+  int32_t* __restrict__ I = idx + (size_t)b * M;
+  float* __restrict__ NX = new_xyz ? new_xyz + (size_t)b * M * 3 : nullptr;
+
+  float px[PPT], py[PPT], pz[PPT];
+  int tb[PPT];  // running min distance as int bits; padding slots -1 never win
+#pragma unroll
+  for (int s = 0; s < PPT; ++s) {
+    const int k = Lay::point(t, s);
+    if (k < N) {
+      px[s] = P[3 * k + 0];
+      py[s] = P[3 * k + 1];
+      pz[s] = P[3 * k + 2];
+      tb[s] = __float_as_int(kInitTemp);
+    } else {
+      px[s] = py[s] = pz[s] = 0.0f;
+      tb[s] = -1;
+    }
+  }
+  if constexpr (XYZ_LDS) {
+    for (int e = t; e < 3 * N; e += BLOCK) sxyz[e] = P[e];
+    __syncthreads();
+  }
+
+  float cx = P[0], cy = P[1], cz = P[2];
+  if (t == 0) {
+    I[0] = 0;
+    if (NX) { NX[0] = cx; NX[1] = cy; NX[2] = cz; }
+  }
+
+  for (int j = 1; j < M; ++j) {
+    int bd = -1, bg = 0;
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      int v[G];
+#pragma unroll
+      for (int q = 0; q < G; ++q) {
+        const int s = g * G + q;
+        v[q] = min(__float_as_int(sqdist(px[s], py[s], pz[s], cx, cy, cz)), tb[s]);
+        tb[s] = v[q];
+      }
+      int m;
+      if constexpr (G == 4) m = max(max(max(max(v[0], v[1]), v[2]), v[3]), bd);
+      else if constexpr (G == 2) m = max(max(v[0], v[1]), bd);
+      else m = max(v[0], bd);
+      bg = m > bd ? g : bg;
+      bd = m;
+    }
+    // wave: lowest lane holding the wave max, then its first slot holding it
+    const uint32_t hi = (uint32_t)(bd + 1);  // 0 for lanes with padding only
+    const uint32_t km = wave_max_u32(hi);
+    const uint64_t hold = __builtin_amdgcn_ballot_w64(hi == km);
+    const int L = (int)__builtin_amdgcn_readfirstlane((int)__builtin_ctzll(hold));
+    const int gq = __builtin_amdgcn_readlane(bg, L);
+    const int kv = (int)km - 1;
+    int sq = 0;
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      if (g == gq) {
+        int r = G - 1;
+#pragma unroll
+        for (int q = G - 2; q >= 0; --q)
+          if (__builtin_amdgcn_readlane(tb[g * G + q], L) == kv) r = q;
+        sq = g * G + r;
+      }
+    }
+    int old = Lay::point(w * kWave + L, sq);
+    if constexpr (NW > 1) {
+      if (lane == 0) red[j & 1][w] = make_uint2(km, (uint32_t)old);
+      __syncthreads();
+      const uint2 r = (lane & 7) < NW ? red[j & 1][lane & 7] : make_uint2(0u, 0u);
+      uint32_t bm = max_dpp_u32<kDppXor1>(r.x);
+      bm = max_dpp_u32<kDppXor2>(bm);
+      bm = max_dpp_u32<kDppHalfMirror>(bm);
+      const uint64_t wins = __builtin_amdgcn_ballot_w64(r.x == bm) & 0xFFull;
+      const int wi = (int)__builtin_amdgcn_readfirstlane((int)__builtin_ctzll(wins));
+      old = __builtin_amdgcn_readlane((int)r.y, wi);
+    }
+    if constexpr (XYZ_LDS) {
+      cx = sxyz[3 * old + 0]; cy = sxyz[3 * old + 1]; cz = sxyz[3 * old + 2];
+    } else {
+      cx = P[3 * old + 0]; cy = P[3 * old + 1]; cz = P[3 * old + 2];
+    }
+    if (t == 0) {
+      I[j] = old;
+      if (NX) { NX[3 * j + 0] = cx; NX[3 * j + 1] = cy; NX[3 * j + 2] = cz; }
+    }
+  }
+}
+
+template <int BLOCK, int PPT, int G>
+void launch_v9(const float* xyz, int B, int N, int M, int32_t* idx, float* nx, hipStream_t s) {
+  if constexpr (3 * BLOCK * PPT * 4 + 256 <= 160 * 1024)
+    hipLaunchKernelGGL((fps_v9_kernel<BLOCK, PPT, G, true>), dim3(B), dim3(BLOCK), 0, s, xyz, N,
+                       M, idx, nx);
+  else
+    hipLaunchKernelGGL((fps_v9_kernel<BLOCK, PPT, G, false>), dim3(B), dim3(BLOCK), 0, s, xyz,
+                       N, M, idx, nx);
+}
+
+template <int BLOCK, int PPT>
+void launch_v2(const float* xyz, int B, int N, int M, int32_t* idx, float* nx, hipStream_t s) {
+  if constexpr (3 * BLOCK * PPT * 4 + 256 <= 160 * 1024)
+    hipLaunchKernelGGL((fps_v2_kernel<BLOCK, PPT, true>), dim3(B), dim3(BLOCK), 0, s, xyz, N, M,
+                       idx, nx);
+  else
+    hipLaunchKernelGGL((fps_v2_kernel<BLOCK, PPT, false>), dim3(B), dim3(BLOCK), 0, s, xyz, N,
+                       M, idx, nx);
+}
+
+}  // namespace
+}  // namespace pn2

@@ -66,12 +66,27 @@ def make_inputs(config, cloud_ids, device, seed=1234):
 class Step:
     """One benchmark step, split in two phases so that the dominant kernel (the SA1 sampler)
     can be timed on its own: sampler() runs FPS + gather of the first SA layer, rest() runs
-    everything after it and returns the step's outputs. __call__ runs both."""
+    everything after it and returns the step's outputs. __call__ runs both.
 
-    def __init__(self, inp):
+    The samplers of SA2..SA4 form a serial chain (each samples the previous layer's output)
+    that keeps only B workgroups busy, so with overlap=True (default) rest() runs that chain
+    on the current stream and forks everything that hangs off it onto a side stream:
+    layer i's ball query / grouping / attention and the FP layer that interpolates onto
+    level i-1 start as soon as sampler i has finished (one event per layer) and run
+    concurrently with samplers i+1.. . The side stream joins back before rest() returns, so
+    the caller sees one ordered stream (and hipGraph capture records the fork/join).
+    Intermediates live on self for the life of the step: nothing made on one stream is freed
+    while the other may still read it."""
+
+    def __init__(self, inp, overlap=True):
         self.inp = inp
         self.kind = CONFIGS[inp["config"]][1]
         self.new_xyz1 = None
+        self.overlap = overlap and inp["xyz"].is_cuda
+        if self.overlap:
+            self.side = torch.cuda.Stream(device=inp["xyz"].device)
+            self.ready = [torch.cuda.Event() for _ in range(4)]
+        self.keep = []
 
     def sampler(self):
         npoint = SSG_SA[0][0] if self.kind == "ssg" else MSG_SA[0][0]
@@ -85,48 +100,76 @@ class Step:
         self.sampler()
         return self.rest()
 
+    def _fork(self, layer):
+        """Context for layer `layer`'s dependent work: the side stream after sampler `layer`."""
+        if not self.overlap:
+            return _Same()
+        main = torch.cuda.current_stream(self.inp["xyz"].device)
+        self.ready[layer].record(main)
+        self.side.wait_event(self.ready[layer])
+        return torch.cuda.stream(self.side)
+
+    def _join(self, outs):
+        if self.overlap:
+            main = torch.cuda.current_stream(self.inp["xyz"].device)
+            main.wait_stream(self.side)
+            if not torch.cuda.is_current_stream_capturing():
+                for t in outs:  # made on the side stream, consumed on main from here on
+                    t.record_stream(main)
+        return outs
+
     def _rest_ssg(self):
         inp = self.inp
-        xyz = [inp["xyz"]]
-        points = [inp["feats"]]  # l0_points: None (cfg2) or rgb+normals (cfg3)
-        outs = []
+        xyz = [inp["xyz"], self.new_xyz1]
+        points = [inp["feats"]] + list(inp["sa_out"])  # l0 = None (cfg2) / rgb+normals (cfg3)
+        # FP layer k interpolates level lvl+1 onto lvl (pointnet2_sem_seg_attention.py:46-53);
+        # level lvl+1's features are the SA4 output (k=0) or the previous FP MLP's stand-in.
+        fp_feat = [inp["sa_out"][3]] + list(inp["fp_out"])
+        sa_outs, fp_outs = [None] * 4, [None] * 4
         for i, (npoint, radius, nsample, _) in enumerate(SSG_SA):
-            if i == 0:
-                new_xyz = self.new_xyz1
-            else:
-                _, new_xyz = tf_sampling.farthest_point_sample_and_gather(npoint, xyz[-1])
-            idx, _ = tf_grouping.query_ball_point(radius, nsample, xyz[-1], new_xyz)
-            new_points, _ = pointnet_util.group_concat(xyz[-1], points[-1], new_xyz, idx,
-                                                       want_grouped_xyz=False)
-            outs.append(new_points)
-            if "attn" in inp:  # attention instead of pooling (attention_layer.py:256-261)
-                Q, K, V = inp["attn"][i]
-                outs.append(attention_layer.attention_reduce(Q, K, V))
-            xyz.append(new_xyz)
-            points.append(inp["sa_out"][i])  # stand-in for the SA MLP output (l{i+1}_points)
-        # FP layers (pointnet2_sem_seg_attention.py:46-53)
-        feat = inp["sa_out"][3]  # l4_points
-        for k in range(4):
-            lvl = 3 - k  # interpolate level lvl+1 -> lvl
-            out = pointnet_util.fp_interpolate(xyz[lvl], xyz[lvl + 1], points[lvl], feat)
-            outs.append(out)
-            feat = inp["fp_out"][k] if k < 3 else None  # stand-in for the FP MLP output
-        return outs
+            if i > 0:
+                xyz.append(tf_sampling.farthest_point_sample_and_gather(npoint, xyz[i])[1])
+            with self._fork(i):
+                new_xyz = xyz[i + 1]
+                idx, _ = tf_grouping.query_ball_point(radius, nsample, xyz[i], new_xyz)
+                new_points, _ = pointnet_util.group_concat(xyz[i], points[i], new_xyz, idx,
+                                                           want_grouped_xyz=False)
+                sa_outs[i] = [new_points]
+                if "attn" in inp:  # attention instead of pooling (attention_layer.py:256-261)
+                    Q, K, V = inp["attn"][i]
+                    sa_outs[i].append(attention_layer.attention_reduce(Q, K, V))
+                k = 3 - i  # the FP layer whose coarse level (i+1) just became available
+                fp_outs[k] = pointnet_util.fp_interpolate(xyz[i], xyz[i + 1], points[i],
+                                                          fp_feat[k])
+        self.keep = xyz
+        return self._join([t for o in sa_outs for t in o] + fp_outs)
 
     def _rest_msg(self):
         inp = self.inp
         xyz, points, new_xyz = inp["xyz"], None, self.new_xyz1
         outs = []
+        kept = [new_xyz]
         for i, (npoint, radii, nsamples, _) in enumerate(MSG_SA):
             if i > 0:
                 _, new_xyz = tf_sampling.farthest_point_sample_and_gather(npoint, xyz)
-            for radius, nsample in zip(radii, nsamples):
-                idx, _ = tf_grouping.query_ball_point(radius, nsample, xyz, new_xyz)
-                gp, _ = pointnet_util.group_concat(xyz, points, new_xyz, idx, xyz_last=True,
-                                                   want_grouped_xyz=False)
-                outs.append(gp)
+                kept.append(new_xyz)
+            with self._fork(i):
+                for radius, nsample in zip(radii, nsamples):
+                    idx, _ = tf_grouping.query_ball_point(radius, nsample, xyz, new_xyz)
+                    gp, _ = pointnet_util.group_concat(xyz, points, new_xyz, idx, xyz_last=True,
+                                                       want_grouped_xyz=False)
+                    outs.append(gp)
             xyz, points = new_xyz, inp["sa_out"][0]
-        return outs
+        self.keep = kept
+        return self._join(outs)
+
+
+class _Same:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        return False
 
 
 def run(inp):
@@ -139,9 +182,8 @@ class GraphStep:
     launches both on the current stream. Inputs stay resident, outputs are overwritten in
     place at every replay."""
 
-    def __init__(self, inp, warmup=2):
-        import torch
-        self.step = Step(inp)
+    def __init__(self, inp, warmup=2, overlap=True):
+        self.step = Step(inp, overlap=overlap)
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):

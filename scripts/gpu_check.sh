@@ -28,9 +28,21 @@ fi
 
 if [ "${SKIP_PROF:-0}" != "1" ]; then
   echo "== rocprofv3 kernel trace"
-  timeout -k 10 ${PROF_TIMEOUT:-600} rocprofv3 --kernel-trace --stats -T --output-format csv -d $OUT/prof_$TAG -o run -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline ${BENCH_ARGS:-} > $OUT/prof_$TAG.log 2>&1
+  timeout -k 10 ${PROF_TIMEOUT:-600} rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o run -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline ${BENCH_ARGS:-} > $OUT/prof_$TAG.log 2>&1
   rc=$?; tail -5 $OUT/prof_$TAG.log; echo "rocprof rc=$rc"
   find $OUT/prof_$TAG -name "*stats*" | head
   [ $rc -eq 0 ] || exit $rc
+fi
+if [ "${SKIP_PMC:-0}" != "1" ]; then
+  # HBM traffic counters, one counter per pass (FETCH_SIZE and WRITE_SIZE do not fit one
+  # TCC pass on gfx950), kernel trace only -- never combined with runtime/sys tracing.
+  for C in FETCH_SIZE WRITE_SIZE; do
+    echo "== rocprofv3 --pmc $C"
+    timeout -k 10 ${PROF_TIMEOUT:-600} rocprofv3 --pmc $C --kernel-trace --output-format csv -d $OUT/pmc_${C}_$TAG -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline ${BENCH_ARGS:-} > $OUT/pmc_${C}_$TAG.log 2>&1
+    rc=$?; tail -3 $OUT/pmc_${C}_$TAG.log; echo "pmc $C rc=$rc"
+    [ $rc -eq 0 ] || exit $rc
+  done
+  python3 tools/pmc_summary.py $OUT/pmc_FETCH_SIZE_$TAG $OUT/pmc_WRITE_SIZE_$TAG > $OUT/pmc_traffic_$TAG.json
+  cat $OUT/pmc_traffic_$TAG.json | head -40
 fi
 echo "== done"

@@ -48,6 +48,12 @@ def test_oracle_reproduces_golden(orc, path):
         assert (idx[~hit] == 0).all() and (cnt[~hit] == 0).all()
         # pts_cnt (GPU kernel output, tf_grouping_g.cu:34) = number of distinct leading slots
         assert (cnt[hit] >= 1).all() and (cnt <= meta["nsample"]).all()
+    elif op == "query_ball_point_gpu":
+        idx, cnt = orc.ball_query(d["xyz1"], d["xyz2"], meta["radius"], meta["nsample"])
+        hit = d["pts_cnt"] > 0
+        assert np.array_equal(cnt, d["pts_cnt"])
+        assert np.array_equal(idx[hit], d["idx"][hit])
+        assert (idx[~hit] == 0).all() and (d["idx"][~hit] == -1).all()
     elif op == "group_point(+grad)":
         assert np.array_equal(orc.ball_query(d["xyz1"], d["xyz2"], 0.3, 32)[0], d["idx"])
         assert np.array_equal(_bits(orc.group_point(d["points"], d["idx"])), _bits(d["out"]))

@@ -4,7 +4,7 @@ import ctypes, importlib, os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np, torch
 pkg = importlib.import_module("pointcloud-segmentation-attention_amd")
-L = pkg.lib()
+L = ctypes.CDLL(os.path.join(os.path.dirname(os.path.abspath(__file__)), "fps_lab", "libpn2fpslab.so"))
 L.pn2_fps_stamp.restype = ctypes.c_int
 L.pn2_fps_stamp.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
 dev = torch.device("cuda:0")

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Sweep the FPS launch table on the GPU: every (variant, block, points-per-thread) of
-pn2_fps_tune for the SA layer sizes, interleaved rounds in ONE process (methodology rule 24),
+pn2_fps_tune (tools/fps_lab/libpn2fpslab.so: v2 and v9 with G = 1/2/4) for the SA layer sizes, interleaved rounds in ONE process (methodology rule 24),
 each result checked index-exact against the production entry point. Prints one JSON line per
 (N, config) with the median and min kernel time (HIP events, B clouds per launch)."""
 import ctypes
@@ -16,10 +16,25 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
+LAB_SO = os.path.join(ROOT, "tools", "fps_lab", "libpn2fpslab.so")
+V2 = [(64, 1), (64, 2), (64, 4), (64, 8), (64, 16), (128, 4), (128, 8), (128, 16), (256, 1),
+      (256, 2), (256, 4), (256, 8), (256, 16), (512, 2), (512, 4), (512, 8), (512, 16),
+      (1024, 1), (1024, 2), (1024, 4), (1024, 8), (1024, 16)]
+V9 = [(bl, pp, g) for bl, pp in [(64, 4), (64, 8), (128, 4), (128, 8), (256, 4), (256, 8),
+                                 (256, 16), (512, 4), (512, 8), (512, 16), (256, 32)]
+      for g in (1, 2, 4)] + [(64, 1, 1), (64, 2, 1), (64, 2, 2), (128, 2, 2), (256, 2, 2)]
+
+
+def candidates(N, slack):
+    c = [(2, bl, pp) for bl, pp in V2 if N <= bl * pp <= max(slack * N, 64)]
+    c += [(90 + g, bl, pp) for bl, pp, g in V9 if N <= bl * pp <= max(slack * N, 64)]
+    return c
+
+
 def main():
-    import torch
+    import torch  # first: the lab .so then shares torch's HIP runtime
     pkg = importlib.import_module("pointcloud-segmentation-attention_amd")
-    L = pkg.lib()
+    L = ctypes.CDLL(LAB_SO)
     L.pn2_fps_tune.restype = ctypes.c_int
     L.pn2_fps_tune.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
@@ -27,26 +42,12 @@ def main():
     dev = torch.device("cuda:0")
     B = int(os.environ.get("TUNE_B", "16"))
     rounds = int(os.environ.get("TUNE_ROUNDS", "5"))
-    sizes = [(64, 16), (256, 64), (1024, 256), (4096, 512), (8192, 1024), (16384, 512)]
-    cfgs = [(64, 1), (64, 2), (64, 4), (64, 8), (64, 16), (128, 4), (128, 8), (128, 16), (256, 1),
-            (256, 2), (256, 4), (256, 8), (256, 16), (512, 2), (512, 4), (512, 8), (512, 16),
-            (1024, 1), (1024, 2), (1024, 4), (1024, 8), (1024, 16)]
+    sizes = [(64, 16), (256, 64), (512, 128), (1024, 256), (4096, 512), (8192, 1024)]
     stream = torch.cuda.current_stream().cuda_stream
-    CULL = [(256, 4, 1), (256, 4, 2), (256, 4, 4), (512, 8, 2), (512, 8, 4), (512, 16, 2),
-            (512, 16, 4), (512, 16, 8), (1024, 8, 2), (1024, 8, 4), (256, 32, 4), (256, 32, 8),
-            (1024, 16, 4), (1024, 16, 8)]
-    CULL5 = CULL + [(64, 16, 4), (128, 8, 4), (128, 16, 4), (256, 16, 4), (256, 8, 4),
-                    (1024, 4, 4)]
-    CULL6 = [(256, 4, 1), (256, 4, 2), (256, 4, 4), (512, 8, 2), (512, 8, 4), (512, 16, 2),
-             (512, 16, 4), (512, 16, 8), (1024, 8, 2), (1024, 8, 4), (256, 32, 4), (256, 32, 8),
-             (1024, 16, 4), (1024, 16, 8), (128, 8, 2), (128, 8, 4), (256, 8, 2), (256, 16, 4),
-             (64, 16, 4), (512, 32, 8), (256, 32, 16)]
-    V8 = [(256, 4), (256, 8), (512, 8), (512, 16), (1024, 8), (1024, 16), (256, 16), (256, 32),
-          (512, 32), (1024, 4), (128, 8), (128, 16), (64, 16), (512, 4)]
-    # exactness of every config on tie-heavy inputs first (grid lattice, duplicates, uniform)
+    # exactness of every candidate on tie-heavy inputs first (grid lattice, duplicates, uniform)
     rng = np.random.default_rng(0)
     g = np.stack(np.meshgrid(*[np.arange(16)] * 3, indexing="ij"), -1).reshape(-1, 3)
-    for N, M in sizes:
+    for N, M in sizes + [(100, 37), (700, 200), (3000, 300)]:
         tests = [np.stack([g[rng.integers(0, len(g), N)] for _ in range(4)]).astype(np.float32),
                  pkg.synth.batch(range(4), N, "uniform")[0],
                  np.repeat(pkg.synth.batch(range(4), N // 3 + 1, "scannet")[0], 3, axis=1)[:, :N]]
@@ -55,19 +56,19 @@ def main():
             xt = torch.from_numpy(x).to(dev)
             ref = pkg.tf_sampling.farthest_point_sample(M, xt)
             out = torch.empty((4, M), dtype=torch.int32, device=dev)
-            checks = [(8, bl, pp) for bl, pp in V8 if N <= bl * pp <= 4 * max(N, 64)]
-            for v, bl, pp in checks:
+            for v, bl, pp in candidates(N, 4):
+                if v == 2:
+                    continue
                 assert L.pn2_fps_tune(xt.data_ptr(), 4, N, M, out.data_ptr(), None, v, bl, pp,
                                       stream) == 0, (v, bl, pp)
                 torch.cuda.synchronize()
                 assert torch.equal(out, ref), f"variant {(v, bl, pp)} differs at N={N}"
-    print(json.dumps({"exactness": "all culled configs index-exact on grid/uniform/dup inputs"}),
+    print(json.dumps({"exactness": "all v9 configs index-exact on grid/uniform/dup inputs"}),
           flush=True)
     for N, M in sizes:
         xyz = torch.from_numpy(pkg.synth.batch(range(B), N, "scannet")[0]).to(dev)
         ref = pkg.tf_sampling.farthest_point_sample(M, xyz)
-        cand = [(v, bl, pp) for v in (2,) for bl, pp in cfgs if N <= bl * pp <= max(4 * N, 64)]
-        cand += [(8, bl, pp) for bl, pp in V8 if N <= bl * pp <= max(2 * N, 64)]
+        cand = candidates(N, 2)
         times = {c: [] for c in cand}
         out = torch.empty((B, M), dtype=torch.int32, device=dev)
         nx = torch.empty((B, M, 3), dtype=torch.float32, device=dev)
