@@ -102,8 +102,6 @@ __global__ void gather_point_grad_kernel(const float* __restrict__ out_g,
 
 constexpr int kMaxRegPoints = 1024 * 16;
 
-// @@LAUNCH_V9@@
-
 int fps_impl(const float* xyz, int B, int N, int M, int32_t* idx, float* nx, void* ws,
              size_t ws_bytes, hipStream_t s) {
   if (B < 0 || N < 0 || M <= 0 || (B > 0 && (!xyz || !idx))) return PN2_EINVAL;
@@ -114,15 +112,16 @@ int fps_impl(const float* xyz, int B, int N, int M, int32_t* idx, float* nx, voi
                        nx);
     PN2_RETURN_LAUNCH();
   }
-  // launch table measured on MI355X (tools/tune_fps.py, B = 16 ScanNet crops)
-  if (N <= 64) launch_v2<64, 1>(xyz, B, N, M, idx, nx, s);
-  else if (N <= 128) launch_v2<64, 2>(xyz, B, N, M, idx, nx, s);
-  else if (N <= 256) launch_v2<64, 4>(xyz, B, N, M, idx, nx, s);
-  else if (N <= 512) launch_v2<128, 4>(xyz, B, N, M, idx, nx, s);
-  else if (N <= 1024) launch_v2<256, 4>(xyz, B, N, M, idx, nx, s);
-  else if (N <= 2048) launch_v2<256, 8>(xyz, B, N, M, idx, nx, s);
-  else if (N <= 4096) launch_v2<512, 8>(xyz, B, N, M, idx, nx, s);
-  else if (N <= 8192) launch_v2<512, 16>(xyz, B, N, M, idx, nx, s);
+  // launch table measured on MI355X (tools/tune_fps.py, B = 16 ScanNet crops; v9 with
+  // groups of 4 slots wherever BLOCK <= 512 fits, v2 beyond)
+  if (N <= 64) launch_v9<64, 1, 1>(xyz, B, N, M, idx, nx, s);
+  else if (N <= 128) launch_v9<64, 2, 2>(xyz, B, N, M, idx, nx, s);
+  else if (N <= 256) launch_v9<64, 4, 4>(xyz, B, N, M, idx, nx, s);
+  else if (N <= 512) launch_v9<64, 8, 4>(xyz, B, N, M, idx, nx, s);
+  else if (N <= 1024) launch_v9<256, 4, 4>(xyz, B, N, M, idx, nx, s);
+  else if (N <= 2048) launch_v9<256, 8, 4>(xyz, B, N, M, idx, nx, s);
+  else if (N <= 4096) launch_v9<256, 16, 4>(xyz, B, N, M, idx, nx, s);
+  else if (N <= 8192) launch_v9<256, 32, 4>(xyz, B, N, M, idx, nx, s);
   else if (N <= kMaxRegPoints) launch_v2<1024, 16>(xyz, B, N, M, idx, nx, s);
   else {
     if (!ws || ws_bytes < (size_t)B * N * sizeof(float)) return PN2_EINVAL;

@@ -181,10 +181,11 @@ struct Lay9 {
   PN2_DEV static constexpr int point(int t, int s) { return W * (s % H) + R * t + s / H; }
 };
 
-template <int BLOCK, int PPT, int G, bool XYZ_LDS>
+template <int BLOCK, int PPT, int G, bool XYZ_LDS, bool STAMP = false>
 __global__ __launch_bounds__(BLOCK) void fps_v9_kernel(const float* __restrict__ xyz, int N,
                                                        int M, int32_t* __restrict__ idx,
                                                        float* __restrict__ new_xyz) {
+  unsigned long long st_acc[6] = {0, 0, 0, 0, 0, 0}, st_prev = 0;
   using Lay = Lay9<BLOCK, PPT>;
   constexpr int NW = BLOCK / kWave;
   static_assert(BLOCK % kWave == 0 && NW <= 8, "the block step reduces 8 DPP lanes");
@@ -227,6 +228,9 @@ __global__ __launch_bounds__(BLOCK) void fps_v9_kernel(const float* __restrict__
     if (NX) { NX[0] = cx; NX[1] = cy; NX[2] = cz; }
   }
 
+  if constexpr (STAMP) {
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_prev)::"memory");
+  }
   for (int j = 1; j < M; ++j) {
     int bd = -1, bg = 0;
 #pragma unroll
@@ -247,7 +251,9 @@ __global__ __launch_bounds__(BLOCK) void fps_v9_kernel(const float* __restrict__
     }
     // wave: lowest lane holding the wave max, then its first slot holding it
     const uint32_t hi = (uint32_t)(bd + 1);  // 0 for lanes with padding only
+    PN2_STAMP(0)
     const uint32_t km = wave_max_u32(hi);
+    PN2_STAMP(1)
     const uint64_t hold = __builtin_amdgcn_ballot_w64(hi == km);
     const int L = (int)__builtin_amdgcn_readfirstlane((int)__builtin_ctzll(hold));
     const int gq = __builtin_amdgcn_readlane(bg, L);
@@ -264,9 +270,11 @@ __global__ __launch_bounds__(BLOCK) void fps_v9_kernel(const float* __restrict__
       }
     }
     int old = Lay::point(w * kWave + L, sq);
+    PN2_STAMP(2)
     if constexpr (NW > 1) {
       if (lane == 0) red[j & 1][w] = make_uint2(km, (uint32_t)old);
       __syncthreads();
+      PN2_STAMP(3)
       const uint2 r = (lane & 7) < NW ? red[j & 1][lane & 7] : make_uint2(0u, 0u);
       uint32_t bm = max_dpp_u32<kDppXor1>(r.x);
       bm = max_dpp_u32<kDppXor2>(bm);
@@ -275,6 +283,7 @@ __global__ __launch_bounds__(BLOCK) void fps_v9_kernel(const float* __restrict__
       const int wi = (int)__builtin_amdgcn_readfirstlane((int)__builtin_ctzll(wins));
       old = __builtin_amdgcn_readlane((int)r.y, wi);
     }
+    PN2_STAMP(4)
     if constexpr (XYZ_LDS) {
       cx = sxyz[3 * old + 0]; cy = sxyz[3 * old + 1]; cz = sxyz[3 * old + 2];
     } else {
@@ -284,6 +293,11 @@ __global__ __launch_bounds__(BLOCK) void fps_v9_kernel(const float* __restrict__
       I[j] = old;
       if (NX) { NX[3 * j + 0] = cx; NX[3 * j + 1] = cy; NX[3 * j + 2] = cz; }
     }
+    PN2_STAMP(5)
+  }
+  if constexpr (STAMP) {
+    if (lane == 0 && blockIdx.x < 16)
+      for (int ph = 0; ph < 6; ++ph) g_stamp[(blockIdx.x * 16 + w) * 8 + ph] = st_acc[ph];
   }
 }
 

@@ -1191,7 +1191,7 @@ int fps_tune_impl(const float* xyz, int B, int N, int M, int32_t* idx, float* nx
 #define PN2_V9G(BL, PP) PN2_V9(BL, PP, 1) PN2_V9(BL, PP, 2) PN2_V9(BL, PP, 4)
     PN2_V9G(64, 4) PN2_V9G(64, 8) PN2_V9G(128, 4) PN2_V9G(128, 8) PN2_V9G(256, 4)
     PN2_V9G(256, 8) PN2_V9G(256, 16) PN2_V9G(512, 4) PN2_V9G(512, 8) PN2_V9G(512, 16)
-    PN2_V9G(256, 32)
+    PN2_V9G(256, 32) PN2_V9(512, 32, 4) PN2_V9(256, 64, 4) PN2_V9(128, 16, 4) PN2_V9(128, 1, 1)
     PN2_V9(64, 1, 1) PN2_V9(64, 2, 1) PN2_V9(64, 2, 2) PN2_V9(128, 2, 2) PN2_V9(256, 2, 2)
 #undef PN2_V9G
 #undef PN2_V9
@@ -1291,6 +1291,14 @@ int pn2_fps_stamp(const float* xyz, int N, int npoint, int32_t* idx, int block, 
     } else
     PN2_S6(512, 16, 4) PN2_S6(1024, 8, 4) PN2_S6(256, 4, 2) PN2_S6(512, 16, 8) { return PN2_EINVAL; }
 #undef PN2_S6
+  } else if (ppt >= 90000) {  // v9 (G = 4) stamped: ppt = 90000 + PP
+#define PN2_S9(BL, PP)                                                                       \
+    if (block == BL && ppt == 90000 + PP) {                                                  \
+      hipLaunchKernelGGL((pn2::fps_v9_kernel<BL, PP, 4, true, true>), dim3(1), dim3(BL), 0, s, \
+                         xyz, N, npoint, idx, nullptr);                                      \
+    } else
+    PN2_S9(256, 32) PN2_S9(512, 16) PN2_S9(256, 4) PN2_S9(256, 16) { return PN2_EINVAL; }
+#undef PN2_S9
   } else if (ppt >= 20000) {  // v8 stamped: ppt = 20000 + PP
 #define PN2_S8(BL, PP)                                                                       \
     if (block == BL && ppt == 20000 + PP) {                                                  \

@@ -10,8 +10,9 @@ L.pn2_fps_stamp.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.
 dev = torch.device("cuda:0")
 names = ["scan", "wave_reduce", "write+barrier", "xwave_reduce", "centre_load", "idx_store"]
 # v6 rows (block < 0): scan = active-cell scans, wave_reduce = lane max + wave reduce, idx_store also holds the setup
-for N, M, bl, pp in [(256, 64, 64, 4), (1024, 256, 256, 4), (8192, 1024, 512, 16), (8192, 1024, 1024, 8),
-                     (8192, 1024, 1024, 20008), (8192, 1024, 512, 20016), (1024, 256, 256, 20004)]:
+names9 = ["scan", "wave_max", "ballot+resolve", "write+barrier", "xwave", "centre+store"]
+for N, M, bl, pp in [(8192, 1024, 512, 16), (8192, 1024, 256, 90032), (8192, 1024, 512, 90016),
+                     (4096, 512, 256, 90016), (1024, 256, 256, 90004), (1024, 256, 256, 4)]:
     x = torch.from_numpy(pkg.synth.batch([0], N, "scannet")[0]).to(dev)
     idx = torch.empty((1, M), dtype=torch.int32, device=dev)
     buf = np.zeros(16 * 8 + 4096, np.uint64)
@@ -26,5 +27,7 @@ for N, M, bl, pp in [(256, 64, 64, 4), (1024, 256, 256, 4), (8192, 1024, 512, 16
         it = buf[128:128 + M].astype(np.int64)
         d = np.diff(it[1:M])
         print("   per-iteration cycles (wave 0), iterations 1..:", [int(np.median(d[i:i + 64])) for i in range(0, len(d), 64)])
+    nm = names9 if pp >= 90000 else names
     print(f"N={N} M={M} block={bl} ppt={pp}: cycles/iter per phase (mean over {nw} waves):",
-          {n: round(v, 1) for n, v in zip(names, a.mean(0))}, "total", round(a.sum(1).mean(), 1))
+          {n: round(v, 1) for n, v in zip(nm, a.mean(0))}, "total", round(a.sum(1).mean(), 1),
+          flush=True)

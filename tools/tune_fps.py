@@ -22,7 +22,8 @@ V2 = [(64, 1), (64, 2), (64, 4), (64, 8), (64, 16), (128, 4), (128, 8), (128, 16
       (1024, 1), (1024, 2), (1024, 4), (1024, 8), (1024, 16)]
 V9 = [(bl, pp, g) for bl, pp in [(64, 4), (64, 8), (128, 4), (128, 8), (256, 4), (256, 8),
                                  (256, 16), (512, 4), (512, 8), (512, 16), (256, 32)]
-      for g in (1, 2, 4)] + [(64, 1, 1), (64, 2, 1), (64, 2, 2), (128, 2, 2), (256, 2, 2)]
+      for g in (1, 2, 4)] + [(64, 1, 1), (64, 2, 1), (64, 2, 2), (128, 2, 2), (256, 2, 2),
+                             (512, 32, 4), (256, 64, 4), (128, 16, 4), (128, 1, 1)]
 
 
 def candidates(N, slack):
@@ -33,6 +34,8 @@ def candidates(N, slack):
 
 def main():
     import torch  # first: the lab .so then shares torch's HIP runtime
+    from oracle import oracle as O
+    O.set_threads(16)
     pkg = importlib.import_module("pointcloud-segmentation-attention_amd")
     L = ctypes.CDLL(LAB_SO)
     L.pn2_fps_tune.restype = ctypes.c_int
@@ -42,7 +45,8 @@ def main():
     dev = torch.device("cuda:0")
     B = int(os.environ.get("TUNE_B", "16"))
     rounds = int(os.environ.get("TUNE_ROUNDS", "5"))
-    sizes = [(64, 16), (256, 64), (512, 128), (1024, 256), (4096, 512), (8192, 1024)]
+    sizes = [(64, 16), (128, 32), (256, 64), (512, 128), (1024, 256), (2048, 256), (4096, 512),
+             (8192, 1024), (16384, 512)]
     stream = torch.cuda.current_stream().cuda_stream
     # exactness of every candidate on tie-heavy inputs first (grid lattice, duplicates, uniform)
     rng = np.random.default_rng(0)
@@ -54,20 +58,19 @@ def main():
         for x in tests:
             x = np.ascontiguousarray(x)
             xt = torch.from_numpy(x).to(dev)
-            ref = pkg.tf_sampling.farthest_point_sample(M, xt)
+            ref = torch.from_numpy(O.fps(x, M)).to(dev)
             out = torch.empty((4, M), dtype=torch.int32, device=dev)
             for v, bl, pp in candidates(N, 4):
-                if v == 2:
-                    continue
                 assert L.pn2_fps_tune(xt.data_ptr(), 4, N, M, out.data_ptr(), None, v, bl, pp,
                                       stream) == 0, (v, bl, pp)
                 torch.cuda.synchronize()
                 assert torch.equal(out, ref), f"variant {(v, bl, pp)} differs at N={N}"
-    print(json.dumps({"exactness": "all v9 configs index-exact on grid/uniform/dup inputs"}),
+    print(json.dumps({"exactness": "all v2/v9 configs index-exact vs the oracle on grid/uniform/dup inputs"}),
           flush=True)
     for N, M in sizes:
-        xyz = torch.from_numpy(pkg.synth.batch(range(B), N, "scannet")[0]).to(dev)
-        ref = pkg.tf_sampling.farthest_point_sample(M, xyz)
+        x = pkg.synth.batch(range(B), N, "scannet")[0]
+        xyz = torch.from_numpy(x).to(dev)
+        ref = torch.from_numpy(O.fps(x, M)).to(dev)
         cand = candidates(N, 2)
         times = {c: [] for c in cand}
         out = torch.empty((B, M), dtype=torch.int32, device=dev)
