@@ -4,20 +4,12 @@
 // (pointnet2_tensorflow/tf_ops/sampling/tf_sampling.cpp:94-123, tf_sampling_g.cu:105-170) and
 // GatherPoint(+Grad) (tf_sampling.cpp:125-178, tf_sampling_g.cu:172-192).
 //
-// Design (MI355X-first, not a translation of the reference's <<<32,512>>> kernel):
-//  * one workgroup per cloud; the cloud's xyz and the running min-distance live in VGPRs
-//    (PPT points per thread), so the N-point sweep of every iteration touches no memory;
-//  * the per-iteration argmax is ONE u64 max: key = (fp32 bits of d) << 32 | ~tiekey, with
-//    tiekey = (k mod 512) << 20 | (k div 512). Since d >= 0 its bits order like the float,
-//    so the max picks the largest distance and, among equal distances, the smallest
-//    (k mod 512, k div 512) — exactly the winner of the reference's per-thread strict '>'
-//    scan (tf_sampling_g.cu:146) followed by its left-biased tree (tf_sampling_g.cu:158);
-//  * wave reduce in registers (DPP + v_permlane16/32_swap), one LDS slot per wave,
-//    double-buffered by iteration parity so ONE barrier per iteration is race-free (the
-//    reference's single dists_i buffer has a write-after-read race, :151-152 vs :165);
-//  * the winner's coordinates come from an LDS copy of the cloud (uniform-address
-//    broadcast read) when it fits, otherwise from global memory (scalar load);
-//  * thread 0 also writes new_xyz, fusing gather_point into the sampler (pointnet_util.py:34).
+// Design (MI355X-first, not a translation of the reference's <<<32,512>>> kernel): one
+// workgroup per cloud with the cloud's xyz and running min-distance in VGPRs, a register scan
+// per iteration and a ballot/DPP argmax whose lane order IS the reference's tie order — see
+// fps_v9_kernel in fps_kernels.h. gather_point is fused (thread 0 writes new_xyz,
+// pointnet_util.py:34). Clouds beyond kMaxRegPoints keep the running min in a caller-provided
+// workspace (fps_ws_kernel). Measured variants live in tools/fps_lab.
 #include "fps_kernels.h"
 
 namespace pn2 {
@@ -112,8 +104,8 @@ int fps_impl(const float* xyz, int B, int N, int M, int32_t* idx, float* nx, voi
                        nx);
     PN2_RETURN_LAUNCH();
   }
-  // launch table measured on MI355X (tools/tune_fps.py, B = 16 ScanNet crops; v9 with
-  // groups of 4 slots wherever BLOCK <= 512 fits, v2 beyond)
+  // launch table measured on MI355X (tools/tune_fps.py, B = 16 ScanNet crops,
+  // profiles/r1/tune_fps.jsonl)
   if (N <= 64) launch_v9<64, 1, 1>(xyz, B, N, M, idx, nx, s);
   else if (N <= 128) launch_v9<64, 2, 2>(xyz, B, N, M, idx, nx, s);
   else if (N <= 256) launch_v9<64, 4, 4>(xyz, B, N, M, idx, nx, s);
@@ -122,7 +114,7 @@ int fps_impl(const float* xyz, int B, int N, int M, int32_t* idx, float* nx, voi
   else if (N <= 2048) launch_v9<256, 8, 4>(xyz, B, N, M, idx, nx, s);
   else if (N <= 4096) launch_v9<256, 16, 4>(xyz, B, N, M, idx, nx, s);
   else if (N <= 8192) launch_v9<256, 32, 4>(xyz, B, N, M, idx, nx, s);
-  else if (N <= kMaxRegPoints) launch_v2<1024, 16>(xyz, B, N, M, idx, nx, s);
+  else if (N <= kMaxRegPoints) launch_v9<512, 32, 4>(xyz, B, N, M, idx, nx, s);
   else {
     if (!ws || ws_bytes < (size_t)B * N * sizeof(float)) return PN2_EINVAL;
     hipLaunchKernelGGL(fps_ws_kernel, dim3(B), dim3(1024), 0, s, xyz, N, M, (float*)ws, idx, nx);

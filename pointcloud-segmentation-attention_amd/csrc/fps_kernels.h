@@ -39,13 +39,6 @@ PN2_DEV constexpr int slot_off(int i) {
 }
 
 
-// Variant 2 of the register sampler: the same selection, cheaper arithmetic.
-//  * the running min-distance is kept as int32 bit patterns: for d >= 0 (or NaN) and
-//    temp in {-1} U [0, 1e38] a signed-int min of the bits is exactly fminf (no IEEE-mode
-//    canonicalisation before every v_min_f32); padding slots hold -1 and never win;
-//  * the argmax is two 32-bit max-reductions (distance, then ~tiekey among the lanes that hold
-//    the maximum distance) whose DPP moves fold into v_max_u32_dpp, instead of one 64-bit
-//    reduction; the cross-wave step is the same pair over the per-wave results.
 // Diagnostic stamps (STAMP builds only; never in a timed production kernel): s_memtime
 // deltas per phase accumulated in SGPRs, lane 0 of each wave writes them to g_stamp.
 __device__ unsigned long long g_stamp[16 * 16 * 8];
@@ -59,102 +52,6 @@ __device__ unsigned long long g_iter[4096];  // STAMP builds: s_memtime at each 
     st_acc[ph] += tt__ - st_prev;                                                  \
     st_prev = tt__;                                                                \
   }
-
-template <int BLOCK, int PPT, bool XYZ_LDS, bool STAMP = false>
-__global__ __launch_bounds__(BLOCK) void fps_v2_kernel(const float* __restrict__ xyz, int N,
-                                                       int M, int32_t* __restrict__ idx,
-                                                       float* __restrict__ new_xyz) {
-  unsigned long long st_acc[6] = {0, 0, 0, 0, 0, 0}, st_prev = 0;
-  constexpr int NW = BLOCK / kWave;
-  static_assert(NW <= 16, "the cross-wave step reduces one 16-lane DPP row");
-  __shared__ uint2 red[2][16];
-  __shared__ float sxyz[XYZ_LDS ? 3 * BLOCK * PPT : 1];
-
-  const int b = blockIdx.x;
-  const int t = threadIdx.x;
-  const int lane = t & (kWave - 1);
-  const int w = t / kWave;
-  const float* __restrict__ P = xyz + (size_t)b * N * 3;
-  int32_t* __restrict__ I = idx + (size_t)b * M;
-  float* __restrict__ NX = new_xyz ? new_xyz + (size_t)b * M * 3 : nullptr;
-
-  float px[PPT], py[PPT], pz[PPT];
-  int tb[PPT];
-#pragma unroll
-  for (int i = 0; i < PPT; ++i) {
-    const int k = t + slot_off<BLOCK, PPT>(i);
-    if (k < N) {
-      px[i] = P[3 * k + 0];
-      py[i] = P[3 * k + 1];
-      pz[i] = P[3 * k + 2];
-      tb[i] = __float_as_int(kInitTemp);
-    } else {
-      px[i] = py[i] = pz[i] = 0.0f;
-      tb[i] = -1;
-    }
-  }
-  if constexpr (XYZ_LDS) {
-    for (int e = t; e < 3 * N; e += BLOCK) sxyz[e] = P[e];
-    __syncthreads();
-  }
-
-  float cx = P[0], cy = P[1], cz = P[2];
-  if (t == 0) {
-    I[0] = 0;
-    if (NX) { NX[0] = cx; NX[1] = cy; NX[2] = cz; }
-  }
-
-  if constexpr (STAMP) {
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_prev)::"memory");
-  }
-  for (int j = 1; j < M; ++j) {
-    int bd = -1, bi = 0;
-#pragma unroll
-    for (int i = 0; i < PPT; ++i) {
-      const int v = min(__float_as_int(sqdist(px[i], py[i], pz[i], cx, cy, cz)), tb[i]);
-      tb[i] = v;
-      if (v > bd) { bd = v; bi = i; }
-    }
-    int off;
-    if constexpr (BLOCK >= 512 || PPT <= 512 / BLOCK) {
-      off = BLOCK * bi;
-    } else {
-      constexpr int R = 512 / BLOCK, Q = PPT / R;
-      off = BLOCK * ((bi % Q) * R + bi / Q);
-    }
-    const uint32_t hi = bd < 0 ? 0u : (uint32_t)bd + 1u;
-    const uint32_t lo = bd < 0 ? 0u : tie_low(t + off);
-    PN2_STAMP(0)
-    uint32_t km = wave_max_u32(hi);
-    uint32_t kl = wave_max_u32(hi == km ? lo : 0u);
-    PN2_STAMP(1)
-    if constexpr (NW > 1) {
-      if (lane == 0) red[j & 1][w] = make_uint2(km, kl);
-      __syncthreads();
-      PN2_STAMP(2)
-      const uint2 r = lane < NW ? red[j & 1][lane] : make_uint2(0u, 0u);
-      km = row16_max_u32(r.x);
-      kl = row16_max_u32(r.x == km ? r.y : 0u);
-    }
-    const int old = tie_decode(uniform_u32(kl));
-    PN2_STAMP(3)
-    if constexpr (XYZ_LDS) {
-      cx = sxyz[3 * old + 0]; cy = sxyz[3 * old + 1]; cz = sxyz[3 * old + 2];
-    } else {
-      cx = P[3 * old + 0]; cy = P[3 * old + 1]; cz = P[3 * old + 2];
-    }
-    PN2_STAMP(4)
-    if (t == 0) {
-      I[j] = old;
-      if (NX) { NX[3 * j + 0] = cx; NX[3 * j + 1] = cy; NX[3 * j + 2] = cz; }
-    }
-    PN2_STAMP(5)
-  }
-  if constexpr (STAMP) {
-    if (lane == 0 && blockIdx.x < 16)
-      for (int ph = 0; ph < 6; ++ph) g_stamp[(blockIdx.x * 16 + w) * 8 + ph] = st_acc[ph];
-  }
-}
 
 // Variant 9 (BLOCK <= 512): v2's register sampler with a cheaper scan and a shorter tail.
 //  * point layout: thread t owns residues R*t .. R*t+R-1 of each 512-wide row (R = 512/BLOCK,
@@ -311,15 +208,6 @@ void launch_v9(const float* xyz, int B, int N, int M, int32_t* idx, float* nx, h
                        N, M, idx, nx);
 }
 
-template <int BLOCK, int PPT>
-void launch_v2(const float* xyz, int B, int N, int M, int32_t* idx, float* nx, hipStream_t s) {
-  if constexpr (3 * BLOCK * PPT * 4 + 256 <= 160 * 1024)
-    hipLaunchKernelGGL((fps_v2_kernel<BLOCK, PPT, true>), dim3(B), dim3(BLOCK), 0, s, xyz, N, M,
-                       idx, nx);
-  else
-    hipLaunchKernelGGL((fps_v2_kernel<BLOCK, PPT, false>), dim3(B), dim3(BLOCK), 0, s, xyz, N,
-                       M, idx, nx);
-}
 
 }  // namespace
 }  // namespace pn2
