@@ -8,16 +8,19 @@
  *   FarthestPointSample  tf_sampling.cpp:94-123, .cu:105-170     → pn2_fps
  *   GatherPoint          tf_sampling.cpp:125-148, .cu:172-181    → pn2_gather_point
  *   GatherPointGrad      tf_sampling.cpp:150-178, .cu:183-192    → pn2_gather_point_grad
- *   QueryBallPoint       tf_grouping.cpp:66-106, _g.cu:3-36      → pn2_ball_query
+ *   QueryBallPoint       tf_grouping.cpp:66-106, _g.cu:3-36      → pn2_ball_query,
+ *                                                                  pn2_ball_query_grid
  *   GroupPoint           tf_grouping.cpp:139-171, _g.cu:40-57    → pn2_group_point
  *   GroupPointGrad       tf_grouping.cpp:174-208, _g.cu:61-78    → pn2_group_point_grad
- *   ThreeNN              tf_interpolate.cpp:157-187, :60-103     → pn2_three_nn
+ *   ThreeNN              tf_interpolate.cpp:157-187, :60-103     → pn2_three_nn,
+ *                                                                  pn2_three_nn_grid
  *   ThreeInterpolate     tf_interpolate.cpp:191-222, :107-127    → pn2_three_interpolate
  *   ThreeInterpolateGrad tf_interpolate.cpp:225-262, :131-153    → pn2_three_interpolate_grad
  *   IDW weights          pointnet_util.py:219-222                → pn2_idw_weights
  *   sample_and_group     pointnet_util.py:16-58 (SSG), :180-191  → pn2_sample_and_group,
  *                                                                  pn2_group_concat
- *   pointnet_fp_module   pointnet_util.py:218-226 (geometry)     → pn2_fp_fused
+ *   pointnet_fp_module   pointnet_util.py:218-226 (geometry)     → pn2_fp_fused,
+ *                                                                  pn2_fp_apply
  *   AttentionLayer.call  attention_layer.py:29-45 (reduction)    → pn2_attn_reduce
  *   SA pooling           pointnet_util.py:130-145, :200          → pn2_group_pool
  *
@@ -98,6 +101,18 @@ int pn2_ball_query(const float* xyz1, const float* xyz2, int B, int N, int M, fl
 /* The float T with  d2 < T  <=>  max(sqrtf(d2),1e-20f) < radius  for every fp32 d2 >= 0.
  * Host function (pure, no GPU). */
 float pn2_ball_threshold(float radius);
+/* ---- spatial grid (grid.h): the same results as the scans, faster on large clouds ----- *
+ * pn2_grid_build: per cloud, bbox + counting sort of xyz (B,N,3) into cells of edge
+ *   `cell_edge` (<= 0: ~2 points per cell of the bbox), grown until at most 32768 cells, into
+ *   `grid` = caller-owned device memory of pn2_grid_size(B, N) bytes, 16-byte aligned.
+ * pn2_ball_query_grid: pn2_ball_query over a grid built on xyz1 (cell_edge = radius is the
+ *   fast choice; any radius > 0 is exact). N <= 131072.
+ * pn2_three_nn_grid (interpolation section): three_nn over a grid built on the known points. */
+size_t pn2_grid_size(int B, int N);
+int pn2_grid_build(const float* xyz, int B, int N, float cell_edge, void* grid,
+                   size_t grid_bytes, pn2_stream_t stream);
+int pn2_ball_query_grid(const void* grid, const float* xyz2, int B, int N, int M, float radius,
+                        int nsample, int32_t* idx, int32_t* pts_cnt, pn2_stream_t stream);
 
 /* out (B,M,nsample,C) = points[b, idx[b,j,k], :] (tf_grouping_g.cu:40-57). */
 int pn2_group_point(const float* points, const int32_t* idx, int B, int N, int C, int M,
@@ -148,6 +163,18 @@ int pn2_idw_weights(const float* dist, int B, int n, float* weight, pn2_stream_t
 int pn2_fp_fused(const float* xyz1, const float* xyz2, const float* points1, int C1,
                  const float* points2, int C2, int B, int n, int m, float* out,
                  pn2_stream_t stream);
+
+/* three_nn over pn2_grid_build(xyz2 = the m known points): the same dist/idx as
+ * pn2_three_nn. `unknown_grid` (optional, a grid over the n unknown points xyz1) only orders
+ * the work so that neighbouring lanes share cells; with it xyz1 may be NULL. */
+int pn2_three_nn_grid(const void* known_grid, const void* unknown_grid, const float* xyz1,
+                      int B, int n, int m, float* dist, int32_t* idx, pn2_stream_t stream);
+/* pn2_fp_fused from a previous three_nn: IDW weights of dist (B,n,3), interpolation of
+ * points2 (B,m,C2) with idx (B,n,3), concat [interp, points1 (B,n,C1)]. `unknown_grid`
+ * (optional, a grid over the n unknown points) only orders the rows for cache reuse. */
+int pn2_fp_apply(const float* dist, const int32_t* idx, const void* unknown_grid,
+                 const float* points1, int C1, const float* points2, int C2, int B, int n, int m,
+                 float* out, pn2_stream_t stream);
 
 /* ---------------------------------------------------------------- attention / pooling --- */
 

@@ -12,9 +12,9 @@ Everything runs the gfx950 kernels of libpn2hip.so (C ABI: include/pn2hip.h).
 The directory name has hyphens, so import it with importlib:
     pn2 = importlib.import_module("pointcloud-segmentation-attention_amd")
 """
-from . import attention_layer, pointnet_util, shard, stack, synth, tf_grouping, \
+from . import attention_layer, grid, pointnet_util, shard, stack, synth, tf_grouping, \
     tf_interpolate, tf_sampling
 from ._lib import LIB_PATH, InvalidArgumentError, Pn2RuntimeError, lib
 
-__all__ = ["tf_sampling", "tf_grouping", "tf_interpolate", "pointnet_util", "attention_layer",
+__all__ = ["tf_sampling", "tf_grouping", "tf_interpolate", "pointnet_util", "attention_layer", "grid",
            "synth", "stack", "shard", "lib", "LIB_PATH", "InvalidArgumentError", "Pn2RuntimeError"]

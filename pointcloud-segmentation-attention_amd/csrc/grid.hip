@@ -1,0 +1,283 @@
+// Ball query over a uniform spatial grid, for gfx950.
+//
+// Same results as the brute-force scan of ball_query.hip and of the reference
+// (query_ball_point_gpu, tf_grouping_g.cu:3-36): the FIRST nsample points in index order with
+// max(sqrtf(d2), 1e-20f) < radius (tested as d2 < T, see pn2_ball_threshold), slots after the
+// last hit repeat the first hit, pts_cnt = hits capped at nsample, 0-filled rows without hits.
+//
+// Why: at SA1 (8192 points, r = 0.1) almost every query has fewer than nsample hits, so the
+// in-order scan with early exit degenerates into 8192 distance tests per query. Here a query
+// tests only the points of the cells its ball overlaps, marks hits in a per-wave bitmask over
+// point INDICES in LDS, and reads the first nsample set bits back in index order — the
+// reference's order, whatever order the cells were visited in.
+//
+// Exactness: every point with d2 < T lies in the scanned cell range. A hit has |p - q| per
+// axis <= r (1 + 3 eps); the range is computed from q -/+ (r + margin) with a margin of 1e-5
+// relative to max(r, |q|, 1), far above fp32 rounding, and the cell of a coordinate,
+// clamp(floor((v - o) * inv)), is a monotone function of v — the same function for points and
+// for the range ends. The hit test itself is the brute-force expression.
+//
+// Grid layout: grid.h. pn2_grid_build sorts each cloud into cells in one workgroup (LDS
+// counting sort); the cell edge is the caller's (the radius, for a ball query) or, when <= 0,
+// chosen for ~2 points per cell of the bounding box; it grows until the cells fit kGridCap.
+#include <math.h>
+
+#include "grid.h"
+
+namespace pn2 {
+namespace {
+
+constexpr int kBuildBlock = 1024;
+constexpr int kMaxBitWords = 4096;  // bitmask words per wave (N <= 131072)
+constexpr float kAutoPointsPerCell = 2.0f;
+
+PN2_DEV float wave_min_f(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, kWave));
+  return v;
+}
+PN2_DEV float wave_max_f(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, kWave));
+  return v;
+}
+PN2_DEV int wave_incl_scan(int v, int lane) {
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const int u = __shfl_up(v, o, kWave);
+    if (lane >= o) v += u;
+  }
+  return v;
+}
+
+__global__ __launch_bounds__(kBuildBlock) void grid_build_kernel(const float* __restrict__ xyz,
+                                                                 int N, float edge,
+                                                                 char* __restrict__ grid) {
+  constexpr int NW = kBuildBlock / kWave;
+  __shared__ uint32_t cnt[kGridCap];
+  __shared__ float red[6][NW];
+  __shared__ int wsum[NW];
+  __shared__ GridHdr sh;
+  const int b = blockIdx.x, t = threadIdx.x, lane = t & (kWave - 1), w = t / kWave;
+  const float* __restrict__ P = xyz + (size_t)b * N * 3;
+  char* G = grid + (size_t)b * grid_stride(N);
+  int* __restrict__ off = (int*)(G + sizeof(GridHdr));
+  float4* __restrict__ pts = (float4*)(G + kGridOffBytes);
+
+  // 1. bounding box
+  float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+  for (int k = t; k < N; k += kBuildBlock) {
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      const float v = P[3 * k + a];
+      mn[a] = fminf(mn[a], v);
+      mx[a] = fmaxf(mx[a], v);
+    }
+  }
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    mn[a] = wave_min_f(mn[a]);
+    mx[a] = wave_max_f(mx[a]);
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int a = 0; a < 3; ++a) { red[a][w] = mn[a]; red[3 + a][w] = mx[a]; }
+  }
+  __syncthreads();
+  if (t == 0) {
+    float lo[3], hi[3];
+    for (int a = 0; a < 3; ++a) {
+      lo[a] = red[a][0];
+      hi[a] = red[3 + a][0];
+      for (int i = 1; i < NW; ++i) { lo[a] = fminf(lo[a], red[a][i]); hi[a] = fmaxf(hi[a], red[3 + a][i]); }
+      if (!(hi[a] >= lo[a])) { lo[a] = 0.0f; hi[a] = 0.0f; }  // N == 0 or NaN-only axis
+    }
+    // cell edge: the caller's, or ~kAutoPointsPerCell points per cell of the bbox volume
+    // (then also at most max(N, 64) cells, which bounds the grid's size for LDS staging);
+    // grown by 1.25x until the cells fit kGridCap;
+    // degenerate extents (inf / NaN coordinates) fall back to one cell (inv = 0)
+    float c = edge;
+    if (!(c > 0.0f)) {
+      const float ext = fmaxf(fmaxf(hi[0] - lo[0], hi[1] - lo[1]), hi[2] - lo[2]);
+      const double cells = fmax((double)N / kAutoPointsPerCell, 1.0);
+      double e = cbrt((double)(hi[0] - lo[0]) * (hi[1] - lo[1]) * (hi[2] - lo[2]) / cells);
+      if (!(e > 0.0)) e = (double)ext / cbrt(cells);
+      c = (float)e;
+      if (!(c > 0.0f)) c = 1.0f;  // all points identical: any edge gives one cell
+    }
+    int n[3] = {1, 1, 1};
+    bool ok = false;
+    for (int it = 0; it < 400 && !ok; ++it) {
+      double cells = 1.0, d[3];
+      for (int a = 0; a < 3; ++a) {
+        d[a] = floor((double)(hi[a] - lo[a]) / (double)c) + 1.0;
+        cells *= d[a];
+      }
+      if (cells <= (double)kGridCap && (edge > 0.0f || cells <= fmax((double)N, (double)kAutoMinCells))) {
+        for (int a = 0; a < 3; ++a) n[a] = (int)d[a];
+        ok = true;
+      } else {
+        c *= 1.25f;
+      }
+    }
+    if (!ok) { n[0] = n[1] = n[2] = 1; c = INFINITY; }
+    sh.ox = lo[0]; sh.oy = lo[1]; sh.oz = lo[2];
+    sh.inv = ok ? 1.0f / c : 0.0f;
+    sh.nx = n[0]; sh.ny = n[1]; sh.nz = n[2];
+    sh.ncell = n[0] * n[1] * n[2];
+    *(GridHdr*)G = sh;
+  }
+  __syncthreads();
+  const GridHdr h = sh;
+  for (int i = t; i < h.ncell; i += kBuildBlock) cnt[i] = 0;
+  __syncthreads();
+
+  // 2. count points per cell
+  auto cell_of = [&](int k) {
+    const int ix = cell_coord(P[3 * k + 0], h.ox, h.inv, h.nx);
+    const int iy = cell_coord(P[3 * k + 1], h.oy, h.inv, h.ny);
+    const int iz = cell_coord(P[3 * k + 2], h.oz, h.inv, h.nz);
+    return (iz * h.ny + iy) * h.nx + ix;
+  };
+  for (int k = t; k < N; k += kBuildBlock) atomicAdd(&cnt[cell_of(k)], 1u);
+  __syncthreads();
+
+  // 3. exclusive scan of the counts (contiguous chunk per thread) -> offsets and cursors
+  const int per = (h.ncell + kBuildBlock - 1) / kBuildBlock;
+  const int s0 = t * per, s1 = min(s0 + per, h.ncell);
+  int sum = 0;
+  for (int i = s0; i < s1; ++i) sum += (int)cnt[i];
+  const int incl = wave_incl_scan(sum, lane);
+  if (lane == kWave - 1) wsum[w] = incl;
+  __syncthreads();
+  int base = incl - sum;
+  for (int i = 0; i < w; ++i) base += wsum[i];
+  for (int i = s0; i < s1; ++i) {
+    const int c = (int)cnt[i];
+    cnt[i] = (uint32_t)base;
+    off[i] = base;
+    base += c;
+  }
+  if (t == 0) off[h.ncell] = N;
+  __syncthreads();
+
+  // 4. scatter the points, sorted by cell (order inside a cell does not matter)
+  for (int k = t; k < N; k += kBuildBlock) {
+    const int pos = (int)atomicAdd(&cnt[cell_of(k)], 1u);
+    pts[pos] = make_float4(P[3 * k + 0], P[3 * k + 1], P[3 * k + 2], __int_as_float(k));
+  }
+}
+
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void ball_query_grid_kernel(
+    const char* __restrict__ grid, const float* __restrict__ xyz2, int N, int M, float radius,
+    float thresh, int ns, int qpb, int words, int32_t* __restrict__ idx,
+    int32_t* __restrict__ pts_cnt) {
+  constexpr int NW = BLOCK / kWave;
+  extern __shared__ uint32_t bits[];  // NW x words
+  const int b = blockIdx.y;
+  const int t = threadIdx.x, lane = t & (kWave - 1), w = t / kWave;
+  const GridView g = grid_view(grid, b, N);
+  const GridHdr& h = g.h;
+  const int* __restrict__ off = g.off;
+  const float4* __restrict__ pts = g.pts;
+  uint32_t* mine = bits + (size_t)w * words;
+  const int wpl = (words + kWave - 1) / kWave;  // bitmask words per lane, in lane order
+
+  const int q_end = min(M, (int)(blockIdx.x + 1) * qpb);
+  for (int q = blockIdx.x * qpb + w; q < q_end; q += NW) {
+    for (int i = lane; i < words; i += kWave) mine[i] = 0u;
+    const float* Q = xyz2 + ((size_t)b * M + q) * 3;
+    const float qx = Q[0], qy = Q[1], qz = Q[2];
+    const float big = fmaxf(fmaxf(fmaxf(fabsf(qx), fabsf(qy)), fmaxf(fabsf(qz), radius)), 1.0f);
+    const float rr = radius + big * 1e-5f;
+    const int x0 = cell_coord(qx - rr, h.ox, h.inv, h.nx), x1 = cell_coord(qx + rr, h.ox, h.inv, h.nx);
+    const int y0 = cell_coord(qy - rr, h.oy, h.inv, h.ny), y1 = cell_coord(qy + rr, h.oy, h.inv, h.ny);
+    const int z0 = cell_coord(qz - rr, h.oz, h.inv, h.nz), z1 = cell_coord(qz + rr, h.oz, h.inv, h.nz);
+    for (int z = z0; z <= z1; ++z) {
+      for (int y = y0; y <= y1; ++y) {
+        const int row = (z * h.ny + y) * h.nx;
+        const int e = off[row + x1 + 1];  // cells x0..x1 of a row are contiguous
+        for (int i = off[row + x0] + lane; i < e; i += kWave) {
+          const float4 p = pts[i];
+          if (sqdist(qx, qy, qz, p.x, p.y, p.z) < thresh) {  // tf_grouping_g.cu:24-25
+            const int k = __float_as_int(p.w);
+            atomicOr(&mine[k >> 5], 1u << (k & 31));
+          }
+        }
+      }
+    }
+    // hits in index order: lane l owns bitmask words [l*wpl, (l+1)*wpl)
+    int pop = 0, myfirst = -1;
+    for (int j = 0; j < wpl; ++j) {
+      const int wi = lane * wpl + j;
+      if (wi < words) {
+        const uint32_t v = mine[wi];
+        if (myfirst < 0 && v) myfirst = 32 * wi + __builtin_ctz(v);
+        pop += __popc(v);
+      }
+    }
+    const int incl = wave_incl_scan(pop, lane);
+    const int total = __shfl(incl, kWave - 1, kWave);
+    const int cnt = min(total, ns);
+    int32_t* __restrict__ row = idx + ((size_t)b * M + q) * ns;
+    int rank = incl - pop;
+    for (int j = 0; j < wpl && rank < ns; ++j) {
+      const int wi = lane * wpl + j;
+      uint32_t v = wi < words ? mine[wi] : 0u;
+      while (v && rank < ns) {
+        row[rank++] = 32 * wi + __builtin_ctz(v);
+        v &= v - 1u;
+      }
+    }
+    const uint64_t has = __ballot(pop > 0);
+    const int first = has ? __shfl(myfirst, __ffsll((unsigned long long)has) - 1, kWave) : 0;
+    for (int p = cnt + lane; p < ns; p += kWave) row[p] = first;  // :26-29 (0 when no hit)
+    if (lane == 0) pts_cnt[(size_t)b * M + q] = cnt;
+  }
+}
+
+}  // namespace
+}  // namespace pn2
+
+extern "C" {
+
+float pn2_ball_threshold(float radius);
+
+size_t pn2_grid_size(int B, int N) {
+  if (B <= 0 || N < 0) return 0;
+  return (size_t)B * pn2::grid_stride(N);
+}
+
+int pn2_grid_build(const float* xyz, int B, int N, float cell_edge, void* grid,
+                   size_t grid_bytes, pn2_stream_t stream) {
+  if (B < 0 || N < 0 || cell_edge != cell_edge) return PN2_EINVAL;
+  if (B == 0) return PN2_OK;
+  if (!grid || grid_bytes < pn2_grid_size(B, N) || (N > 0 && !xyz)) return PN2_EINVAL;
+  if ((uintptr_t)grid % 16 || B > 65535) return PN2_EINVAL;
+  hipLaunchKernelGGL(pn2::grid_build_kernel, dim3(B), dim3(pn2::kBuildBlock), 0,
+                     (hipStream_t)stream, xyz, N, cell_edge, (char*)grid);
+  PN2_RETURN_LAUNCH();
+}
+
+int pn2_ball_query_grid(const void* grid, const float* xyz2, int B, int N, int M, float radius,
+                        int nsample, int32_t* idx, int32_t* pts_cnt, pn2_stream_t stream) {
+  if (!(radius > 0.0f) || nsample <= 0 || B < 0 || N < 0 || M < 0) return PN2_EINVAL;
+  if ((long long)B * M == 0) return PN2_OK;
+  if (!grid || !xyz2 || !idx || !pts_cnt || B > 65535) return PN2_EINVAL;
+  const int words = (N + 31) / 32;
+  if (words > pn2::kMaxBitWords) return PN2_EINVAL;
+  constexpr int BLOCK = 256, NW = BLOCK / pn2::kWave;
+  // ~2048 workgroups over the batch, a whole number of queries per wave
+  const long long queries = (long long)B * M;
+  long long qpb = (queries + 2047) / 2048;
+  qpb = ((qpb + NW - 1) / NW) * NW;
+  const unsigned gx = (unsigned)((M + qpb - 1) / qpb);
+  const size_t lds = (size_t)NW * (words > 0 ? words : 1) * 4;
+  hipLaunchKernelGGL((pn2::ball_query_grid_kernel<BLOCK>), dim3(gx, B), dim3(BLOCK), lds,
+                     (hipStream_t)stream, (const char*)grid, xyz2, N, M, radius,
+                     pn2_ball_threshold(radius), nsample, (int)qpb, words, idx, pts_cnt);
+  PN2_RETURN_LAUNCH();
+}
+
+}  // extern "C"

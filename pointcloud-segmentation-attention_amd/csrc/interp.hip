@@ -22,9 +22,10 @@
 // triple in LDS and writes the [interp, points1] rows; for short layers (FP1-FP3) the channel
 // range is split over extra workgroups (grid.z) so that the chip is full, and the copy is
 // float4-vectorised when the channel counts allow.
+#include <algorithm>
 #include <type_traits>
 
-#include "common.h"
+#include "grid.h"
 
 namespace pn2 {
 namespace {
@@ -133,6 +134,98 @@ __global__ __launch_bounds__(kNNBlock) void three_nn_kernel(const float* __restr
   }
 }
 
+// three_nn over a spatial grid of the KNOWN points (grid.h): the same (d, k)-lexicographic
+// top 3 as the scan, visiting cells in cubic shells of Chebyshev radius s around the unknown
+// point's cell until the third-best distance is below the squared gap to every unvisited cell
+// (with a relative and an absolute slack far above fp32 rounding), or the shells cover the
+// grid. Cells hold points in arbitrary order, which the lexicographic insert makes
+// irrelevant. One lane per unknown point; when `ugrid` (a grid over the UNKNOWN points) is
+// given, lane i takes the i-th unknown in cell order, so the lanes of a wave share cells.
+// LDS: the known grid (sorted points + offsets) is staged once per workgroup when it fits.
+template <int BLOCK, bool LDS>
+__global__ __launch_bounds__(BLOCK) void three_nn_grid_kernel(
+    const void* __restrict__ kgrid, int m, const void* __restrict__ ugrid,
+    const float* __restrict__ xyz1, int n, float* __restrict__ dist, int32_t* __restrict__ idx) {
+  extern __shared__ float4 s_pts[];  // LDS: m sorted known points, then ncell+1 offsets
+  const int b = blockIdx.y;
+  const int i = blockIdx.x * BLOCK + threadIdx.x;
+  const GridView g = grid_view(kgrid, b, m);
+  const GridHdr& h = g.h;
+  const float4* __restrict__ pts = g.pts;
+  const int* __restrict__ off = g.off;
+  // the whole known grid of this cloud, once per workgroup, when its cell count is within
+  // what the launch sized the LDS for (automatic-edge grids always are)
+  if (LDS && h.ncell <= max(m, kAutoMinCells)) {
+    int* s_off = (int*)(s_pts + m);
+    for (int e = threadIdx.x; e < m; e += BLOCK) s_pts[e] = g.pts[e];
+    for (int e = threadIdx.x; e <= h.ncell; e += BLOCK) s_off[e] = g.off[e];
+    __syncthreads();
+    pts = s_pts;
+    off = s_off;
+  }
+  if (i >= n) return;  // no barriers below
+  float px, py, pz;
+  int u;
+  if (ugrid) {
+    const float4 U = grid_view(ugrid, b, n).pts[i];
+    px = U.x; py = U.y; pz = U.z;
+    u = __float_as_int(U.w);
+  } else {
+    const float* U = xyz1 + ((size_t)b * n + i) * 3;
+    px = U[0]; py = U[1]; pz = U[2];
+    u = i;
+  }
+  Best3 best;
+  best3_init(best);
+  auto visit = [&](int lo, int hi) {  // sorted points [lo, hi)
+    for (int e = lo; e < hi; ++e) {
+      const float4 q = pts[e];
+      best3_insert_lex(best, sqdist(q.x, q.y, q.z, px, py, pz), __float_as_int(q.w));
+    }
+  };
+  const int cx = cell_coord(px, h.ox, h.inv, h.nx);
+  const int cy = cell_coord(py, h.oy, h.inv, h.ny);
+  const int cz = cell_coord(pz, h.oz, h.inv, h.nz);
+  const float edge = 1.0f / h.inv;
+  for (int s = 0;; ++s) {
+    const int xl = cx - s, xh = cx + s, yl = cy - s, yh = cy + s, zl = cz - s, zh = cz + s;
+    const int x0 = max(xl, 0), x1 = min(xh, h.nx - 1);
+    for (int z = max(zl, 0); z <= min(zh, h.nz - 1); ++z) {
+      for (int y = max(yl, 0); y <= min(yh, h.ny - 1); ++y) {
+        const int row = (z * h.ny + y) * h.nx;
+        if (s == 0 || z == zl || z == zh || y == yl || y == yh) {
+          visit(off[row + x0], off[row + x1 + 1]);  // a face row: all of x0..x1
+        } else {
+          if (xl >= 0) visit(off[row + xl], off[row + xl + 1]);
+          if (xh < h.nx) visit(off[row + xh], off[row + xh + 1]);
+        }
+      }
+    }
+    if (xl <= 0 && yl <= 0 && zl <= 0 && xh >= h.nx - 1 && yh >= h.ny - 1 && zh >= h.nz - 1)
+      break;  // every cell visited
+    if (best.d3 < __builtin_inff()) {
+      float gap = __builtin_inff();
+      // d = distance from p to the face at cell boundary c of an axis with origin o; the
+      // slack covers the rounding of the cell assignment and of the face coordinate
+      auto face = [&](float d, float pc, float o, int c) {
+        const float fc = o + (float)c * edge;
+        gap = fminf(gap, d - 1e-5f * (fabsf(pc) + fabsf(o) + fabsf(fc) + (float)c * edge) - 1e-30f);
+      };
+      if (xl > 0) face(px - (h.ox + (float)xl * edge), px, h.ox, xl);
+      if (xh < h.nx - 1) face((h.ox + (float)(xh + 1) * edge) - px, px, h.ox, xh + 1);
+      if (yl > 0) face(py - (h.oy + (float)yl * edge), py, h.oy, yl);
+      if (yh < h.ny - 1) face((h.oy + (float)(yh + 1) * edge) - py, py, h.oy, yh + 1);
+      if (zl > 0) face(pz - (h.oz + (float)zl * edge), pz, h.oz, zl);
+      if (zh < h.nz - 1) face((h.oz + (float)(zh + 1) * edge) - pz, pz, h.oz, zh + 1);
+      if (gap > 0.0f && best.d3 < gap * gap * 0.9999f) break;
+    }
+  }
+  float* D = dist + ((size_t)b * n + u) * 3;
+  int32_t* I = idx + ((size_t)b * n + u) * 3;
+  D[0] = best.d1; D[1] = best.d2; D[2] = best.d3;
+  I[0] = best.i1; I[1] = best.i2; I[2] = best.i3;
+}
+
 __global__ void idw_kernel(const float* __restrict__ dist, int total, float* __restrict__ weight) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total) return;
@@ -194,29 +287,49 @@ __global__ __launch_bounds__(kBlock) void three_interp_grad_kernel(
 
 // pointnet_fp_module geometry. Workgroup (x, b, z): unknown points [64x, 64x+64) of cloud b,
 // output channels [z*cw, (z+1)*cw) of the Cout = C2 + C1 concat row (in units of VEC floats).
-template <int VEC>
+// PRE: the three neighbours come from a previous three_nn (pdist, pidx) instead of the scan;
+// with `ugrid` (a grid over the unknown points) the workgroup's 64 rows are 64 consecutive
+// points in cell order, so their neighbours' feature rows are shared through the caches.
+template <int VEC, bool PRE>
 __global__ __launch_bounds__(kNNBlock) void fp_fused_kernel(
     const float* __restrict__ xyz1, const float* __restrict__ xyz2,
+    const float* __restrict__ pdist, const int32_t* __restrict__ pidx,
+    const void* __restrict__ ugrid,
     const float* __restrict__ points1, int C1, const float* __restrict__ points2, int C2, int n,
     int m, int cw, FastDiv div_cw, float* __restrict__ out) {
   using VecT = typename std::conditional<VEC == 4, float4, float>::type;
-  __shared__ float4 sk[kNNTile];
+  __shared__ float4 sk[PRE ? 1 : kNNTile];
   __shared__ int4 s_idx[kNNRows];
   __shared__ float4 s_w[kNNRows];
+  __shared__ int s_row[PRE ? kNNRows : 1];
   const int b = blockIdx.y;
   const int j0 = blockIdx.x * kNNRows;
-  const int jl = threadIdx.x / kNNGroup;
-  const int j = j0 + jl;
-  const bool valid = j < n;
-  const float* U = xyz1 + ((size_t)b * n + (valid ? j : 0)) * 3;
-  Best3 best;
-  best3_init(best);
-  scan_known(xyz2 + (size_t)b * m * 3, m, U[0], U[1], U[2], sk, best);
-  if ((threadIdx.x & (kNNGroup - 1)) == 0) {
-    float w1, w2, w3;
-    idw(best.d1, best.d2, best.d3, w1, w2, w3);
-    s_idx[jl] = make_int4(best.i1, best.i2, best.i3, 0);
-    s_w[jl] = make_float4(w1, w2, w3, 0.0f);
+  if constexpr (PRE) {
+    int jj = j0 + (int)threadIdx.x;
+    if (threadIdx.x < kNNRows && jj < n) {
+      if (ugrid) jj = __float_as_int(grid_view(ugrid, b, n).pts[jj].w);
+      s_row[threadIdx.x] = jj;
+      const float* D = pdist + ((size_t)b * n + jj) * 3;
+      const int32_t* I = pidx + ((size_t)b * n + jj) * 3;
+      float w1, w2, w3;
+      idw(D[0], D[1], D[2], w1, w2, w3);
+      s_idx[threadIdx.x] = make_int4(I[0], I[1], I[2], 0);
+      s_w[threadIdx.x] = make_float4(w1, w2, w3, 0.0f);
+    }
+  } else {
+    const int jl = threadIdx.x / kNNGroup;
+    const int j = j0 + jl;
+    const bool valid = j < n;
+    const float* U = xyz1 + ((size_t)b * n + (valid ? j : 0)) * 3;
+    Best3 best;
+    best3_init(best);
+    scan_known(xyz2 + (size_t)b * m * 3, m, U[0], U[1], U[2], sk, best);
+    if ((threadIdx.x & (kNNGroup - 1)) == 0) {
+      float w1, w2, w3;
+      idw(best.d1, best.d2, best.d3, w1, w2, w3);
+      s_idx[jl] = make_int4(best.i1, best.i2, best.i3, 0);
+      s_w[jl] = make_float4(w1, w2, w3, 0.0f);
+    }
   }
   __syncthreads();
   const int Cout = C2 + C1;             // floats
@@ -233,7 +346,9 @@ __global__ __launch_bounds__(kNNBlock) void fp_fused_kernel(
   for (int e = threadIdx.x; e < elems; e += kNNBlock) {
     const int rl = (int)fdiv((uint32_t)e, div_cw);
     const int c = cb + (e - rl * width);
-    const int r = j0 + rl;
+    int r;
+    if constexpr (PRE) r = s_row[rl];
+    else r = j0 + rl;
     VecT v;
     if (c < c2v) {  // three_interpolate (tf_interpolate.cpp:119): ((p1*w1)+(p2*w2))+(p3*w3)
       const int4 I = s_idx[rl];
@@ -263,6 +378,36 @@ int batch_chunk(int B, int n, int C, int rows) {
   long long ch = ((1LL << 32) - 1) / (per_b > 0 ? per_b : 1);
   if ((long long)n * ch >= (1LL << 31)) ch = ((1LL << 31) - 1) / (n > 0 ? n : 1);
   return (int)(ch < B ? ch : B);
+}
+
+// Launch of fp_fused_kernel: the search (xyz1, xyz2) or precomputed neighbours (pdist, pidx).
+int fp_launch(const float* xyz1, const float* xyz2, const float* pdist, const int32_t* pidx,
+              const void* ugrid, const float* points1, int C1, const float* points2, int C2,
+              int B, int n, int m, float* out, hipStream_t stream) {
+  const bool pre = pdist != nullptr;
+  const int Cout = C1 + C2;
+  const bool vec4 = (C1 % 4 == 0) && (C2 % 4 == 0) &&
+                    ((((uintptr_t)points1 | (uintptr_t)points2 | (uintptr_t)out) & 15) == 0);
+  const int VEC = vec4 ? 4 : 1;
+  const int coutv = Cout / VEC;
+  const int row_blocks = (n + kNNRows - 1) / kNNRows;
+  // split the channels over grid.z until ~2 workgroups per CU, keeping >= 16 vector columns
+  // per workgroup and (search variant) not re-running a long known-point scan too often
+  int zsplit = 1;
+  while ((long long)row_blocks * B * zsplit < 512 && coutv / (zsplit * 2) >= 16 &&
+         (pre || (long long)m * zsplit * 2 <= 4096))
+    zsplit *= 2;
+  const int cw = (coutv + zsplit - 1) / zsplit;
+  if ((long long)kNNRows * cw * cw >= (1LL << 32)) return PN2_EINVAL;
+  const dim3 grid(row_blocks, B, zsplit);
+  const FastDiv div = make_fastdiv((uint32_t)cw);
+#define PN2_FP(V, P)                                                                           \
+  hipLaunchKernelGGL((fp_fused_kernel<V, P>), grid, dim3(kNNBlock), 0, stream, xyz1, xyz2,    \
+                     pdist, pidx, ugrid, points1, C1, points2, C2, n, m, cw, div, out)
+  if (vec4) { if (pre) PN2_FP(4, true); else PN2_FP(4, false); }
+  else { if (pre) PN2_FP(1, true); else PN2_FP(1, false); }
+#undef PN2_FP
+  PN2_RETURN_LAUNCH();
 }
 
 }  // namespace
@@ -351,29 +496,38 @@ int pn2_fp_fused(const float* xyz1, const float* xyz2, const float* points1, int
   if ((long long)B * n == 0 || C1 + C2 == 0) return PN2_OK;
   if (!xyz1 || !out || (m > 0 && !xyz2) || (C2 > 0 && !points2)) return PN2_EINVAL;
   if (m == 0 && C2 > 0) return PN2_EINVAL;  // nothing to interpolate from
-  const int Cout = C1 + C2;
-  const bool vec4 = (C1 % 4 == 0) && (C2 % 4 == 0) &&
-                    ((((uintptr_t)points1 | (uintptr_t)points2 | (uintptr_t)out) & 15) == 0);
-  const int VEC = vec4 ? 4 : 1;
-  const int coutv = Cout / VEC;
-  const int row_blocks = (n + pn2::kNNRows - 1) / pn2::kNNRows;
-  // split the channels over grid.z until ~2 workgroups per CU, keeping >= 64 vector columns
-  // per workgroup and not re-running a long known-point scan too often
-  int zsplit = 1;
-  while ((long long)row_blocks * B * zsplit < 512 && coutv / (zsplit * 2) >= 16 &&
-         (long long)m * zsplit * 2 <= 4096)
-    zsplit *= 2;
-  const int cw = (coutv + zsplit - 1) / zsplit;
-  if ((long long)pn2::kNNRows * cw * cw >= (1LL << 32)) return PN2_EINVAL;
-  const dim3 grid(row_blocks, B, zsplit);
-  if (vec4)
-    hipLaunchKernelGGL(pn2::fp_fused_kernel<4>, grid, dim3(pn2::kNNBlock), 0, (hipStream_t)stream,
-                       xyz1, xyz2, points1, C1, points2, C2, n, m, cw,
-                       pn2::make_fastdiv((uint32_t)cw), out);
+  return pn2::fp_launch(xyz1, xyz2, nullptr, nullptr, nullptr, points1, C1, points2, C2, B, n,
+                        m, out, (hipStream_t)stream);
+}
+
+int pn2_fp_apply(const float* dist, const int32_t* idx, const void* unknown_grid,
+                 const float* points1, int C1, const float* points2, int C2, int B, int n, int m,
+                 float* out, pn2_stream_t stream) {
+  if (B < 0 || n < 0 || m < 0 || C1 < 0 || C2 < 0 || B > 65535) return PN2_EINVAL;
+  if (!points1 && C1 != 0) return PN2_EINVAL;
+  if ((long long)B * n == 0 || C1 + C2 == 0) return PN2_OK;
+  if (!dist || !idx || !out || (C2 > 0 && !points2)) return PN2_EINVAL;
+  if (m == 0 && C2 > 0) return PN2_EINVAL;
+  return pn2::fp_launch(nullptr, nullptr, dist, idx, unknown_grid, points1, C1, points2, C2, B,
+                        n, m, out, (hipStream_t)stream);
+}
+
+int pn2_three_nn_grid(const void* known_grid, const void* unknown_grid, const float* xyz1,
+                      int B, int n, int m, float* dist, int32_t* idx, pn2_stream_t stream) {
+  if (B < 0 || n < 0 || m < 0 || B > 65535) return PN2_EINVAL;
+  if ((long long)B * n == 0) return PN2_OK;
+  if (!known_grid || !dist || !idx || (!unknown_grid && !xyz1)) return PN2_EINVAL;
+  constexpr int BLOCK = 256;
+  const dim3 grid((n + BLOCK - 1) / BLOCK, B);
+  // an automatic-edge known grid has at most max(m, kAutoMinCells) cells (grid.h); an
+  // explicit-edge one may have up to kGridCap and is read from global memory
+  const size_t lds = (size_t)m * 16 + (size_t)(std::max(m, pn2::kAutoMinCells) + 1) * 4;
+  if (lds <= 64 * 1024)
+    hipLaunchKernelGGL((pn2::three_nn_grid_kernel<BLOCK, true>), grid, dim3(BLOCK), lds,
+                       (hipStream_t)stream, known_grid, m, unknown_grid, xyz1, n, dist, idx);
   else
-    hipLaunchKernelGGL(pn2::fp_fused_kernel<1>, grid, dim3(pn2::kNNBlock), 0, (hipStream_t)stream,
-                       xyz1, xyz2, points1, C1, points2, C2, n, m, cw,
-                       pn2::make_fastdiv((uint32_t)cw), out);
+    hipLaunchKernelGGL((pn2::three_nn_grid_kernel<BLOCK, false>), grid, dim3(BLOCK), 0,
+                       (hipStream_t)stream, known_grid, m, unknown_grid, xyz1, n, dist, idx);
   PN2_RETURN_LAUNCH();
 }
 

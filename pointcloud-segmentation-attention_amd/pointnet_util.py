@@ -140,15 +140,16 @@ def group_pool(new_points, pooling="max", grouped_xyz=None):
     return out
 
 
-def fp_interpolate(xyz1, xyz2, points1, points2):
+def fp_interpolate(xyz1, xyz2, points1, points2, known_grid=None, unknown_grid=None):
     """Geometry of pointnet_fp_module (pointnet_util.py:218-228), before its MLP:
     three_nn, IDW weights, three_interpolate and concat [interpolated, points1].
-    Returns (B, n, C2 + C1)."""
+    Returns (B, n, C2 + C1). known_grid / unknown_grid: optional grid.PointGrid over xyz2 /
+    xyz1 for the neighbour search (built here when the search is large)."""
     xyz1 = device_tensor(xyz1, "xyz1", torch.float32)
     xyz2 = device_tensor(xyz2, "xyz2", torch.float32)
     points2 = device_tensor(points2, "points2", torch.float32)
     if _needs_grad(points1, points2):
-        dist, idx = tf_interpolate.three_nn(xyz1, xyz2)
+        dist, idx = tf_interpolate.three_nn(xyz1, xyz2, known_grid, unknown_grid)
         weight = tf_interpolate.idw_weights(dist)
         interp = tf_interpolate.three_interpolate(points2, idx, weight)
         return interp if points1 is None else torch.cat([interp, points1], dim=2)
@@ -160,6 +161,13 @@ def fp_interpolate(xyz1, xyz2, points1, points2):
     else:
         C1 = 0
     out = torch.empty((B, n, C2 + C1), dtype=torch.float32, device=xyz1.device)
-    check(lib().pn2_fp_fused(ptr(xyz1), ptr(xyz2), ptr(points1), C1, ptr(points2), C2, B, n, m,
-                             ptr(out), stream_of(xyz1)), "fp_interpolate")
+    if known_grid is not None or tf_interpolate.use_grid(n, m):
+        dist, idx = tf_interpolate.three_nn(xyz1, xyz2, known_grid, unknown_grid)
+        check(lib().pn2_fp_apply(ptr(dist), ptr(idx),
+                                 None if unknown_grid is None else ptr(unknown_grid.buf),
+                                 ptr(points1), C1, ptr(points2), C2, B, n, m, ptr(out),
+                                 stream_of(xyz1)), "fp_interpolate")
+    else:
+        check(lib().pn2_fp_fused(ptr(xyz1), ptr(xyz2), ptr(points1), C1, ptr(points2), C2, B, n,
+                                 m, ptr(out), stream_of(xyz1)), "fp_interpolate")
     return out

@@ -89,8 +89,21 @@ class Step:
         self.keep = []
 
     def sampler(self):
+        """SA1 FPS + gather. With overlap, the SA1 ball-query grid over the input cloud is
+        built on the side stream meanwhile (it needs only xyz) and joined before returning."""
         npoint = SSG_SA[0][0] if self.kind == "ssg" else MSG_SA[0][0]
-        _, self.new_xyz1 = tf_sampling.farthest_point_sample_and_gather(npoint, self.inp["xyz"])
+        xyz = self.inp["xyz"]
+        self.grid1 = None
+        build = (self.overlap and self.kind == "ssg"
+                 and int(xyz.shape[1]) >= tf_grouping.GRID_MIN_POINTS)
+        if build:
+            main = torch.cuda.current_stream(xyz.device)
+            self.side.wait_stream(main)
+            with torch.cuda.stream(self.side):
+                self.grid1 = tf_grouping.BallGrid(xyz, SSG_SA[0][1])
+        _, self.new_xyz1 = tf_sampling.farthest_point_sample_and_gather(npoint, xyz)
+        if build:
+            main.wait_stream(self.side)
         return self.new_xyz1
 
     def rest(self):
@@ -131,7 +144,8 @@ class Step:
                 xyz.append(tf_sampling.farthest_point_sample_and_gather(npoint, xyz[i])[1])
             with self._fork(i):
                 new_xyz = xyz[i + 1]
-                idx, _ = tf_grouping.query_ball_point(radius, nsample, xyz[i], new_xyz)
+                idx, _ = tf_grouping.query_ball_point(radius, nsample, xyz[i], new_xyz,
+                                                      grid=self.grid1 if i == 0 else None)
                 new_points, _ = pointnet_util.group_concat(xyz[i], points[i], new_xyz, idx,
                                                            want_grouped_xyz=False)
                 sa_outs[i] = [new_points]
@@ -139,8 +153,10 @@ class Step:
                     Q, K, V = inp["attn"][i]
                     sa_outs[i].append(attention_layer.attention_reduce(Q, K, V))
                 k = 3 - i  # the FP layer whose coarse level (i+1) just became available
-                fp_outs[k] = pointnet_util.fp_interpolate(xyz[i], xyz[i + 1], points[i],
-                                                          fp_feat[k])
+                # FP4's unknown points are SA1's input cloud: the SA1 grid orders its search
+                fp_outs[k] = pointnet_util.fp_interpolate(
+                    xyz[i], xyz[i + 1], points[i], fp_feat[k],
+                    unknown_grid=self.grid1 if i == 0 else None)
         self.keep = xyz
         return self._join([t for o in sa_outs for t in o] + fp_outs)
 

@@ -8,9 +8,27 @@ knn=True path of sample_and_group uses them, and no attention model sets it.
 import torch
 
 from ._lib import InvalidArgumentError, check, device_tensor, lib, ptr, stream_of
+from .grid import PointGrid
 
 
-def query_ball_point(radius, nsample, xyz1, xyz2):
+# Clouds at least this large (and query batches at least this large) use the spatial grid
+# (ball_grid.hip); smaller ones the in-order LDS scan (ball_query.hip). Both are exact and
+# return identical results; the switch is purely a speed choice (tools/tune_bq.py).
+GRID_MIN_POINTS = 2048
+GRID_MIN_QUERIES = 1024
+
+
+class BallGrid(PointGrid):
+    """Spatial grid over xyz1 (B, N, 3) for query_ball_point (grid.PointGrid with cell edge =
+    radius), reusable for any number of query batches and radii."""
+
+    def __init__(self, xyz1, radius):
+        if not radius > 0:
+            raise InvalidArgumentError("QueryBallPoint expects positive radius")
+        super().__init__(xyz1, float(radius), name="QueryBallPoint")
+
+
+def query_ball_point(radius, nsample, xyz1, xyz2, grid=None):
     """tf_grouping.py:8-20.
 
     Input:
@@ -18,6 +36,8 @@ def query_ball_point(radius, nsample, xyz1, xyz2):
         nsample: int32, number of points selected in each ball region
         xyz1: (batch_size, ndataset, 3) float32 array, input points
         xyz2: (batch_size, npoint, 3) float32 array, query points
+        grid: optional BallGrid built over xyz1 (extension: lets callers build it early,
+              e.g. concurrently with the sampler); built here when the cloud is large
     Output:
         idx: (batch_size, npoint, nsample) int32 array, indices to input points
         pts_cnt: (batch_size, npoint) int32 array, number of unique points in each local region
@@ -36,8 +56,16 @@ def query_ball_point(radius, nsample, xyz1, xyz2):
     M, ns = int(xyz2.shape[1]), int(nsample)
     idx = torch.empty((B, M, ns), dtype=torch.int32, device=xyz1.device)
     pts_cnt = torch.empty((B, M), dtype=torch.int32, device=xyz1.device)
-    check(lib().pn2_ball_query(ptr(xyz1), ptr(xyz2), B, N, M, float(radius), ns, ptr(idx),
-                               ptr(pts_cnt), stream_of(xyz1)), "QueryBallPoint")
+    if grid is None and N >= GRID_MIN_POINTS and B * M >= GRID_MIN_QUERIES:
+        grid = BallGrid(xyz1, radius)
+    if grid is not None:
+        if not grid.matches(xyz1):
+            raise InvalidArgumentError("QueryBallPoint grid was built over a different xyz1")
+        check(lib().pn2_ball_query_grid(ptr(grid.buf), ptr(xyz2), B, N, M, float(radius), ns,
+                                        ptr(idx), ptr(pts_cnt), stream_of(xyz1)), "QueryBallPoint")
+    else:
+        check(lib().pn2_ball_query(ptr(xyz1), ptr(xyz2), B, N, M, float(radius), ns, ptr(idx),
+                                   ptr(pts_cnt), stream_of(xyz1)), "QueryBallPoint")
     return idx, pts_cnt
 
 

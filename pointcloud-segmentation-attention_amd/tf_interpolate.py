@@ -6,14 +6,28 @@ shapes, dtypes and error messages). The reference registers these ops for DEVICE
 import torch
 
 from ._lib import InvalidArgumentError, check, device_tensor, lib, ptr, stream_of
+from .grid import PointGrid
 
 
-def three_nn(xyz1, xyz2):
+# three_nn searches over a grid of the known points when the brute-force scan would test at
+# least this many (unknown, known) pairs per cloud and the known cloud is this large
+# (identical results either way; tools/tune_nn.py measured the switch).
+GRID_MIN_PAIRS = 1 << 21
+GRID_MIN_KNOWN = 512
+
+
+def use_grid(n, m):
+    return n * m >= GRID_MIN_PAIRS and m >= GRID_MIN_KNOWN
+
+
+def three_nn(xyz1, xyz2, known_grid=None, unknown_grid=None):
     """tf_interpolate.py:8-17.
 
     Input:
         xyz1: (b,n,3) float32 array, unknown points
         xyz2: (b,m,3) float32 array, known points
+        known_grid / unknown_grid: optional grid.PointGrid over xyz2 / xyz1 (extension; the
+            known grid is built here when the search is large)
     Output:
         dist: (b,n,3) float32 array, (squared) distances to known points
         idx: (b,n,3) int32 array, indices to known points
@@ -27,8 +41,18 @@ def three_nn(xyz1, xyz2):
     B, n, m = int(xyz1.shape[0]), int(xyz1.shape[1]), int(xyz2.shape[1])
     dist = torch.empty((B, n, 3), dtype=torch.float32, device=xyz1.device)
     idx = torch.empty((B, n, 3), dtype=torch.int32, device=xyz1.device)
-    check(lib().pn2_three_nn(ptr(xyz1), ptr(xyz2), B, n, m, ptr(dist), ptr(idx),
-                             stream_of(xyz1)), "ThreeNN")
+    if known_grid is None and use_grid(n, m):
+        known_grid = PointGrid(xyz2, 0.0, name="ThreeNN")
+    if known_grid is not None:
+        if not known_grid.matches(xyz2) or (unknown_grid is not None and not unknown_grid.matches(xyz1)):
+            raise InvalidArgumentError("ThreeNN grid was built over different points")
+        check(lib().pn2_three_nn_grid(ptr(known_grid.buf),
+                                      None if unknown_grid is None else ptr(unknown_grid.buf),
+                                      ptr(xyz1), B, n, m, ptr(dist), ptr(idx), stream_of(xyz1)),
+              "ThreeNN")
+    else:
+        check(lib().pn2_three_nn(ptr(xyz1), ptr(xyz2), B, n, m, ptr(dist), ptr(idx),
+                                 stream_of(xyz1)), "ThreeNN")
     return dist, idx
 
 

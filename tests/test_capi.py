@@ -73,6 +73,22 @@ def test_argument_checks_return_einval_without_launching(pn2):
     assert lib.pn2_three_nn(None, None, 0, 10, 10, None, None, None) == 0
 
 
+def test_grid_contract(pn2):
+    lib = pn2.lib()
+    E = -22
+    per = lib.pn2_grid_size(1, 0)
+    assert per > 0 and per % 16 == 0
+    assert lib.pn2_grid_size(3, 1000) == 3 * (per + 1000 * 16)
+    assert lib.pn2_grid_build(None, 1, 100, 0.1, None, 0, None) == E           # no buffer
+    assert lib.pn2_grid_build(None, 1, 100, float("nan"), None, 0, None) == E  # NaN edge
+    assert lib.pn2_grid_build(None, 0, 100, 0.1, None, 0, None) == 0           # empty batch
+    assert lib.pn2_ball_query_grid(None, None, 1, 10, 10, 0.1, 0, None, None, None) == E
+    assert lib.pn2_ball_query_grid(None, None, 1, 200000, 10, 0.1, 8, None, None, None) == E
+    assert lib.pn2_three_nn_grid(None, None, None, 1, 10, 10, None, None, None) == E
+    assert lib.pn2_three_nn_grid(None, None, None, 0, 10, 10, None, None, None) == 0
+    assert lib.pn2_fp_apply(None, None, None, None, 3, None, 4, 1, 4, 4, None, None) == E
+
+
 def test_fps_workspace_contract(pn2):
     lib = pn2.lib()
     cap = lib.pn2_fps_max_points()

@@ -158,6 +158,45 @@ def test_ball_query_no_hit_and_boundary(env):
     assert 0 < rcnt[0, 0] < len(xs)
 
 
+GRID_CASES = [
+    ("scannet", 2, 8192, 1024, 0.1, 32),   # SA1 (what the stack runs on the grid)
+    ("scannet", 1, 16384, 512, 0.4, 128),  # MSG
+    ("scannet", 2, 3000, 300, 0.2, 64),    # N not a multiple of 32
+    ("uniform", 2, 700, 200, 0.05, 8),
+    ("dup", 2, 2048, 64, 0.1, 16),         # zero extent: one cell
+    ("grid", 2, 4096, 500, 1.0, 16),       # exact lattice distances at the radius
+    ("scannet", 1, 4096, 256, 0.004, 8),   # tiny radius: cell edge grows to fit the cell cap
+    ("scannet", 1, 2048, 128, 5.0, 64),    # ball covers the cloud
+]
+
+
+@pytest.mark.parametrize("kind,B,N,M,r,ns", GRID_CASES)
+def test_ball_query_grid_equals_scan(env, kind, B, N, M, r, ns):
+    """The spatial-grid path (ball_grid.hip) returns exactly the in-order scan's idx and
+    pts_cnt, and the oracle's; queries also far outside the cloud's bounding box."""
+    pkg, O, torch, dev = env
+    x = _cloud(pkg, kind, B, N)
+    q = O.gather_point(x, O.fps(x, M)) if kind != "grid" else x[:, :M].copy()
+    q[:, :3] = np.array([[50.0, 50.0, 50.0], [-3.0, 0.5, 0.5], [0.5, 0.5, 9.0]], np.float32)
+    xt, qt = torch.from_numpy(x).to(dev), torch.from_numpy(q).to(dev)
+    grid = pkg.tf_grouping.BallGrid(xt, r)
+    gi, gc = pkg.tf_grouping.query_ball_point(r, ns, xt, qt, grid=grid)
+    ri, rc = O.ball_query(x, q, r, ns)
+    assert np.array_equal(gc.cpu().numpy(), rc)
+    assert np.array_equal(gi.cpu().numpy(), ri)
+    # the same grid serves another radius exactly
+    gi2, gc2 = pkg.tf_grouping.query_ball_point(2 * r, ns, xt, qt, grid=grid)
+    ri2, rc2 = O.ball_query(x, q, 2 * r, ns)
+    assert np.array_equal(gc2.cpu().numpy(), rc2) and np.array_equal(gi2.cpu().numpy(), ri2)
+    # and the in-order scan agrees
+    L = pkg.lib()
+    si = torch.empty_like(gi)
+    sc = torch.empty_like(gc)
+    assert L.pn2_ball_query(xt.data_ptr(), qt.data_ptr(), B, N, M, r, ns, si.data_ptr(),
+                            sc.data_ptr(), torch.cuda.current_stream().cuda_stream) == 0
+    assert torch.equal(si, gi) and torch.equal(sc, gc)
+
+
 @pytest.mark.parametrize("kind,B,N,M,r,ns", BQ_CASES[:6])
 def test_ball_query_vs_reference_kernel(env, kind, B, N, M, r, ns):
     """query_ball_point_gpu (tf_grouping_g.cu:3-36) itself, on this GPU."""
@@ -240,6 +279,56 @@ def test_three_nn_ties(env):
     rd, ri = O.three_nn(x1, x2)
     assert np.array_equal(i.cpu().numpy(), ri)
     assert np.array_equal(_bits(d.cpu().numpy()), _bits(rd))
+
+
+NN_GRID_CASES = [
+    ("fp4", 2, 8192, 1024),      # FP4 of the stack: unknowns = the cloud, knowns = its FPS
+    ("scannet", 2, 3000, 700),
+    ("grid", 2, 2000, 600),      # lattice: exact distance ties everywhere
+    ("far", 1, 1000, 512),       # unknowns far outside the known cloud's bbox
+    ("dup", 2, 700, 600),        # known cloud of one repeated point (one cell)
+    ("scannet", 2, 500, 2),      # m < 3: unfilled slots stay (inf, 0)
+    ("scannet", 1, 300, 1),
+]
+
+
+@pytest.mark.parametrize("kind,B,n,m", NN_GRID_CASES)
+def test_three_nn_grid(env, kind, B, n, m):
+    """three_nn over a grid of the known points (interp.hip three_nn_grid_kernel) gives the
+    scan's (and the oracle's) idx and dist bit-exactly, with and without the unknown grid
+    ordering the work; fp_interpolate over it equals the fused scan."""
+    pkg, O, torch, dev = env
+    if kind == "fp4":
+        x1 = _cloud(pkg, "scannet", B, n, seed=4)
+        x2 = O.gather_point(x1, O.fps(x1, m))
+    elif kind == "far":
+        x1 = _cloud(pkg, "uniform", B, n, seed=4) * np.float32(20.0) - np.float32(10.0)
+        x2 = _cloud(pkg, "scannet", B, m, seed=6)
+    else:
+        x1 = _cloud(pkg, kind if kind != "dup" else "scannet", B, n, seed=4)
+        x2 = _cloud(pkg, kind, B, m, seed=8)
+        if kind == "grid":
+            x1 = x1 + np.float32(0.5)
+    t1, t2 = torch.from_numpy(x1).to(dev), torch.from_numpy(x2).to(dev)
+    rd, ri = O.three_nn(x1, x2)
+    ug = pkg.grid.PointGrid(t1, 0.1)
+    # automatic cell edge (LDS-staged search) and a fine explicit edge (more cells than
+    # points: the search reads the grid from global memory)
+    for kg in (pkg.grid.PointGrid(t2), pkg.grid.PointGrid(t2, 0.02)):
+        for u in (None, ug):
+            d, i = pkg.tf_interpolate.three_nn(t1, t2, known_grid=kg, unknown_grid=u)
+            assert np.array_equal(i.cpu().numpy(), ri)
+            assert np.array_equal(_bits(d.cpu().numpy()), _bits(rd))
+    if m >= 3:
+        p1 = torch.from_numpy(pkg.synth.features_uniform(1, (B, n, 8))).to(dev)
+        p2 = torch.from_numpy(pkg.synth.features_uniform(2, (B, m, 16))).to(dev)
+        L = pkg.lib()
+        fused = torch.empty((B, n, 24), device=dev)
+        assert L.pn2_fp_fused(t1.data_ptr(), t2.data_ptr(), p1.data_ptr(), 8, p2.data_ptr(), 16,
+                              B, n, m, fused.data_ptr(), torch.cuda.current_stream().cuda_stream) == 0
+        for u in (None, ug):
+            a = pkg.pointnet_util.fp_interpolate(t1, t2, p1, p2, known_grid=kg, unknown_grid=u)
+            assert torch.equal(a, fused)
 
 
 @pytest.mark.parametrize("C", [1, 16, 128, 512])

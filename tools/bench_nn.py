@@ -1,0 +1,55 @@
+#!/usr/bin/env python3
+"""Micro-benchmark of the three_nn paths at FP4 size (B=16, n=8192 cloud points, m=1024 FPS
+centres): brute-force scan, grid search (LDS-staged / global), with and without the unknown
+grid ordering. HIP events, median of 20."""
+import importlib
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    import torch
+    pkg = importlib.import_module("pointcloud-segmentation-attention_amd")
+    from oracle import oracle as O
+    dev = torch.device("cuda:0")
+    B, n, m = 16, 8192, 1024
+    x = pkg.synth.batch(range(B), n, "scannet")[0]
+    t1 = torch.from_numpy(x).to(dev)
+    _, k = pkg.tf_sampling.farthest_point_sample_and_gather(m, t1)
+    L = pkg.lib()
+    st = torch.cuda.current_stream().cuda_stream
+    dist = torch.empty((B, n, 3), device=dev)
+    idx = torch.empty((B, n, 3), dtype=torch.int32, device=dev)
+
+    def timeit(fn, reps=20):
+        ts = []
+        for _ in range(3):
+            fn()
+        for _ in range(reps):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record(); fn(); b.record(); b.synchronize()
+            ts.append(a.elapsed_time(b) * 1e3)
+        return statistics.median(ts)
+
+    ug = pkg.grid.PointGrid(t1, 0.1)
+    res = {}
+    res["scan"] = timeit(lambda: L.pn2_three_nn(t1.data_ptr(), k.data_ptr(), B, n, m, dist.data_ptr(), idx.data_ptr(), st))
+    ref = (dist.clone(), idx.clone())
+    for edge in (0.0, 0.15, 0.2, 0.28, 0.4):
+        kg = pkg.grid.PointGrid(k, edge)
+        for name, u in (("rand", None), ("sorted", ug)):
+            r = timeit(lambda: L.pn2_three_nn_grid(kg.buf.data_ptr(), None if u is None else u.buf.data_ptr(), t1.data_ptr(), B, n, m, dist.data_ptr(), idx.data_ptr(), st))
+            assert torch.equal(idx, ref[1]) and torch.equal(dist, ref[0])
+            res[f"grid edge={edge} {name}"] = r
+    res["build known grid"] = timeit(lambda: pkg.grid.PointGrid(k, 0.0))
+    res["build cloud grid"] = timeit(lambda: pkg.grid.PointGrid(t1, 0.1))
+    print(json.dumps({k_: round(v, 1) for k_, v in res.items()}, indent=1))
+
+
+if __name__ == "__main__":
+    main()
