@@ -19,6 +19,10 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+# The step runs on 4 streams (sampler chain + 3 side lanes) plus 2 setup streams; HIP maps
+# streams to hardware queues round-robin, and with its default of 4 queues a side lane
+# would share the chain's queue and sit in front of the next step's sampler. 8 <= 32.
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 
 PKG = "pointcloud-segmentation-attention_amd"
 METRIC = "8192-pt clouds/sec through SA+FP layers, 1/2/4/8 MI355X; HBM GB/s vs peak"
@@ -103,6 +107,9 @@ def main():
                     help="launch every op from Python instead of replaying the captured hipGraphs")
     ap.add_argument("--no-overlap", action="store_true",
                     help="run the whole step on one stream (no side stream beside the sampler chain)")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="join every step before the next (no overlap of step k's side work "
+                         "with step k+1's samplers)")
     args = ap.parse_args()
 
     import torch
@@ -125,21 +132,26 @@ def main():
     torch.cuda.synchronize()
 
     overlap = not args.no_overlap
-    step = pkg.stack.Step(inp, overlap=overlap)
-    graph = None if args.eager else pkg.stack.GraphStep(inp, overlap=overlap)
+    pipelined = overlap and not args.no_pipeline
+    if pipelined:
+        pipe = pkg.stack.Pipeline(inp, graphs=not args.eager)
+    else:
+        step = pkg.stack.Step(inp, overlap=overlap)
+        graph = None if args.eager else pkg.stack.GraphStep(inp, overlap=overlap)
 
     def run_step(events=None):
+        if pipelined:
+            return pipe.run(events)
         if graph is not None:
             return graph.replay(events)
-        if events is not None:
-            events[0].record()
-        step.sampler()
-        if events is not None:
-            events[1].record()
-        return step.rest()
+        return step.run(events)
+
+    def finish():
+        return pipe.join() if pipelined else None
 
     for _ in range(args.warmup):
         run_step()
+    finish()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(args.steps)]
 
@@ -152,6 +164,7 @@ def main():
     t0 = time.perf_counter()
     for k in range(args.steps):
         outs = run_step(ev[k])
+    outs = finish() or outs
     torch.cuda.synchronize()
     barrier()
     elapsed = pkg.shard.max_over_ranks(time.perf_counter() - t0, dev)
@@ -181,7 +194,8 @@ def main():
                        "clouds_per_gpu": B, "global_batch": world * B, "points": N,
                        "parallelism": f"dp{world} (batch split)",
                        "launch": "eager" if args.eager else "hipGraph replay",
-                       "streams": "sampler chain + side stream" if overlap else "one stream"},
+                       "streams": ("sampler chain + 3 side streams" if overlap else "one stream")
+                       + (", steps software-pipelined over 2 buffer sets" if pipelined else "")},
             "roofline": {"kernel": f"SA1 sampler (FPS + gather fused): {B} clouds x {N} pts "
                                    f"-> {M1}, one workgroup per cloud",
                          "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS,

@@ -22,6 +22,8 @@ SSG_FP_OUT = (256, 256, 128, 128)
 MSG_SA = ((512, (0.1, 0.2, 0.4), (16, 32, 128), (64, 128, 128)),
           (128, (0.2, 0.4, 0.8), (32, 64, 128), (128, 256, 256)))
 
+NSIDE = 3  # side streams of the overlapped step
+
 CONFIGS = {
     # name: (points per cloud, kind, with_features, attention)
     "cfg2": (8192, "ssg", False, False),
@@ -63,129 +65,219 @@ def make_inputs(config, cloud_ids, device, seed=1234):
     return inp
 
 
+_SIDE = {}
+
+
+def side_stream(dev, lane):
+    """The process-wide side stream of `lane` on `dev`: every Step shares them, so the
+    sampler chain (the current stream) and the side lanes stay on distinct hardware queues
+    (HIP maps streams to GPU_MAX_HW_QUEUES queues round-robin at creation)."""
+    key = (str(dev), lane)
+    if key not in _SIDE:
+        _SIDE[key] = torch.cuda.Stream(device=dev)
+    return _SIDE[key]
+
+
+class Task:
+    """One piece of a step: `fn` runs on stream `lane` (0 = the sampler chain, 1.. = side
+    streams) after the tasks named in `deps` (same-lane order is implicit)."""
+
+    def __init__(self, name, lane, deps, fn):
+        self.name, self.lane, self.deps, self.fn = name, lane, tuple(deps), fn
+
+
 class Step:
-    """One benchmark step, split in two phases so that the dominant kernel (the SA1 sampler)
-    can be timed on its own: sampler() runs FPS + gather of the first SA layer, rest() runs
-    everything after it and returns the step's outputs. __call__ runs both.
+    """One benchmark step as a list of tasks over streams.
 
-    The samplers of SA2..SA4 form a serial chain (each samples the previous layer's output)
-    that keeps only B workgroups busy, so with overlap=True (default) rest() runs that chain
-    on the current stream and forks everything that hangs off it onto a side stream:
-    layer i's ball query / grouping / attention and the FP layer that interpolates onto
-    level i-1 start as soon as sampler i has finished (one event per layer) and run
-    concurrently with samplers i+1.. . The side stream joins back before rest() returns, so
-    the caller sees one ordered stream (and hipGraph capture records the fork/join).
-    Intermediates live on self for the life of the step: nothing made on one stream is freed
-    while the other may still read it."""
+    The FPS samplers form a serial chain (each samples the previous layer's output) that
+    keeps only B workgroups busy; it runs on lane 0 with nothing else in its way. Everything
+    that hangs off sampler i -- layer i's ball query / grouping / attention (lane 1) and the
+    FP layer that interpolates onto level i-1 (lane 2; MSG: one lane per radius) -- waits for
+    that sampler only and runs concurrently with the samplers after it and with each other.
+    The SA1 ball-query grid needs only the input cloud and is built on lane 1 while SA1 is
+    sampled. Lanes join lane 0 at the end of the step.
 
-    def __init__(self, inp, overlap=True):
+    With overlap=False every task runs in order on the current stream (lanes collapse).
+    run() executes the tasks eagerly; GraphStep captures one hipGraph per task and replays
+    them with the same cross-stream events, so the graph executor never reorders the chain
+    behind side work. `sampler_events` brackets the SA1 sampler task (bench.py's roofline).
+    Intermediates live on self for the life of the step."""
+
+    SAMPLER = "fps1"
+
+    def __init__(self, inp, overlap=True, streams=None):
         self.inp = inp
         self.kind = CONFIGS[inp["config"]][1]
-        self.new_xyz1 = None
         self.overlap = overlap and inp["xyz"].is_cuda
+        self.v = {}  # intermediates by name
+        self.tasks = self._tasks_ssg() if self.kind == "ssg" else self._tasks_msg()
+        self.ran = False
+        self.synced_inputs = False
+        self.nlanes = 1 + max(t.lane for t in self.tasks)
         if self.overlap:
-            self.side = torch.cuda.Stream(device=inp["xyz"].device)
-            self.ready = [torch.cuda.Event() for _ in range(4)]
-        self.keep = []
+            dev = inp["xyz"].device
+            self.streams = [None] + (list(streams[1:self.nlanes]) if streams else
+                                     [side_stream(dev, lane) for lane in range(1, self.nlanes)])
+            self.done = {t.name: torch.cuda.Event() for t in self.tasks}
+            self.lane_done = [torch.cuda.Event() for _ in range(self.nlanes)]
 
-    def sampler(self):
-        """SA1 FPS + gather. With overlap, the SA1 ball-query grid over the input cloud is
-        built on the side stream meanwhile (it needs only xyz) and joined before returning."""
-        npoint = SSG_SA[0][0] if self.kind == "ssg" else MSG_SA[0][0]
-        xyz = self.inp["xyz"]
-        self.grid1 = None
-        build = (self.overlap and self.kind == "ssg"
-                 and int(xyz.shape[1]) >= tf_grouping.GRID_MIN_POINTS)
-        if build:
-            main = torch.cuda.current_stream(xyz.device)
-            self.side.wait_stream(main)
-            with torch.cuda.stream(self.side):
-                self.grid1 = tf_grouping.BallGrid(xyz, SSG_SA[0][1])
-        _, self.new_xyz1 = tf_sampling.farthest_point_sample_and_gather(npoint, xyz)
-        if build:
-            main.wait_stream(self.side)
-        return self.new_xyz1
-
-    def rest(self):
-        return self._rest_ssg() if self.kind == "ssg" else self._rest_msg()
-
-    def __call__(self):
-        self.sampler()
-        return self.rest()
-
-    def _fork(self, layer):
-        """Context for layer `layer`'s dependent work: the side stream after sampler `layer`."""
-        if not self.overlap:
-            return _Same()
-        main = torch.cuda.current_stream(self.inp["xyz"].device)
-        self.ready[layer].record(main)
-        self.side.wait_event(self.ready[layer])
-        return torch.cuda.stream(self.side)
-
-    def _join(self, outs):
-        if self.overlap:
-            main = torch.cuda.current_stream(self.inp["xyz"].device)
-            main.wait_stream(self.side)
-            if not torch.cuda.is_current_stream_capturing():
-                for t in outs:  # made on the side stream, consumed on main from here on
-                    t.record_stream(main)
-        return outs
-
-    def _rest_ssg(self):
-        inp = self.inp
-        xyz = [inp["xyz"], self.new_xyz1]
+    # ------------------------------------------------------------------ task lists
+    def _tasks_ssg(self):
+        inp, v = self.inp, self.v
+        big = int(inp["xyz"].shape[1]) >= tf_grouping.GRID_MIN_POINTS
         points = [inp["feats"]] + list(inp["sa_out"])  # l0 = None (cfg2) / rgb+normals (cfg3)
         # FP layer k interpolates level lvl+1 onto lvl (pointnet2_sem_seg_attention.py:46-53);
         # level lvl+1's features are the SA4 output (k=0) or the previous FP MLP's stand-in.
         fp_feat = [inp["sa_out"][3]] + list(inp["fp_out"])
-        sa_outs, fp_outs = [None] * 4, [None] * 4
-        for i, (npoint, radius, nsample, _) in enumerate(SSG_SA):
-            if i > 0:
-                xyz.append(tf_sampling.farthest_point_sample_and_gather(npoint, xyz[i])[1])
-            with self._fork(i):
-                new_xyz = xyz[i + 1]
-                idx, _ = tf_grouping.query_ball_point(radius, nsample, xyz[i], new_xyz,
-                                                      grid=self.grid1 if i == 0 else None)
-                new_points, _ = pointnet_util.group_concat(xyz[i], points[i], new_xyz, idx,
+        v["xyz"] = [inp["xyz"], None, None, None, None]
+        v["sa"], v["fp"] = [None] * 4, [None] * 4
+        tasks = []
+        if big:  # the SA1 grid over the input cloud (also orders FP4's neighbour search)
+            tasks.append(Task("grid1", 1, (), lambda: v.__setitem__(
+                "grid1", tf_grouping.BallGrid(inp["xyz"], SSG_SA[0][1]))))
+
+        def fps(i):
+            def f():
+                v["xyz"][i + 1] = tf_sampling.farthest_point_sample_and_gather(
+                    SSG_SA[i][0], v["xyz"][i])[1]
+            return f
+
+        def sa(i):
+            def f():
+                _, radius, nsample, _ = SSG_SA[i]
+                xyz, new_xyz = v["xyz"][i], v["xyz"][i + 1]
+                idx, _ = tf_grouping.query_ball_point(radius, nsample, xyz, new_xyz,
+                                                      grid=v.get("grid1") if i == 0 else None)
+                new_points, _ = pointnet_util.group_concat(xyz, points[i], new_xyz, idx,
                                                            want_grouped_xyz=False)
-                sa_outs[i] = [new_points]
+                out = [new_points]
                 if "attn" in inp:  # attention instead of pooling (attention_layer.py:256-261)
-                    Q, K, V = inp["attn"][i]
-                    sa_outs[i].append(attention_layer.attention_reduce(Q, K, V))
+                    out.append(attention_layer.attention_reduce(*inp["attn"][i]))
+                v["sa"][i] = out
+            return f
+
+        def fp(i):
+            def f():
                 k = 3 - i  # the FP layer whose coarse level (i+1) just became available
-                # FP4's unknown points are SA1's input cloud: the SA1 grid orders its search
-                fp_outs[k] = pointnet_util.fp_interpolate(
-                    xyz[i], xyz[i + 1], points[i], fp_feat[k],
-                    unknown_grid=self.grid1 if i == 0 else None)
-        self.keep = xyz
-        return self._join([t for o in sa_outs for t in o] + fp_outs)
+                v["fp"][k] = pointnet_util.fp_interpolate(
+                    v["xyz"][i], v["xyz"][i + 1], points[i], fp_feat[k],
+                    unknown_grid=v.get("grid1") if i == 0 else None)
+            return f
 
-    def _rest_msg(self):
-        inp = self.inp
-        xyz, points, new_xyz = inp["xyz"], None, self.new_xyz1
-        outs = []
-        kept = [new_xyz]
-        for i, (npoint, radii, nsamples, _) in enumerate(MSG_SA):
-            if i > 0:
-                _, new_xyz = tf_sampling.farthest_point_sample_and_gather(npoint, xyz)
-                kept.append(new_xyz)
-            with self._fork(i):
-                for radius, nsample in zip(radii, nsamples):
-                    idx, _ = tf_grouping.query_ball_point(radius, nsample, xyz, new_xyz)
-                    gp, _ = pointnet_util.group_concat(xyz, points, new_xyz, idx, xyz_last=True,
-                                                       want_grouped_xyz=False)
-                    outs.append(gp)
-            xyz, points = new_xyz, inp["sa_out"][0]
-        self.keep = kept
-        return self._join(outs)
+        # lane 0: SA1's sampler alone (it is what bench.py times), then SA2..SA4's samplers as
+        # one task (short; one boundary instead of three on the critical chain)
+        tasks.append(Task("fps1", 0, (), fps(0)))
+        tasks.append(Task("fps234", 0, (), lambda: [fps(i)() for i in (1, 2, 3)]))
+        grid_dep = ("grid1",) if big else ()
+        tasks.append(Task("sa1", 1, ("fps1",), sa(0)))
+        tasks.append(Task("fp4", 2, ("fps1",) + grid_dep, fp(0)))
+        for i in (1, 2, 3):
+            tasks.append(Task(f"sa{i + 1}", 1, ("fps234",), sa(i)))
+        tasks.append(Task("fp3", 2, ("fps234",), fp(1)))
+        tasks.append(Task("fp2", 3, ("fps234",), fp(2)))
+        tasks.append(Task("fp1", 3, ("fps234",), fp(3)))
+        return tasks
 
+    def _tasks_msg(self):
+        inp, v = self.inp, self.v
+        v["xyz"] = [inp["xyz"], None, None]
+        v["gp"] = {}
+        tasks = []
 
-class _Same:
-    def __enter__(self):
-        return self
+        def fps(i):
+            def f():
+                v["xyz"][i + 1] = tf_sampling.farthest_point_sample_and_gather(
+                    MSG_SA[i][0], v["xyz"][i])[1]
+            return f
 
-    def __exit__(self, *exc):
-        return False
+        def grp(i, r):
+            def f():
+                radius, nsample = MSG_SA[i][1][r], MSG_SA[i][2][r]
+                points = None if i == 0 else inp["sa_out"][0]
+                xyz, new_xyz = v["xyz"][i], v["xyz"][i + 1]
+                idx, _ = tf_grouping.query_ball_point(radius, nsample, xyz, new_xyz)
+                v["gp"][(i, r)] = pointnet_util.group_concat(xyz, points, new_xyz, idx,
+                                                             xyz_last=True,
+                                                             want_grouped_xyz=False)[0]
+            return f
+
+        for i in range(len(MSG_SA)):
+            tasks.append(Task(f"fps{i + 1}", 0, (), fps(i)))
+            for r in range(len(MSG_SA[i][1])):
+                tasks.append(Task(f"sa{i + 1}_{r}", 1 + r, (f"fps{i + 1}",), grp(i, r)))
+        return tasks
+
+    def outputs(self):
+        v = self.v
+        if self.kind == "ssg":
+            return [t for o in v["sa"] for t in o] + list(v["fp"])
+        return [v["gp"][k] for k in sorted(v["gp"])]
+
+    # ------------------------------------------------------------------ execution
+    def _stream(self, lane, main):
+        return main if (lane == 0 or not self.overlap) else self.streams[lane]
+
+    def run(self, sampler_events=None, launch=None, join=True):
+        """Execute every task: launch(task) (default: its fn) on its lane's stream after its
+        cross-lane dependencies; lanes join the current stream at the end unless join=False
+        (then call join() before reading the outputs)."""
+        main = torch.cuda.current_stream(self.inp["xyz"].device) if self.inp["xyz"].is_cuda \
+            else None
+        launch = launch or (lambda t: t.fn())
+        self.ran = True
+        if not self.overlap:
+            for t in self.tasks:
+                if t.name == self.SAMPLER and sampler_events is not None:
+                    sampler_events[0].record()
+                launch(t)
+                if t.name == self.SAMPLER and sampler_events is not None:
+                    sampler_events[1].record()
+            return self.outputs()
+        lane_of = {t.name: t.lane for t in self.tasks}
+        if not self.synced_inputs:  # the resident inputs were written on the current stream
+            for lane in range(1, self.nlanes):
+                self.streams[lane].wait_stream(main)
+            self.synced_inputs = True
+        for t in self.tasks:
+            st = self._stream(t.lane, main)
+            for d in t.deps:
+                if lane_of[d] != t.lane:
+                    st.wait_event(self.done[d])
+            timed = t.name == self.SAMPLER and sampler_events is not None
+            with torch.cuda.stream(st):
+                if timed:
+                    sampler_events[0].record(st)
+                launch(t)
+            if any(t.name in u.deps for u in self.tasks):
+                if timed:  # one event both times the sampler and releases its dependents
+                    self.done[t.name] = sampler_events[1]
+                self.done[t.name].record(st)
+            elif timed:
+                sampler_events[1].record(st)
+        # the step's side work is complete when lane 1 is: lanes 2.. hand their last work to it
+        # (off the critical chain), so the chain waits on ONE event before reusing buffers
+        for lane in range(2, self.nlanes):
+            self.lane_done[lane].record(self.streams[lane])
+            self.streams[1].wait_event(self.lane_done[lane])
+        self.lane_done[1].record(self.streams[1])
+        return self.join() if join else None
+
+    def join(self):
+        """Make the current stream wait for every lane; returns the outputs (None before the
+        first run)."""
+        if not self.ran:
+            return None
+        outs = self.outputs()
+        if self.overlap:
+            main = torch.cuda.current_stream(self.inp["xyz"].device)
+            main.wait_event(self.lane_done[1])
+            if not torch.cuda.is_current_stream_capturing():
+                for o in outs:  # made on side streams, consumed on the current stream from here
+                    o.record_stream(main)
+        return outs
+
+    def __call__(self):
+        return self.run()
 
 
 def run(inp):
@@ -194,33 +286,81 @@ def run(inp):
 
 
 class GraphStep:
-    """The step captured as two hipGraphs (sampler, rest) sharing one memory pool; replay()
-    launches both on the current stream. Inputs stay resident, outputs are overwritten in
-    place at every replay."""
+    """The step with every task captured as its own hipGraph (one shared memory pool), each
+    on its lane's stream; replay() relaunches them with the same cross-stream events as the
+    eager step. Inputs stay resident, outputs are overwritten in place at every replay."""
 
     def __init__(self, inp, warmup=2, overlap=True):
         self.step = Step(inp, overlap=overlap)
-        side = torch.cuda.Stream()
-        side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(side):
+        dev = inp["xyz"].device
+        warm = side_stream(dev, "warm")
+        warm.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(warm):
             for _ in range(warmup):
-                self.step()
-        torch.cuda.current_stream().wait_stream(side)
-        self.g_sampler = torch.cuda.CUDAGraph()
-        self.g_rest = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.g_sampler):
-            self.step.sampler()
-        with torch.cuda.graph(self.g_rest, pool=self.g_sampler.pool()):
-            self.outs = self.step.rest()
+                self.step.run()
+        torch.cuda.current_stream(dev).wait_stream(warm)
+        torch.cuda.synchronize(dev)
+        # One memory pool PER LANE: graphs of one lane replay in capture order on one stream,
+        # so a block one of them frees may be reused by a later one; graphs of different
+        # lanes replay concurrently and must never share a block. (Tensors passed between
+        # lanes live in self.step.v and are never freed.)
+        pools = {}
+        self.graphs = {}
+        cap = side_stream(dev, "capture")
 
-    def replay(self, sampler_events=None):
-        if sampler_events is not None:
-            sampler_events[0].record()
-        self.g_sampler.replay()
-        if sampler_events is not None:
-            sampler_events[1].record()
-        self.g_rest.replay()
+        def capture(t):
+            g = torch.cuda.CUDAGraph()
+            st = torch.cuda.current_stream(dev)
+            cap.wait_stream(st)
+            lane = t.lane if self.step.overlap else 0
+            if lane not in pools:
+                pools[lane] = torch.cuda.graph_pool_handle()
+            with torch.cuda.graph(g, pool=pools[lane], stream=cap):
+                t.fn()
+            st.wait_stream(cap)
+            self.graphs[t.name] = g
+
+        self.step.run(launch=capture)
+        torch.cuda.synchronize(dev)
+        self.outs = self.step.outputs()
+
+    def replay(self, sampler_events=None, join=True):
+        self.step.run(sampler_events, launch=lambda t: self.graphs[t.name].replay(), join=join)
         return self.outs
+
+    def join(self):
+        self.step.join()
+        return self.outs
+
+
+class Pipeline:
+    """Consecutive steps software-pipelined over two buffer sets: step k runs on set k % 2,
+    its side-lane work (ball query, grouping, attention, FP) finishing while step k+1's
+    sampler chain already runs on the shared lane-0 stream. Before a set is reused (step
+    k+2) lane 0 waits for that set's side lanes, so no buffer is overwritten while read.
+    Every step still does all of its work; run(k) returns after enqueueing, join() waits."""
+
+    def __init__(self, inp, graphs=True, overlap=True):
+        mk = (lambda: GraphStep(inp, overlap=overlap)) if graphs else \
+            (lambda: Step(inp, overlap=overlap))
+        self.sets = [mk(), mk()]
+        self.k = 0
+
+    def run(self, sampler_events=None):
+        s = self.sets[self.k % 2]
+        self.k += 1
+        if isinstance(s, GraphStep):
+            s.step.join()  # lane 0 waits for this set's previous side work (long finished)
+            return s.replay(sampler_events, join=False)
+        s.join()
+        return s.run(sampler_events, join=False)
+
+    def join(self):
+        """Wait for everything enqueued; returns the outputs of the last step run."""
+        for s in self.sets:
+            s.join()
+        return self.sets[(self.k - 1) % 2].join()
+
 
 
 def sa_fp_bytes(config, B):

@@ -525,3 +525,21 @@ def test_side_stream_overlap_matches_single_stream(env, config, B):
     torch.cuda.synchronize()
     for a, b in zip(single, outs):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("graphs", [True, False])
+def test_pipelined_steps_match_single_stream(env, graphs):
+    """Software-pipelined steps (two buffer sets, bench.py's default) produce, in both sets,
+    exactly the single-stream step's outputs."""
+    pkg, O, torch, dev = env
+    inp = pkg.stack.make_inputs("cfg2", list(range(30, 34)), dev)
+    single = [o.clone() for o in pkg.stack.Step(inp, overlap=False)()]
+    pipe = pkg.stack.Pipeline(inp, graphs=graphs)
+    for _ in range(5):
+        pipe.run()
+    last = pipe.join()
+    torch.cuda.synchronize()
+    for outs in [last] + [s.join() for s in pipe.sets]:
+        assert len(outs) == len(single)
+        for a, b in zip(single, outs):
+            assert torch.equal(a, b)

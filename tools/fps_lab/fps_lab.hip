@@ -1307,6 +1307,7 @@ int fps_tune_impl(const float* xyz, int B, int N, int M, int32_t* idx, float* nx
     PN2_V9G(64, 4) PN2_V9G(64, 8) PN2_V9G(128, 4) PN2_V9G(128, 8) PN2_V9G(256, 4)
     PN2_V9G(256, 8) PN2_V9G(256, 16) PN2_V9G(512, 4) PN2_V9G(512, 8) PN2_V9G(512, 16)
     PN2_V9G(256, 32) PN2_V9(512, 32, 4) PN2_V9(256, 64, 4) PN2_V9(128, 16, 4) PN2_V9(128, 1, 1)
+    PN2_V9(64, 16, 4) PN2_V9(64, 32, 4) PN2_V9(128, 32, 4)
     PN2_V9(64, 1, 1) PN2_V9(64, 2, 1) PN2_V9(64, 2, 2) PN2_V9(128, 2, 2) PN2_V9(256, 2, 2)
 #undef PN2_V9G
 #undef PN2_V9

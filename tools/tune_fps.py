@@ -23,7 +23,8 @@ V2 = [(64, 1), (64, 2), (64, 4), (64, 8), (64, 16), (128, 4), (128, 8), (128, 16
 V9 = [(bl, pp, g) for bl, pp in [(64, 4), (64, 8), (128, 4), (128, 8), (256, 4), (256, 8),
                                  (256, 16), (512, 4), (512, 8), (512, 16), (256, 32)]
       for g in (1, 2, 4)] + [(64, 1, 1), (64, 2, 1), (64, 2, 2), (128, 2, 2), (256, 2, 2),
-                             (512, 32, 4), (256, 64, 4), (128, 16, 4), (128, 1, 1)]
+                             (512, 32, 4), (256, 64, 4), (128, 16, 4), (128, 1, 1),
+                             (64, 16, 4), (64, 32, 4), (128, 32, 4)]
 
 
 def candidates(N, slack):
