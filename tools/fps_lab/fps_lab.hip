@@ -7,6 +7,139 @@
 namespace pn2 {
 namespace {
 
+// Variant 11 (measured SLOWER than v9: 808 vs 768 us at SA1; tools/stamp_fps.py shows the
+// uniform-index moves and readlane chains cost more latency than the branch chain and the
+// LDS centre load they replace). v9's layout and scan with a shorter tail. The winner's slot inside its group
+// and its coordinates are read straight out of the winning lane's registers with
+// uniform-index register moves (s_set_gpr_idx + v_readlane: no branch chain), and each
+// wave publishes (max, index, x, y, z) so that after the barrier the new centre comes from
+// v_readlane of the winning wave's entry instead of a dependent LDS load. No LDS copy of
+// the cloud is needed.
+template <int BLOCK, int PPT, int G, bool STAMP = false>
+__global__ __launch_bounds__(BLOCK) void fps_v11_kernel(const float* __restrict__ xyz, int N,
+                                                        int M, int32_t* __restrict__ idx,
+                                                        float* __restrict__ new_xyz) {
+  unsigned long long st_acc[6] = {0, 0, 0, 0, 0, 0}, st_prev = 0;
+  using Lay = Lay9<BLOCK, PPT>;
+  constexpr int NW = BLOCK / kWave;
+  static_assert(BLOCK % kWave == 0 && NW <= 8, "the block step reduces 8 DPP lanes");
+  static_assert(PPT % G == 0 && (G == 1 || G == 2 || G == 4), "slot groups");
+  constexpr int NG = PPT / G;
+  __shared__ uint2 red_k[2][8];
+  __shared__ float4 red_c[2][8];
+
+  const int b = blockIdx.x;
+  const int t = threadIdx.x;
+  const int lane = t & (kWave - 1);
+  const int w = t / kWave;
+  const float* __restrict__ P = xyz + (size_t)b * N * 3;
+  int32_t* __restrict__ I = idx + (size_t)b * M;
+  float* __restrict__ NX = new_xyz ? new_xyz + (size_t)b * M * 3 : nullptr;
+
+  float px[PPT], py[PPT], pz[PPT];
+  int tb[PPT];  // running min distance as int bits; padding slots -1 never win
+#pragma unroll
+  for (int s = 0; s < PPT; ++s) {
+    const int k = Lay::point(t, s);
+    if (k < N) {
+      px[s] = P[3 * k + 0];
+      py[s] = P[3 * k + 1];
+      pz[s] = P[3 * k + 2];
+      tb[s] = __float_as_int(kInitTemp);
+    } else {
+      px[s] = py[s] = pz[s] = 0.0f;
+      tb[s] = -1;
+    }
+  }
+
+  float cx = P[0], cy = P[1], cz = P[2];
+  if (t == 0) {
+    I[0] = 0;
+    if (NX) { NX[0] = cx; NX[1] = cy; NX[2] = cz; }
+  }
+
+  if constexpr (STAMP) {
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_prev)::"memory");
+  }
+  for (int j = 1; j < M; ++j) {
+    int bd = -1, bg = 0;
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      int v[G];
+#pragma unroll
+      for (int q = 0; q < G; ++q) {
+        const int s = g * G + q;
+        v[q] = min(__float_as_int(sqdist(px[s], py[s], pz[s], cx, cy, cz)), tb[s]);
+        tb[s] = v[q];
+      }
+      int m;
+      if constexpr (G == 4) m = max(max(max(max(v[0], v[1]), v[2]), v[3]), bd);
+      else if constexpr (G == 2) m = max(max(v[0], v[1]), bd);
+      else m = max(v[0], bd);
+      bg = m > bd ? g : bg;
+      bd = m;
+    }
+    const uint32_t hi = (uint32_t)(bd + 1);  // 0 for lanes with padding only
+    PN2_STAMP(0)
+    const uint32_t km = wave_max_u32(hi);
+    PN2_STAMP(1)
+    // lowest lane holding the wave max (lane order is tie order), its first slot holding it
+    const uint64_t hold = __builtin_amdgcn_ballot_w64(hi == km);
+    const int L = (int)__builtin_amdgcn_readfirstlane((int)__builtin_ctzll(hold));
+    // everything below is wave-uniform (SGPRs): scalar compares, uniform-index moves
+    const int base = __builtin_amdgcn_readlane(bg, L) * G;
+    const int kv = __builtin_amdgcn_readfirstlane((int)km) - 1;
+    int sq = base + G - 1;
+#pragma unroll
+    for (int q = G - 2; q >= 0; --q)
+      if (__builtin_amdgcn_readlane(tb[base + q], L) == kv) sq = base + q;
+    sq = __builtin_amdgcn_readfirstlane(sq);
+    int old = Lay::point(w * kWave + L, sq);
+    float wx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(px[sq]), L));
+    float wy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(py[sq]), L));
+    float wz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(pz[sq]), L));
+    PN2_STAMP(2)
+    if constexpr (NW > 1) {
+      if (lane == 0) {
+        red_k[j & 1][w] = make_uint2(km, (uint32_t)old);
+        red_c[j & 1][w] = make_float4(wx, wy, wz, 0.0f);
+      }
+      __syncthreads();
+      PN2_STAMP(3)
+      const int e = lane & 7;
+      const uint2 r = e < NW ? red_k[j & 1][e] : make_uint2(0u, 0u);
+      const float4 c = red_c[j & 1][e < NW ? e : 0];
+      uint32_t bm = max_dpp_u32<kDppXor1>(r.x);
+      if constexpr (NW > 2) bm = max_dpp_u32<kDppXor2>(bm);
+      if constexpr (NW > 4) bm = max_dpp_u32<kDppHalfMirror>(bm);
+      const uint64_t wins = __builtin_amdgcn_ballot_w64(r.x == bm) & 0xFFull;
+      const int wi = (int)__builtin_amdgcn_readfirstlane((int)__builtin_ctzll(wins));
+      old = __builtin_amdgcn_readlane((int)r.y, wi);
+      wx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(c.x), wi));
+      wy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(c.y), wi));
+      wz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(c.z), wi));
+    }
+    PN2_STAMP(4)
+    cx = wx; cy = wy; cz = wz;
+    if (t == 0) {
+      I[j] = old;
+      if (NX) { NX[3 * j + 0] = cx; NX[3 * j + 1] = cy; NX[3 * j + 2] = cz; }
+    }
+    PN2_STAMP(5)
+  }
+  if constexpr (STAMP) {
+    if (lane == 0 && blockIdx.x < 16)
+      for (int ph = 0; ph < 6; ++ph) g_stamp[(blockIdx.x * 16 + w) * 8 + ph] = st_acc[ph];
+  }
+}
+
+template <int BLOCK, int PPT, int G>
+void launch_v11(const float* xyz, int B, int N, int M, int32_t* idx, float* nx, hipStream_t s) {
+  hipLaunchKernelGGL((fps_v11_kernel<BLOCK, PPT, G>), dim3(B), dim3(BLOCK), 0, s, xyz, N, M, idx,
+                     nx);
+}
+
+
 // Variant 2 of the register sampler: the same selection, cheaper arithmetic.
 //  * the running min-distance is kept as int32 bit patterns: for d >= 0 (or NaN) and
 //    temp in {-1} U [0, 1e38] a signed-int min of the bits is exactly fminf (no IEEE-mode
@@ -1296,6 +1429,19 @@ int fps_tune_impl(const float* xyz, int B, int N, int M, int32_t* idx, float* nx
   }
   PN2_FPS_CONFIGS(PN2_X)
 #undef PN2_X
+  if (variant >= 111 && variant <= 114) {  // v11, variant = 110 + G
+    const int G = variant - 110;
+#define PN2_V11(BL, PP, GG)                                                    \
+    if (block == BL && ppt == PP && G == GG) {                                 \
+      launch_v11<BL, PP, GG>(xyz, B, N, M, idx, nx, s);                        \
+      PN2_RETURN_LAUNCH();                                                     \
+    }
+    PN2_V11(64, 1, 1) PN2_V11(64, 2, 2) PN2_V11(64, 4, 4) PN2_V11(64, 8, 4) PN2_V11(256, 4, 4)
+    PN2_V11(256, 8, 4) PN2_V11(256, 16, 4) PN2_V11(256, 32, 4) PN2_V11(512, 16, 4)
+    PN2_V11(512, 32, 4) PN2_V11(128, 8, 4) PN2_V11(64, 16, 4) PN2_V11(128, 4, 4)
+    PN2_V11(256, 32, 2) PN2_V11(512, 16, 2) PN2_V11(256, 64, 4)
+#undef PN2_V11
+  }
   if (variant >= 91 && variant <= 94) {  // v9, variant = 90 + G (slots per max3 group)
     const int G = variant - 90;
 #define PN2_V9(BL, PP, GG)                                                     \
@@ -1407,6 +1553,14 @@ int pn2_fps_stamp(const float* xyz, int N, int npoint, int32_t* idx, int block, 
     } else
     PN2_S6(512, 16, 4) PN2_S6(1024, 8, 4) PN2_S6(256, 4, 2) PN2_S6(512, 16, 8) { return PN2_EINVAL; }
 #undef PN2_S6
+  } else if (ppt >= 110000) {  // v11 (G = 4) stamped: ppt = 110000 + PP
+#define PN2_S11(BL, PP)                                                                      \
+    if (block == BL && ppt == 110000 + PP) {                                                 \
+      hipLaunchKernelGGL((pn2::fps_v11_kernel<BL, PP, 4, true>), dim3(1), dim3(BL), 0, s,    \
+                         xyz, N, npoint, idx, nullptr);                                      \
+    } else
+    PN2_S11(256, 32) PN2_S11(512, 16) PN2_S11(256, 4) { return PN2_EINVAL; }
+#undef PN2_S11
   } else if (ppt >= 90000) {  // v9 (G = 4) stamped: ppt = 90000 + PP
 #define PN2_S9(BL, PP)                                                                       \
     if (block == BL && ppt == 90000 + PP) {                                                  \

@@ -27,8 +27,14 @@ V9 = [(bl, pp, g) for bl, pp in [(64, 4), (64, 8), (128, 4), (128, 8), (256, 4),
                              (64, 16, 4), (64, 32, 4), (128, 32, 4)]
 
 
+V11 = [(64, 1, 1), (64, 2, 2), (64, 4, 4), (64, 8, 4), (256, 4, 4), (256, 8, 4), (256, 16, 4),
+       (256, 32, 4), (512, 16, 4), (512, 32, 4), (128, 8, 4), (64, 16, 4), (128, 4, 4),
+       (256, 32, 2), (512, 16, 2), (256, 64, 4)]
+
+
 def candidates(N, slack):
     c = [(2, bl, pp) for bl, pp in V2 if N <= bl * pp <= max(slack * N, 64)]
+    c += [(110 + g, bl, pp) for bl, pp, g in V11 if N <= bl * pp <= max(slack * N, 64)]
     c += [(90 + g, bl, pp) for bl, pp, g in V9 if N <= bl * pp <= max(slack * N, 64)]
     return c
 
