@@ -10,6 +10,8 @@
  *   GatherPointGrad      tf_sampling.cpp:150-178, .cu:183-192    → pn2_gather_point_grad
  *   QueryBallPoint       tf_grouping.cpp:66-106, _g.cu:3-36      → pn2_ball_query,
  *                                                                  pn2_ball_query_grid
+ *   SelectionSort        tf_grouping.cpp:108-137, _g.cu:83-123   → pn2_select_top_k
+ *   knn_point            tf_grouping.py:48-73                    → pn2_knn_point
  *   GroupPoint           tf_grouping.cpp:139-171, _g.cu:40-57    → pn2_group_point
  *   GroupPointGrad       tf_grouping.cpp:174-208, _g.cu:61-78    → pn2_group_point_grad
  *   ThreeNN              tf_interpolate.cpp:157-187, :60-103     → pn2_three_nn,
@@ -21,7 +23,8 @@
  *                                                                  pn2_group_concat
  *   pointnet_fp_module   pointnet_util.py:218-226 (geometry)     → pn2_fp_fused,
  *                                                                  pn2_fp_apply
- *   AttentionLayer.call  attention_layer.py:29-45 (reduction)    → pn2_attn_reduce
+ *   AttentionLayer.call  attention_layer.py:29-45 (reduction)    → pn2_attn_reduce,
+ *                                                                  pn2_attn_reduce_grad
  *   SA pooling           pointnet_util.py:130-145, :200          → pn2_group_pool
  *
  * (reference paths are under pointnet2_tensorflow/tf_ops/{sampling,grouping,interpolation_3d},
@@ -114,6 +117,21 @@ int pn2_grid_build(const float* xyz, int B, int N, float cell_edge, void* grid,
 int pn2_ball_query_grid(const void* grid, const float* xyz2, int B, int N, int M, float radius,
                         int nsample, int32_t* idx, int32_t* pts_cnt, pn2_stream_t stream);
 
+/* ---- k nearest neighbours ---------------------------------------------------------- *
+ * pn2_select_top_k: select_top_k / SelectionSort (tf_grouping.py:22-31, tf_grouping_g.cu:
+ *   83-123): outi, out (B,m,n) = each row of dist (B,m,n) after the reference's k-step
+ *   partial selection sort (first minimum by position, swapped to the front), i.e. the k
+ *   smallest first, ties in the order those swaps leave them, the rest permuted by the same
+ *   swaps. 0 < k <= min(n, 1024). workspace: pn2_select_top_k_workspace_size(B,m,k) bytes.
+ * pn2_knn_point: knn_point (tf_grouping.py:48-73): val, idx (B,m,k) = the first k columns of
+ *   select_top_k(k, dist) for dist[b,j,t] = sum over the c channels of (xyz1[b,t]-xyz2[b,j])^2
+ *   (summed left to right); the (B,m,n) matrix is never materialised. */
+int pn2_select_top_k(const float* dist, int B, int m, int n, int k, int32_t* outi, float* out,
+                     int32_t* workspace, pn2_stream_t stream);
+size_t pn2_select_top_k_workspace_size(int B, int m, int k);
+int pn2_knn_point(const float* xyz1, const float* xyz2, int B, int n, int m, int c, int k,
+                  float* val, int32_t* idx, pn2_stream_t stream);
+
 /* out (B,M,nsample,C) = points[b, idx[b,j,k], :] (tf_grouping_g.cu:40-57). */
 int pn2_group_point(const float* points, const int32_t* idx, int B, int N, int C, int M,
                     int nsample, float* out, pn2_stream_t stream);
@@ -185,6 +203,12 @@ int pn2_fp_apply(const float* dist, const int32_t* idx, const void* unknown_grid
  * out[4h:4h+4] = aᵀ V_h. C must be a multiple of 4. */
 int pn2_attn_reduce(const float* Q, const float* K, const float* V, int B, int M, int ns,
                     int C, float* out, pn2_stream_t stream);
+/* Backward of pn2_attn_reduce (TF autodiff of attention_layer.py:35-42): grad_Q (B,M,C),
+ * grad_K / grad_V (B,M,ns,C) from grad_out (B,M,C). Every element written (no accumulation);
+ * 16-byte aligned buffers, C % 4 == 0. */
+int pn2_attn_reduce_grad(const float* Q, const float* K, const float* V, const float* grad_out,
+                         int B, int M, int ns, int C, float* grad_Q, float* grad_K,
+                         float* grad_V, pn2_stream_t stream);
 /* Per-group pooling over nsample (pointnet_util.py:130-145): x (B,M,ns,C) → out (B,M,C),
  * or (B,M,2C) = [avg, max] for PN2_POOL_MAX_AND_AVG. grouped_xyz (B,M,ns,3) is read only
  * by PN2_POOL_WEIGHTED_AVG (w = exp(-5|xyz|)/sum). */

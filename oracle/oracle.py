@@ -23,6 +23,8 @@ REF_GPU_SO = os.path.join(HERE, "_ref", "libref_gpu.so")
 _P, _I, _F = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
 
 _ORACLE_SIGS = {
+    "pn2o_selection_sort": [_P, _I, _I, _I, _I, _P, _P],
+    "pn2o_knn_point": [_P, _P, _I, _I, _I, _I, _I, _P, _P],
     "pn2o_set_threads": [_I],
     "pn2o_fps": [_P, _I, _I, _I, _P],
     "pn2o_gather_point": [_P, _P, _I, _I, _I, _P],
@@ -48,6 +50,7 @@ _REF_CPU_SIGS = {
     "pn2ref_three_interpolate_grad": [_I, _I, _I, _I, _P, _P, _P, _P],
 }
 _REF_GPU_SIGS = {
+    "pn2ref_selection_sort": [_P, _I, _I, _I, _I, _P, _P],
     "pn2ref_fps": [_P, _I, _I, _I, _P],
     "pn2ref_gather_point": [_P, _P, _I, _I, _I, _P],
     "pn2ref_query_ball_point": [_P, _P, _I, _I, _I, _F, _I, _P, _P],
@@ -313,6 +316,27 @@ def ref_three_interpolate_grad(m, idx, weight, grad_out):
 
 
 # ---------------------------------------------------------------- the geometric stack on CPU
+
+def selection_sort(dist, k):
+    """select_top_k(k, dist) -> (outi, out), both (B,m,n) (tf_grouping.py:22-31)."""
+    dist = _f32(dist)
+    B, m, n = dist.shape
+    outi = np.zeros((B, m, n), np.int32)
+    out = np.zeros((B, m, n), np.float32)
+    olib().pn2o_selection_sort(_p(dist), B, m, n, int(k), _p(outi), _p(out))
+    return outi, out
+
+
+def knn_point(k, xyz1, xyz2):
+    """knn_point(k, xyz1, xyz2) -> (val, idx), (B,m,k) (tf_grouping.py:48-73)."""
+    xyz1, xyz2 = _f32(xyz1), _f32(xyz2)
+    B, n, c = xyz1.shape
+    m = xyz2.shape[1]
+    val = np.zeros((B, m, k), np.float32)
+    idx = np.zeros((B, m, k), np.int32)
+    olib().pn2o_knn_point(_p(xyz1), _p(xyz2), B, n, m, c, int(k), _p(val), _p(idx))
+    return val, idx
+
 
 def run_stack_cpu(inp_np, config):
     """The same step as stack.run(), on the CPU restatement (numpy inputs)."""

@@ -364,3 +364,65 @@ void pn2o_group_pool(const float* x, const float* gxyz, int B, int M, int ns, in
     free(w);
   }
 }
+
+/* select_top_k / SelectionSort, tf_grouping.py:22-31 -> selection_sort_gpu, tf_grouping_g.cu:83-123,
+ * restated literally: each row of dist (B,m,n) is copied with its positions, then for
+ * s = 0..k-1 the first position of the minimum over [s, n) (strict '<', :108) is swapped
+ * with s (:113-120). outi/out (B,m,n) are the whole permuted rows, as the reference writes. */
+void pn2o_selection_sort(const float* dist, int B, int m, int n, int k, int32_t* outi,
+                         float* out) {
+  RFOR
+  for (int b = 0; b < B; ++b) {
+    for (int j = 0; j < m; ++j) {
+      const size_t r = ((size_t)b * m + j) * n;
+      for (int s = 0; s < n; ++s) { out[r + s] = dist[r + s]; outi[r + s] = s; }
+      for (int s = 0; s < k && s < n; ++s) {
+        int mn = s;
+        for (int t = s + 1; t < n; ++t)
+          if (out[r + t] < out[r + mn]) mn = t;
+        if (mn != s) {
+          const float tv = out[r + mn]; out[r + mn] = out[r + s]; out[r + s] = tv;
+          const int32_t ti = outi[r + mn]; outi[r + mn] = outi[r + s]; outi[r + s] = ti;
+        }
+      }
+    }
+  }
+}
+
+/* knn_point, tf_grouping.py:48-73: dist = reduce_sum((xyz1 - xyz2)**2, -1) over the c
+ * channels (summed left to right, as Eigen's scalar inner reduction does), then
+ * select_top_k(k, dist) and the first k columns: val (B,m,k), idx (B,m,k). */
+void pn2o_knn_point(const float* xyz1, const float* xyz2, int B, int n, int m, int c, int k,
+                    float* val, int32_t* idx) {
+  RFOR
+  for (int b = 0; b < B; ++b) {
+    float* d = (float*)malloc(sizeof(float) * (n > 0 ? n : 1));
+    int32_t* p = (int32_t*)malloc(sizeof(int32_t) * (n > 0 ? n : 1));
+    for (int j = 0; j < m; ++j) {
+      const float* q = xyz2 + ((size_t)b * m + j) * c;
+      for (int t = 0; t < n; ++t) {
+        const float* x = xyz1 + ((size_t)b * n + t) * c;
+        float acc = 0.f;
+        for (int a = 0; a < c; ++a) {
+          const float e = x[a] - q[a];
+          acc = a == 0 ? e * e : acc + e * e;
+        }
+        d[t] = acc;
+        p[t] = t;
+      }
+      for (int s = 0; s < k && s < n; ++s) {
+        int mn = s;
+        for (int t = s + 1; t < n; ++t)
+          if (d[t] < d[mn]) mn = t;
+        if (mn != s) {
+          const float tv = d[mn]; d[mn] = d[s]; d[s] = tv;
+          const int32_t ti = p[mn]; p[mn] = p[s]; p[s] = ti;
+        }
+        val[((size_t)b * m + j) * k + s] = d[s];
+        idx[((size_t)b * m + j) * k + s] = p[s];
+      }
+    }
+    free(d);
+    free(p);
+  }
+}

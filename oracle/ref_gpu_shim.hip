@@ -15,6 +15,7 @@ void queryBallPointLauncher(int b, int n, int m, float radius, int nsample, cons
                             const float* xyz2, int* idx, int* pts_cnt);
 void groupPointLauncher(int b, int n, int c, int m, int nsample, const float* points,
                         const int* idx, float* out);
+void selectionSortLauncher(int b, int n, int m, int k, const float* dist, int* outi, float* out);
 
 extern "C" {
 // tf_sampling.cpp:114-118: temp workspace of 32 x n floats
@@ -34,6 +35,12 @@ int pn2ref_gather_point(const float* inp, const int32_t* idx, int b, int n, int 
 int pn2ref_query_ball_point(const float* xyz1, const float* xyz2, int b, int n, int m,
                             float radius, int nsample, int32_t* idx, int32_t* pts_cnt) {
   queryBallPointLauncher(b, n, m, radius, nsample, xyz1, xyz2, idx, pts_cnt);
+  return (int)hipDeviceSynchronize();
+}
+// tf_grouping.cpp:134 -> selection_sort_gpu (tf_grouping_g.cu:83-123)
+int pn2ref_selection_sort(const float* dist, int b, int m, int n, int k, int32_t* outi,
+                          float* out) {
+  selectionSortLauncher(b, n, m, k, dist, outi, out);
   return (int)hipDeviceSynchronize();
 }
 int pn2ref_group_point(const float* points, const int32_t* idx, int b, int n, int c, int m,

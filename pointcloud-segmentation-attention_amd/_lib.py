@@ -43,6 +43,9 @@ SIGNATURES = {
     "pn2_gather_point_grad": (_I, [_P, _P, _I, _I, _I, _P, _P]),
     "pn2_ball_query": (_I, [_P, _P, _I, _I, _I, _F, _I, _P, _P, _P]),
     "pn2_ball_threshold": (_F, [_F]),
+    "pn2_select_top_k": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _P]),
+    "pn2_select_top_k_workspace_size": (_S, [_I, _I, _I]),
+    "pn2_knn_point": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _P, _P]),
     "pn2_grid_size": (_S, [_I, _I]),
     "pn2_grid_build": (_I, [_P, _I, _I, _F, _P, _S, _P]),
     "pn2_ball_query_grid": (_I, [_P, _P, _I, _I, _I, _F, _I, _P, _P, _P]),
@@ -59,6 +62,7 @@ SIGNATURES = {
     "pn2_idw_weights": (_I, [_P, _I, _I, _P, _P]),
     "pn2_fp_fused": (_I, [_P, _P, _P, _I, _P, _I, _I, _I, _I, _P, _P]),
     "pn2_attn_reduce": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P]),
+    "pn2_attn_reduce_grad": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P]),
     "pn2_group_pool": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _P]),
 }
 

@@ -132,6 +132,71 @@ __global__ __launch_bounds__(kBlock) void attn_reduce_generic_kernel(
   }
 }
 
+// Backward of the reduction (what TF's autodiff of attention_layer.py:35-42 computes), one wave
+// per (group, head), lanes striding over the ns pseudo-keys. With s_i = q.K_i / 2,
+// a = softmax(s), o = sum_i a_i V_i and the incoming gradient dO (4 floats per head):
+//   dV_i = a_i dO,   ds_i = a_i (dO.V_i - dO.o),   dK_i = ds_i q / 2,   dq = sum_i ds_i K_i / 2.
+// The forward is recomputed (max, normaliser, o) so nothing is stored between the passes.
+__global__ __launch_bounds__(kBlock) void attn_reduce_grad_kernel(
+    const float* __restrict__ Q, const float* __restrict__ K, const float* __restrict__ V,
+    const float* __restrict__ dO, int G, int ns, int C, float* __restrict__ dQ,
+    float* __restrict__ dK, float* __restrict__ dV) {
+  const int lane = lane_id();
+  const int H = C / 4;
+  const long long tasks = (long long)G * H;
+  const long long nwaves = (long long)gridDim.x * kWavesPerBlock;
+  for (long long task = (long long)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave; task < tasks;
+       task += nwaves) {
+    const long long g = task / H;
+    const int h = (int)(task - g * H);
+    const float4 q = *reinterpret_cast<const float4*>(Q + g * C + 4 * h);
+    const float4 go = *reinterpret_cast<const float4*>(dO + g * C + 4 * h);
+    const size_t off = (size_t)g * ns * C + (size_t)h * 4 * ns;  // reshape quirk (:35-36)
+    const float* Kh = K + off;
+    const float* Vh = V + off;
+    float mx = -__builtin_inff();
+    for (int s = lane; s < ns; s += kWave)
+      mx = fmaxf(mx, dot4(q, *reinterpret_cast<const float4*>(Kh + 4 * s)) / 2.0f);
+    mx = seg_max<kWave>(mx);
+    float sum = 0.f;
+    float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int s = lane; s < ns; s += kWave) {
+      const float e = expf(dot4(q, *reinterpret_cast<const float4*>(Kh + 4 * s)) / 2.0f - mx);
+      const float4 v = *reinterpret_cast<const float4*>(Vh + 4 * s);
+      sum = sum + e;
+      o.x = o.x + e * v.x;
+      o.y = o.y + e * v.y;
+      o.z = o.z + e * v.z;
+      o.w = o.w + e * v.w;
+    }
+    sum = seg_sum<kWave>(sum);
+    const float inv = 1.0f / sum;
+    const float go_o = dot4(go, make_float4(seg_sum<kWave>(o.x) * inv, seg_sum<kWave>(o.y) * inv,
+                                            seg_sum<kWave>(o.z) * inv, seg_sum<kWave>(o.w) * inv));
+    float4 gq = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int s = lane; s < ns; s += kWave) {
+      const float4 k = *reinterpret_cast<const float4*>(Kh + 4 * s);
+      const float4 v = *reinterpret_cast<const float4*>(Vh + 4 * s);
+      const float a = expf(dot4(q, k) / 2.0f - mx) * inv;
+      const float ds = a * (dot4(go, v) - go_o);
+      const float hds = ds / 2.0f;
+      *reinterpret_cast<float4*>(dV + off + 4 * s) =
+          make_float4(a * go.x, a * go.y, a * go.z, a * go.w);
+      *reinterpret_cast<float4*>(dK + off + 4 * s) =
+          make_float4(hds * q.x, hds * q.y, hds * q.z, hds * q.w);
+      gq.x = gq.x + hds * k.x;
+      gq.y = gq.y + hds * k.y;
+      gq.z = gq.z + hds * k.z;
+      gq.w = gq.w + hds * k.w;
+    }
+    gq.x = seg_sum<kWave>(gq.x);
+    gq.y = seg_sum<kWave>(gq.y);
+    gq.z = seg_sum<kWave>(gq.z);
+    gq.w = seg_sum<kWave>(gq.w);
+    if (lane == 0) *reinterpret_cast<float4*>(dQ + g * C + 4 * h) = gq;
+  }
+}
+
 // One wave per group, lanes over channels (pointnet_util.py:130-145).
 __global__ __launch_bounds__(kBlock) void group_pool_kernel(const float* __restrict__ x,
                                                             const float* __restrict__ gxyz, int G,
@@ -213,6 +278,23 @@ int pn2_attn_reduce(const float* Q, const float* K, const float* V, int B, int M
     hipLaunchKernelGGL(pn2::attn_reduce_generic_kernel,
                        dim3(pn2::grid_for(G * (C / 4))), dim3(pn2::kBlock), 0, s, Q, K, V,
                        (int)G, ns, C, out);
+  PN2_RETURN_LAUNCH();
+}
+
+int pn2_attn_reduce_grad(const float* Q, const float* K, const float* V, const float* grad_out,
+                         int B, int M, int ns, int C, float* grad_Q, float* grad_K,
+                         float* grad_V, pn2_stream_t stream) {
+  if (B < 0 || M < 0 || ns <= 0 || C < 0 || (C % 4) != 0) return PN2_EINVAL;
+  const long long G = (long long)B * M;
+  if (G == 0 || C == 0) return PN2_OK;
+  if (!Q || !K || !V || !grad_out || !grad_Q || !grad_K || !grad_V || G > INT32_MAX)
+    return PN2_EINVAL;
+  if ((((uintptr_t)Q | (uintptr_t)K | (uintptr_t)V | (uintptr_t)grad_out | (uintptr_t)grad_Q |
+        (uintptr_t)grad_K | (uintptr_t)grad_V) & 15) != 0)
+    return PN2_EINVAL;
+  hipLaunchKernelGGL(pn2::attn_reduce_grad_kernel, dim3(pn2::grid_for(G * (C / 4))),
+                     dim3(pn2::kBlock), 0, (hipStream_t)stream, Q, K, V, grad_out, (int)G, ns, C,
+                     grad_Q, grad_K, grad_V);
   PN2_RETURN_LAUNCH();
 }
 

@@ -73,16 +73,16 @@ def sample_and_group(npoint, radius, nsample, xyz, points, knn=False, use_xyz=Tr
         idx: (batch_size, npoint, nsample) int32
         grouped_xyz: (batch_size, npoint, nsample, 3), centred on new_xyz
     """
-    if knn:
-        raise NotImplementedError(
-            "sample_and_group(knn=True) needs knn_point/select_top_k (SURVEY §8(f) row 2)")
     xyz = device_tensor(xyz, "xyz", torch.float32)
     if _needs_grad(xyz):
         fps_idx = tf_sampling.farthest_point_sample(npoint, xyz)
         new_xyz = tf_sampling.gather_point(xyz, fps_idx)
     else:
         _, new_xyz = tf_sampling.farthest_point_sample_and_gather(npoint, xyz)
-    idx, _ = tf_grouping.query_ball_point(radius, nsample, xyz, new_xyz.detach())
+    if knn:  # pointnet_util.py:35-36
+        _, idx = tf_grouping.knn_point(nsample, xyz, new_xyz.detach())
+    else:
+        idx, _ = tf_grouping.query_ball_point(radius, nsample, xyz, new_xyz.detach())
     new_points, grouped_xyz = group_concat(xyz, points, new_xyz, idx, use_xyz=use_xyz)
     return new_xyz, new_points, idx, grouped_xyz
 

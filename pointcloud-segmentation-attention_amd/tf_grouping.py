@@ -2,8 +2,10 @@
 pointnet2_tensorflow/tf_ops/grouping/tf_grouping.py (same names, argument order, shapes,
 dtypes and error messages), running the gfx950 kernels of libpn2hip.so.
 
-select_top_k / knn_point (tf_grouping.py:22-31,48-73) are the §8(f) "next" row: only the
-knn=True path of sample_and_group uses them, and no attention model sets it.
+select_top_k / knn_point (tf_grouping.py:22-31,48-73) run knn.hip: one wavefront per query
+row, radix select + the reference's selection-sort swaps replayed on at most 3k candidates,
+so ties come out in exactly the reference's order; knn_point never builds the (b,m,n)
+distance matrix.
 """
 import torch
 
@@ -67,6 +69,62 @@ def query_ball_point(radius, nsample, xyz1, xyz2, grid=None):
         check(lib().pn2_ball_query(ptr(xyz1), ptr(xyz2), B, N, M, float(radius), ns, ptr(idx),
                                    ptr(pts_cnt), stream_of(xyz1)), "QueryBallPoint")
     return idx, pts_cnt
+
+
+def select_top_k(k, dist):
+    """tf_grouping.py:22-31 (SelectionSort, tf_grouping_g.cu:83-123).
+
+    Input:
+        k: int32, number of k SMALLEST elements selected
+        dist: (b,m,n) float32 array, distance matrix, m query points, n dataset points
+    Output:
+        idx: (b,m,n) int32 array, first k in n are indices to the top k
+        dist_out: (b,m,n) float32 array, first k in n are the top k
+    """
+    if int(k) <= 0:  # tf_grouping.cpp:113
+        raise InvalidArgumentError("SelectionSort expects positive k")
+    if dist.dim() != 3:  # tf_grouping.cpp:118
+        raise InvalidArgumentError("SelectionSort expects (b,m,n) dist shape.")
+    dist = device_tensor(dist, "dist", torch.float32)
+    B, m, n = (int(s) for s in dist.shape)
+    k = int(k)
+    if k > n:
+        raise InvalidArgumentError("SelectionSort expects k <= n")
+    outi = torch.empty((B, m, n), dtype=torch.int32, device=dist.device)
+    out = torch.empty((B, m, n), dtype=torch.float32, device=dist.device)
+    ws = torch.empty((max(lib().pn2_select_top_k_workspace_size(B, m, k), 16),),
+                     dtype=torch.uint8, device=dist.device)
+    check(lib().pn2_select_top_k(ptr(dist), B, m, n, k, ptr(outi), ptr(out), ptr(ws),
+                                 stream_of(dist)), "SelectionSort")
+    return outi, out
+
+
+def knn_point(k, xyz1, xyz2):
+    """tf_grouping.py:48-73.
+
+    Input:
+        k: int32, number of k in k-nn search
+        xyz1: (batch_size, ndataset, c) float32 array, input points
+        xyz2: (batch_size, npoint, c) float32 array, query points
+    Output:
+        val: (batch_size, npoint, k) float32 array, L2 distances (squared, as the reference's
+             reduce_sum of squares)
+        idx: (batch_size, npoint, k) int32 array, indices to input points
+    """
+    if xyz1.dim() != 3 or xyz2.dim() != 3 or xyz1.shape[0] != xyz2.shape[0] \
+            or xyz1.shape[2] != xyz2.shape[2]:
+        raise InvalidArgumentError("knn_point expects (b,n,c) xyz1 and (b,m,c) xyz2")
+    xyz1 = device_tensor(xyz1, "xyz1", torch.float32)
+    xyz2 = device_tensor(xyz2, "xyz2", torch.float32)
+    B, n, c = (int(s) for s in xyz1.shape)
+    m, k = int(xyz2.shape[1]), int(k)
+    if not 0 < k <= n:
+        raise InvalidArgumentError("SelectionSort expects positive k")
+    val = torch.empty((B, m, k), dtype=torch.float32, device=xyz1.device)
+    idx = torch.empty((B, m, k), dtype=torch.int32, device=xyz1.device)
+    check(lib().pn2_knn_point(ptr(xyz1), ptr(xyz2), B, n, m, c, k, ptr(val), ptr(idx),
+                              stream_of(xyz1)), "knn_point")
+    return val, idx
 
 
 def _check_group(points, idx, name="GroupPoint"):

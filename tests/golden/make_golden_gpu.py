@@ -77,6 +77,18 @@ def bq_case(name, x, q, r, ns, src):
          xyz1=x, xyz2=q, idx=idx.cpu().numpy(), pts_cnt=cnt.cpu().numpy())
 
 
+def sel_case(name, d, k, src):
+    B, m, n = d.shape
+    dt = torch.from_numpy(d).to(DEV)
+    outi = torch.zeros((B, m, n), dtype=torch.int32, device=DEV)
+    out = torch.zeros((B, m, n), dtype=torch.float32, device=DEV)
+    assert O.ref_gpu().pn2ref_selection_sort(dt.data_ptr(), B, m, n, k, outi.data_ptr(),
+                                             out.data_ptr()) == 0
+    save(name, {"op": "selection_sort", "k": k, "inputs": src,
+                "ref": "tf_grouping_g.cu:83-123 (selection_sort_gpu) compiled for gfx950"},
+         dist=d, outi=outi.cpu().numpy(), out=out.cpu().numpy())
+
+
 def main():
     if not O.have_ref_gpu():
         raise SystemExit("oracle/_ref/libref_gpu.so missing: build it with `make -C oracle ref`")
@@ -103,6 +115,13 @@ def main():
     bq_case("bqg_scannet_sa2", x, x[:, ::4].copy(), 0.2, 32, "ScanNet crop (1,1024), SA2 radius")
     x = synth.batch([9], 300, "uniform")[0]
     bq_case("bqg_uniform_sparse", x, x[:, ::6].copy(), 0.05, 8, "uniform (1,300), r=.05: cnt < ns")
+    rng = np.random.default_rng(11)
+    sel_case("sel_ties", rng.integers(0, 4, (2, 16, 96)).astype(np.float32), 24,
+             "integer distances in [0,4): ties everywhere, k=24")
+    x = synth.batch([10], 1024, "scannet")[0]
+    q = x[:, ::32].copy()
+    d = ((x[:, None, :, :] - q[:, :, None, :]) ** 2).sum(-1).astype(np.float32)
+    sel_case("sel_scannet", d, 32, "squared distances of 32 queries to a (1,1024) ScanNet crop")
 
 
 if __name__ == "__main__":

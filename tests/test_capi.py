@@ -66,6 +66,8 @@ def test_argument_checks_return_einval_without_launching(pn2):
     assert lib.pn2_ball_query(None, None, 1, 10, 10, 0.0, 8, None, None, None) == E  # radius
     assert lib.pn2_ball_query(None, None, 1, 10, 10, 0.1, 0, None, None, None) == E  # nsample
     assert lib.pn2_attn_reduce(None, None, None, 1, 1, 32, 6, None, None) == E  # C % 4
+    assert lib.pn2_attn_reduce_grad(None, None, None, None, 1, 1, 32, 8, None, None, None,
+                                    None) == E  # null buffers
     assert lib.pn2_group_pool(None, None, 1, 1, 4, 8, 7, None, None) == E       # mode
     assert lib.pn2_fp_fused(None, None, None, 3, None, 4, 1, 4, 4, None, None) == E  # C1 w/o points1
     # empty work is a no-op, not an error (nothing is launched)

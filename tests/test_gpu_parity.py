@@ -378,6 +378,41 @@ def test_attention_reduce(env, ns, C):
     np.testing.assert_allclose(got, O.attn_reduce(Q, K, V), **TOL)
 
 
+def _torch_attention(Q, K, V):
+    """attention_layer.py:35-42 in plain torch (float64 on the CPU): the test's reference for
+    the floating-point attention kernels, reshape quirk included."""
+    import torch
+    B, M, ns, C = K.shape
+    H = C // 4
+    q = Q.reshape(B, M, H, 1, 4)
+    k = K.reshape(B, M, H, ns, 4)
+    v = V.reshape(B, M, H, ns, 4)
+    w = torch.softmax(q @ k.transpose(-1, -2) / 2.0, dim=-1)
+    return (w @ v).reshape(B, M, C)
+
+
+@pytest.mark.parametrize("ns,C", [(32, 64), (16, 128), (128, 256), (24, 12)])
+def test_attention_reduce_grad(env, ns, C):
+    """Backward of the attention reduction (pn2_attn_reduce_grad, through autograd) against
+    torch autograd of the same math in float64; rtol = atol = 1e-5."""
+    pkg, O, torch, dev = env
+    rng = np.random.default_rng(ns + C)
+    B, M = 2, 19
+    Q = rng.uniform(-1, 1, (B, M, C)).astype(np.float32)
+    K = rng.uniform(-1, 1, (B, M, ns, C)).astype(np.float32)
+    V = rng.uniform(-1, 1, (B, M, ns, C)).astype(np.float32)
+    G = rng.uniform(-1, 1, (B, M, C)).astype(np.float32)
+    ts = [torch.from_numpy(a).to(dev).requires_grad_(True) for a in (Q, K, V)]
+    out = pkg.attention_layer.attention_reduce(*ts)
+    out.backward(torch.from_numpy(G).to(dev))
+    rs = [torch.from_numpy(a).double().requires_grad_(True) for a in (Q, K, V)]
+    ref = _torch_attention(*rs)
+    ref.backward(torch.from_numpy(G).double())
+    np.testing.assert_allclose(out.detach().cpu().numpy(), ref.detach().numpy(), **TOL)
+    for t, r in zip(ts, rs):
+        np.testing.assert_allclose(t.grad.cpu().numpy(), r.grad.numpy(), **TOL)
+
+
 @pytest.mark.parametrize("mode", ["max", "avg", "weighted_avg", "max_and_avg"])
 def test_group_pool(env, mode):
     pkg, O, torch, dev = env
@@ -498,6 +533,10 @@ def test_hip_reproduces_golden(env, path):
             g = pkg.tf_interpolate.three_interpolate_grad(T(d["points"]), T(d["idx"]),
                                                           T(d["weight"]), T(d["grad_out"]))
             np.testing.assert_allclose(g.cpu().numpy(), d["grad_points"], **TOL)
+    elif op == "selection_sort":
+        oi, oo = pkg.tf_grouping.select_top_k(int(meta["k"]), T(d["dist"]))
+        assert np.array_equal(oi.cpu().numpy(), d["outi"])
+        assert np.array_equal(_bits(oo.cpu().numpy()), _bits(d["out"]))
     elif op == "farthest_point_sample":
         idx, new_xyz = pkg.tf_sampling.farthest_point_sample_and_gather(int(meta["npoint"]),
                                                                         T(d["xyz"]))
@@ -543,3 +582,66 @@ def test_pipelined_steps_match_single_stream(env, graphs):
         assert len(outs) == len(single)
         for a, b in zip(single, outs):
             assert torch.equal(a, b)
+
+
+def _ties(rng, shape, levels):
+    return rng.integers(0, levels, shape).astype(np.float32)
+
+
+@pytest.mark.parametrize("kind,B,m,n,k", [
+    ("uniform", 2, 37, 300, 16), ("ties", 2, 40, 200, 32), ("ties", 1, 64, 64, 64),
+    ("signed", 2, 17, 129, 1), ("ties", 2, 33, 1000, 100), ("dups", 1, 8, 40, 8)])
+def test_select_top_k(env, kind, B, m, n, k):
+    """select_top_k (knn.hip) against the oracle's literal selection sort and the reference's
+    selection_sort_gpu on this GPU: both (b,m,n) outputs bit-exact, ties included (the swaps
+    of the partial selection sort decide their order)."""
+    pkg, O, torch, dev = env
+    rng = np.random.default_rng(n + k)
+    if kind == "uniform":
+        d = rng.random((B, m, n)).astype(np.float32)
+    elif kind == "signed":
+        d = rng.standard_normal((B, m, n)).astype(np.float32)
+    elif kind == "dups":
+        d = np.zeros((B, m, n), np.float32)
+    else:
+        d = _ties(rng, (B, m, n), 5)
+    outi, out = pkg.tf_grouping.select_top_k(k, torch.from_numpy(d).to(dev))
+    ri, ro = O.selection_sort(d, k)
+    assert np.array_equal(outi.cpu().numpy(), ri)
+    assert np.array_equal(_bits(out.cpu().numpy()), _bits(ro))
+    if O.have_ref_gpu():
+        dt = torch.from_numpy(d).to(dev)
+        gi = torch.zeros((B, m, n), dtype=torch.int32, device=dev)
+        go = torch.zeros((B, m, n), dtype=torch.float32, device=dev)
+        assert O.ref_gpu().pn2ref_selection_sort(dt.data_ptr(), B, m, n, k, gi.data_ptr(),
+                                                 go.data_ptr()) == 0
+        assert np.array_equal(gi.cpu().numpy(), ri), "oracle differs from selection_sort_gpu"
+
+
+@pytest.mark.parametrize("kind,B,n,m,c,k", [
+    ("scannet", 2, 2048, 256, 3, 32), ("grid", 2, 1000, 100, 3, 16), ("uniform", 1, 500, 64, 6, 8),
+    ("dup", 1, 300, 10, 3, 20), ("scannet", 1, 8192, 128, 3, 64)])
+def test_knn_point(env, kind, B, n, m, c, k):
+    pkg, O, torch, dev = env
+    if c == 3:
+        x = _cloud(pkg, kind, B, n)
+    else:
+        x = np.random.default_rng(c).random((B, n, c)).astype(np.float32)
+    q = x[:, ::max(1, n // m)][:, :m].copy()
+    val, idx = pkg.tf_grouping.knn_point(k, torch.from_numpy(x).to(dev), torch.from_numpy(q).to(dev))
+    rv, ri = O.knn_point(k, x, q)
+    assert np.array_equal(idx.cpu().numpy(), ri)
+    assert np.array_equal(_bits(val.cpu().numpy()), _bits(rv))
+
+
+def test_sample_and_group_knn(env):
+    pkg, O, torch, dev = env
+    x = _cloud(pkg, "scannet", 2, 2048, seed=3)
+    pts = pkg.synth.features_uniform(5, (2, 2048, 8))
+    new_xyz, new_points, idx, grouped_xyz = pkg.pointnet_util.sample_and_group(
+        128, 0.2, 16, torch.from_numpy(x).to(dev), torch.from_numpy(pts).to(dev), knn=True)
+    rnx = O.gather_point(x, O.fps(x, 128))
+    _, ridx = O.knn_point(16, x, rnx)
+    assert np.array_equal(idx.cpu().numpy(), ridx)
+    rnp, rgx = O.group_concat(x, pts, rnx, ridx)
+    assert np.array_equal(_bits(new_points.cpu().numpy()), _bits(rnp))

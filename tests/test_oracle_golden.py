@@ -72,6 +72,10 @@ def test_oracle_reproduces_golden(orc, path):
     elif op == "three_interpolate":
         out = orc.three_interpolate(d["points"], d["idx"], d["weight"])
         assert np.array_equal(_bits(out), _bits(d["out"]))
+    elif op == "selection_sort":
+        oi, oo = orc.selection_sort(d["dist"], int(meta["k"]))
+        assert np.array_equal(oi, d["outi"])
+        assert np.array_equal(_bits(oo), _bits(d["out"]))
     elif op == "farthest_point_sample":
         idx = orc.fps(d["xyz"], int(meta["npoint"]))
         assert np.array_equal(idx, d["idx"]), f"{(idx != d['idx']).sum()} FPS indices differ"
@@ -136,3 +140,21 @@ def test_fps_restatement_known_answers(orc):
     x[0, 30] = [0, 0, 2]
     x[0, 542] = [2, 0, 0]
     assert orc.fps(x, 2).tolist() == [[0, 30]]
+
+
+def test_selection_sort_known_answers(orc):
+    """selection_sort_gpu (tf_grouping_g.cu:104-120) moves the element at position s to the
+    minimum's old position, so equal values do not come out in index order: for
+    [2, 1, 2, 0] and k = 3 the third pick is the 2 at index 2, not the one at index 0
+    (index 0 was swapped behind it in step 0)."""
+    d = np.array([[[2, 1, 2, 0]]], np.float32)
+    outi, out = orc.selection_sort(d, 3)
+    assert outi.tolist() == [[[3, 1, 2, 0]]]
+    assert out.tolist() == [[[0, 1, 2, 2]]]
+    # all equal: no swap ever happens, identity order
+    outi, _ = orc.selection_sort(np.zeros((1, 1, 6), np.float32), 4)
+    assert outi.tolist() == [[[0, 1, 2, 3, 4, 5]]]
+    # knn_point = squared distances + the same selection sort
+    x = np.array([[[0, 0, 0], [1, 0, 0], [0, 1, 0], [3, 0, 0]]], np.float32)
+    val, idx = orc.knn_point(2, x, x[:, :1])
+    assert idx.tolist() == [[[0, 1]]] and val.tolist() == [[[0.0, 1.0]]]
