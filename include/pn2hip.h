@@ -5,7 +5,7 @@
  * inline TF graph fragment) of the reference and keeps its argument meaning:
  *
  *   reference op / fragment                                     → entry point here
- *   FarthestPointSample  tf_sampling.cpp:94-123, .cu:105-170     → pn2_fps
+ *   FarthestPointSample  tf_sampling.cpp:94-123, .cu:105-170     → pn2_fps (+_gather, _chain)
  *   GatherPoint          tf_sampling.cpp:125-148, .cu:172-181    → pn2_gather_point
  *   GatherPointGrad      tf_sampling.cpp:150-178, .cu:183-192    → pn2_gather_point_grad
  *   QueryBallPoint       tf_grouping.cpp:66-106, _g.cu:3-36      → pn2_ball_query,
@@ -84,6 +84,13 @@ size_t pn2_fps_workspace_size(int B, int N);
 int pn2_fps_ws(const float* xyz, int B, int N, int npoint, int32_t* idx, float* new_xyz,
                void* workspace, size_t workspace_bytes, pn2_stream_t stream);
 
+/* The SSG sampler chain in ONE launch: stage 0 samples npoint[0] of the N points of each
+ * cloud, stage i samples npoint[i] of stage i-1's output (pointnet2_sem_seg*.py:29-50 samples
+ * 8192 -> 1024 -> 256 -> 64 -> 16). idx[i] (B,npoint[i]) and new_xyz[i] (B,npoint[i],3) are
+ * exactly what pn2_fps_gather returns for that stage's input. N <= 8192, npoint[i] <= 1024 for
+ * every stage that feeds another, 1 <= nstages <= 4. Host arrays of device pointers. */
+int pn2_fps_chain(const float* xyz, int B, int N, int nstages, const int* npoint,
+                  int32_t* const* idx, float* const* new_xyz, pn2_stream_t stream);
 /* out (B,M,3) = inp[b, idx[b,j], :]; inp must have 3 channels (tf_sampling.cpp:131). */
 int pn2_gather_point(const float* inp, const int32_t* idx, int B, int N, int M, float* out,
                      pn2_stream_t stream);

@@ -38,6 +38,7 @@ SIGNATURES = {
     "pn2_fps_gather": (_I, [_P, _I, _I, _I, _P, _P, _P]),
     "pn2_fps_max_points": (_I, []),
     "pn2_fps_workspace_size": (_S, [_I, _I]),
+    "pn2_fps_chain": (_I, [_P, _I, _I, _I, _P, _P, _P, _P]),
     "pn2_fps_ws": (_I, [_P, _I, _I, _I, _P, _P, _P, _S, _P]),
     "pn2_gather_point": (_I, [_P, _P, _I, _I, _I, _P, _P]),
     "pn2_gather_point_grad": (_I, [_P, _P, _I, _I, _I, _P, _P]),

@@ -78,26 +78,24 @@ struct Lay9 {
   PN2_DEV static constexpr int point(int t, int s) { return W * (s % H) + R * t + s / H; }
 };
 
-template <int BLOCK, int PPT, int G, bool XYZ_LDS, bool STAMP = false>
-__global__ __launch_bounds__(BLOCK) void fps_v9_kernel(const float* __restrict__ xyz, int N,
-                                                       int M, int32_t* __restrict__ idx,
-                                                       float* __restrict__ new_xyz) {
+// The v9 sampler for one cloud, run by threads 0..BLOCK-1 of the calling workgroup (BLOCK ==
+// blockDim.x, or BLOCK == 64 for wave 0 alone: a one-wave body has no barrier).
+//   P     the cloud's N points (xyz AoS, global or LDS), loaded into registers once;
+//   CXYZ  where the winners' coordinates are read each iteration (an LDS copy of P, or P);
+//   I, NX the cloud's idx (M) and new_xyz (M x 3) outputs in global memory (NX may be null);
+//   SNEXT optional LDS array that receives new_xyz too (the next sampler's input).
+template <int BLOCK, int PPT, int G, bool STAMP = false>
+PN2_DEV void fps_v9_body(const float* P, int N, int M, const float* CXYZ, int32_t* I, float* NX,
+                         float* SNEXT, uint2 (*red)[8]) {
   unsigned long long st_acc[6] = {0, 0, 0, 0, 0, 0}, st_prev = 0;
   using Lay = Lay9<BLOCK, PPT>;
   constexpr int NW = BLOCK / kWave;
   static_assert(BLOCK % kWave == 0 && NW <= 8, "the block step reduces 8 DPP lanes");
   static_assert(PPT % G == 0 && (G == 1 || G == 2 || G == 4), "slot groups");
   constexpr int NG = PPT / G;
-  __shared__ uint2 red[2][8];
-  __shared__ float sxyz[XYZ_LDS ? 3 * BLOCK * PPT : 1];
-
-  const int b = blockIdx.x;
   const int t = threadIdx.x;
   const int lane = t & (kWave - 1);
   const int w = t / kWave;
-  const float* __restrict__ P = xyz + (size_t)b * N * 3;
-  int32_t* __restrict__ I = idx + (size_t)b * M;
-  float* __restrict__ NX = new_xyz ? new_xyz + (size_t)b * M * 3 : nullptr;
 
   float px[PPT], py[PPT], pz[PPT];
   int tb[PPT];  // running min distance as int bits; padding slots -1 never win
@@ -114,15 +112,11 @@ __global__ __launch_bounds__(BLOCK) void fps_v9_kernel(const float* __restrict__
       tb[s] = -1;
     }
   }
-  if constexpr (XYZ_LDS) {
-    for (int e = t; e < 3 * N; e += BLOCK) sxyz[e] = P[e];
-    __syncthreads();
-  }
-
   float cx = P[0], cy = P[1], cz = P[2];
   if (t == 0) {
     I[0] = 0;
     if (NX) { NX[0] = cx; NX[1] = cy; NX[2] = cz; }
+    if (SNEXT) { SNEXT[0] = cx; SNEXT[1] = cy; SNEXT[2] = cz; }
   }
 
   if constexpr (STAMP) {
@@ -181,14 +175,11 @@ __global__ __launch_bounds__(BLOCK) void fps_v9_kernel(const float* __restrict__
       old = __builtin_amdgcn_readlane((int)r.y, wi);
     }
     PN2_STAMP(4)
-    if constexpr (XYZ_LDS) {
-      cx = sxyz[3 * old + 0]; cy = sxyz[3 * old + 1]; cz = sxyz[3 * old + 2];
-    } else {
-      cx = P[3 * old + 0]; cy = P[3 * old + 1]; cz = P[3 * old + 2];
-    }
+    cx = CXYZ[3 * old + 0]; cy = CXYZ[3 * old + 1]; cz = CXYZ[3 * old + 2];
     if (t == 0) {
       I[j] = old;
       if (NX) { NX[3 * j + 0] = cx; NX[3 * j + 1] = cy; NX[3 * j + 2] = cz; }
+      if (SNEXT) { SNEXT[3 * j + 0] = cx; SNEXT[3 * j + 1] = cy; SNEXT[3 * j + 2] = cz; }
     }
     PN2_STAMP(5)
   }
@@ -196,6 +187,23 @@ __global__ __launch_bounds__(BLOCK) void fps_v9_kernel(const float* __restrict__
     if (lane == 0 && blockIdx.x < 16)
       for (int ph = 0; ph < 6; ++ph) g_stamp[(blockIdx.x * 16 + w) * 8 + ph] = st_acc[ph];
   }
+}
+
+template <int BLOCK, int PPT, int G, bool XYZ_LDS, bool STAMP = false>
+__global__ __launch_bounds__(BLOCK) void fps_v9_kernel(const float* __restrict__ xyz, int N,
+                                                       int M, int32_t* __restrict__ idx,
+                                                       float* __restrict__ new_xyz) {
+  __shared__ uint2 red[2][8];
+  __shared__ float sxyz[XYZ_LDS ? 3 * BLOCK * PPT : 1];
+  const int b = blockIdx.x;
+  const float* __restrict__ P = xyz + (size_t)b * N * 3;
+  if constexpr (XYZ_LDS) {
+    for (int e = threadIdx.x; e < 3 * N; e += BLOCK) sxyz[e] = P[e];
+    __syncthreads();
+  }
+  fps_v9_body<BLOCK, PPT, G, STAMP>(P, N, M, XYZ_LDS ? sxyz : P, idx + (size_t)b * M,
+                                    new_xyz ? new_xyz + (size_t)b * M * 3 : nullptr, nullptr,
+                                    red);
 }
 
 template <int BLOCK, int PPT, int G>

@@ -164,18 +164,28 @@ class Step:
                     unknown_grid=v.get("grid1") if i == 0 else None)
             return f
 
-        # lane 0: SA1's sampler alone (it is what bench.py times), then SA2..SA4's samplers as
-        # one task (short; one boundary instead of three on the critical chain)
-        tasks.append(Task("fps1", 0, (), fps(0)))
-        tasks.append(Task("fps234", 0, (), lambda: [fps(i)() for i in (1, 2, 3)]))
+        npoints = [sa_[0] for sa_ in SSG_SA]
         grid_dep = ("grid1",) if big else ()
-        tasks.append(Task("sa1", 1, ("fps1",), sa(0)))
-        tasks.append(Task("fp4", 2, ("fps1",) + grid_dep, fp(0)))
+        if tf_sampling.chain_supported(int(inp["xyz"].shape[1]), npoints):
+            # lane 0: the four samplers as ONE launch (pn2_fps_chain; what bench.py times)
+            def chain():
+                outs = tf_sampling.farthest_point_sample_chain(npoints, inp["xyz"])
+                for i, (_, nx) in enumerate(outs):
+                    v["xyz"][i + 1] = nx
+            tasks.append(Task("fps1", 0, (), chain))
+            sampled = ("fps1",) * 4
+        else:
+            # lane 0: SA1's sampler alone, then SA2..SA4's samplers as one task
+            tasks.append(Task("fps1", 0, (), fps(0)))
+            tasks.append(Task("fps234", 0, (), lambda: [fps(i)() for i in (1, 2, 3)]))
+            sampled = ("fps1", "fps234", "fps234", "fps234")
+        tasks.append(Task("sa1", 1, (sampled[0],), sa(0)))
+        tasks.append(Task("fp4", 2, (sampled[0],) + grid_dep, fp(0)))
         for i in (1, 2, 3):
-            tasks.append(Task(f"sa{i + 1}", 1, ("fps234",), sa(i)))
-        tasks.append(Task("fp3", 2, ("fps234",), fp(1)))
-        tasks.append(Task("fp2", 3, ("fps234",), fp(2)))
-        tasks.append(Task("fp1", 3, ("fps234",), fp(3)))
+            tasks.append(Task(f"sa{i + 1}", 1, (sampled[i],), sa(i)))
+        tasks.append(Task("fp3", 2, (sampled[1],), fp(1)))
+        tasks.append(Task("fp2", 3, (sampled[2],), fp(2)))
+        tasks.append(Task("fp1", 3, (sampled[3],), fp(3)))
         return tasks
 
     def _tasks_msg(self):

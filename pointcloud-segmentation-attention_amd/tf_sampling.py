@@ -5,6 +5,8 @@ dtypes and error messages), running the gfx950 kernels of libpn2hip.so.
 prob_sample is not provided: no model of the reference calls it (only the __main__ demo of
 tf_sampling.py:61-90).
 """
+import ctypes
+
 import torch
 
 from ._lib import InvalidArgumentError, check, device_tensor, lib, ptr, stream_of
@@ -46,6 +48,43 @@ def farthest_point_sample_and_gather(npoint, inp):
     """(idx, new_xyz) = (farthest_point_sample(npoint, inp), gather_point(inp, idx)) in one
     kernel (pointnet_util.py:34)."""
     return _fps(npoint, inp, True)
+
+
+CHAIN_MAX_POINTS = 8192   # pn2_fps_chain: first stage's points per cloud
+CHAIN_MAX_FEED = 1024     # points one stage hands to the next
+CHAIN_MAX_STAGES = 4
+
+
+def chain_supported(N, npoints):
+    return (N <= CHAIN_MAX_POINTS and 1 <= len(npoints) <= CHAIN_MAX_STAGES
+            and all(0 < m <= CHAIN_MAX_FEED for m in npoints[:-1]) and npoints[-1] > 0)
+
+
+def farthest_point_sample_chain(npoints, inp):
+    """The samplers of consecutive SA layers in one launch (pn2_fps_chain): stage i samples
+    npoints[i] points of stage i-1's new_xyz (stage 0 of inp (B,N,3)). Returns
+    [(idx_i, new_xyz_i)], each exactly farthest_point_sample_and_gather(npoints[i], input_i)."""
+    if inp.dim() != 3 or inp.shape[2] != 3:  # tf_sampling.cpp:105
+        raise InvalidArgumentError("FarthestPointSample expects (batch_size,num_points,3) inp shape")
+    npoints = [int(m) for m in npoints]
+    if any(m <= 0 for m in npoints):  # tf_sampling.cpp:99
+        raise InvalidArgumentError("FarthestPointSample expects positive npoint")
+    inp = device_tensor(inp, "inp", torch.float32)
+    B, N = int(inp.shape[0]), int(inp.shape[1])
+    if not chain_supported(N, npoints):
+        raise InvalidArgumentError(
+            f"farthest_point_sample_chain supports N <= {CHAIN_MAX_POINTS}, <= {CHAIN_MAX_STAGES} "
+            f"stages and <= {CHAIN_MAX_FEED} points fed between stages")
+    outs = [(torch.empty((B, m), dtype=torch.int32, device=inp.device),
+             torch.empty((B, m, 3), dtype=torch.float32, device=inp.device)) for m in npoints]
+    k = len(npoints)
+    arr_i = (ctypes.c_int * k)(*npoints)
+    arr_idx = (ctypes.c_void_p * k)(*[o[0].data_ptr() for o in outs])
+    arr_nx = (ctypes.c_void_p * k)(*[o[1].data_ptr() for o in outs])
+    check(lib().pn2_fps_chain(ptr(inp), B, N, k, ctypes.addressof(arr_i),
+                              ctypes.addressof(arr_idx), ctypes.addressof(arr_nx),
+                              stream_of(inp)), "FarthestPointSample")
+    return outs
 
 
 def _check_gather(inp, idx, name="GatherPoint"):

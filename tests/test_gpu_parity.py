@@ -645,3 +645,22 @@ def test_sample_and_group_knn(env):
     assert np.array_equal(idx.cpu().numpy(), ridx)
     rnp, rgx = O.group_concat(x, pts, rnx, ridx)
     assert np.array_equal(_bits(new_points.cpu().numpy()), _bits(rnp))
+
+
+@pytest.mark.parametrize("kind,B,N,npoints", [
+    ("scannet", 3, 8192, [1024, 256, 64, 16]), ("uniform", 2, 3000, [700, 128, 32]),
+    ("grid", 2, 4096, [512, 100]), ("dup", 1, 700, [40, 20, 5, 3]), ("uniform", 2, 64, [16]),
+    ("scannet", 1, 8192, [1024, 1000, 900, 50])])
+def test_fps_chain(env, kind, B, N, npoints):
+    """pn2_fps_chain (every SSG sampler of a cloud in one workgroup) gives exactly the
+    per-stage farthest_point_sample_and_gather results, and the oracle's indices."""
+    pkg, O, torch, dev = env
+    x = _cloud(pkg, kind, B, N)
+    xt = torch.from_numpy(x).to(dev)
+    outs = pkg.tf_sampling.farthest_point_sample_chain(npoints, xt)
+    cur, cur_np = xt, x
+    for (idx, nx), m in zip(outs, npoints):
+        ridx, rnx = pkg.tf_sampling.farthest_point_sample_and_gather(m, cur)
+        assert torch.equal(idx, ridx) and torch.equal(nx, rnx)
+        assert np.array_equal(idx.cpu().numpy(), O.fps(cur_np, m))
+        cur, cur_np = nx, nx.cpu().numpy()
