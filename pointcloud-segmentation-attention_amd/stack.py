@@ -82,8 +82,11 @@ class Task:
     """One piece of a step: `fn` runs on stream `lane` (0 = the sampler chain, 1.. = side
     streams) after the tasks named in `deps` (same-lane order is implicit)."""
 
-    def __init__(self, name, lane, deps, fn):
+    def __init__(self, name, lane, deps, fn, direct=False):
         self.name, self.lane, self.deps, self.fn = name, lane, tuple(deps), fn
+        # direct: one C launch into fixed buffers; GraphStep launches it as is (a one-kernel
+        # graph costs more queue time than the kernel launch itself)
+        self.direct = direct
 
 
 class Step:
@@ -168,11 +171,17 @@ class Step:
         grid_dep = ("grid1",) if big else ()
         if tf_sampling.chain_supported(int(inp["xyz"].shape[1]), npoints):
             # lane 0: the four samplers as ONE launch (pn2_fps_chain; what bench.py times)
+            xyz = inp["xyz"]
+            B = int(xyz.shape[0])
+            v["chain"] = [(torch.empty((B, m), dtype=torch.int32, device=xyz.device),
+                           torch.empty((B, m, 3), dtype=torch.float32, device=xyz.device))
+                          for m in npoints]
+            for i, (_, nx) in enumerate(v["chain"]):
+                v["xyz"][i + 1] = nx
+
             def chain():
-                outs = tf_sampling.farthest_point_sample_chain(npoints, inp["xyz"])
-                for i, (_, nx) in enumerate(outs):
-                    v["xyz"][i + 1] = nx
-            tasks.append(Task("fps1", 0, (), chain))
+                tf_sampling.farthest_point_sample_chain(npoints, xyz, out=v["chain"])
+            tasks.append(Task("fps1", 0, (), chain, direct=True))
             sampled = ("fps1",) * 4
         else:
             # lane 0: SA1's sampler alone, then SA2..SA4's samplers as one task
@@ -319,6 +328,8 @@ class GraphStep:
         cap = side_stream(dev, "capture")
 
         def capture(t):
+            if t.direct:
+                return
             g = torch.cuda.CUDAGraph()
             st = torch.cuda.current_stream(dev)
             cap.wait_stream(st)
@@ -335,7 +346,8 @@ class GraphStep:
         self.outs = self.step.outputs()
 
     def replay(self, sampler_events=None, join=True):
-        self.step.run(sampler_events, launch=lambda t: self.graphs[t.name].replay(), join=join)
+        self.step.run(sampler_events, join=join,
+                      launch=lambda t: t.fn() if t.direct else self.graphs[t.name].replay())
         return self.outs
 
     def join(self):
@@ -347,8 +359,10 @@ class Pipeline:
     """Consecutive steps software-pipelined over two buffer sets: step k runs on set k % 2,
     its side-lane work (ball query, grouping, attention, FP) finishing while step k+1's
     sampler chain already runs on the shared lane-0 stream. Before a set is reused (step
-    k+2) lane 0 waits for that set's side lanes, so no buffer is overwritten while read.
-    Every step still does all of its work; run(k) returns after enqueueing, join() waits."""
+    k+2) the HOST waits for that set's side lanes (finished mid-way through step k+1's
+    chain), so no buffer is overwritten while read and lane 0 carries no wait packet between
+    chains. Every step still does all of its work; run(k) returns after enqueueing, join()
+    waits."""
 
     def __init__(self, inp, graphs=True, overlap=True):
         mk = (lambda: GraphStep(inp, overlap=overlap)) if graphs else \
@@ -360,7 +374,10 @@ class Pipeline:
         s = self.sets[self.k % 2]
         self.k += 1
         if isinstance(s, GraphStep):
-            s.step.join()  # lane 0 waits for this set's previous side work (long finished)
+            if s.step.ran and s.step.overlap:
+                s.step.lane_done[1].synchronize()  # this set's previous side work
+            else:
+                s.step.join()
             return s.replay(sampler_events, join=False)
         s.join()
         return s.run(sampler_events, join=False)

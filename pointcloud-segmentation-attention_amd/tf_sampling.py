@@ -60,10 +60,11 @@ def chain_supported(N, npoints):
             and all(0 < m <= CHAIN_MAX_FEED for m in npoints[:-1]) and npoints[-1] > 0)
 
 
-def farthest_point_sample_chain(npoints, inp):
+def farthest_point_sample_chain(npoints, inp, out=None):
     """The samplers of consecutive SA layers in one launch (pn2_fps_chain): stage i samples
     npoints[i] points of stage i-1's new_xyz (stage 0 of inp (B,N,3)). Returns
-    [(idx_i, new_xyz_i)], each exactly farthest_point_sample_and_gather(npoints[i], input_i)."""
+    [(idx_i, new_xyz_i)], each exactly farthest_point_sample_and_gather(npoints[i], input_i).
+    `out` optionally supplies those tensors (written in place, e.g. a step's fixed buffers)."""
     if inp.dim() != 3 or inp.shape[2] != 3:  # tf_sampling.cpp:105
         raise InvalidArgumentError("FarthestPointSample expects (batch_size,num_points,3) inp shape")
     npoints = [int(m) for m in npoints]
@@ -75,8 +76,18 @@ def farthest_point_sample_chain(npoints, inp):
         raise InvalidArgumentError(
             f"farthest_point_sample_chain supports N <= {CHAIN_MAX_POINTS}, <= {CHAIN_MAX_STAGES} "
             f"stages and <= {CHAIN_MAX_FEED} points fed between stages")
-    outs = [(torch.empty((B, m), dtype=torch.int32, device=inp.device),
-             torch.empty((B, m, 3), dtype=torch.float32, device=inp.device)) for m in npoints]
+    if out is None:
+        outs = [(torch.empty((B, m), dtype=torch.int32, device=inp.device),
+                 torch.empty((B, m, 3), dtype=torch.float32, device=inp.device)) for m in npoints]
+    else:
+        outs = list(out)
+        for (i_, x_), m in zip(outs, npoints):
+            if (i_.shape != (B, m) or i_.dtype != torch.int32 or x_.shape != (B, m, 3)
+                    or x_.dtype != torch.float32 or not i_.is_contiguous()
+                    or not x_.is_contiguous() or i_.device != inp.device
+                    or x_.device != inp.device) or len(outs) != len(npoints):
+                raise InvalidArgumentError("farthest_point_sample_chain: out tensors must be "
+                                           "contiguous int32 (B,m) / float32 (B,m,3) on inp's device")
     k = len(npoints)
     arr_i = (ctypes.c_int * k)(*npoints)
     arr_idx = (ctypes.c_void_p * k)(*[o[0].data_ptr() for o in outs])
