@@ -82,8 +82,7 @@ def pmc_traffic(config, B):
         return None, None
     with open(files[-1]) as f:
         d = json.load(f)
-    ks = [k for k in d["kernels"] if k.startswith("fps_chain")] or \
-        [k for k in d["kernels"] if k.startswith("fps_v")]
+    ks = [k for k in d["kernels"] if k.startswith("fps_v")]
     if not ks:
         return None, None
     k = max(ks, key=lambda k: d["kernels"][k]["fetch_bytes"] or 0)  # SA1 = largest sampler
@@ -180,18 +179,10 @@ def main():
         by = pkg.stack.sa_fp_bytes(args.config, B)
         step_bytes = sum(by.values())
         N, _, _, _ = pkg.stack.CONFIGS[args.config]
-        if args.config != "cfg5":
-            npts = [sa_[0] for sa_ in pkg.stack.SSG_SA]
-            chained = pkg.tf_sampling.chain_supported(N, npts)
-        else:
-            npts, chained = [pkg.stack.MSG_SA[0][0]], False
-        if not chained:
-            npts = npts[:1]
-        # algorithmic bytes of the timed sampler launch (FPS + fused gather, every stage it
-        # runs): read N_i x 12, write M_i x (4 + 12) per cloud
-        ns_in = [N] + npts[:-1]
-        fps_bytes = B * sum(n_ * 12 + m_ * 16 for n_, m_ in zip(ns_in, npts))
-        M1 = npts[0]
+        M1 = (pkg.stack.MSG_SA if args.config == "cfg5" else pkg.stack.SSG_SA)[0][0]
+        # algorithmic bytes of the timed SA1 sampler launch (FPS + fused gather): read the
+        # cloud once (N x 12), write idx + new_xyz (M1 x (4 + 12)), per cloud
+        fps_bytes = B * (N * 12 + M1 * 16)
         achieved = fps_bytes / (fps_ms * 1e-3) / 1e9
         traffic, traffic_src = pmc_traffic(args.config, B)
         result = {
@@ -204,17 +195,17 @@ def main():
             "config": {"workload": WORKLOADS[args.config], "config": args.config,
                        "clouds_per_gpu": B, "global_batch": world * B, "points": N,
                        "parallelism": f"dp{world} (batch split)",
-                       "launch": "eager" if args.eager else "hipGraph replay",
+                       "launch": "eager" if args.eager else
+                       "samplers: direct launches; side lanes: hipGraph replay",
                        "streams": ("sampler chain + 3 side streams" if overlap else "one stream")
                        + (", steps software-pipelined over 2 buffer sets" if pipelined else "")},
-            "roofline": {"kernel": ("sampler chain (FPS + gather fused, SA1..SA4 in one launch): "
-                                    if chained else "SA1 sampler (FPS + gather fused): ")
-                                   + f"{B} clouds x {N} pts -> " + " -> ".join(map(str, npts))
-                                   + ", one workgroup per cloud",
+            "roofline": {"kernel": f"SA1 sampler (FPS + gather fused): {B} clouds x {N} pts -> "
+                                   f"{M1}, one workgroup per cloud",
                          "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS,
                          "traffic": traffic, "traffic_source": traffic_src,
                          "avg_launch_ms": fps_ms, "algorithmic_bytes_per_launch": fps_bytes,
+                         "ns_per_iteration": fps_ms * 1e6 / max(1, M1 - 1),
                          "note": "latency-bound serial argmax (M-1 dependent block-wide "
                                  "reductions); the HBM fraction is structurally low"},
             "step_hbm": {"algorithmic_bytes": step_bytes,

@@ -84,11 +84,13 @@ size_t pn2_fps_workspace_size(int B, int N);
 int pn2_fps_ws(const float* xyz, int B, int N, int npoint, int32_t* idx, float* new_xyz,
                void* workspace, size_t workspace_bytes, pn2_stream_t stream);
 
-/* The SSG sampler chain in ONE launch: stage 0 samples npoint[0] of the N points of each
- * cloud, stage i samples npoint[i] of stage i-1's output (pointnet2_sem_seg*.py:29-50 samples
+/* The SSG sampler chain: stage 0 samples npoint[0] of the N points of each cloud, stage i
+ * samples npoint[i] of stage i-1's output (pointnet2_sem_seg*.py:29-50 samples
  * 8192 -> 1024 -> 256 -> 64 -> 16). idx[i] (B,npoint[i]) and new_xyz[i] (B,npoint[i],3) are
- * exactly what pn2_fps_gather returns for that stage's input. N <= 8192, npoint[i] <= 1024 for
- * every stage that feeds another, 1 <= nstages <= 4. Host arrays of device pointers. */
+ * exactly what pn2_fps_gather returns for that stage's input. N <= pn2_fps_max_points(),
+ * npoint[i] <= 1024 for every stage that feeds another, 1 <= nstages <= 4. Host arrays of
+ * device pointers. At most two launches on `stream`: a first stage over N > 1024 points as
+ * the ordinary sampler, then every remaining stage fused in one launch. */
 int pn2_fps_chain(const float* xyz, int B, int N, int nstages, const int* npoint,
                   int32_t* const* idx, float* const* new_xyz, pn2_stream_t stream);
 /* out (B,M,3) = inp[b, idx[b,j], :]; inp must have 3 channels (tf_sampling.cpp:131). */

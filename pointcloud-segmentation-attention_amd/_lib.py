@@ -12,7 +12,8 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libpn2hip.so")
+# PN2HIP_LIB: an alternative build of the same ABI (A/B measurements in tools/)
+LIB_PATH = os.environ.get("PN2HIP_LIB") or os.path.join(_HERE, "libpn2hip.so")
 
 PN2_EINVAL = -22
 PN2_USE_XYZ = 1

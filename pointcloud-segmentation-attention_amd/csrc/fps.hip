@@ -94,17 +94,20 @@ __global__ void gather_point_grad_kernel(const float* __restrict__ out_g,
 
 constexpr int kMaxRegPoints = 1024 * 16;
 
-// ---- sampler chain: SA1..SAk's samplers of one cloud in ONE workgroup --------------------
+// ---- sampler chain: SA1..SAk's samplers of one cloud, stage 2.. in ONE workgroup -----------
 // The SSG stack samples 8192 -> 1024 -> 256 -> 64 -> 16, each stage from the previous stage's
-// output. One launch runs every stage of a cloud back to back (no kernel boundary, no event
-// between stages): stage 0 reads the cloud from HBM (with an LDS copy for the centre
-// lookups), every later stage reads its points from the LDS array the previous stage filled
-// as it went. Each stage writes its idx and new_xyz to global memory exactly as pn2_fps_gather
-// does, with the same per-size configuration as fps_impl (BLOCK 256, or wave 0 alone).
+// output. pn2_fps_chain runs a big first stage (N > kChainNext) as the ordinary sampler
+// kernel, then every remaining stage of a cloud back to back in one workgroup (no kernel
+// boundary, no event between stages): the tail kernel's first stage reads its points from
+// HBM (with an LDS copy for the centre lookups), every later stage reads them from the LDS
+// array the previous stage filled as it went. Each stage writes its idx and new_xyz to global
+// memory exactly as pn2_fps_gather does, with the same per-size configuration as fps_impl
+// (BLOCK 256, or wave 0 alone). (Fusing the 8192-point stage too was measured slower: the
+// fused kernel's SA1 loop ran ~4% behind the same loop in its own kernel, more than the
+// launch it saved -- profiles/r1/chain_split.log.)
 constexpr int kChainMax = 4;
 constexpr int kChainBlock = 256;
-constexpr int kChainFirst = 8192;  // stage 0 points (LDS copy 96 KiB)
-constexpr int kChainNext = 1024;   // points fed from one stage to the next (LDS, x2)
+constexpr int kChainNext = 1024;  // points per fused stage (LDS: input copy + 2 hand-over arrays)
 
 struct FpsChain {
   int stages;
@@ -113,34 +116,30 @@ struct FpsChain {
   float* nx[kChainMax];
 };
 
-// one stage for one cloud: the configuration fps_impl uses for this N
+// one stage (N <= kChainNext) for one cloud: the configuration fps_impl uses for this N
 PN2_DEV void chain_stage(const float* P, int N, int M, const float* CXYZ, int32_t* I, float* NX,
                          float* SNEXT, uint2 (*red)[8]) {
   const bool w0 = threadIdx.x < kWave;
   if (N <= 64) { if (w0) fps_v9_body<64, 1, 1>(P, N, M, CXYZ, I, NX, SNEXT, red); }
   else if (N <= 128) { if (w0) fps_v9_body<64, 2, 2>(P, N, M, CXYZ, I, NX, SNEXT, red); }
-  else if (N <= 256) { if (w0) fps_v9_body<64, 4, 4>(P, N, M, CXYZ, I, NX, SNEXT, red); }
-  else if (N <= 512) { if (w0) fps_v9_body<64, 8, 4>(P, N, M, CXYZ, I, NX, SNEXT, red); }
-  else if (N <= 1024) fps_v9_body<256, 4, 4>(P, N, M, CXYZ, I, NX, SNEXT, red);
-  else if (N <= 2048) fps_v9_body<256, 8, 4>(P, N, M, CXYZ, I, NX, SNEXT, red);
-  else if (N <= 4096) fps_v9_body<256, 16, 4>(P, N, M, CXYZ, I, NX, SNEXT, red);
-  else fps_v9_body<256, 32, 4>(P, N, M, CXYZ, I, NX, SNEXT, red);
+  else if (N <= 256) { if (w0) fps_v9_body<64, 4, 4, false, true>(P, N, M, CXYZ, I, NX, SNEXT, red); }
+  else if (N <= 512) { if (w0) fps_v9_body<64, 8, 4, false, true>(P, N, M, CXYZ, I, NX, SNEXT, red); }
+  else fps_v9_body<256, 4, 2, false, true>(P, N, M, CXYZ, I, NX, SNEXT, red);
 }
 
 __global__ __launch_bounds__(kChainBlock) void fps_chain_kernel(const float* __restrict__ xyz,
                                                                 FpsChain c) {
   __shared__ uint2 red[2][8];
-  __shared__ float sxyz[3 * kChainFirst];
+  __shared__ float sxyz[3 * kChainNext];
   __shared__ float snew[2][3 * kChainNext];
   const int b = blockIdx.x;
   const float* __restrict__ P = xyz + (size_t)b * c.n[0] * 3;
   for (int e = threadIdx.x; e < 3 * c.n[0]; e += kChainBlock) sxyz[e] = P[e];
   __syncthreads();
   for (int i = 0; i < c.stages; ++i) {
-    const float* src = i == 0 ? P : snew[(i - 1) & 1];
     const float* cxyz = i == 0 ? sxyz : snew[(i - 1) & 1];
     float* next = i + 1 < c.stages ? snew[i & 1] : nullptr;
-    chain_stage(src, c.n[i], c.m[i], cxyz, c.idx[i] + (size_t)b * c.m[i],
+    chain_stage(cxyz, c.n[i], c.m[i], cxyz, c.idx[i] + (size_t)b * c.m[i],
                 c.nx[i] + (size_t)b * c.m[i] * 3, next, red);
     __syncthreads();  // stage i's LDS output complete before stage i+1 reads it
   }
@@ -157,15 +156,15 @@ int fps_impl(const float* xyz, int B, int N, int M, int32_t* idx, float* nx, voi
     PN2_RETURN_LAUNCH();
   }
   // launch table measured on MI355X (tools/tune_fps.py, B = 16 ScanNet crops,
-  // profiles/r1/tune_fps.jsonl)
+  // profiles/r1/tune_fps.jsonl; lane-resolve variants: profiles/r1/tune_fps_lres.jsonl)
   if (N <= 64) launch_v9<64, 1, 1>(xyz, B, N, M, idx, nx, s);
   else if (N <= 128) launch_v9<64, 2, 2>(xyz, B, N, M, idx, nx, s);
-  else if (N <= 256) launch_v9<64, 4, 4>(xyz, B, N, M, idx, nx, s);
-  else if (N <= 512) launch_v9<64, 8, 4>(xyz, B, N, M, idx, nx, s);
-  else if (N <= 1024) launch_v9<256, 4, 4>(xyz, B, N, M, idx, nx, s);
-  else if (N <= 2048) launch_v9<256, 8, 4>(xyz, B, N, M, idx, nx, s);
-  else if (N <= 4096) launch_v9<256, 16, 4>(xyz, B, N, M, idx, nx, s);
-  else if (N <= 8192) launch_v9<256, 32, 4>(xyz, B, N, M, idx, nx, s);
+  else if (N <= 256) launch_v9<64, 4, 4, true>(xyz, B, N, M, idx, nx, s);
+  else if (N <= 512) launch_v9<64, 8, 4, true>(xyz, B, N, M, idx, nx, s);
+  else if (N <= 1024) launch_v9<256, 4, 2, true>(xyz, B, N, M, idx, nx, s);
+  else if (N <= 2048) launch_v9<256, 8, 2, true>(xyz, B, N, M, idx, nx, s);
+  else if (N <= 4096) launch_v9<256, 16, 4, true>(xyz, B, N, M, idx, nx, s);
+  else if (N <= 8192) launch_v9<256, 32, 4, true>(xyz, B, N, M, idx, nx, s);
   else if (N <= kMaxRegPoints) launch_v9<512, 32, 4>(xyz, B, N, M, idx, nx, s);
   else {
     if (!ws || ws_bytes < (size_t)B * N * sizeof(float)) return PN2_EINVAL;
@@ -183,31 +182,37 @@ int pn2_fps_max_points(void) { return pn2::kMaxRegPoints; }
 
 int pn2_fps_chain(const float* xyz, int B, int N, int nstages, const int* npoint,
                   int32_t* const* idx, float* const* new_xyz, pn2_stream_t stream) {
-  if (B < 0 || N <= 0 || N > pn2::kChainFirst || nstages < 1 || nstages > pn2::kChainMax ||
+  if (B < 0 || N <= 0 || N > pn2::kMaxRegPoints || nstages < 1 || nstages > pn2::kChainMax ||
       !npoint || !idx || !new_xyz)
     return PN2_EINVAL;
-  pn2::FpsChain c;
-  c.stages = nstages;
-  int n = N;
   for (int i = 0; i < nstages; ++i) {
-    const int m = npoint[i];
-    if (m <= 0 || !idx[i] || !new_xyz[i]) return PN2_EINVAL;
-    if (i + 1 < nstages && m > pn2::kChainNext) return PN2_EINVAL;
-    c.n[i] = n;
-    c.m[i] = m;
-    c.idx[i] = idx[i];
-    c.nx[i] = new_xyz[i];
-    n = m;
-  }
-  for (int i = nstages; i < pn2::kChainMax; ++i) {
-    c.n[i] = c.m[i] = 0;
-    c.idx[i] = nullptr;
-    c.nx[i] = nullptr;
+    if (npoint[i] <= 0 || !idx[i] || !new_xyz[i]) return PN2_EINVAL;
+    if (i + 1 < nstages && npoint[i] > pn2::kChainNext) return PN2_EINVAL;
   }
   if (B == 0) return PN2_OK;
   if (!xyz || B > 65535) return PN2_EINVAL;
-  hipLaunchKernelGGL(pn2::fps_chain_kernel, dim3(B), dim3(pn2::kChainBlock), 0,
-                     (hipStream_t)stream, xyz, c);
+  hipStream_t s = (hipStream_t)stream;
+  int first = 0;  // first stage of the fused tail
+  if (N > pn2::kChainNext) {  // the big first stage as its own sampler launch
+    const int rc = pn2::fps_impl(xyz, B, N, npoint[0], idx[0], new_xyz[0], nullptr, 0, s);
+    if (rc != PN2_OK) return rc;
+    if (nstages == 1) return PN2_OK;
+    xyz = new_xyz[0];
+    N = npoint[0];
+    first = 1;
+  }
+  pn2::FpsChain c;
+  c.stages = nstages - first;
+  int n = N;
+  for (int i = 0; i < pn2::kChainMax; ++i) {
+    const bool on = i < c.stages;
+    c.n[i] = on ? n : 0;
+    c.m[i] = on ? npoint[first + i] : 0;
+    c.idx[i] = on ? idx[first + i] : nullptr;
+    c.nx[i] = on ? new_xyz[first + i] : nullptr;
+    if (on) n = c.m[i];
+  }
+  hipLaunchKernelGGL(pn2::fps_chain_kernel, dim3(B), dim3(pn2::kChainBlock), 0, s, xyz, c);
   PN2_RETURN_LAUNCH();
 }
 

@@ -84,7 +84,10 @@ struct Lay9 {
 //   CXYZ  where the winners' coordinates are read each iteration (an LDS copy of P, or P);
 //   I, NX the cloud's idx (M) and new_xyz (M x 3) outputs in global memory (NX may be null);
 //   SNEXT optional LDS array that receives new_xyz too (the next sampler's input).
-template <int BLOCK, int PPT, int G, bool STAMP = false>
+// LRES: every lane resolves its own winning slot with VALU selects right after the scan
+// (independent of, so interleaved with, the wave max), leaving one v_readlane after the ballot
+// instead of the scalar compare chain over the groups.
+template <int BLOCK, int PPT, int G, bool STAMP = false, bool LRES = false>
 PN2_DEV void fps_v9_body(const float* P, int N, int M, const float* CXYZ, int32_t* I, float* NX,
                          float* SNEXT, uint2 (*red)[8]) {
   unsigned long long st_acc[6] = {0, 0, 0, 0, 0, 0}, st_prev = 0;
@@ -97,22 +100,43 @@ PN2_DEV void fps_v9_body(const float* P, int N, int M, const float* CXYZ, int32_
   const int lane = t & (kWave - 1);
   const int w = t / kWave;
 
-  float px[PPT], py[PPT], pz[PPT];
+  // Coordinates as float2 pairs of slots (2h, 2h+1): the distance is computed with packed
+  // v_pk_* ops on register pairs the allocator cannot split (one op per 2 points).
+  using f2 = float __attribute__((ext_vector_type(2)));
+  constexpr bool PK = PPT % 2 == 0;
+  constexpr int NP = PK ? PPT / 2 : 1;
+  f2 vx[NP], vy[NP], vz[NP];
+  float px[PK ? 1 : PPT], py[PK ? 1 : PPT], pz[PK ? 1 : PPT];
   int tb[PPT];  // running min distance as int bits; padding slots -1 never win
+  // Branch-free loads (padding slots read point 0 and are masked after): all PPT loads are in
+  // flight together instead of one load + wait per slot. From CXYZ, the LDS copy when there
+  // is one (P == CXYZ otherwise).
+  (void)P;
+  float lx[PPT], ly[PPT], lz[PPT];
 #pragma unroll
   for (int s = 0; s < PPT; ++s) {
     const int k = Lay::point(t, s);
-    if (k < N) {
-      px[s] = P[3 * k + 0];
-      py[s] = P[3 * k + 1];
-      pz[s] = P[3 * k + 2];
-      tb[s] = __float_as_int(kInitTemp);
+    const int kk = k < N ? k : 0;
+    lx[s] = CXYZ[3 * kk + 0];
+    ly[s] = CXYZ[3 * kk + 1];
+    lz[s] = CXYZ[3 * kk + 2];
+  }
+#pragma unroll
+  for (int s = 0; s < PPT; ++s) {
+    const bool in = Lay::point(t, s) < N;
+    lx[s] = in ? lx[s] : 0.0f;
+    ly[s] = in ? ly[s] : 0.0f;
+    lz[s] = in ? lz[s] : 0.0f;
+    tb[s] = in ? __float_as_int(kInitTemp) : -1;
+    if constexpr (PK) {
+      vx[s / 2][s % 2] = lx[s];
+      vy[s / 2][s % 2] = ly[s];
+      vz[s / 2][s % 2] = lz[s];
     } else {
-      px[s] = py[s] = pz[s] = 0.0f;
-      tb[s] = -1;
+      px[s] = lx[s]; py[s] = ly[s]; pz[s] = lz[s];
     }
   }
-  float cx = P[0], cy = P[1], cz = P[2];
+  float cx = CXYZ[0], cy = CXYZ[1], cz = CXYZ[2];
   if (t == 0) {
     I[0] = 0;
     if (NX) { NX[0] = cx; NX[1] = cy; NX[2] = cz; }
@@ -123,6 +147,21 @@ PN2_DEV void fps_v9_body(const float* P, int N, int M, const float* CXYZ, int32_
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_prev)::"memory");
   }
   for (int j = 1; j < M; ++j) {
+    int dv[PPT];  // this iteration's squared distances as int bits
+    if constexpr (PK) {
+      const f2 c2x = {cx, cx}, c2y = {cy, cy}, c2z = {cz, cz};
+#pragma unroll
+      for (int h = 0; h < NP; ++h) {  // same rounding sequence as sqdist(), two points per op
+        const f2 dx = vx[h] - c2x, dy = vy[h] - c2y, dz = vz[h] - c2z;
+        const f2 d = (dx * dx + dy * dy) + dz * dz;
+        dv[2 * h] = __float_as_int(d.x);
+        dv[2 * h + 1] = __float_as_int(d.y);
+      }
+    } else {
+#pragma unroll
+      for (int s = 0; s < PPT; ++s)
+        dv[s] = __float_as_int(sqdist(px[s], py[s], pz[s], cx, cy, cz));
+    }
     int bd = -1, bg = 0;
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
@@ -130,7 +169,7 @@ PN2_DEV void fps_v9_body(const float* P, int N, int M, const float* CXYZ, int32_
 #pragma unroll
       for (int q = 0; q < G; ++q) {
         const int s = g * G + q;
-        v[q] = min(__float_as_int(sqdist(px[s], py[s], pz[s], cx, cy, cz)), tb[s]);
+        v[q] = min(dv[s], tb[s]);
         tb[s] = v[q];
       }
       int m;
@@ -142,22 +181,42 @@ PN2_DEV void fps_v9_body(const float* P, int N, int M, const float* CXYZ, int32_
     }
     // wave: lowest lane holding the wave max, then its first slot holding it
     const uint32_t hi = (uint32_t)(bd + 1);  // 0 for lanes with padding only
+    int ls = 0;  // LRES: this lane's first slot holding bd
+    if constexpr (LRES) {
+      int a[G > 1 ? G - 1 : 1];
+#pragma unroll
+      for (int q = 0; q + 1 < G; ++q) a[q] = tb[q];
+#pragma unroll
+      for (int g = 1; g < NG; ++g) {
+        const bool sel = bg == g;
+#pragma unroll
+        for (int q = 0; q + 1 < G; ++q) a[q] = sel ? tb[g * G + q] : a[q];
+      }
+      int r = G - 1;
+#pragma unroll
+      for (int q = G - 2; q >= 0; --q) r = a[q] == bd ? q : r;
+      ls = bg * G + r;
+    }
     PN2_STAMP(0)
     const uint32_t km = wave_max_u32(hi);
     PN2_STAMP(1)
     const uint64_t hold = __builtin_amdgcn_ballot_w64(hi == km);
     const int L = (int)__builtin_amdgcn_readfirstlane((int)__builtin_ctzll(hold));
-    const int gq = __builtin_amdgcn_readlane(bg, L);
-    const int kv = (int)km - 1;
     int sq = 0;
+    if constexpr (LRES) {
+      sq = __builtin_amdgcn_readlane(ls, L);
+    } else {
+      const int gq = __builtin_amdgcn_readlane(bg, L);
+      const int kv = (int)km - 1;
 #pragma unroll
-    for (int g = 0; g < NG; ++g) {
-      if (g == gq) {
-        int r = G - 1;
+      for (int g = 0; g < NG; ++g) {
+        if (g == gq) {
+          int r = G - 1;
 #pragma unroll
-        for (int q = G - 2; q >= 0; --q)
-          if (__builtin_amdgcn_readlane(tb[g * G + q], L) == kv) r = q;
-        sq = g * G + r;
+          for (int q = G - 2; q >= 0; --q)
+            if (__builtin_amdgcn_readlane(tb[g * G + q], L) == kv) r = q;
+          sq = g * G + r;
+        }
       }
     }
     int old = Lay::point(w * kWave + L, sq);
@@ -189,7 +248,7 @@ PN2_DEV void fps_v9_body(const float* P, int N, int M, const float* CXYZ, int32_
   }
 }
 
-template <int BLOCK, int PPT, int G, bool XYZ_LDS, bool STAMP = false>
+template <int BLOCK, int PPT, int G, bool XYZ_LDS, bool STAMP = false, bool LRES = false>
 __global__ __launch_bounds__(BLOCK) void fps_v9_kernel(const float* __restrict__ xyz, int N,
                                                        int M, int32_t* __restrict__ idx,
                                                        float* __restrict__ new_xyz) {
@@ -201,19 +260,19 @@ __global__ __launch_bounds__(BLOCK) void fps_v9_kernel(const float* __restrict__
     for (int e = threadIdx.x; e < 3 * N; e += BLOCK) sxyz[e] = P[e];
     __syncthreads();
   }
-  fps_v9_body<BLOCK, PPT, G, STAMP>(P, N, M, XYZ_LDS ? sxyz : P, idx + (size_t)b * M,
+  fps_v9_body<BLOCK, PPT, G, STAMP, LRES>(P, N, M, XYZ_LDS ? sxyz : P, idx + (size_t)b * M,
                                     new_xyz ? new_xyz + (size_t)b * M * 3 : nullptr, nullptr,
                                     red);
 }
 
-template <int BLOCK, int PPT, int G>
+template <int BLOCK, int PPT, int G, bool LRES = false>
 void launch_v9(const float* xyz, int B, int N, int M, int32_t* idx, float* nx, hipStream_t s) {
   if constexpr (3 * BLOCK * PPT * 4 + 256 <= 160 * 1024)
-    hipLaunchKernelGGL((fps_v9_kernel<BLOCK, PPT, G, true>), dim3(B), dim3(BLOCK), 0, s, xyz, N,
-                       M, idx, nx);
+    hipLaunchKernelGGL((fps_v9_kernel<BLOCK, PPT, G, true, false, LRES>), dim3(B), dim3(BLOCK),
+                       0, s, xyz, N, M, idx, nx);
   else
-    hipLaunchKernelGGL((fps_v9_kernel<BLOCK, PPT, G, false>), dim3(B), dim3(BLOCK), 0, s, xyz,
-                       N, M, idx, nx);
+    hipLaunchKernelGGL((fps_v9_kernel<BLOCK, PPT, G, false, false, LRES>), dim3(B), dim3(BLOCK),
+                       0, s, xyz, N, M, idx, nx);
 }
 
 

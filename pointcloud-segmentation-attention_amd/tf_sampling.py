@@ -50,7 +50,7 @@ def farthest_point_sample_and_gather(npoint, inp):
     return _fps(npoint, inp, True)
 
 
-CHAIN_MAX_POINTS = 8192   # pn2_fps_chain: first stage's points per cloud
+CHAIN_MAX_POINTS = 16384  # pn2_fps_chain: first stage's points per cloud (pn2_fps_max_points)
 CHAIN_MAX_FEED = 1024     # points one stage hands to the next
 CHAIN_MAX_STAGES = 4
 
@@ -61,7 +61,8 @@ def chain_supported(N, npoints):
 
 
 def farthest_point_sample_chain(npoints, inp, out=None):
-    """The samplers of consecutive SA layers in one launch (pn2_fps_chain): stage i samples
+    """The samplers of consecutive SA layers (pn2_fps_chain: a big first stage, then the rest
+    fused in one launch): stage i samples
     npoints[i] points of stage i-1's new_xyz (stage 0 of inp (B,N,3)). Returns
     [(idx_i, new_xyz_i)], each exactly farthest_point_sample_and_gather(npoints[i], input_i).
     `out` optionally supplies those tensors (written in place, e.g. a step's fixed buffers)."""

@@ -1,0 +1,38 @@
+#!/usr/bin/env python3
+"""Time the fused SSG sampler chain (pn2_fps_chain) against its four stages launched one by
+one (farthest_point_sample_and_gather), B = 16 ScanNet crops, nothing else on the GPU."""
+import importlib, json, os, statistics, sys
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+
+pkg = importlib.import_module("pointcloud-segmentation-attention_amd")
+dev = torch.device("cuda:0")
+B, N, npts = 16, 8192, [1024, 256, 64, 16]
+x = torch.from_numpy(pkg.synth.batch(range(B), N, "scannet")[0]).to(dev)
+ts = pkg.tf_sampling
+
+
+def timeit(fn, reps=20):
+    for _ in range(3):
+        fn()
+    out = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        fn()
+        b.record()
+        b.synchronize()
+        out.append(a.elapsed_time(b) * 1e3)
+    return statistics.median(out)
+
+
+res = {"chain_us": timeit(lambda: ts.farthest_point_sample_chain(npts, x))}
+for k in (1, 2, 3):  # the chain cut after k stages
+    res[f"chain{k}_us"] = timeit(lambda k=k: ts.farthest_point_sample_chain(npts[:k], x))
+ins = [x]
+for m in npts:
+    ins.append(ts.farthest_point_sample_and_gather(m, ins[-1])[1])
+for i, m in enumerate(npts):
+    res[f"stage{i + 1}_us"] = timeit(lambda i=i, m=m: ts.farthest_point_sample_and_gather(m, ins[i]))
+res["stages_sum_us"] = sum(res[f"stage{i + 1}_us"] for i in range(4))
+print(json.dumps({k: round(v, 1) for k, v in res.items()}))

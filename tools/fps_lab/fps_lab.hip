@@ -1442,6 +1442,20 @@ int fps_tune_impl(const float* xyz, int B, int N, int M, int32_t* idx, float* nx
     PN2_V11(256, 32, 2) PN2_V11(512, 16, 2) PN2_V11(256, 64, 4)
 #undef PN2_V11
   }
+  if (variant == 95 || variant == 96) {  // v9 with the lane-parallel slot resolve (G = 4 / 2)
+    const int G = variant == 95 ? 4 : 2;
+#define PN2_V9L(BL, PP, GG)                                                    \
+    if (block == BL && ppt == PP && G == GG) {                                 \
+      launch_v9<BL, PP, GG, true>(xyz, B, N, M, idx, nx, s);                   \
+      PN2_RETURN_LAUNCH();                                                     \
+    }
+    PN2_V9L(256, 32, 4) PN2_V9L(256, 32, 2) PN2_V9L(512, 16, 4) PN2_V9L(256, 4, 4)
+    PN2_V9L(256, 4, 2) PN2_V9L(256, 16, 4) PN2_V9L(64, 4, 4) PN2_V9L(64, 4, 2) PN2_V9L(128, 8, 4)
+    PN2_V9L(256, 8, 4) PN2_V9L(64, 16, 4) PN2_V9L(256, 64, 4) PN2_V9L(64, 8, 4) PN2_V9L(64, 8, 2)
+    PN2_V9L(256, 8, 2) PN2_V9L(256, 16, 2) PN2_V9L(512, 32, 4) PN2_V9L(64, 2, 2)
+    PN2_V9L(512, 32, 2) PN2_V9L(128, 4, 2)
+#undef PN2_V9L
+  }
   if (variant >= 91 && variant <= 94) {  // v9, variant = 90 + G (slots per max3 group)
     const int G = variant - 90;
 #define PN2_V9(BL, PP, GG)                                                     \
@@ -1561,7 +1575,7 @@ int pn2_fps_stamp(const float* xyz, int N, int npoint, int32_t* idx, int block, 
     } else
     PN2_S11(256, 32) PN2_S11(512, 16) PN2_S11(256, 4) { return PN2_EINVAL; }
 #undef PN2_S11
-  } else if (ppt >= 90000) {  // v9 (G = 4) stamped: ppt = 90000 + PP
+  } else if (ppt >= 90000 && ppt < 95000) {  // v9 (G = 4) stamped: ppt = 90000 + PP
 #define PN2_S9(BL, PP)                                                                       \
     if (block == BL && ppt == 90000 + PP) {                                                  \
       hipLaunchKernelGGL((pn2::fps_v9_kernel<BL, PP, 4, true, true>), dim3(1), dim3(BL), 0, s, \
@@ -1569,6 +1583,14 @@ int pn2_fps_stamp(const float* xyz, int N, int npoint, int32_t* idx, int block, 
     } else
     PN2_S9(256, 32) PN2_S9(512, 16) PN2_S9(256, 4) PN2_S9(256, 16) { return PN2_EINVAL; }
 #undef PN2_S9
+  } else if (ppt >= 95000 && ppt < 96000) {  // v9 lane-resolve (G = 4) stamped: 95000 + PP
+#define PN2_S9L(BL, PP)                                                                      \
+    if (block == BL && ppt == 95000 + PP) {                                                  \
+      hipLaunchKernelGGL((pn2::fps_v9_kernel<BL, PP, 4, true, true, true>), dim3(1), dim3(BL), \
+                         0, s, xyz, N, npoint, idx, nullptr);                                \
+    } else
+    PN2_S9L(256, 32) PN2_S9L(256, 4) { return PN2_EINVAL; }
+#undef PN2_S9L
   } else if (ppt >= 20000) {  // v8 stamped: ppt = 20000 + PP
 #define PN2_S8(BL, PP)                                                                       \
     if (block == BL && ppt == 20000 + PP) {                                                  \

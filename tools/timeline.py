@@ -12,10 +12,10 @@ def short(n):
 
 rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-starts = [i for i, r in enumerate(rows) if "fps_chain" in r["Kernel_Name"]]
+starts = [i for i, r in enumerate(rows) if "fps_v" in r["Kernel_Name"]
+          and r.get("Grid_Size_X") in ("4096", "8192", "16384")]
 if not starts:
-    starts = [i for i, r in enumerate(rows) if "fps_v" in r["Kernel_Name"]
-              and r.get("Grid_Size_X") in ("4096", "8192", "16384")]
+    starts = [i for i, r in enumerate(rows) if "fps_chain" in r["Kernel_Name"]]
 which = int(sys.argv[2]) if len(sys.argv) > 2 else -3
 i0 = starts[which]
 i1 = starts[which + 1] if which + 1 < len(starts) else len(rows)

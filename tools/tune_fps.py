@@ -32,8 +32,23 @@ V11 = [(64, 1, 1), (64, 2, 2), (64, 4, 4), (64, 8, 4), (256, 4, 4), (256, 8, 4),
        (256, 32, 2), (512, 16, 2), (256, 64, 4)]
 
 
+V9L = [(256, 32, 4), (256, 32, 2), (512, 16, 4), (256, 4, 4), (256, 4, 2), (256, 16, 4),
+       (64, 4, 4), (64, 4, 2), (128, 8, 4), (256, 8, 4), (64, 16, 4), (256, 64, 4), (64, 8, 4),
+       (64, 8, 2), (256, 8, 2), (256, 16, 2), (512, 32, 4), (64, 2, 2), (512, 32, 2), (128, 4, 2)]
+ONLY = os.environ.get("TUNE_ONLY")  # e.g. "91-96": restrict to these variant numbers
+
+
 def candidates(N, slack):
+    c = _candidates(N, slack)
+    if ONLY:
+        lo, hi = (int(x) for x in ONLY.split("-"))
+        c = [x for x in c if lo <= x[0] <= hi]
+    return c
+
+
+def _candidates(N, slack):
     c = [(2, bl, pp) for bl, pp in V2 if N <= bl * pp <= max(slack * N, 64)]
+    c += [(95 if g == 4 else 96, bl, pp) for bl, pp, g in V9L if N <= bl * pp <= max(slack * N, 64)]
     c += [(110 + g, bl, pp) for bl, pp, g in V11 if N <= bl * pp <= max(slack * N, 64)]
     c += [(90 + g, bl, pp) for bl, pp, g in V9 if N <= bl * pp <= max(slack * N, 64)]
     return c
@@ -54,6 +69,8 @@ def main():
     rounds = int(os.environ.get("TUNE_ROUNDS", "5"))
     sizes = [(64, 16), (128, 32), (256, 64), (512, 128), (1024, 256), (2048, 256), (4096, 512),
              (8192, 1024), (16384, 512)]
+    if os.environ.get("TUNE_SIZES"):  # e.g. "8192:1024,1024:256"
+        sizes = [tuple(int(v) for v in t.split(":")) for t in os.environ["TUNE_SIZES"].split(",")]
     stream = torch.cuda.current_stream().cuda_stream
     # exactness of every candidate on tie-heavy inputs first (grid lattice, duplicates, uniform)
     rng = np.random.default_rng(0)
