@@ -22,7 +22,7 @@ SSG_FP_OUT = (256, 256, 128, 128)
 MSG_SA = ((512, (0.1, 0.2, 0.4), (16, 32, 128), (64, 128, 128)),
           (128, (0.2, 0.4, 0.8), (32, 64, 128), (128, 256, 256)))
 
-NSIDE = 3  # side streams of the overlapped step
+NSIDE = 4  # side streams of the overlapped step (SSG)
 
 CONFIGS = {
     # name: (points per cloud, kind, with_features, attention)
@@ -93,10 +93,12 @@ class Step:
     """One benchmark step as a list of tasks over streams.
 
     The FPS samplers form a serial chain (each samples the previous layer's output) that
-    keeps only B workgroups busy; it runs on lane 0 with nothing else in its way. Everything
-    that hangs off sampler i -- layer i's ball query / grouping / attention (lane 1) and the
-    FP layer that interpolates onto level i-1 (lane 2; MSG: one lane per radius) -- waits for
-    that sampler only and runs concurrently with the samplers after it and with each other.
+    keeps only B workgroups busy. The SA1 sampler (~85 % of the chain) runs on lane 0 with
+    nothing else in its way; SA2..SA4's samplers run fused on lane 4, so with pipelining the
+    next step's SA1 sampler follows this one back to back. Everything that hangs off sampler
+    i -- layer i's ball query / grouping / attention (lane 1) and the FP layer that
+    interpolates onto level i-1 (lanes 2-3; MSG: one lane per radius) -- waits for that
+    sampler only and runs concurrently with the samplers after it and with each other.
     The SA1 ball-query grid needs only the input cloud and is built on lane 1 while SA1 is
     sampled. Lanes join lane 0 at the end of the step.
 
@@ -179,17 +181,18 @@ class Step:
             for i, (_, nx) in enumerate(v["chain"]):
                 v["xyz"][i + 1] = nx
 
-            # lane 0: SA1's sampler, then SA2..SA4's samplers fused in one launch (both direct
-            # launches into fixed buffers; bench.py times "fps1")
+            # lane 0: SA1's sampler alone (bench.py times it); lane 4: SA2..SA4's samplers
+            # fused in one launch, so the next step's SA1 sampler follows this one directly.
+            # Both are direct launches into fixed buffers.
             tasks.append(Task("fps1", 0, (), lambda: tf_sampling.farthest_point_sample_chain(
                 npoints[:1], xyz, out=v["chain"][:1]), direct=True))
-            tasks.append(Task("fps234", 0, (), lambda: tf_sampling.farthest_point_sample_chain(
+            tasks.append(Task("fps234", 4, ("fps1",), lambda: tf_sampling.farthest_point_sample_chain(
                 npoints[1:], v["xyz"][1], out=v["chain"][1:]), direct=True))
             sampled = ("fps1", "fps234", "fps234", "fps234")
         else:
-            # lane 0: SA1's sampler alone, then SA2..SA4's samplers as one task
+            # lane 0: SA1's sampler alone; lane 4: SA2..SA4's samplers as one task
             tasks.append(Task("fps1", 0, (), fps(0)))
-            tasks.append(Task("fps234", 0, (), lambda: [fps(i)() for i in (1, 2, 3)]))
+            tasks.append(Task("fps234", 4, ("fps1",), lambda: [fps(i)() for i in (1, 2, 3)]))
             sampled = ("fps1", "fps234", "fps234", "fps234")
         tasks.append(Task("sa1", 1, (sampled[0],), sa(0)))
         tasks.append(Task("fp4", 2, (sampled[0],) + grid_dep, fp(0)))
