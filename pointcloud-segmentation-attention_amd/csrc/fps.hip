@@ -130,11 +130,11 @@ PN2_DEV void chain_stage(const float* P, int N, int M, const float* CXYZ, int32_
 __global__ __launch_bounds__(kChainBlock) void fps_chain_kernel(const float* __restrict__ xyz,
                                                                 FpsChain c) {
   __shared__ uint2 red[2][8];
-  __shared__ float sxyz[3 * kChainNext];
+  __shared__ __attribute__((aligned(16))) float sxyz[3 * kChainNext];
   __shared__ float snew[2][3 * kChainNext];
   const int b = blockIdx.x;
   const float* __restrict__ P = xyz + (size_t)b * c.n[0] * 3;
-  for (int e = threadIdx.x; e < 3 * c.n[0]; e += kChainBlock) sxyz[e] = P[e];
+  copy_to_lds<kChainBlock>(sxyz, P, 3 * c.n[0]);
   __syncthreads();
   for (int i = 0; i < c.stages; ++i) {
     const float* cxyz = i == 0 ? sxyz : snew[(i - 1) & 1];

@@ -1442,6 +1442,19 @@ int fps_tune_impl(const float* xyz, int B, int N, int M, int32_t* idx, float* nx
     PN2_V11(256, 32, 2) PN2_V11(512, 16, 2) PN2_V11(256, 64, 4)
 #undef PN2_V11
   }
+  if (variant == 97 || variant == 98) {  // v9 lane resolve + atomic block step (G = 4 / 2)
+    const int G = variant == 97 ? 4 : 2;
+#define PN2_V9A(BL, PP, GG)                                                    \
+    if (block == BL && ppt == PP && G == GG) {                                 \
+      launch_v9<BL, PP, GG, true, true>(xyz, B, N, M, idx, nx, s);             \
+      PN2_RETURN_LAUNCH();                                                     \
+    }
+    PN2_V9A(256, 32, 4) PN2_V9A(256, 32, 2) PN2_V9A(512, 16, 4) PN2_V9A(256, 4, 4)
+    PN2_V9A(256, 4, 2) PN2_V9A(256, 16, 4) PN2_V9A(256, 8, 4) PN2_V9A(256, 8, 2)
+    PN2_V9A(256, 16, 2) PN2_V9A(512, 32, 4) PN2_V9A(512, 32, 2) PN2_V9A(128, 4, 2)
+    PN2_V9A(128, 8, 4) PN2_V9A(512, 8, 2) PN2_V9A(512, 4, 2)
+#undef PN2_V9A
+  }
   if (variant == 95 || variant == 96) {  // v9 with the lane-parallel slot resolve (G = 4 / 2)
     const int G = variant == 95 ? 4 : 2;
 #define PN2_V9L(BL, PP, GG)                                                    \
@@ -1591,6 +1604,14 @@ int pn2_fps_stamp(const float* xyz, int N, int npoint, int32_t* idx, int block, 
     } else
     PN2_S9L(256, 32) PN2_S9L(256, 4) { return PN2_EINVAL; }
 #undef PN2_S9L
+  } else if (ppt >= 97000 && ppt < 98000) {  // v9 lane-resolve + atomic (G = 4): 97000 + PP
+#define PN2_S9A(BL, PP)                                                                      \
+    if (block == BL && ppt == 97000 + PP) {                                                  \
+      hipLaunchKernelGGL((pn2::fps_v9_kernel<BL, PP, 4, true, true, true, true>), dim3(1),   \
+                         dim3(BL), 0, s, xyz, N, npoint, idx, nullptr);                      \
+    } else
+    PN2_S9A(256, 32) PN2_S9A(256, 4) { return PN2_EINVAL; }
+#undef PN2_S9A
   } else if (ppt >= 20000) {  // v8 stamped: ppt = 20000 + PP
 #define PN2_S8(BL, PP)                                                                       \
     if (block == BL && ppt == 20000 + PP) {                                                  \

@@ -11,8 +11,8 @@ dev = torch.device("cuda:0")
 names = ["scan", "wave_reduce", "write+barrier", "xwave_reduce", "centre_load", "idx_store"]
 # v6 rows (block < 0): scan = active-cell scans, wave_reduce = lane max + wave reduce, idx_store also holds the setup
 names9 = ["scan", "wave_max", "ballot+resolve", "write+barrier", "xwave", "centre+store"]
-RUNS = [(8192, 1024, 256, 90032), (8192, 1024, 256, 95032), (1024, 256, 256, 90004),
-        (1024, 256, 256, 95004)]
+RUNS = [(8192, 1024, 256, 95032), (8192, 1024, 256, 97032), (1024, 256, 256, 95004),
+        (1024, 256, 256, 97004)]
 for N, M, bl, pp in RUNS:
     x = torch.from_numpy(pkg.synth.batch([0], N, "scannet")[0]).to(dev)
     idx = torch.empty((1, M), dtype=torch.int32, device=dev)
@@ -29,6 +29,9 @@ for N, M, bl, pp in RUNS:
         d = np.diff(it[1:M])
         print("   per-iteration cycles (wave 0), iterations 1..:", [int(np.median(d[i:i + 64])) for i in range(0, len(d), 64)])
     nm = names9 if pp >= 90000 else names
+    if 97000 <= pp < 98000:
+        nm = ["scan+lane_resolve", "wave_max", "ballot+readlane", "atomic+barrier", "read+decode",
+              "centre+store"]
     if 95000 <= pp < 96000:
         nm = ["scan+lane_resolve", "wave_max", "ballot+readlane", "write+barrier", "xwave",
               "centre+store"]

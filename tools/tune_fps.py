@@ -35,6 +35,9 @@ V11 = [(64, 1, 1), (64, 2, 2), (64, 4, 4), (64, 8, 4), (256, 4, 4), (256, 8, 4),
 V9L = [(256, 32, 4), (256, 32, 2), (512, 16, 4), (256, 4, 4), (256, 4, 2), (256, 16, 4),
        (64, 4, 4), (64, 4, 2), (128, 8, 4), (256, 8, 4), (64, 16, 4), (256, 64, 4), (64, 8, 4),
        (64, 8, 2), (256, 8, 2), (256, 16, 2), (512, 32, 4), (64, 2, 2), (512, 32, 2), (128, 4, 2)]
+V9A = [(256, 32, 4), (256, 32, 2), (512, 16, 4), (256, 4, 4), (256, 4, 2), (256, 16, 4),
+       (256, 8, 4), (256, 8, 2), (256, 16, 2), (512, 32, 4), (512, 32, 2), (128, 4, 2),
+       (128, 8, 4), (512, 8, 2), (512, 4, 2)]
 ONLY = os.environ.get("TUNE_ONLY")  # e.g. "91-96": restrict to these variant numbers
 
 
@@ -49,6 +52,7 @@ def candidates(N, slack):
 def _candidates(N, slack):
     c = [(2, bl, pp) for bl, pp in V2 if N <= bl * pp <= max(slack * N, 64)]
     c += [(95 if g == 4 else 96, bl, pp) for bl, pp, g in V9L if N <= bl * pp <= max(slack * N, 64)]
+    c += [(97 if g == 4 else 98, bl, pp) for bl, pp, g in V9A if N <= bl * pp <= max(slack * N, 64)]
     c += [(110 + g, bl, pp) for bl, pp, g in V11 if N <= bl * pp <= max(slack * N, 64)]
     c += [(90 + g, bl, pp) for bl, pp, g in V9 if N <= bl * pp <= max(slack * N, 64)]
     return c
