@@ -12,6 +12,20 @@
 // workspace (fps_ws_kernel). Measured variants live in tools/fps_lab.
 #include "fps_kernels.h"
 
+// Code placement of the SA1 (256 x 32) sampler's iteration loop. The loop runs ~6 % slower
+// when it starts at an address = 0 mod 8 than at 4 mod 8 (tools/pad_fps.py,
+// profiles/r1/pad_fps.log). tools/place_sa1_loop.py compiles this file, reads where the
+// loop landed and writes build/sa1_pad.h: the number of s_nop placed before the loop (run
+// once per launch) that moves it to the measured best offset.
+#ifndef PN2_SA1_PAD
+#if __has_include("build/sa1_pad.h")
+#include "build/sa1_pad.h"
+#endif
+#endif
+#ifndef PN2_SA1_PAD
+#define PN2_SA1_PAD -1
+#endif
+
 namespace pn2 {
 namespace {
 
@@ -130,11 +144,11 @@ PN2_DEV void chain_stage(const float* P, int N, int M, const float* CXYZ, int32_
 __global__ __launch_bounds__(kChainBlock) void fps_chain_kernel(const float* __restrict__ xyz,
                                                                 FpsChain c) {
   __shared__ uint2 red[2][8];
-  __shared__ __attribute__((aligned(16))) float sxyz[3 * kChainNext];
+  __shared__ float sxyz[3 * kChainNext];
   __shared__ float snew[2][3 * kChainNext];
   const int b = blockIdx.x;
   const float* __restrict__ P = xyz + (size_t)b * c.n[0] * 3;
-  copy_to_lds<kChainBlock>(sxyz, P, 3 * c.n[0]);
+  for (int e = threadIdx.x; e < 3 * c.n[0]; e += kChainBlock) sxyz[e] = P[e];
   __syncthreads();
   for (int i = 0; i < c.stages; ++i) {
     const float* cxyz = i == 0 ? sxyz : snew[(i - 1) & 1];
@@ -164,7 +178,7 @@ int fps_impl(const float* xyz, int B, int N, int M, int32_t* idx, float* nx, voi
   else if (N <= 1024) launch_v9<256, 4, 2, true>(xyz, B, N, M, idx, nx, s);
   else if (N <= 2048) launch_v9<256, 8, 2, true>(xyz, B, N, M, idx, nx, s);
   else if (N <= 4096) launch_v9<256, 16, 4, true>(xyz, B, N, M, idx, nx, s);
-  else if (N <= 8192) launch_v9<256, 32, 4, true>(xyz, B, N, M, idx, nx, s);
+  else if (N <= 8192) launch_v9<256, 32, 4, true, false, PN2_SA1_PAD>(xyz, B, N, M, idx, nx, s);
   else if (N <= kMaxRegPoints) launch_v9<512, 32, 4>(xyz, B, N, M, idx, nx, s);
   else {
     if (!ws || ws_bytes < (size_t)B * N * sizeof(float)) return PN2_EINVAL;

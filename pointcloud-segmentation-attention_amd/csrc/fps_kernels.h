@@ -91,7 +91,10 @@ struct Lay9 {
 // -- then a barrier and a broadcast read, instead of publish / barrier / DPP max / ballot over
 // the waves' entries. Three rotating slots: slot (j+1) % 3 is cleared by thread 0 before
 // iteration j's barrier, after every read of it (iteration j-2, before barrier j-1).
-template <int BLOCK, int PPT, int G, bool STAMP = false, bool LRES = false, bool ATOM = false>
+// PAD >= 0: that many s_nop right before the iteration loop, shifting the loop's code address
+// by 4 * PAD bytes (code-placement experiments, tools/pad_fps.py; the product uses PAD = -1).
+template <int BLOCK, int PPT, int G, bool STAMP = false, bool LRES = false, bool ATOM = false,
+          int PAD = -1>
 PN2_DEV void fps_v9_body(const float* P, int N, int M, const float* CXYZ, int32_t* I, float* NX,
                          float* SNEXT, uint2 (*red)[8]) {
   unsigned long long st_acc[6] = {0, 0, 0, 0, 0, 0}, st_prev = 0;
@@ -155,6 +158,7 @@ PN2_DEV void fps_v9_body(const float* P, int N, int M, const float* CXYZ, int32_
   if constexpr (STAMP) {
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_prev)::"memory");
   }
+  if constexpr (PAD > 0) asm volatile(".rept %0\n\ts_nop 0\n\t.endr" ::"n"(PAD));
   for (int j = 1; j < M; ++j) {
     int dv[PPT];  // this iteration's squared distances as int bits
     if constexpr (PK) {
@@ -264,45 +268,31 @@ PN2_DEV void fps_v9_body(const float* P, int N, int M, const float* CXYZ, int32_
   }
 }
 
-// Copy a cloud's n floats into LDS: 16-byte loads when the source is 16-byte aligned.
-template <int BLOCK>
-PN2_DEV void copy_to_lds(float* dst, const float* __restrict__ src, int n) {
-  if ((reinterpret_cast<uintptr_t>(src) & 15) == 0) {
-    const int n4 = n >> 2;
-    const float4* s4 = reinterpret_cast<const float4*>(src);
-    float4* d4 = reinterpret_cast<float4*>(dst);
-    for (int e = threadIdx.x; e < n4; e += BLOCK) d4[e] = s4[e];
-    for (int e = 4 * n4 + threadIdx.x; e < n; e += BLOCK) dst[e] = src[e];
-  } else {
-    for (int e = threadIdx.x; e < n; e += BLOCK) dst[e] = src[e];
-  }
-}
-
 template <int BLOCK, int PPT, int G, bool XYZ_LDS, bool STAMP = false, bool LRES = false,
-          bool ATOM = false>
+          bool ATOM = false, int PAD = -1>
 __global__ __launch_bounds__(BLOCK) void fps_v9_kernel(const float* __restrict__ xyz, int N,
                                                        int M, int32_t* __restrict__ idx,
                                                        float* __restrict__ new_xyz) {
   __shared__ uint2 red[2][8];
-  __shared__ __attribute__((aligned(16))) float sxyz[XYZ_LDS ? 3 * BLOCK * PPT : 4];
+  __shared__ float sxyz[XYZ_LDS ? 3 * BLOCK * PPT : 1];
   const int b = blockIdx.x;
   const float* __restrict__ P = xyz + (size_t)b * N * 3;
   if constexpr (XYZ_LDS) {
-    copy_to_lds<BLOCK>(sxyz, P, 3 * N);
+    for (int e = threadIdx.x; e < 3 * N; e += BLOCK) sxyz[e] = P[e];
     __syncthreads();
   }
-  fps_v9_body<BLOCK, PPT, G, STAMP, LRES, ATOM>(P, N, M, XYZ_LDS ? sxyz : P, idx + (size_t)b * M,
+  fps_v9_body<BLOCK, PPT, G, STAMP, LRES, ATOM, PAD>(P, N, M, XYZ_LDS ? sxyz : P, idx + (size_t)b * M,
                                     new_xyz ? new_xyz + (size_t)b * M * 3 : nullptr, nullptr,
                                     red);
 }
 
-template <int BLOCK, int PPT, int G, bool LRES = false, bool ATOM = false>
+template <int BLOCK, int PPT, int G, bool LRES = false, bool ATOM = false, int PAD = -1>
 void launch_v9(const float* xyz, int B, int N, int M, int32_t* idx, float* nx, hipStream_t s) {
   if constexpr (3 * BLOCK * PPT * 4 + 256 <= 160 * 1024)
-    hipLaunchKernelGGL((fps_v9_kernel<BLOCK, PPT, G, true, false, LRES, ATOM>), dim3(B),
+    hipLaunchKernelGGL((fps_v9_kernel<BLOCK, PPT, G, true, false, LRES, ATOM, PAD>), dim3(B),
                        dim3(BLOCK), 0, s, xyz, N, M, idx, nx);
   else
-    hipLaunchKernelGGL((fps_v9_kernel<BLOCK, PPT, G, false, false, LRES, ATOM>), dim3(B),
+    hipLaunchKernelGGL((fps_v9_kernel<BLOCK, PPT, G, false, false, LRES, ATOM, PAD>), dim3(B),
                        dim3(BLOCK), 0, s, xyz, N, M, idx, nx);
 }
 

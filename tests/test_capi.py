@@ -111,3 +111,18 @@ def test_ball_threshold_equals_sqrt_predicate(pn2, r):
     s = np.maximum(np.sqrt(cand), np.float32(1e-20))
     assert np.array_equal(cand < T, s < r32)
     assert lib.pn2_ball_threshold(0.0) == 0.0
+
+
+def test_sa1_sampler_loop_placement():
+    """The SA1 sampler's iteration loop sits at a code offset = 4 mod 8 in the built library
+    (the placement measured ~6 % faster than 0 mod 8; tools/place_sa1_loop.py chooses it)."""
+    import sys
+    import tempfile
+    if not os.path.exists("/opt/rocm/lib/llvm/bin/llvm-objdump"):
+        pytest.skip("llvm-objdump not available")
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import place_sa1_loop
+    with tempfile.TemporaryDirectory() as t:
+        off = place_sa1_loop.loop_offset(
+            os.path.join(ROOT, "pointcloud-segmentation-attention_amd", "libpn2hip.so"), t)
+    assert off % 8 == 4, off

@@ -1640,6 +1640,42 @@ int pn2_fps_stamp(const float* xyz, int N, int npoint, int32_t* idx, int block, 
 }
 
 // Tuning entry (not part of include/pn2hip.h): run one (variant, block, ppt) instantiation.
+// Placement experiment: the 256 x 32 LRES sampler with `pad` s_nop at the top of its loop
+// (the lab is built with -falign-loops=64, so pad * 4 bytes = the body's offset in a line).
+extern "C++" {
+template <int PAD>
+static void launch_pad(const float* xyz, int B, int N, int M, int32_t* idx, float* nx,
+                       hipStream_t s) {
+  hipLaunchKernelGGL((pn2::fps_v9_kernel<256, 32, 4, true, false, true, false, PAD>), dim3(B),
+                     dim3(256), 0, s, xyz, N, M, idx, nx);
+}
+}
+int pn2_fps_pad(const float* xyz, int B, int N, int npoint, int32_t* idx, float* new_xyz, int pad,
+                pn2_stream_t stream) {
+  if (N > 8192 || N < 1) return PN2_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  switch (pad) {
+    case 0: launch_pad<0>(xyz, B, N, npoint, idx, new_xyz, s); break;
+    case 1: launch_pad<1>(xyz, B, N, npoint, idx, new_xyz, s); break;
+    case 2: launch_pad<2>(xyz, B, N, npoint, idx, new_xyz, s); break;
+    case 3: launch_pad<3>(xyz, B, N, npoint, idx, new_xyz, s); break;
+    case 4: launch_pad<4>(xyz, B, N, npoint, idx, new_xyz, s); break;
+    case 5: launch_pad<5>(xyz, B, N, npoint, idx, new_xyz, s); break;
+    case 6: launch_pad<6>(xyz, B, N, npoint, idx, new_xyz, s); break;
+    case 7: launch_pad<7>(xyz, B, N, npoint, idx, new_xyz, s); break;
+    case 8: launch_pad<8>(xyz, B, N, npoint, idx, new_xyz, s); break;
+    case 9: launch_pad<9>(xyz, B, N, npoint, idx, new_xyz, s); break;
+    case 10: launch_pad<10>(xyz, B, N, npoint, idx, new_xyz, s); break;
+    case 11: launch_pad<11>(xyz, B, N, npoint, idx, new_xyz, s); break;
+    case 12: launch_pad<12>(xyz, B, N, npoint, idx, new_xyz, s); break;
+    case 13: launch_pad<13>(xyz, B, N, npoint, idx, new_xyz, s); break;
+    case 14: launch_pad<14>(xyz, B, N, npoint, idx, new_xyz, s); break;
+    case 15: launch_pad<15>(xyz, B, N, npoint, idx, new_xyz, s); break;
+    default: return PN2_EINVAL;
+  }
+  PN2_RETURN_LAUNCH();
+}
+
 int pn2_fps_tune(const float* xyz, int B, int N, int npoint, int32_t* idx, float* new_xyz,
                  int variant, int block, int ppt, pn2_stream_t stream) {
   return pn2::fps_tune_impl(xyz, B, N, npoint, idx, new_xyz, variant, block, ppt,
