@@ -197,8 +197,7 @@ def main():
                        "parallelism": f"dp{world} (batch split)",
                        "launch": "eager" if args.eager else
                        "samplers: direct launches; side lanes: hipGraph replay",
-                       "streams": ("SA1 sampler + 4 side streams" if overlap and args.config != "cfg5"
-                                   else "sampler + 3 side streams" if overlap else "one stream")
+                       "streams": ("SA1 sampler + 4 side streams" if overlap else "one stream")
                        + (", steps software-pipelined over 2 buffer sets" if pipelined else "")},
             "roofline": {"kernel": f"SA1 sampler (FPS + gather fused): {B} clouds x {N} pts -> "
                                    f"{M1}, one workgroup per cloud",

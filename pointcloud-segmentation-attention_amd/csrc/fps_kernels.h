@@ -281,9 +281,9 @@ __global__ __launch_bounds__(BLOCK) void fps_v9_kernel(const float* __restrict__
     for (int e = threadIdx.x; e < 3 * N; e += BLOCK) sxyz[e] = P[e];
     __syncthreads();
   }
-  fps_v9_body<BLOCK, PPT, G, STAMP, LRES, ATOM, PAD>(P, N, M, XYZ_LDS ? sxyz : P, idx + (size_t)b * M,
-                                    new_xyz ? new_xyz + (size_t)b * M * 3 : nullptr, nullptr,
-                                    red);
+  fps_v9_body<BLOCK, PPT, G, STAMP, LRES, ATOM, PAD>(
+      P, N, M, XYZ_LDS ? sxyz : P, idx + (size_t)b * M,
+      new_xyz ? new_xyz + (size_t)b * M * 3 : nullptr, nullptr, red);
 }
 
 template <int BLOCK, int PPT, int G, bool LRES = false, bool ATOM = false, int PAD = -1>

@@ -209,10 +209,19 @@ class Step:
         v["gp"] = {}
         tasks = []
 
+        xyz0 = inp["xyz"]
+        B = int(xyz0.shape[0])
+        # the samplers write into fixed buffers (direct launches, no one-kernel graphs)
+        v["fps_out"] = [(torch.empty((B, sa_[0]), dtype=torch.int32, device=xyz0.device),
+                         torch.empty((B, sa_[0], 3), dtype=torch.float32, device=xyz0.device))
+                        for sa_ in MSG_SA]
+        for i, (_, nx) in enumerate(v["fps_out"]):
+            v["xyz"][i + 1] = nx
+
         def fps(i):
             def f():
-                v["xyz"][i + 1] = tf_sampling.farthest_point_sample_and_gather(
-                    MSG_SA[i][0], v["xyz"][i])[1]
+                tf_sampling.farthest_point_sample_chain([MSG_SA[i][0]], v["xyz"][i],
+                                                        out=v["fps_out"][i:i + 1])
             return f
 
         def grp(i, r):
@@ -226,8 +235,13 @@ class Step:
                                                              want_grouped_xyz=False)[0]
             return f
 
+        nr = max(len(sa_[1]) for sa_ in MSG_SA)
         for i in range(len(MSG_SA)):
-            tasks.append(Task(f"fps{i + 1}", 0, (), fps(i)))
+            # lane 0: SA1's sampler only; the later samplers run on lane nr + 1 after it
+            if i == 0:
+                tasks.append(Task("fps1", 0, (), fps(0), direct=True))
+            else:
+                tasks.append(Task(f"fps{i + 1}", nr + 1, (f"fps{i}",), fps(i), direct=True))
             for r in range(len(MSG_SA[i][1])):
                 tasks.append(Task(f"sa{i + 1}_{r}", 1 + r, (f"fps{i + 1}",), grp(i, r)))
         return tasks
