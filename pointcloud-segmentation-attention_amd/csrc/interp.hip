@@ -336,16 +336,18 @@ __global__ __launch_bounds__(kNNBlock) void fp_fused_kernel(
   const int c2v = C2 / VEC, coutv = Cout / VEC;
   const int cb = blockIdx.z * cw;       // first vector column of this workgroup
   const int ce = min(coutv, cb + cw);
-  const int width = ce - cb;
-  if (width <= 0) return;
+  if (ce <= cb) return;
+  // element e -> (row e / cw, column cb + e % cw); the last channel slice can be narrower
+  // than cw (coutv % zsplit != 0), its surplus columns are skipped
   const int nrows = min(kNNRows, n - j0);
-  const int elems = nrows * width;
+  const int elems = nrows * cw;
   const VecT* P2 = reinterpret_cast<const VecT*>(points2 + (size_t)b * m * C2);
   const VecT* P1 = reinterpret_cast<const VecT*>(points1 + (size_t)b * n * C1);
   VecT* O = reinterpret_cast<VecT*>(out + (size_t)b * n * Cout);
   for (int e = threadIdx.x; e < elems; e += kNNBlock) {
     const int rl = (int)fdiv((uint32_t)e, div_cw);
-    const int c = cb + (e - rl * width);
+    const int c = cb + (e - rl * cw);
+    if (c >= ce) continue;
     int r;
     if constexpr (PRE) r = s_row[rl];
     else r = j0 + rl;

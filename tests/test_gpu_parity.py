@@ -349,7 +349,12 @@ def test_three_interpolate_and_idw(env, C):
 
 @pytest.mark.parametrize("n,m,C1,C2", [(64, 16, 256, 512), (256, 64, 128, 256),
                                        (1024, 256, 64, 256), (8192, 1024, 0, 128),
-                                       (8192, 1024, 6, 128), (300, 5, 3, 7)])
+                                       (8192, 1024, 6, 128), (300, 5, 3, 7),
+                                       # channel counts whose vector columns do not split
+                                       # evenly over the workgroups' channel slices
+                                       # (__graft_entry__.smoke's FP layer: 2048 <- 256, 9 + 64)
+                                       (2048, 256, 9, 64), (2048, 256, 9, 67), (1024, 128, 5, 60),
+                                       (4096, 512, 9, 64), (8192, 1024, 9, 70), (512, 64, 12, 52)])
 def test_fp_fused(env, n, m, C1, C2):
     pkg, O, torch, dev = env
     x1 = _cloud(pkg, "scannet", 2, n, seed=11)
