@@ -107,6 +107,10 @@ def main():
                     help="launch every op from Python instead of replaying the captured hipGraphs")
     ap.add_argument("--no-overlap", action="store_true",
                     help="run the whole step on one stream (no side stream beside the sampler chain)")
+    ap.add_argument("--time-every", type=int, default=1,
+                    help="bracket every Nth timed step's SA1 sampler with HIP events (diagnostic)")
+    ap.add_argument("--sets", type=int, default=3,
+                    help="buffer sets the pipelined steps rotate over (>= 2)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="join every step before the next (no overlap of step k's side work "
                          "with step k+1's samplers)")
@@ -134,7 +138,7 @@ def main():
     overlap = not args.no_overlap
     pipelined = overlap and not args.no_pipeline
     if pipelined:
-        pipe = pkg.stack.Pipeline(inp, graphs=not args.eager)
+        pipe = pkg.stack.Pipeline(inp, graphs=not args.eager, nsets=args.sets)
     else:
         step = pkg.stack.Step(inp, overlap=overlap)
         graph = None if args.eager else pkg.stack.GraphStep(inp, overlap=overlap)
@@ -163,13 +167,14 @@ def main():
     barrier()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        outs = run_step(ev[k])
+        outs = run_step(ev[k] if k % args.time_every == 0 else None)
     outs = finish() or outs
     torch.cuda.synchronize()
     barrier()
     elapsed = pkg.shard.max_over_ranks(time.perf_counter() - t0, dev)
 
-    fps_ms = sum(a.elapsed_time(b) for a, b in ev) / len(ev)  # SA1 sampler, per launch
+    timed = [ev[k] for k in range(args.steps) if k % args.time_every == 0]
+    fps_ms = sum(a.elapsed_time(b) for a, b in timed) / len(timed)  # SA1 sampler, per launch
     # per-cloud output checksums, gathered (outside the timed region) so ranks can be compared
     sums = pkg.shard.gather_checksums(pkg.shard.cloud_checksums(outs, B))
 
@@ -198,7 +203,7 @@ def main():
                        "launch": "eager" if args.eager else
                        "samplers: direct launches; side lanes: hipGraph replay",
                        "streams": ("SA1 sampler + 4 side streams" if overlap else "one stream")
-                       + (", steps software-pipelined over 2 buffer sets" if pipelined else "")},
+                       + (f", steps software-pipelined over {args.sets} buffer sets" if pipelined else "")},
             "roofline": {"kernel": f"SA1 sampler (FPS + gather fused): {B} clouds x {N} pts -> "
                                    f"{M1}, one workgroup per cloud",
                          "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS,

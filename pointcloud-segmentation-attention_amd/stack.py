@@ -277,11 +277,12 @@ class Step:
             for lane in range(1, self.nlanes):
                 self.streams[lane].wait_stream(main)
             self.synced_inputs = True
+        done = dict(self.done)  # this run's release events (the timed sampler's is its end event)
         for t in self.tasks:
             st = self._stream(t.lane, main)
             for d in t.deps:
                 if lane_of[d] != t.lane:
-                    st.wait_event(self.done[d])
+                    st.wait_event(done[d])
             timed = t.name == self.SAMPLER and sampler_events is not None
             with torch.cuda.stream(st):
                 if timed:
@@ -289,8 +290,8 @@ class Step:
                 launch(t)
             if any(t.name in u.deps for u in self.tasks):
                 if timed:  # one event both times the sampler and releases its dependents
-                    self.done[t.name] = sampler_events[1]
-                self.done[t.name].record(st)
+                    done[t.name] = sampler_events[1]
+                done[t.name].record(st)
             elif timed:
                 sampler_events[1].record(st)
         # the step's side work is complete when lane 1 is: lanes 2.. hand their last work to it
@@ -376,22 +377,22 @@ class GraphStep:
 
 
 class Pipeline:
-    """Consecutive steps software-pipelined over two buffer sets: step k runs on set k % 2,
-    its side-lane work (ball query, grouping, attention, FP) finishing while step k+1's
-    sampler chain already runs on the shared lane-0 stream. Before a set is reused (step
-    k+2) the HOST waits for that set's side lanes (finished mid-way through step k+1's
-    chain), so no buffer is overwritten while read and lane 0 carries no wait packet between
-    chains. Every step still does all of its work; run(k) returns after enqueueing, join()
-    waits."""
+    """Consecutive steps software-pipelined over `nsets` buffer sets: step k runs on set
+    k % nsets, its side-lane work (the later samplers, ball query, grouping, attention, FP)
+    finishing while the following steps' SA1 samplers already run on the shared lane-0
+    stream. Before a set is reused (step k + nsets) the HOST waits for that set's side lanes,
+    so no buffer is overwritten while read and lane 0 carries no wait packet between
+    samplers; with 3 sets the side work of a step has two sampler periods to finish. Every
+    step still does all of its work; run(k) returns after enqueueing, join() waits."""
 
-    def __init__(self, inp, graphs=True, overlap=True):
+    def __init__(self, inp, graphs=True, overlap=True, nsets=3):
         mk = (lambda: GraphStep(inp, overlap=overlap)) if graphs else \
             (lambda: Step(inp, overlap=overlap))
-        self.sets = [mk(), mk()]
+        self.sets = [mk() for _ in range(max(2, nsets))]
         self.k = 0
 
     def run(self, sampler_events=None):
-        s = self.sets[self.k % 2]
+        s = self.sets[self.k % len(self.sets)]
         self.k += 1
         if isinstance(s, GraphStep):
             if s.step.ran and s.step.overlap:
@@ -406,8 +407,7 @@ class Pipeline:
         """Wait for everything enqueued; returns the outputs of the last step run."""
         for s in self.sets:
             s.join()
-        return self.sets[(self.k - 1) % 2].join()
-
+        return self.sets[(self.k - 1) % len(self.sets)].join()
 
 
 def sa_fp_bytes(config, B):
