@@ -26,6 +26,11 @@
  *   AttentionLayer.call  attention_layer.py:29-45 (reduction)    → pn2_attn_reduce,
  *                                                                  pn2_attn_reduce_grad
  *   SA pooling           pointnet_util.py:130-145, :200          → pn2_group_pool
+ *   pointnet_sa_module   pointnet_util.py:106-145 (group, conv2d  → pn2_group_mlp
+ *     MLP, pooling; tf_util.py:120-185 conv2d + batch_norm)
+ *   pointnet_fp_module   pointnet_util.py:218-238 (interp + MLP)  → pn2_fp_mlp
+ *   conv1d head          tf_util.py:52-117, pointnet2_sem_seg.py  → pn2_shared_mlp
+ *                        :57-60 (fc1, fc2)
  *
  * (reference paths are under pointnet2_tensorflow/tf_ops/{sampling,grouping,interpolation_3d},
  *  pointnet2_tensorflow/utils and attention_points/attention_scannet.)
@@ -63,6 +68,17 @@ typedef void* pn2_stream_t; /* hipStream_t */
 #define PN2_POOL_AVG 1
 #define PN2_POOL_WEIGHTED_AVG 2
 #define PN2_POOL_MAX_AND_AVG 3
+#define PN2_POOL_NONE (-1) /* pn2_group_mlp: per-point output, no pooling */
+
+/* shared-MLP layers (pn2_group_mlp / pn2_fp_mlp / pn2_shared_mlp) */
+#define PN2_MLP_MAX_LAYERS 6
+#define PN2_MLP_RELU 1 /* activation_fn = tf.nn.relu (tf_util.conv2d's default) */
+
+typedef struct pn2_mlp_layer {
+  const void* packed; /* pn2_mlp_pack output (device, 16-byte aligned)                    */
+  int cin, cout;      /* the conv's input / output channels                              */
+  int flags;          /* PN2_MLP_RELU                                                    */
+} pn2_mlp_layer;
 
 const char* pn2_version(void);
 const char* pn2_strerror(int status);
@@ -223,6 +239,45 @@ int pn2_attn_reduce_grad(const float* Q, const float* K, const float* V, const f
  * by PN2_POOL_WEIGHTED_AVG (w = exp(-5|xyz|)/sum). */
 int pn2_group_pool(const float* x, const float* grouped_xyz, int B, int M, int ns, int C,
                    int mode, float* out, pn2_stream_t stream);
+
+/* ---------------------------------------------------------------- shared MLP ------------ */
+
+/* One 1x1-conv layer of tf_util.conv2d / conv1d in inference mode (tf_util.py:165-185):
+ *   y[o] = act(((sum_f x[f] * weight[f][o]) + bias[o]) * bn_scale[o] + bn_shift[o])
+ * with bn_scale = gamma / sqrt(moving_var + eps), bn_shift = beta - moving_mean * bn_scale
+ * (tf.contrib.layers.batch_norm, is_training=False; tf_util.py:512-531). weight (cin,cout)
+ * is TF's [1,1,cin,cout] kernel, row-major. bias, bn_scale, bn_shift (cout) may be NULL
+ * (bn_scale and bn_shift together). Packs into `packed` (pn2_mlp_packed_size bytes, 16-byte
+ * aligned device memory); stored as scale and (bias*scale + shift). */
+size_t pn2_mlp_packed_size(int cin, int cout);
+int pn2_mlp_pack(const float* weight, const float* bias, const float* bn_scale,
+                 const float* bn_shift, int cin, int cout, void* packed, size_t packed_bytes,
+                 pn2_stream_t stream);
+
+/* pointnet_sa_module after sampling and ball query (pointnet_util.py:106-145, MSG :184-200):
+ * group + centre + concat exactly as pn2_group_concat (flags), then `nlayers` packed layers
+ * (layers[0].cin = the grouped width; layers[i+1].cin = layers[i].cout), then pooling over the
+ * nsample neighbours:
+ *   pool = PN2_POOL_MAX / AVG / WEIGHTED_AVG → out (B,M,cout); PN2_POOL_MAX_AND_AVG →
+ *   (B,M,2*cout) = [avg, max]; PN2_POOL_NONE → out (B,M,nsample,cout) (the per-point
+ *   features the attention SA modules feed to AttentionLayer, attention_layer.py:229-263).
+ * Products and sums in fp32 on the matrix cores; the grouped input and the per-layer
+ * activations stay on chip. Host array `layers`. */
+int pn2_group_mlp(const float* xyz, const float* points, const float* new_xyz,
+                  const int32_t* idx, int B, int N, int C, int M, int nsample, int flags,
+                  int nlayers, const pn2_mlp_layer* layers, int pool, float* out,
+                  pn2_stream_t stream);
+/* pointnet_fp_module (pointnet_util.py:218-238): IDW weights of dist (B,n,3) + interpolation
+ * of points2 (B,m,C2) at nn_idx (B,n,3) + concat [interp, points1 (B,n,C1)] (bit-identical to
+ * pn2_fp_apply's output) fed to the packed layers → out (B,n,cout). points1 may be NULL
+ * (C1 = 0). dist / nn_idx come from pn2_three_nn or pn2_three_nn_grid. */
+int pn2_fp_mlp(const float* dist, const int32_t* nn_idx, const float* points1, int C1,
+               const float* points2, int C2, int B, int n, int m, int nlayers,
+               const pn2_mlp_layer* layers, float* out, pn2_stream_t stream);
+/* Per-point MLP over rows: x (rows,cin) → out (rows,cout) (tf_util.conv1d with kernel 1,
+ * e.g. the fc1/fc2 head of pointnet2_sem_seg.py:57-60). */
+int pn2_shared_mlp(const float* x, long long rows, int cin, int nlayers,
+                   const pn2_mlp_layer* layers, float* out, pn2_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -258,6 +258,50 @@ def group_pool(x, grouped_xyz, mode):
     return out
 
 
+# ---------------------------------------------------------------- shared MLP (float64)
+# The dense half of pointnet_sa_module / pointnet_fp_module restated in numpy float64: the bar
+# for the fp32 matrix-core kernels of csrc/mlp.hip (floating point: within a tolerance, stated
+# in tests/test_gpu_mlp.py).
+
+BN_EPSILON = 1e-3  # tf.contrib.layers.batch_norm default (tf_util.py:527-531)
+
+
+def mlp_f64(x, layers):
+    """tf_util.conv2d 1x1 in inference mode, layer by layer (tf_util.py:165-185):
+    y = act(((x W) + b - moving_mean) * gamma / sqrt(moving_variance + eps) + beta).
+    layers: dicts with weights (cin,cout) [, biases, gamma, beta, moving_mean,
+    moving_variance], relu (bool)."""
+    y = np.asarray(x, np.float64)
+    for L in layers:
+        y = y @ np.asarray(L["weights"], np.float64)
+        if L.get("biases") is not None:
+            y = y + np.asarray(L["biases"], np.float64)
+        if L.get("gamma") is not None:
+            g = np.asarray(L["gamma"], np.float64)
+            mean = np.asarray(L["moving_mean"], np.float64)
+            var = np.asarray(L["moving_variance"], np.float64)
+            y = (y - mean) * (g / np.sqrt(var + BN_EPSILON)) + np.asarray(L["beta"], np.float64)
+        if L.get("relu", True):
+            y = np.maximum(y, 0.0)
+    return y
+
+
+def pool_f64(x, grouped_xyz, mode):
+    """Pooling over nsample (pointnet_util.py:130-145), x (B,M,ns,C) -> (B,M,C')."""
+    x = np.asarray(x, np.float64)
+    if mode == "max":
+        return x.max(axis=2)
+    if mode == "avg":
+        return x.mean(axis=2)
+    if mode == "weighted_avg":
+        d = np.sqrt((np.asarray(grouped_xyz, np.float64) ** 2).sum(-1, keepdims=True))
+        e = np.exp(-d * 5)
+        return (x * (e / e.sum(axis=2, keepdims=True))).sum(axis=2)
+    if mode == "max_and_avg":
+        return np.concatenate([x.mean(axis=2), x.max(axis=2)], axis=-1)
+    raise ValueError(mode)
+
+
 # ---------------------------------------------------------------- reference CPU code
 
 def ref_ball_query(xyz1, xyz2, radius, nsample, fill=-1):

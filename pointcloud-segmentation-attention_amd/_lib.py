@@ -19,6 +19,9 @@ PN2_EINVAL = -22
 PN2_USE_XYZ = 1
 PN2_XYZ_LAST = 2
 POOL_MODES = {"max": 0, "avg": 1, "weighted_avg": 2, "max_and_avg": 3}
+PN2_POOL_NONE = -1
+PN2_MLP_MAX_LAYERS = 6
+PN2_MLP_RELU = 1
 
 
 class InvalidArgumentError(ValueError):
@@ -30,6 +33,13 @@ class Pn2RuntimeError(RuntimeError):
 
 
 _P, _I, _F, _S = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_size_t
+_LL = ctypes.c_longlong
+
+
+class MlpLayer(ctypes.Structure):
+    """struct pn2_mlp_layer (include/pn2hip.h)."""
+    _fields_ = [("packed", ctypes.c_void_p), ("cin", ctypes.c_int), ("cout", ctypes.c_int),
+                ("flags", ctypes.c_int)]
 
 # name -> (restype, argtypes); mirrors include/pn2hip.h (tests/test_capi.py checks the header)
 SIGNATURES = {
@@ -66,6 +76,11 @@ SIGNATURES = {
     "pn2_attn_reduce": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P]),
     "pn2_attn_reduce_grad": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P]),
     "pn2_group_pool": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _P]),
+    "pn2_mlp_packed_size": (_S, [_I, _I]),
+    "pn2_mlp_pack": (_I, [_P, _P, _P, _P, _I, _I, _P, _S, _P]),
+    "pn2_group_mlp": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _I, _P, _P]),
+    "pn2_fp_mlp": (_I, [_P, _P, _P, _I, _P, _I, _I, _I, _I, _I, _P, _P, _P]),
+    "pn2_shared_mlp": (_I, [_P, _LL, _I, _I, _P, _P, _P]),
 }
 
 _lib = None

@@ -1,0 +1,678 @@
+// Shared point-wise MLP (1x1 conv + bias + inference batch norm + ReLU) fused with the step
+// before it (grouping, or three-point interpolation) and the pooling after it, gfx950.
+//
+// Replaces, per SA layer, the TF graph of pointnet_util.py:106-145 (pointnet_sa_module):
+//   sample_and_group's grouped [xyz - new_xyz, points]  (pointnet_util.py:39-56, MSG :186-193)
+//   -> for each mlp width: tf_util.conv2d(1x1) = conv + bias_add + batch_norm + relu
+//      (tf_util.py:165-185, batch_norm_template :512-531, inference mode)
+//   -> reduce_max / reduce_mean / weighted_avg / max_and_avg over nsample (:130-145, :200)
+// and per FP layer pointnet_fp_module's interpolation + concat + MLP (pointnet_util.py:218-238),
+// plus plain per-point MLPs (the conv1d head fc1/fc2, pointnet2_sem_seg.py:57-60).
+//
+// Design: one workgroup owns P = 32*R point rows (whole groups, or one slice
+// of a group larger than P). The rows' input features are gathered ONCE into LDS; every layer
+// then runs from LDS to LDS on the fp32 matrix cores (v_mfma_f32_32x32x2_f32: exact fp32
+// products, fp32 accumulation — TF's conv2d is fp32 too), and the last layer is pooled in
+// registers, so the (rows x width) activations never touch HBM. The reference materialises
+// new_points (B,M,ns,3+C) and every layer's output in HBM.
+//
+// MFMA orientation. For layer outputs that feed another layer the product is computed as
+// Y^T = W^T X^T (A = weights: output feature on the lane, B = activations: point on the lane):
+// the accumulator's rows are 4 consecutive features per register quad, stored to LDS as one
+// 16-byte write per quad. The LAST layer swaps A and B (Y = X W): the accumulator holds 16 of
+// the tile's 32 points per lane for one output feature, so pooling over a group is a register
+// max/sum plus one lane^32 exchange, and per-point outputs are 128-byte row segments.
+// Both orientations read the operands through the same lane maps, so one packed weight format
+// serves every layer: Wp[to][c][h][i][s] = W[8c + 4h + s][32*to + i] (pn2_mlp_pack), one
+// float4 per lane per 4 MFMAs, and activations are read as act[p][8c + 4h .. +3].
+#include "common.h"
+
+namespace pn2 {
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int kBlock = 256;
+constexpr int kWaves = kBlock / kWave;
+constexpr int kMaxGroupsPerWG = 16;  // P / ns_pad with P <= 128, ns_pad >= 8
+
+enum Src : int { kSrcGroup = 0, kSrcFP = 1, kSrcRows = 2 };
+enum Layout : int { kPointsOnly = 0, kXyzOnly = 1, kXyzFirst = 2, kXyzLast = 3 };
+
+struct LayerDev {
+  const float4* w;     // packed weights [cout32][cin8][64] float4
+  const float* scale;  // [cout32*32]
+  const float* shift;  // [cout32*32]
+  int cin8, cout32, cout, relu;
+};
+
+struct Params {
+  LayerDev L[PN2_MLP_MAX_LAYERS];
+  int nl;
+  int width0;            // layer-0 input width in LDS (cin8*8)
+  int stride0, stride1;  // LDS row strides (floats) of the activation buffers
+  int off1, off_part, off_run, off_meta;  // float offsets into dynamic LDS
+  FastDiv div_w0;
+  // group source
+  const float* xyz;
+  const float* points;
+  const float* new_xyz;
+  const int32_t* idx;
+  int N, C, M, ns, lg_ns_pad, layout, ngroups, passes, gpw;
+  // fp source
+  const float* dist;
+  const int32_t* nn;
+  const float* p1;
+  const float* p2;
+  int C1, C2, n, m;
+  // rows source
+  const float* x;
+  int cin;
+  long long rows;
+  int pool;
+  float* out;
+};
+
+PN2_DEV float act(float v, int relu) { return relu ? fmaxf(v, 0.f) : v; }
+
+// weight = (1/d)/sum(1/d), d = max(dist, 1e-10)  (pointnet_util.py:219-222); same fp32 order
+// as interp.hip's idw(), so the interpolated features are bit-identical to pn2_fp_apply's.
+PN2_DEV void idw3(float d1, float d2, float d3, float& w1, float& w2, float& w3) {
+  const float r1 = 1.0f / fmaxf(d1, 1e-10f);
+  const float r2 = 1.0f / fmaxf(d2, 1e-10f);
+  const float r3 = 1.0f / fmaxf(d3, 1e-10f);
+  const float norm = (r1 + r2) + r3;
+  w1 = r1 / norm;
+  w2 = r2 / norm;
+  w3 = r3 / norm;
+}
+
+template <int SRC, int R>
+__global__ __launch_bounds__(kBlock) void mlp_kernel(const Params prm) {
+  constexpr int P = 32 * R;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* act0 = smem;
+  float* act1 = smem + prm.off1;
+  float* part = smem + prm.off_part;  // pool partials [R][4][2][coutp]
+  float* run = smem + prm.off_run;    // running pool over passes [2][coutp]
+  int* s_src = reinterpret_cast<int*>(smem + prm.off_meta);  // [P] source row (or -1)
+  int* s_aux = s_src + P;                                      // [P] group centre / base row
+  float* s_pw = reinterpret_cast<float*>(s_aux + P);           // [P] pool weight per slot
+  float* s_fw = s_pw + P;                                      // [P*3] IDW weights (fp source)
+  int* s_fi = reinterpret_cast<int*>(s_fw + 3 * P);            // [P*3] neighbour rows
+  float* s_norm = reinterpret_cast<float*>(s_fi + 3 * P);      // [kMaxGroupsPerWG]
+
+  const int tid = threadIdx.x;
+  const int lane = lane_id();
+  const int wave = tid / kWave;
+  const int col = lane & 31;
+  const int h = lane >> 5;
+  const int ns_pad = 1 << prm.lg_ns_pad;
+  const bool pooled = (SRC == kSrcGroup) && prm.pool >= 0;
+  const LayerDev& LL = prm.L[prm.nl - 1];
+  const int coutp = LL.cout32 * 32;
+
+  for (int pass = 0; pass < prm.passes; ++pass) {
+    // ---- 1. per-slot metadata -----------------------------------------------------------
+    if (tid < P) {
+      const int p = tid;
+      int src = -1, aux = 0;
+      float pw = 0.f;
+      if (SRC == kSrcGroup) {
+        int g, k;
+        if (prm.passes == 1) {
+          g = blockIdx.x * prm.gpw + (p >> prm.lg_ns_pad);
+          k = p & (ns_pad - 1);
+        } else {
+          g = blockIdx.x;
+          k = pass * P + p;
+        }
+        if (g < prm.ngroups) {
+          const int b = g / prm.M;
+          const int kk = k < prm.ns ? k : 0;  // padding slots repeat the first neighbour
+          src = b * prm.N + prm.idx[(size_t)g * prm.ns + kk];
+          aux = g;
+          if (k < prm.ns) {
+            pw = 1.f;
+            if (prm.pool == PN2_POOL_WEIGHTED_AVG) {
+              // exp(-5 |grouped_xyz|) (pointnet_util.py:136-137)
+              const float* q = prm.xyz + (size_t)src * 3;
+              const float* c = prm.new_xyz + (size_t)g * 3;
+              const float dx = q[0] - c[0], dy = q[1] - c[1], dz = q[2] - c[2];
+              pw = expf(-sqrtf((dx * dx + dy * dy) + dz * dz) * 5.0f);
+            }
+          }
+        }
+      } else {
+        const long long row = (long long)blockIdx.x * P + p;
+        if (row < prm.rows) {
+          src = (int)row;
+          if (SRC == kSrcFP) {
+            const int b = (int)(row / prm.n);
+            const float* d = prm.dist + row * 3;
+            const int32_t* ii = prm.nn + row * 3;
+            float w1, w2, w3;
+            idw3(d[0], d[1], d[2], w1, w2, w3);
+            s_fw[3 * p] = w1;
+            s_fw[3 * p + 1] = w2;
+            s_fw[3 * p + 2] = w3;
+            s_fi[3 * p] = b * prm.m + ii[0];
+            s_fi[3 * p + 1] = b * prm.m + ii[1];
+            s_fi[3 * p + 2] = b * prm.m + ii[2];
+          }
+        }
+      }
+      s_src[p] = src;
+      s_aux[p] = aux;
+      s_pw[p] = pw;
+    }
+    if (pooled && prm.pool == PN2_POOL_WEIGHTED_AVG && pass == 0) {
+      // normaliser sum(exp(-5|grouped_xyz|)) over the group's ns entries (:138-139)
+      if (prm.passes == 1) {
+        __syncthreads();
+        for (int gi = wave; gi < prm.gpw; gi += kWaves) {
+          float v = 0.f;
+          for (int k = lane; k < ns_pad; k += kWave) v += s_pw[(gi << prm.lg_ns_pad) + k];
+          v = seg_sum<kWave>(v);
+          if (lane == 0) s_norm[gi] = v;
+        }
+      } else {
+        const int g = blockIdx.x;
+        const int b = g / prm.M;
+        const float* c = prm.new_xyz + (size_t)g * 3;
+        float v = 0.f;
+        for (int k = tid; k < prm.ns; k += kBlock) {
+          const float* q = prm.xyz + ((size_t)b * prm.N + prm.idx[(size_t)g * prm.ns + k]) * 3;
+          const float dx = q[0] - c[0], dy = q[1] - c[1], dz = q[2] - c[2];
+          v += expf(-sqrtf((dx * dx + dy * dy) + dz * dz) * 5.0f);
+        }
+        v = seg_sum<kWave>(v);
+        if (lane == 0) s_norm[8 + wave] = v;
+        __syncthreads();
+        if (tid == 0) s_norm[0] = (s_norm[8] + s_norm[9]) + (s_norm[10] + s_norm[11]);
+      }
+    }
+    __syncthreads();
+    if (pooled && prm.pool == PN2_POOL_WEIGHTED_AVG && tid < P) {
+      const int gi = prm.passes == 1 ? (tid >> prm.lg_ns_pad) : 0;
+      s_pw[tid] = s_pw[tid] / s_norm[gi];
+    }
+
+    // ---- 2. gather the input rows into act0 [P][width0] ---------------------------------
+    {
+      const int W = prm.width0;
+      for (int e = tid; e < P * W; e += kBlock) {
+        const int p = (int)fdiv((uint32_t)e, prm.div_w0);
+        const int f = e - p * W;
+        const int src = s_src[p];
+        float v = 0.f;
+        if (src >= 0) {
+          if (SRC == kSrcGroup) {
+            int cx = -1, cp = f, cin;
+            const int lay = prm.layout;
+            if (lay == kXyzOnly) { cx = f; cin = 3; }
+            else if (lay == kXyzFirst) { cin = prm.C + 3; if (f < 3) cx = f; else cp = f - 3; }
+            else if (lay == kXyzLast) { cin = prm.C + 3; if (f >= prm.C) cx = f - prm.C; }
+            else cin = prm.C;
+            if (f < cin) {
+              if (cx >= 0)  // pointnet_util.py:40 (fp32 subtraction, bit-exact)
+                v = prm.xyz[(size_t)src * 3 + cx] - prm.new_xyz[(size_t)s_aux[p] * 3 + cx];
+              else
+                v = prm.points[(size_t)src * prm.C + cp];
+            }
+          } else if (SRC == kSrcFP) {
+            if (f < prm.C2) {  // three_interpolate (tf_interpolate.cpp:107-127)
+              const float a = prm.p2[(size_t)s_fi[3 * p] * prm.C2 + f] * s_fw[3 * p];
+              const float b = prm.p2[(size_t)s_fi[3 * p + 1] * prm.C2 + f] * s_fw[3 * p + 1];
+              const float c = prm.p2[(size_t)s_fi[3 * p + 2] * prm.C2 + f] * s_fw[3 * p + 2];
+              v = (a + b) + c;
+            } else if (f < prm.C2 + prm.C1) {  // concat [interp, points1] (:226)
+              v = prm.p1[(size_t)src * prm.C1 + (f - prm.C2)];
+            }
+          } else {
+            if (f < prm.cin) v = prm.x[(size_t)src * prm.cin + f];
+          }
+        }
+        act0[p * prm.stride0 + f] = v;
+      }
+    }
+    __syncthreads();
+
+    // ---- 3. the layers ------------------------------------------------------------------
+    for (int l = 0; l < prm.nl; ++l) {
+      const LayerDev& Ld = prm.L[l];
+      const float* in = (l & 1) ? act1 : act0;
+      float* outb = (l & 1) ? act0 : act1;
+      const int Sin = (l & 1) ? prm.stride1 : prm.stride0;
+      const int Sout = (l & 1) ? prm.stride0 : prm.stride1;
+      const bool last = (l == prm.nl - 1);
+      const int nitems = R * Ld.cout32;
+      const int cin8 = Ld.cin8;
+      for (int item = wave; item < nitems; item += kWaves) {
+        const int to = item / R;
+        const int rt = item - to * R;
+        const float4* wp = Ld.w + (size_t)to * cin8 * kWave + lane;
+        const float* ap = in + (32 * rt + col) * Sin + 4 * h;
+        f32x16 acc;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+        // weights through a 4-deep register ring (L2 latency), activations one chunk ahead
+        float4 w0 = wp[0];
+        float4 w1 = wp[(cin8 > 1 ? 1 : 0) * kWave];
+        float4 w2 = wp[(cin8 > 2 ? 2 : 0) * kWave];
+        float4 w3 = wp[(cin8 > 3 ? 3 : 0) * kWave];
+        for (int c = 0; c < cin8; c += 4) {
+#define PN2_MLP_STEP(WR, CI)                                                                \
+  if ((CI) < cin8) {                                                                        \
+    const float4 a = *reinterpret_cast<const float4*>(ap + 8 * (CI));                       \
+    const float4 wc = WR;                                                                   \
+    const int nx = (CI) + 4 < cin8 ? (CI) + 4 : (CI);                                       \
+    WR = wp[(size_t)nx * kWave];                                                            \
+    if (last) {                                                                             \
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, wc.x, acc, 0, 0, 0);                  \
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, wc.y, acc, 0, 0, 0);                  \
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, wc.z, acc, 0, 0, 0);                  \
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, wc.w, acc, 0, 0, 0);                  \
+    } else {                                                                                \
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wc.x, a.x, acc, 0, 0, 0);                  \
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wc.y, a.y, acc, 0, 0, 0);                  \
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wc.z, a.z, acc, 0, 0, 0);                  \
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wc.w, a.w, acc, 0, 0, 0);                  \
+    }                                                                                       \
+  }
+          PN2_MLP_STEP(w0, c)
+          PN2_MLP_STEP(w1, c + 1)
+          PN2_MLP_STEP(w2, c + 2)
+          PN2_MLP_STEP(w3, c + 3)
+#undef PN2_MLP_STEP
+        }
+        if (!last) {
+          // rows = features 32*to + 8q + 4h + e (e = reg & 3), column = point 32*rt + col
+          float* op = outb + (32 * rt + col) * Sout + 32 * to + 4 * h;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int fb = 32 * to + 8 * q + 4 * h;
+            const float4 s = *reinterpret_cast<const float4*>(Ld.scale + fb);
+            const float4 t = *reinterpret_cast<const float4*>(Ld.shift + fb);
+            float4 y;
+            y.x = act(acc[4 * q + 0] * s.x + t.x, Ld.relu);
+            y.y = act(acc[4 * q + 1] * s.y + t.y, Ld.relu);
+            y.z = act(acc[4 * q + 2] * s.z + t.z, Ld.relu);
+            y.w = act(acc[4 * q + 3] * s.w + t.w, Ld.relu);
+            *reinterpret_cast<float4*>(op + 8 * q) = y;
+          }
+        } else {
+          // rows = points 32*rt + (r&3) + 8(r>>2) + 4h, column = feature fo
+          const int fo = 32 * to + col;
+          const float s = Ld.scale[fo], t = Ld.shift[fo];
+          float y[16];
+#pragma unroll
+          for (int r = 0; r < 16; ++r) y[r] = act(acc[r] * s + t, Ld.relu);
+          if (!pooled) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int p = 32 * rt + (r & 3) + 8 * (r >> 2) + 4 * h;
+              if (s_src[p] < 0 || fo >= Ld.cout) continue;
+              long long orow;
+              if (SRC == kSrcGroup) {
+                // per-point output of the group's k-th neighbour (no pooling)
+                int k = (prm.passes == 1) ? (p & (ns_pad - 1)) : pass * P + p;
+                if (k >= prm.ns) continue;
+                orow = (long long)s_aux[p] * prm.ns + k;
+              } else {
+                orow = (long long)blockIdx.x * P + p;
+              }
+              prm.out[orow * Ld.cout + fo] = y[r];
+            }
+          } else {
+            // per local group u of this row tile: u = r >> (lg-1) for ns_pad 8/16, else 0
+            const int lg = prm.lg_ns_pad;
+            const int gpt = lg >= 5 ? 1 : (32 >> lg);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              if (u >= gpt) break;
+              float mx = -__builtin_inff(), sm = 0.f;
+#pragma unroll
+              for (int r = 0; r < 16; ++r) {
+                const int ur = lg >= 5 ? 0 : (r >> (lg - 1));
+                if (ur != u) continue;
+                const int p = 32 * rt + (r & 3) + 8 * (r >> 2) + 4 * h;
+                mx = fmaxf(mx, y[r]);
+                sm = sm + y[r] * s_pw[p];
+              }
+              mx = fmaxf(mx, __shfl_xor(mx, 32, kWave));
+              sm = sm + __shfl_xor(sm, 32, kWave);
+              if (h == 0) {
+                float* pp = part + ((size_t)(rt * 4 + u) * 2) * coutp + fo;
+                pp[0] = mx;
+                pp[coutp] = sm;
+              }
+            }
+          }
+        }
+      }
+      __syncthreads();
+    }
+
+    // ---- 4. pooling: combine the row-tile partials of each group, store -----------------
+    if (pooled) {
+      const int cout = LL.cout;
+      const bool first = pass == 0, final = pass == prm.passes - 1;
+      const int ngr = prm.passes == 1 ? prm.gpw : 1;
+      const int lg = prm.lg_ns_pad;
+      for (int gi = 0; gi < ngr; ++gi) {
+        const int g = prm.passes == 1 ? blockIdx.x * prm.gpw + gi : blockIdx.x;
+        if (g >= prm.ngroups) break;
+        int rt0, nrt, u;
+        if (prm.passes > 1) { rt0 = 0; nrt = R; u = 0; }
+        else if (lg >= 5) { nrt = ns_pad >> 5; rt0 = gi * nrt; u = 0; }
+        else { const int gpt = 32 >> lg; rt0 = gi / gpt; nrt = 1; u = gi - rt0 * gpt; }
+        for (int fo = tid; fo < cout; fo += kBlock) {
+          float mx = -__builtin_inff(), sm = 0.f;
+          for (int rt = rt0; rt < rt0 + nrt; ++rt) {
+            const float* pp = part + ((size_t)(rt * 4 + u) * 2) * coutp + fo;
+            mx = fmaxf(mx, pp[0]);
+            sm = sm + pp[coutp];
+          }
+          if (prm.passes > 1) {
+            if (!first) { mx = fmaxf(mx, run[fo]); sm = run[coutp + fo] + sm; }
+            run[fo] = mx;
+            run[coutp + fo] = sm;
+          }
+          if (final) {
+            const int pool = prm.pool;
+            const float avg = sm / (float)prm.ns;
+            if (pool == PN2_POOL_MAX) prm.out[(size_t)g * cout + fo] = mx;
+            else if (pool == PN2_POOL_AVG) prm.out[(size_t)g * cout + fo] = avg;
+            else if (pool == PN2_POOL_WEIGHTED_AVG) prm.out[(size_t)g * cout + fo] = sm;
+            else {  // max_and_avg: concat [avg, max] (pointnet_util.py:145)
+              prm.out[(size_t)g * 2 * cout + fo] = avg;
+              prm.out[(size_t)g * 2 * cout + cout + fo] = mx;
+            }
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// Packed layer: Wp [cout32][cin8][2][32][4] then scale [cout32*32] then shift [cout32*32].
+// scale = bn_scale (1 without BN), shift = bias*scale + bn_shift; padded rows/columns are 0.
+__global__ void mlp_pack_kernel(const float* __restrict__ W, const float* __restrict__ bias,
+                                const float* __restrict__ bn_scale,
+                                const float* __restrict__ bn_shift, int cin, int cout, int cin8,
+                                int cout32, float* __restrict__ packed) {
+  const long long nw = (long long)cout32 * cin8 * 256;
+  const long long total = nw + 2LL * cout32 * 32;
+  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (long long)gridDim.x * blockDim.x) {
+    float v = 0.f;
+    if (e < nw) {
+      const int s = (int)(e & 3);
+      const int i = (int)((e >> 2) & 31);
+      const int hh = (int)((e >> 7) & 1);
+      const long long tc = e >> 8;
+      const int c = (int)(tc % cin8);
+      const int to = (int)(tc / cin8);
+      const int f = 8 * c + 4 * hh + s, o = 32 * to + i;
+      if (f < cin && o < cout) v = W[(size_t)f * cout + o];
+    } else {
+      const long long r = e - nw;
+      const int which = (int)(r / (cout32 * 32));
+      const int o = (int)(r % (cout32 * 32));
+      if (o < cout) {
+        const float sc = bn_scale ? bn_scale[o] : 1.f;
+        if (which == 0) v = sc;
+        else v = (bias ? bias[o] : 0.f) * sc + (bn_shift ? bn_shift[o] : 0.f);
+      }
+    }
+    packed[e] = v;
+  }
+}
+
+int next_pow2(int v) {
+  int p = 1;
+  while (p < v) p <<= 1;
+  return p;
+}
+int ilog2(int v) {
+  int l = 0;
+  while ((1 << l) < v) ++l;
+  return l;
+}
+
+constexpr size_t kLdsLimit = 160 * 1024;
+
+// Fill the layer table and LDS layout for R row tiles; returns LDS bytes (0 = invalid).
+size_t plan(Params& prm, int nl, const pn2_mlp_layer* layers, int cin0, int R, bool pooled) {
+  const int P = 32 * R;
+  int w0 = ((cin0 + 7) / 8) * 8, w1 = 0;
+  for (int l = 0; l < nl; ++l) {
+    const pn2_mlp_layer& L = layers[l];
+    const int cin8 = (L.cin + 7) / 8, cout32 = (L.cout + 31) / 32;
+    const float* base = static_cast<const float*>(L.packed);
+    prm.L[l].w = reinterpret_cast<const float4*>(base);
+    prm.L[l].scale = base + (size_t)cout32 * cin8 * 256;
+    prm.L[l].shift = prm.L[l].scale + cout32 * 32;
+    prm.L[l].cin8 = cin8;
+    prm.L[l].cout32 = cout32;
+    prm.L[l].cout = L.cout;
+    prm.L[l].relu = (L.flags & PN2_MLP_RELU) ? 1 : 0;
+    if (l < nl - 1) {  // layer l writes buffer (l+1)&1
+      if ((l + 1) & 1) w1 = w1 > cout32 * 32 ? w1 : cout32 * 32;
+      else w0 = w0 > cout32 * 32 ? w0 : cout32 * 32;
+    }
+  }
+  prm.nl = nl;
+  prm.width0 = ((cin0 + 7) / 8) * 8;
+  prm.div_w0 = make_fastdiv((uint32_t)prm.width0);
+  // row strides = 4 (mod 32) floats: the 16-byte reads/writes of 8 consecutive rows hit
+  // distinct bank quads
+  prm.stride0 = ((w0 + 31) / 32) * 32 + 4;
+  prm.stride1 = ((w1 + 31) / 32) * 32 + 4;
+  const int coutp = prm.L[nl - 1].cout32 * 32;
+  size_t off = (size_t)P * prm.stride0;
+  prm.off1 = (int)off;
+  off += (size_t)P * (w1 ? prm.stride1 : 0);
+  prm.off_part = (int)off;
+  if (pooled) off += (size_t)R * 4 * 2 * coutp;
+  prm.off_run = (int)off;
+  if (pooled) off += 2 * (size_t)coutp;
+  prm.off_meta = (int)off;
+  off += (size_t)P * 9 + kMaxGroupsPerWG;
+  return off * sizeof(float);
+}
+
+int check_layers(int nl, const pn2_mlp_layer* layers, int cin0) {
+  if (nl < 1 || nl > PN2_MLP_MAX_LAYERS || !layers) return PN2_EINVAL;
+  int cin = cin0;
+  for (int l = 0; l < nl; ++l) {
+    if (!layers[l].packed || layers[l].cin != cin || layers[l].cout <= 0) return PN2_EINVAL;
+    if ((reinterpret_cast<uintptr_t>(layers[l].packed) & 15) != 0) return PN2_EINVAL;
+    cin = layers[l].cout;
+  }
+  return PN2_OK;
+}
+
+// Dynamic LDS beyond the 64 KiB default is opted into once per instantiation.
+template <int SRC, int R>
+int launch_one(const Params& prm, long long nblocks, size_t lds, hipStream_t s) {
+  static const hipError_t attr = hipFuncSetAttribute(
+      reinterpret_cast<const void*>(&mlp_kernel<SRC, R>),
+      hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsLimit);
+  if (attr != hipSuccess) return (int)attr;
+  hipLaunchKernelGGL((mlp_kernel<SRC, R>), dim3((unsigned)nblocks), dim3(kBlock), lds, s, prm);
+  PN2_RETURN_LAUNCH();
+}
+
+template <int SRC>
+int launch_rows_R(Params& prm, int R, long long nblocks, size_t lds, hipStream_t s) {
+  if (nblocks <= 0) return PN2_OK;
+  if (nblocks > 0x7fffffffLL) return PN2_EINVAL;
+  if (R == 1) return launch_one<SRC, 1>(prm, nblocks, lds, s);
+  if (R == 2) return launch_one<SRC, 2>(prm, nblocks, lds, s);
+  return launch_one<SRC, 4>(prm, nblocks, lds, s);
+}
+
+// Row tiles per workgroup: enough (row tile, output tile) items that the four waves all work
+// on the narrowest layer, within the LDS limit, and not fewer workgroups than CUs when the
+// work allows it.
+int choose_R(Params& prm, int nl, const pn2_mlp_layer* layers, int cin0, bool pooled,
+             long long tiles32, int min_R, size_t* lds_out) {
+  int min_c32 = 1 << 30;
+  for (int l = 0; l < nl; ++l) {
+    const int c32 = (layers[l].cout + 31) / 32;
+    min_c32 = c32 < min_c32 ? c32 : min_c32;
+  }
+  int want = min_c32 >= 4 ? 1 : (min_c32 >= 2 ? 2 : 4);
+  while (want > min_R && tiles32 / want < 256) want >>= 1;
+  if (want < min_R) want = min_R;
+  for (int R = want; R >= min_R; R >>= 1) {
+    const size_t lds = plan(prm, nl, layers, cin0, R, pooled);
+    if (lds <= kLdsLimit) {
+      *lds_out = lds;
+      return R;
+    }
+    if (R == 1) break;
+  }
+  return 0;
+}
+
+}  // namespace
+}  // namespace pn2
+
+extern "C" {
+
+size_t pn2_mlp_packed_size(int cin, int cout) {
+  if (cin <= 0 || cout <= 0) return 0;
+  const size_t cin8 = (size_t)(cin + 7) / 8, cout32 = (size_t)(cout + 31) / 32;
+  return (cout32 * cin8 * 256 + 2 * cout32 * 32) * sizeof(float);
+}
+
+int pn2_mlp_pack(const float* weight, const float* bias, const float* bn_scale,
+                 const float* bn_shift, int cin, int cout, void* packed, size_t packed_bytes,
+                 pn2_stream_t stream) {
+  if (cin <= 0 || cout <= 0 || !weight || !packed) return PN2_EINVAL;
+  if (packed_bytes < pn2_mlp_packed_size(cin, cout)) return PN2_EINVAL;
+  if ((!bn_scale) != (!bn_shift)) return PN2_EINVAL;
+  if ((reinterpret_cast<uintptr_t>(packed) & 15) != 0) return PN2_EINVAL;
+  const int cin8 = (cin + 7) / 8, cout32 = (cout + 31) / 32;
+  const long long total = (long long)cout32 * cin8 * 256 + 2LL * cout32 * 32;
+  long long blocks = (total + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(pn2::mlp_pack_kernel, dim3((unsigned)blocks), dim3(256), 0,
+                     (hipStream_t)stream, weight, bias, bn_scale, bn_shift, cin, cout, cin8,
+                     cout32, static_cast<float*>(packed));
+  PN2_RETURN_LAUNCH();
+}
+
+int pn2_group_mlp(const float* xyz, const float* points, const float* new_xyz,
+                  const int32_t* idx, int B, int N, int C, int M, int nsample, int flags,
+                  int nlayers, const pn2_mlp_layer* layers, int pool, float* out,
+                  pn2_stream_t stream) {
+  using namespace pn2;
+  if (B < 0 || N < 0 || C < 0 || M < 0 || nsample <= 0) return PN2_EINVAL;
+  if (pool < PN2_POOL_NONE || pool > PN2_POOL_MAX_AND_AVG) return PN2_EINVAL;
+  int layout, cin0;
+  if (!points) { layout = kXyzOnly; cin0 = 3; }
+  else if (!(flags & PN2_USE_XYZ)) { layout = kPointsOnly; cin0 = C; }
+  else { layout = (flags & PN2_XYZ_LAST) ? kXyzLast : kXyzFirst; cin0 = C + 3; }
+  int rc = check_layers(nlayers, layers, cin0);
+  if (rc) return rc;
+  const long long ngroups = (long long)B * M;
+  if (ngroups == 0) return PN2_OK;
+  if (!xyz || !new_xyz || !idx || !out || ngroups > 0x7fffffffLL) return PN2_EINVAL;
+  if ((long long)B * N > 0x7fffffffLL || ngroups * nsample > 0x7fffffffLL) return PN2_EINVAL;
+  const int ns_pad = nsample < 8 ? 8 : next_pow2(nsample);
+  const bool pooled = pool >= 0;
+  Params prm = {};
+  size_t lds = 0;
+  // a single-pass workgroup holds whole groups: P = 32R must be a multiple of ns_pad, or
+  // the group is processed in ns_pad / P passes of one workgroup
+  const long long tiles32 = (ngroups * ns_pad + 31) / 32;
+  const int R = choose_R(prm, nlayers, layers, cin0, pooled, tiles32, 1, &lds);
+  if (!R) return PN2_EINVAL;
+  const int P = 32 * R;
+  prm.xyz = xyz;
+  prm.points = points;
+  prm.new_xyz = new_xyz;
+  prm.idx = idx;
+  prm.N = N;
+  prm.C = C;
+  prm.M = M;
+  prm.ns = nsample;
+  prm.lg_ns_pad = ilog2(ns_pad);
+  prm.layout = layout;
+  prm.ngroups = (int)ngroups;
+  prm.pool = pool;
+  prm.out = out;
+  long long nblocks;
+  if (ns_pad <= P) {
+    prm.passes = 1;
+    prm.gpw = P / ns_pad;
+    nblocks = (ngroups + prm.gpw - 1) / prm.gpw;
+  } else {
+    prm.passes = ns_pad / P;
+    prm.gpw = 1;
+    nblocks = ngroups;
+  }
+  if (pooled && prm.gpw > kMaxGroupsPerWG) return PN2_EINVAL;
+  return launch_rows_R<kSrcGroup>(prm, R, nblocks, lds, (hipStream_t)stream);
+}
+
+int pn2_fp_mlp(const float* dist, const int32_t* nn_idx, const float* points1, int C1,
+               const float* points2, int C2, int B, int n, int m, int nlayers,
+               const pn2_mlp_layer* layers, float* out, pn2_stream_t stream) {
+  using namespace pn2;
+  if (B < 0 || n < 0 || m < 0 || C1 < 0 || C2 <= 0) return PN2_EINVAL;
+  if (C1 > 0 && !points1) return PN2_EINVAL;
+  int rc = check_layers(nlayers, layers, C1 + C2);
+  if (rc) return rc;
+  const long long rows = (long long)B * n;
+  if (rows == 0) return PN2_OK;
+  if (!dist || !nn_idx || !points2 || !out || m < 1) return PN2_EINVAL;
+  if (rows > 0x7fffffffLL || (long long)B * m > 0x7fffffffLL) return PN2_EINVAL;
+  Params prm = {};
+  size_t lds = 0;
+  const int R = choose_R(prm, nlayers, layers, C1 + C2, false, (rows + 31) / 32, 1, &lds);
+  if (!R) return PN2_EINVAL;
+  prm.dist = dist;
+  prm.nn = nn_idx;
+  prm.p1 = points1;
+  prm.p2 = points2;
+  prm.C1 = C1;
+  prm.C2 = C2;
+  prm.n = n;
+  prm.m = m;
+  prm.rows = rows;
+  prm.passes = 1;
+  prm.pool = PN2_POOL_NONE;
+  prm.out = out;
+  const long long nblocks = (rows + 32 * R - 1) / (32 * R);
+  return launch_rows_R<kSrcFP>(prm, R, nblocks, lds, (hipStream_t)stream);
+}
+
+int pn2_shared_mlp(const float* x, long long rows, int cin, int nlayers,
+                   const pn2_mlp_layer* layers, float* out, pn2_stream_t stream) {
+  using namespace pn2;
+  if (rows < 0 || cin <= 0) return PN2_EINVAL;
+  int rc = check_layers(nlayers, layers, cin);
+  if (rc) return rc;
+  if (rows == 0) return PN2_OK;
+  if (!x || !out || rows > 0x7fffffffLL) return PN2_EINVAL;
+  Params prm = {};
+  size_t lds = 0;
+  const int R = choose_R(prm, nlayers, layers, cin, false, (rows + 31) / 32, 1, &lds);
+  if (!R) return PN2_EINVAL;
+  prm.x = x;
+  prm.cin = cin;
+  prm.rows = rows;
+  prm.passes = 1;
+  prm.pool = PN2_POOL_NONE;
+  prm.out = out;
+  const long long nblocks = (rows + 32 * R - 1) / (32 * R);
+  return launch_rows_R<kSrcRows>(prm, R, nblocks, lds, (hipStream_t)stream);
+}
+
+}  // extern "C"

@@ -1,14 +1,19 @@
 """The hot-path geometry of pointnet2_tensorflow/utils/pointnet_util.py on gfx950.
 
-sample_and_group / sample_and_group_all keep the reference signatures and return values; the
-dense MLP / BN parts of pointnet_sa_module / pointnet_fp_module are out of scope (torch
-provides them), so this module exposes the geometric halves of those layers:
+sample_and_group / sample_and_group_all keep the reference signatures and return values.
+The geometric halves of the SA / FP layers:
 
   sample_and_group          pointnet_util.py:16-58    FPS + gather + ball query + fused group
   sample_and_group_all      pointnet_util.py:61-87
   sample_and_group_msg      pointnet_util.py:180-193  one FPS, several (radius, nsample) scales
   group_pool                pointnet_util.py:130-145  max / avg / weighted_avg / max_and_avg
   fp_interpolate            pointnet_util.py:218-228  three_nn + IDW + interpolate + concat
+
+The whole layers, shared MLP included (tf_util.py for the parameters):
+
+  pointnet_sa_module        pointnet_util.py:90-163   group + MLP + pooling in one kernel
+  pointnet_sa_module_msg    pointnet_util.py:166-201  one fused kernel per scale
+  pointnet_fp_module        pointnet_util.py:204-238  interpolation + MLP in one kernel
 
 Without autograd the fused kernels run (fewest launches, one pass over HBM); when a gradient
 is required, the composition of differentiable ops (gather_point, group_point,
@@ -17,9 +22,9 @@ reference's registered gradients.
 """
 import torch
 
-from . import tf_grouping, tf_interpolate, tf_sampling
-from ._lib import (POOL_MODES, PN2_USE_XYZ, PN2_XYZ_LAST, InvalidArgumentError, check,
-                   device_tensor, lib, ptr, stream_of)
+from . import tf_grouping, tf_interpolate, tf_sampling, tf_util
+from ._lib import (POOL_MODES, PN2_POOL_NONE, PN2_USE_XYZ, PN2_XYZ_LAST, InvalidArgumentError,
+                   check, device_tensor, lib, ptr, stream_of)
 
 
 def _is_empty_points(points):
@@ -170,4 +175,151 @@ def fp_interpolate(xyz1, xyz2, points1, points2, known_grid=None, unknown_grid=N
     else:
         check(lib().pn2_fp_fused(ptr(xyz1), ptr(xyz2), ptr(points1), C1, ptr(points2), C2, B, n,
                                  m, ptr(out), stream_of(xyz1)), "fp_interpolate")
+    return out
+
+
+# ---------------------------------------------------------------- whole SA / FP layers -----
+
+def group_mlp(xyz, points, new_xyz, idx, mlp, pooling="max", use_xyz=True, xyz_last=False):
+    """Fused group + centre + concat (as group_concat) -> shared MLP `mlp` (a
+    tf_util.SharedMLP) -> pooling over nsample (pn2_group_mlp). pooling: 'max', 'avg',
+    'weighted_avg', 'max_and_avg' -> (B, M, C') or None -> per-point (B, M, ns, C)."""
+    xyz = device_tensor(xyz, "xyz", torch.float32)
+    new_xyz = device_tensor(new_xyz, "new_xyz", torch.float32)
+    idx = device_tensor(idx, "idx", torch.int32)
+    B, N = int(xyz.shape[0]), int(xyz.shape[1])
+    M, ns = int(idx.shape[1]), int(idx.shape[2])
+    if _is_empty_points(points):
+        points, C = None, 0
+    else:
+        points = device_tensor(points, "points", torch.float32)
+        C = int(points.shape[2])
+    if pooling is not None and pooling not in POOL_MODES:
+        raise InvalidArgumentError(f"unknown pooling {pooling!r}")
+    mode = PN2_POOL_NONE if pooling is None else POOL_MODES[pooling]
+    cout = mlp.cout
+    if pooling is None:
+        shape = (B, M, ns, cout)
+    else:
+        shape = (B, M, 2 * cout if pooling == "max_and_avg" else cout)
+    out = torch.empty(shape, dtype=torch.float32, device=xyz.device)
+    flags = (PN2_USE_XYZ if use_xyz else 0) | (PN2_XYZ_LAST if xyz_last else 0)
+    tab, n = mlp.table()
+    check(lib().pn2_group_mlp(ptr(xyz), ptr(points), ptr(new_xyz), ptr(idx), B, N, C, M, ns,
+                              flags, n, tab, mode, ptr(out), stream_of(xyz)), "group_mlp")
+    return out
+
+
+def _pool_torch(x, pooling, grouped_xyz):
+    # pointnet_util.py:130-145 (keep_dims=False)
+    if pooling == "max":
+        return x.max(dim=2).values
+    if pooling == "avg":
+        return x.mean(dim=2)
+    if pooling == "weighted_avg":
+        e = torch.exp(-torch.linalg.norm(grouped_xyz, dim=-1, keepdim=True) * 5)
+        return (x * (e / e.sum(dim=2, keepdim=True))).sum(dim=2)
+    if pooling == "max_and_avg":
+        return torch.cat([x.mean(dim=2), x.max(dim=2).values], dim=-1)
+    raise InvalidArgumentError(f"unknown pooling {pooling!r}")
+
+
+def pointnet_sa_module(xyz, points, npoint, radius, nsample, mlp, mlp2, group_all, is_training,
+                       bn_decay, scope, bn=True, pooling='max', knn=False, use_xyz=True,
+                       use_nchw=False, params=None):
+    """pointnet_util.py:90-163. Returns (new_xyz (B,npoint,3), new_points (B,npoint,mlp[-1] or
+    mlp2[-1]), idx (B,npoint,nsample)). Variables come from `params` (tf_util.ParamStore,
+    default tf_util.default_store()) under '<scope>/conv<i>/...' and '<scope>/conv_post_<i>/...'.
+
+    Inference (is_training False, no autograd): FPS + ball query, then ONE kernel for group,
+    MLP and pooling (pn2_group_mlp), and mlp2 as a per-point MLP. Training: the same ops
+    composed from differentiable torch ops (batch-statistics batch norm)."""
+    store = params if params is not None else tf_util.default_store()
+    xyz = device_tensor(xyz, "xyz", torch.float32)
+    scopes = [f"{scope}/conv{i}" for i in range(len(mlp))]
+    post = [f"{scope}/conv_post_{i}" for i in range(len(mlp2 or []))]
+    if group_all:
+        new_xyz, new_points, idx, grouped_xyz = sample_and_group_all(xyz, points, use_xyz)
+    elif is_training or _needs_grad(xyz, points) or knn:
+        new_xyz, new_points, idx, grouped_xyz = sample_and_group(npoint, radius, nsample, xyz,
+                                                                 points, knn, use_xyz)
+    else:
+        _, new_xyz = tf_sampling.farthest_point_sample_and_gather(npoint, xyz)
+        idx, _ = tf_grouping.query_ball_point(radius, nsample, xyz, new_xyz)
+        new_points = None
+    cin = (0 if _is_empty_points(points) else int(points.shape[2])) + (
+        3 if (use_xyz or _is_empty_points(points)) else 0)
+    if is_training or _needs_grad(xyz, points):
+        layers = tf_util.torch_layers(store, scopes, cin, mlp, bn=bn)
+        x = tf_util.mlp_torch(new_points, layers, is_training, bn_decay)
+        x = _pool_torch(x, pooling, grouped_xyz)
+        if mlp2:
+            c = int(x.shape[-1])
+            x = tf_util.mlp_torch(x, tf_util.torch_layers(store, post, c, mlp2, bn=bn),
+                                  is_training, bn_decay)
+        return new_xyz, x, idx
+    fused = tf_util.packed_mlp(store, scopes, cin, mlp, bn=bn)
+    # group_all: one group of all N points centred on (0,0,0) (pointnet_util.py:72-87)
+    x = group_mlp(xyz, points, new_xyz, idx, fused, pooling, use_xyz=use_xyz)
+    if mlp2:
+        c = int(x.shape[-1])
+        x = tf_util.packed_mlp(store, post, c, mlp2, bn=bn)(x)
+    return new_xyz, x, idx
+
+
+def pointnet_sa_module_msg(xyz, points, npoint, radius_list, nsample_list, mlp_list,
+                           is_training, bn_decay, scope, bn=True, use_xyz=True, use_nchw=False,
+                           params=None):
+    """pointnet_util.py:166-201: one FPS, then per scale i a ball query and the fused
+    group ([points, xyz] order, :191) + MLP ('<scope>/conv<i>_<j>') + max pool; the scales'
+    features are concatenated. Returns (new_xyz, new_points_concat)."""
+    store = params if params is not None else tf_util.default_store()
+    xyz = device_tensor(xyz, "xyz", torch.float32)
+    training = is_training or _needs_grad(xyz, points)
+    if training:
+        new_xyz = tf_sampling.gather_point(xyz, tf_sampling.farthest_point_sample(npoint, xyz))
+    else:
+        _, new_xyz = tf_sampling.farthest_point_sample_and_gather(npoint, xyz)
+    C = 0 if _is_empty_points(points) else int(points.shape[2])
+    cin = C + (3 if (use_xyz or C == 0) else 0)
+    outs = []
+    for i, (radius, nsample) in enumerate(zip(radius_list, nsample_list)):
+        scopes = [f"{scope}/conv{i}_{j}" for j in range(len(mlp_list[i]))]
+        idx, _ = tf_grouping.query_ball_point(radius, nsample, xyz, new_xyz.detach())
+        if training:
+            gp, _ = group_concat(xyz, points, new_xyz, idx, use_xyz=use_xyz, xyz_last=True)
+            layers = tf_util.torch_layers(store, scopes, cin, mlp_list[i], bn=bn)
+            outs.append(tf_util.mlp_torch(gp, layers, is_training, bn_decay).max(dim=2).values)
+        else:
+            fused = tf_util.packed_mlp(store, scopes, cin, mlp_list[i], bn=bn)
+            outs.append(group_mlp(xyz, points, new_xyz, idx, fused, "max", use_xyz=use_xyz,
+                                  xyz_last=True))
+    return new_xyz, torch.cat(outs, dim=-1)
+
+
+def pointnet_fp_module(xyz1, xyz2, points1, points2, mlp, is_training, bn_decay, scope, bn=True,
+                       params=None, known_grid=None, unknown_grid=None):
+    """pointnet_util.py:204-238: three_nn, IDW weights, three_interpolate, concat
+    [interp, points1], MLP ('<scope>/conv_<i>'). Inference: three_nn (grid search when large)
+    then ONE kernel for weights + interpolation + concat + MLP (pn2_fp_mlp)."""
+    store = params if params is not None else tf_util.default_store()
+    xyz1 = device_tensor(xyz1, "xyz1", torch.float32)
+    xyz2 = device_tensor(xyz2, "xyz2", torch.float32)
+    points2 = device_tensor(points2, "points2", torch.float32)
+    scopes = [f"{scope}/conv_{i}" for i in range(len(mlp))]
+    C1 = 0 if points1 is None else int(points1.shape[2])
+    C2 = int(points2.shape[2])
+    if is_training or _needs_grad(points1, points2):
+        x = fp_interpolate(xyz1, xyz2, points1, points2, known_grid, unknown_grid)
+        layers = tf_util.torch_layers(store, scopes, C1 + C2, mlp, bn=bn)
+        return tf_util.mlp_torch(x, layers, is_training, bn_decay)
+    fused = tf_util.packed_mlp(store, scopes, C1 + C2, mlp, bn=bn)
+    dist, idx = tf_interpolate.three_nn(xyz1, xyz2, known_grid, unknown_grid)
+    B, n, m = int(xyz1.shape[0]), int(xyz1.shape[1]), int(xyz2.shape[1])
+    if points1 is not None:
+        points1 = device_tensor(points1, "points1", torch.float32)
+    out = torch.empty((B, n, fused.cout), dtype=torch.float32, device=xyz1.device)
+    tab, nl = fused.table()
+    check(lib().pn2_fp_mlp(ptr(dist), ptr(idx), ptr(points1), C1, ptr(points2), C2, B, n, m, nl,
+                           tab, ptr(out), stream_of(xyz1)), "fp_mlp")
     return out
