@@ -22,7 +22,9 @@ sys.path.insert(0, ROOT)
 # The step runs on 4 streams (sampler chain + 3 side lanes) plus 2 setup streams; HIP maps
 # streams to hardware queues round-robin, and with its default of 4 queues a side lane
 # would share the chain's queue and sit in front of the next step's sampler. 8 <= 32.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# The whole-model step gives each of its 3 buffer sets 4 private side streams: 16 queues keep
+# every stream on its own queue (the pool allows <= 32).
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
 
 PKG = "pointcloud-segmentation-attention_amd"
 METRIC = "8192-pt clouds/sec through SA+FP layers, 1/2/4/8 MI355X; HBM GB/s vs peak"
@@ -114,6 +116,12 @@ def main():
     ap.add_argument("--no-pipeline", action="store_true",
                     help="join every step before the next (no overlap of step k's side work "
                          "with step k+1's samplers)")
+    ap.add_argument("--model", action="store_true",
+                    help="the step is the whole segmentation model's inference forward "
+                         "(SA/FP geometry + fused MLPs + head) instead of the geometry alone")
+    ap.add_argument("--e2e-steps", type=int, default=20,
+                    help="after the geometric measurement, time this many whole-model steps "
+                         "(reported as 'e2e'; 0 = skip)")
     args = ap.parse_args()
 
     import torch
@@ -132,51 +140,70 @@ def main():
 
     B = args.batch or (8 if args.config == "cfg5" else 16)
     ids = pkg.shard.shard_ids(rank, world, B)  # contiguous batch split
-    inp = pkg.stack.make_inputs(args.config, ids, dev)
-    torch.cuda.synchronize()
-
-    overlap = not args.no_overlap
-    pipelined = overlap and not args.no_pipeline
-    if pipelined:
-        pipe = pkg.stack.Pipeline(inp, graphs=not args.eager, nsets=args.sets)
-    else:
-        step = pkg.stack.Step(inp, overlap=overlap)
-        graph = None if args.eager else pkg.stack.GraphStep(inp, overlap=overlap)
-
-    def run_step(events=None):
-        if pipelined:
-            return pipe.run(events)
-        if graph is not None:
-            return graph.replay(events)
-        return step.run(events)
-
-    def finish():
-        return pipe.join() if pipelined else None
-
-    for _ in range(args.warmup):
-        run_step()
-    finish()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(args.steps)]
 
     def barrier():
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
 
-    barrier()
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        outs = run_step(ev[k] if k % args.time_every == 0 else None)
-    outs = finish() or outs
-    torch.cuda.synchronize()
-    barrier()
-    elapsed = pkg.shard.max_over_ranks(time.perf_counter() - t0, dev)
+    def measure(model, steps, warmup):
+        """W warm-up steps, then K timed steps between barrier + synchronize; returns
+        (max-over-ranks elapsed seconds, mean SA1-sampler ms, last outputs)."""
+        inp = pkg.stack.make_inputs(args.config, ids, dev, model=model)
+        torch.cuda.synchronize()
+        overlap = not args.no_overlap
+        pipelined = overlap and not args.no_pipeline
+        if pipelined:
+            pipe = pkg.stack.Pipeline(inp, graphs=not args.eager, nsets=args.sets,
+                                      private_streams=model)
+        else:
+            step = pkg.stack.Step(inp, overlap=overlap)
+            graph = None if args.eager else pkg.stack.GraphStep(inp, overlap=overlap)
 
-    timed = [ev[k] for k in range(args.steps) if k % args.time_every == 0]
-    fps_ms = sum(a.elapsed_time(b) for a, b in timed) / len(timed)  # SA1 sampler, per launch
+        def run_step(events=None):
+            if pipelined:
+                return pipe.run(events)
+            if graph is not None:
+                return graph.replay(events)
+            return step.run(events)
+
+        def finish():
+            return pipe.join() if pipelined else None
+
+        for _ in range(warmup):
+            run_step()
+        finish()
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(steps)]
+        barrier()
+        t0 = time.perf_counter()
+        outs = None
+        for k in range(steps):
+            outs = run_step(ev[k] if k % args.time_every == 0 else None)
+        outs = finish() or outs
+        torch.cuda.synchronize()
+        barrier()
+        elapsed = pkg.shard.max_over_ranks(time.perf_counter() - t0, dev)
+        timed = [ev[k] for k in range(steps) if k % args.time_every == 0]
+        fps_ms = sum(a.elapsed_time(b) for a, b in timed) / len(timed)  # SA1 sampler, per launch
+        return elapsed, fps_ms, outs
+
+    overlap = not args.no_overlap
+    pipelined = overlap and not args.no_pipeline
+    elapsed, fps_ms, outs = measure(args.model, args.steps, args.warmup)
     # per-cloud output checksums, gathered (outside the timed region) so ranks can be compared
     sums = pkg.shard.gather_checksums(pkg.shard.cloud_checksums(outs, B))
+    e2e = None
+    if not args.model and args.e2e_steps > 0 and pkg.stack.CONFIGS[args.config][1] == "ssg":
+        e_el, e_fps, e_outs = measure(True, args.e2e_steps, min(args.warmup, 5))
+        e_sums = pkg.shard.gather_checksums(pkg.shard.cloud_checksums(e_outs, B))
+        e2e = {"value": world * B * args.e2e_steps / e_el, "unit": "clouds/s",
+               "ms_per_step": e_el / args.e2e_steps * 1e3, "steps": args.e2e_steps,
+               "sa1_sampler_ms": e_fps, "checksum": float(e_sums.sum().item()),
+               "model": "pointnet2_sem_seg" + ("_features" if args.config == "cfg3" else "")
+                        + " inference forward: SA x4 (fused group + MLP + max pool), "
+                          "FP x4 (fused interpolation + MLP), fc1+fc2 head fused into FP4; "
+                          "fp32 matrix cores; reference initialisers, fixed seed"}
 
     if rank == 0:
         clouds = world * B * args.steps
@@ -196,8 +223,10 @@ def main():
             "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic: SplitMix64 ScanNet-crop clouds (8192 drawn with replacement from "
-                    "12k surface points); U[-1,1) stand-ins for the MLP outputs",
-            "config": {"workload": WORKLOADS[args.config], "config": args.config,
+                    "12k surface points); " + ("random-init model weights (reference "
+                    "initialisers)" if args.model else "U[-1,1) stand-ins for the MLP outputs"),
+            "config": {"workload": ("whole-model inference forward, " if args.model else "")
+                       + WORKLOADS[args.config], "config": args.config,
                        "clouds_per_gpu": B, "global_batch": world * B, "points": N,
                        "parallelism": f"dp{world} (batch split)",
                        "launch": "eager" if args.eager else
@@ -218,7 +247,9 @@ def main():
                          "frac": step_bytes * world / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBPS},
             "checksum": float(sums.sum().item()),
         }
-        if world == 1 and not args.no_cpu_baseline:
+        if e2e is not None:
+            result["e2e"] = e2e
+        if world == 1 and not args.no_cpu_baseline and not args.model:
             try:
                 result["cpu_baseline"] = cpu_baseline(args.config, B, args.cpu_seconds,
                                                       args.cpu_threads)

@@ -52,7 +52,10 @@ struct Params {
   int width0;            // layer-0 input width in LDS (cin8*8)
   int stride0, stride1;  // LDS row strides (floats) of the activation buffers
   int off1, off_part, off_run, off_meta;  // float offsets into dynamic LDS
-  FastDiv div_w0;
+  // input row = segment A (+ segment B) (+ zero padding up to width0); nA/nB = units per row
+  // (float4 chunks when vecA/vecB, else floats), offA/offB = LDS column of the segment
+  int nA, nB, offA, offB, vecA, vecB, cin_total;
+  FastDiv divA, divB, div_pad;
   // group source
   const float* xyz;
   const float* points;
@@ -71,7 +74,23 @@ struct Params {
   long long rows;
   int pool;
   float* out;
+  unsigned long long* stamp;  // PN2_MLP_STAMP builds: per-workgroup phase timestamps
 };
+
+#ifdef PN2_MLP_STAMP
+// s_memtime at phase boundaries of the first kStampWG workgroups (wave 0), slot k of 16
+constexpr int kStampWG = 4096;
+#define PN2_STAMP(k)                                                                    \
+  do {                                                                                 \
+    if (prm.stamp && blockIdx.x < kStampWG && threadIdx.x == 0)                        \
+      prm.stamp[blockIdx.x * 16 + (k)] = __builtin_amdgcn_s_memtime();                 \
+  } while (0)
+unsigned long long* g_stamp = nullptr;
+#else
+#define PN2_STAMP(k) \
+  do {               \
+  } while (0)
+#endif
 
 PN2_DEV float act(float v, int relu) { return relu ? fmaxf(v, 0.f) : v; }
 
@@ -87,8 +106,333 @@ PN2_DEV void idw3(float d1, float d2, float d3, float& w1, float& w2, float& w3)
   w3 = r3 / norm;
 }
 
+
+// One output tile over RG row tiles: cin8 chunks of 8 input features, 4 MFMAs per chunk and
+// row tile (k = 8c + 4h + s, s = 0..3); every weight fragment serves the RG row tiles'
+// independent accumulators. wp = the tile's packed weights at this lane, ap = this lane's
+// activation row (+4h) in the first row tile, rstride = floats between row tiles. Chunks run
+// in groups of G with the next group's weights and activations loaded (and pinned there by
+// sched_barrier) before the current group's MFMAs are issued; the last group re-loads itself
+// (branch-free), then a remainder of single chunks.
+// LAST: Y = X W (points in the accumulator rows) instead of Y^T = W^T X^T.
+template <bool LAST, int RG>
+PN2_DEV void mma_item(const float4* __restrict__ wp, const float* ap, int rstride, int cin8,
+                      f32x16 (&acc)[RG]) {
+  constexpr int G = RG >= 2 ? 2 : 4;  // 16 MFMAs (~1000 cycles) per group either way
+#pragma unroll
+  for (int r = 0; r < RG; ++r)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[r][i] = 0.f;
+  auto mma4 = [&](const float4& w, const float4& a, f32x16& c) {
+    if (LAST) {
+      c = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, w.x, c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, w.y, c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, w.z, c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, w.w, c, 0, 0, 0);
+    } else {
+      c = __builtin_amdgcn_mfma_f32_32x32x2f32(w.x, a.x, c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_32x32x2f32(w.y, a.y, c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_32x32x2f32(w.z, a.z, c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_32x32x2f32(w.w, a.w, c, 0, 0, 0);
+    }
+  };
+  auto act4 = [&](int r, int c) {
+    return *reinterpret_cast<const float4*>(ap + r * rstride + 8 * c);
+  };
+  const int cg = cin8 - cin8 % G;
+  float4 wA[G], aA[G][RG], wB[G], aB[G][RG];
+  auto load = [&](float4* w, float4 (*a)[RG], int c) {
+#pragma unroll
+    for (int u = 0; u < G; ++u) {
+      w[u] = wp[(size_t)(c + u) * kWave];
+#pragma unroll
+      for (int r = 0; r < RG; ++r) a[u][r] = act4(r, c + u);
+    }
+  };
+  auto compute = [&](const float4* w, float4 (*a)[RG]) {
+#pragma unroll
+    for (int u = 0; u < G; ++u)
+#pragma unroll
+      for (int r = 0; r < RG; ++r) mma4(w[u], a[u][r], acc[r]);
+  };
+  if (cg > 0) {
+    load(wA, aA, 0);
+    for (int c = 0; c < cg; c += 2 * G) {
+      const bool two = c + G < cg;
+      load(wB, aB, two ? c + G : c);
+      __builtin_amdgcn_sched_barrier(0);
+      compute(wA, aA);
+      __builtin_amdgcn_sched_barrier(0);
+      if (!two) break;
+      load(wA, aA, c + 2 * G < cg ? c + 2 * G : c);
+      __builtin_amdgcn_sched_barrier(0);
+      compute(wB, aB);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  for (int c = cg; c < cin8; ++c) {
+    const float4 w = wp[(size_t)c * kWave];
+#pragma unroll
+    for (int r = 0; r < RG; ++r) mma4(w, act4(r, c), acc[r]);
+  }
+}
+
+// One segment of every slot's input row: n units per row (float4 chunks or floats), fetched
+// by fetch(p, j) and stored at LDS column off + j*units. Batches of kGatherUnroll independent
+// units per thread: every load of a batch is issued before the first LDS store, so the L2/HBM
+// latency is paid once per batch.
+template <typename T, int P, typename F>
+PN2_DEV void gather_segment(int n, FastDiv div_n, int off, float* act, int stride, F fetch) {
+  constexpr int V = sizeof(T) / sizeof(float);
+  constexpr int kGatherUnroll = V == 4 ? 4 : 8;
+  const int total = P * n;
+  for (int e0 = threadIdx.x; e0 < total; e0 += kBlock * kGatherUnroll) {
+    T vals[kGatherUnroll];
+#pragma unroll
+    for (int u = 0; u < kGatherUnroll; ++u) {
+      const int e = e0 + u * kBlock;
+      if (e < total) {
+        const int p = (int)fdiv((uint32_t)e, div_n);
+        vals[u] = fetch(p, e - p * n);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kGatherUnroll; ++u) {
+      const int e = e0 + u * kBlock;
+      if (e < total) {
+        const int p = (int)fdiv((uint32_t)e, div_n);
+        float* dst = act + p * stride + off + V * (e - p * n);
+        if constexpr (V == 4) {
+          if ((off & 3) == 0) {
+            *reinterpret_cast<float4*>(dst) = vals[u];
+          } else {
+            dst[0] = vals[u].x;
+            dst[1] = vals[u].y;
+            dst[2] = vals[u].z;
+            dst[3] = vals[u].w;
+          }
+        } else {
+          *dst = vals[u];
+        }
+      }
+    }
+  }
+}
+
+PN2_DEV float4 f4mul(float4 a, float w) { return make_float4(a.x * w, a.y * w, a.z * w, a.w * w); }
+PN2_DEV float4 f4add(float4 a, float4 b) {
+  return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
+
+// The input rows of the workgroup's P slots into act0 [P][width0]: the source's segments
+// then zeros up to width0.
+template <int SRC, int P>
+PN2_DEV void gather_rows(const Params& prm, float* act0, const int* s_src, const int* s_aux,
+                         const float* s_fw, const int* s_fi) {
+  const int S = prm.stride0;
+  if (SRC == kSrcGroup) {
+    // grouped points rows, then the centred xyz (pointnet_util.py:39-56 / :186-193)
+    const float* pts = prm.points;
+    const int C = prm.C;
+    if (prm.nA) {
+      if (prm.vecA)
+        gather_segment<float4, P>(prm.nA, prm.divA, prm.offA, act0, S, [&](int p, int j) {
+          const int src = s_src[p];
+          return src < 0 ? make_float4(0.f, 0.f, 0.f, 0.f)
+                         : *reinterpret_cast<const float4*>(pts + (size_t)src * C + 4 * j);
+        });
+      else
+        gather_segment<float, P>(prm.nA, prm.divA, prm.offA, act0, S, [&](int p, int j) {
+          const int src = s_src[p];
+          return src < 0 ? 0.f : pts[(size_t)src * C + j];
+        });
+    }
+    if (prm.nB)
+      gather_segment<float, P>(3, prm.divB, prm.offB, act0, S, [&](int p, int j) {
+        const int src = s_src[p];
+        // pointnet_util.py:40: fp32 subtraction, bit-exact with pn2_group_concat
+        return src < 0 ? 0.f
+                       : prm.xyz[(size_t)src * 3 + j] - prm.new_xyz[(size_t)s_aux[p] * 3 + j];
+      });
+  } else if (SRC == kSrcFP) {
+    // interpolation (tf_interpolate.cpp:107-127: ((p1*w1) + (p2*w2)) + (p3*w3)), then points1
+    const float* p2 = prm.p2;
+    const int C2 = prm.C2;
+    if (prm.vecA)
+      gather_segment<float4, P>(prm.nA, prm.divA, 0, act0, S, [&](int p, int j) {
+        if (s_src[p] < 0) return make_float4(0.f, 0.f, 0.f, 0.f);
+        const float4 a = *reinterpret_cast<const float4*>(p2 + (size_t)s_fi[3 * p] * C2 + 4 * j);
+        const float4 b = *reinterpret_cast<const float4*>(p2 + (size_t)s_fi[3 * p + 1] * C2 + 4 * j);
+        const float4 c = *reinterpret_cast<const float4*>(p2 + (size_t)s_fi[3 * p + 2] * C2 + 4 * j);
+        return f4add(f4add(f4mul(a, s_fw[3 * p]), f4mul(b, s_fw[3 * p + 1])),
+                     f4mul(c, s_fw[3 * p + 2]));
+      });
+    else
+      gather_segment<float, P>(prm.nA, prm.divA, 0, act0, S, [&](int p, int j) {
+        if (s_src[p] < 0) return 0.f;
+        const float a = p2[(size_t)s_fi[3 * p] * C2 + j] * s_fw[3 * p];
+        const float b = p2[(size_t)s_fi[3 * p + 1] * C2 + j] * s_fw[3 * p + 1];
+        const float c = p2[(size_t)s_fi[3 * p + 2] * C2 + j] * s_fw[3 * p + 2];
+        return (a + b) + c;
+      });
+    const float* p1 = prm.p1;
+    const int C1 = prm.C1;
+    if (prm.nB) {  // concat [interp, points1] (pointnet_util.py:226)
+      if (prm.vecB)
+        gather_segment<float4, P>(prm.nB, prm.divB, prm.offB, act0, S, [&](int p, int j) {
+          const int src = s_src[p];
+          return src < 0 ? make_float4(0.f, 0.f, 0.f, 0.f)
+                         : *reinterpret_cast<const float4*>(p1 + (size_t)src * C1 + 4 * j);
+        });
+      else
+        gather_segment<float, P>(prm.nB, prm.divB, prm.offB, act0, S, [&](int p, int j) {
+          const int src = s_src[p];
+          return src < 0 ? 0.f : p1[(size_t)src * C1 + j];
+        });
+    }
+  } else {
+    const float* x = prm.x;
+    const int cin = prm.cin;
+    if (prm.vecA)
+      gather_segment<float4, P>(prm.nA, prm.divA, 0, act0, S, [&](int p, int j) {
+        const int src = s_src[p];
+        return src < 0 ? make_float4(0.f, 0.f, 0.f, 0.f)
+                       : *reinterpret_cast<const float4*>(x + (size_t)src * cin + 4 * j);
+      });
+    else
+      gather_segment<float, P>(prm.nA, prm.divA, 0, act0, S, [&](int p, int j) {
+        const int src = s_src[p];
+        return src < 0 ? 0.f : x[(size_t)src * cin + j];
+      });
+  }
+  const int npad = prm.width0 - prm.cin_total;
+  if (npad > 0)
+    for (int e = threadIdx.x; e < P * npad; e += kBlock) {
+      const int p = (int)fdiv((uint32_t)e, prm.div_pad);
+      act0[p * S + prm.cin_total + (e - p * npad)] = 0.f;
+    }
+}
+
+// Row-tile groups per layer: at most kMaxRG row tiles share an item (register budget of two
+// waves per SIMD), and layers narrower than the 4 waves split further so every wave works.
+constexpr int kMaxRG = 2;
+__host__ __device__ inline int item_split(int R, int c32) {
+  int nsplit = R > kMaxRG ? R / kMaxRG : 1;
+  while (nsplit < R && nsplit * c32 < kWaves) nsplit <<= 1;
+  return nsplit;
+}
+
+// What a layer item needs from the kernel (LDS carve, lane coordinates, pooling state).
+struct Ctx {
+  const Params* prm;
+  float* act0;
+  float* act1;
+  float* part;
+  const int* s_src;
+  const int* s_aux;
+  const float* s_pw;
+  int lane, col, h, ns_pad, coutp;
+  bool pooled;
+};
+
+// One item of layer l: the MFMA product, then either the intermediate epilogue (scale,
+// shift, activation, 16-byte writes into the other LDS buffer) or the last layer's (per-point
+// stores, or per-group pooling partials in LDS).
+template <int SRC, int R, int RG>
+PN2_DEV void layer_item(const Ctx& cx, int l, bool last, int to, int rt0, int pass) {
+  constexpr int P = 32 * R;
+  const Params& prm = *cx.prm;
+  const LayerDev& Ld = prm.L[l];
+  const float* in = (l & 1) ? cx.act1 : cx.act0;
+  const int Sin = (l & 1) ? prm.stride1 : prm.stride0;
+  const int lane = cx.lane, col = cx.col, h = cx.h;
+  const float4* wp = Ld.w + (size_t)to * Ld.cin8 * kWave + lane;
+  const float* ap = in + (32 * rt0 + col) * Sin + 4 * h;
+  f32x16 acc[RG];
+  if (!last) {
+    float* outb = (l & 1) ? cx.act0 : cx.act1;
+    const int Sout = (l & 1) ? prm.stride0 : prm.stride1;
+    // epilogue parameters first: their latency hides under the K loop
+    float4 sc[4], sh[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int fb = 32 * to + 8 * q + 4 * h;
+      sc[q] = *reinterpret_cast<const float4*>(Ld.scale + fb);
+      sh[q] = *reinterpret_cast<const float4*>(Ld.shift + fb);
+    }
+    mma_item<false, RG>(wp, ap, 32 * Sin, Ld.cin8, acc);
+#pragma unroll
+    for (int r = 0; r < RG; ++r) {
+      // rows = features 32*to + 8q + 4h + e (e = reg & 3), column = point 32*(rt0+r) + col
+      float* op = outb + (32 * (rt0 + r) + col) * Sout + 32 * to + 4 * h;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        float4 y;
+        y.x = act(acc[r][4 * q + 0] * sc[q].x + sh[q].x, Ld.relu);
+        y.y = act(acc[r][4 * q + 1] * sc[q].y + sh[q].y, Ld.relu);
+        y.z = act(acc[r][4 * q + 2] * sc[q].z + sh[q].z, Ld.relu);
+        y.w = act(acc[r][4 * q + 3] * sc[q].w + sh[q].w, Ld.relu);
+        *reinterpret_cast<float4*>(op + 8 * q) = y;
+      }
+    }
+    return;
+  }
+  const int fo = 32 * to + col;
+  const float s = Ld.scale[fo], t = Ld.shift[fo];
+  mma_item<true, RG>(wp, ap, 32 * Sin, Ld.cin8, acc);
+#pragma unroll
+  for (int r = 0; r < RG; ++r) {
+    const int rt = rt0 + r;
+    // rows = points 32*rt + (i&3) + 8(i>>2) + 4h, column = feature fo
+    float y[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) y[i] = act(acc[r][i] * s + t, Ld.relu);
+    if (!cx.pooled) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int p = 32 * rt + (i & 3) + 8 * (i >> 2) + 4 * h;
+        if (cx.s_src[p] < 0 || fo >= Ld.cout) continue;
+        long long orow;
+        if (SRC == kSrcGroup) {
+          // per-point output of the group's k-th neighbour (no pooling)
+          const int k = (prm.passes == 1) ? (p & (cx.ns_pad - 1)) : pass * P + p;
+          if (k >= prm.ns) continue;
+          orow = (long long)cx.s_aux[p] * prm.ns + k;
+        } else {
+          orow = (long long)blockIdx.x * P + p;
+        }
+        prm.out[orow * Ld.cout + fo] = y[i];
+      }
+    } else {
+      // per local group u of this row tile: u = i >> (lg-1) for ns_pad 8/16, else 0
+      const int lg = prm.lg_ns_pad;
+      const int gpt = lg >= 5 ? 1 : (32 >> lg);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (u >= gpt) break;
+        float mx = -__builtin_inff(), sm = 0.f;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int ui = lg >= 5 ? 0 : (i >> (lg - 1));
+          if (ui != u) continue;
+          const int p = 32 * rt + (i & 3) + 8 * (i >> 2) + 4 * h;
+          mx = fmaxf(mx, y[i]);
+          sm = sm + y[i] * cx.s_pw[p];
+        }
+        mx = fmaxf(mx, __shfl_xor(mx, 32, kWave));
+        sm = sm + __shfl_xor(sm, 32, kWave);
+        if (h == 0) {
+          float* pp = cx.part + ((size_t)(rt * 4 + u) * 2) * cx.coutp + fo;
+          pp[0] = mx;
+          pp[cx.coutp] = sm;
+        }
+      }
+    }
+  }
+}
+
 template <int SRC, int R>
-__global__ __launch_bounds__(kBlock) void mlp_kernel(const Params prm) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2, 2))) void mlp_kernel(const Params prm) {
   constexpr int P = 32 * R;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* act0 = smem;
@@ -111,7 +455,9 @@ __global__ __launch_bounds__(kBlock) void mlp_kernel(const Params prm) {
   const bool pooled = (SRC == kSrcGroup) && prm.pool >= 0;
   const LayerDev& LL = prm.L[prm.nl - 1];
   const int coutp = LL.cout32 * 32;
+  const Ctx ctx{&prm, act0, act1, part, s_src, s_aux, s_pw, lane, col, h, ns_pad, coutp, pooled};
 
+  PN2_STAMP(0);
   for (int pass = 0; pass < prm.passes; ++pass) {
     // ---- 1. per-slot metadata -----------------------------------------------------------
     if (tid < P) {
@@ -199,159 +545,29 @@ __global__ __launch_bounds__(kBlock) void mlp_kernel(const Params prm) {
     }
 
     // ---- 2. gather the input rows into act0 [P][width0] ---------------------------------
-    {
-      const int W = prm.width0;
-      for (int e = tid; e < P * W; e += kBlock) {
-        const int p = (int)fdiv((uint32_t)e, prm.div_w0);
-        const int f = e - p * W;
-        const int src = s_src[p];
-        float v = 0.f;
-        if (src >= 0) {
-          if (SRC == kSrcGroup) {
-            int cx = -1, cp = f, cin;
-            const int lay = prm.layout;
-            if (lay == kXyzOnly) { cx = f; cin = 3; }
-            else if (lay == kXyzFirst) { cin = prm.C + 3; if (f < 3) cx = f; else cp = f - 3; }
-            else if (lay == kXyzLast) { cin = prm.C + 3; if (f >= prm.C) cx = f - prm.C; }
-            else cin = prm.C;
-            if (f < cin) {
-              if (cx >= 0)  // pointnet_util.py:40 (fp32 subtraction, bit-exact)
-                v = prm.xyz[(size_t)src * 3 + cx] - prm.new_xyz[(size_t)s_aux[p] * 3 + cx];
-              else
-                v = prm.points[(size_t)src * prm.C + cp];
-            }
-          } else if (SRC == kSrcFP) {
-            if (f < prm.C2) {  // three_interpolate (tf_interpolate.cpp:107-127)
-              const float a = prm.p2[(size_t)s_fi[3 * p] * prm.C2 + f] * s_fw[3 * p];
-              const float b = prm.p2[(size_t)s_fi[3 * p + 1] * prm.C2 + f] * s_fw[3 * p + 1];
-              const float c = prm.p2[(size_t)s_fi[3 * p + 2] * prm.C2 + f] * s_fw[3 * p + 2];
-              v = (a + b) + c;
-            } else if (f < prm.C2 + prm.C1) {  // concat [interp, points1] (:226)
-              v = prm.p1[(size_t)src * prm.C1 + (f - prm.C2)];
-            }
-          } else {
-            if (f < prm.cin) v = prm.x[(size_t)src * prm.cin + f];
-          }
-        }
-        act0[p * prm.stride0 + f] = v;
-      }
-    }
+    PN2_STAMP(1);
+    gather_rows<SRC, P>(prm, act0, s_src, s_aux, s_fw, s_fi);
     __syncthreads();
+    PN2_STAMP(2);
 
     // ---- 3. the layers ------------------------------------------------------------------
+    // An item = one 32-column output tile over RG of the R row tiles; layers narrower than
+    // the 4 waves split the row tiles so every wave works (nsplit row groups).
     for (int l = 0; l < prm.nl; ++l) {
       const LayerDev& Ld = prm.L[l];
-      const float* in = (l & 1) ? act1 : act0;
-      float* outb = (l & 1) ? act0 : act1;
-      const int Sin = (l & 1) ? prm.stride1 : prm.stride0;
-      const int Sout = (l & 1) ? prm.stride0 : prm.stride1;
-      const bool last = (l == prm.nl - 1);
-      const int nitems = R * Ld.cout32;
-      const int cin8 = Ld.cin8;
+      const bool last = l == prm.nl - 1;
+      const int c32 = Ld.cout32;
+      const int nsplit = item_split(R, c32);
+      const int rg_tiles = R / nsplit;
+      const int nitems = nsplit * c32;
       for (int item = wave; item < nitems; item += kWaves) {
-        const int to = item / R;
-        const int rt = item - to * R;
-        const float4* wp = Ld.w + (size_t)to * cin8 * kWave + lane;
-        const float* ap = in + (32 * rt + col) * Sin + 4 * h;
-        f32x16 acc;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) acc[i] = 0.f;
-        // weights through a 4-deep register ring (L2 latency), activations one chunk ahead
-        float4 w0 = wp[0];
-        float4 w1 = wp[(cin8 > 1 ? 1 : 0) * kWave];
-        float4 w2 = wp[(cin8 > 2 ? 2 : 0) * kWave];
-        float4 w3 = wp[(cin8 > 3 ? 3 : 0) * kWave];
-        for (int c = 0; c < cin8; c += 4) {
-#define PN2_MLP_STEP(WR, CI)                                                                \
-  if ((CI) < cin8) {                                                                        \
-    const float4 a = *reinterpret_cast<const float4*>(ap + 8 * (CI));                       \
-    const float4 wc = WR;                                                                   \
-    const int nx = (CI) + 4 < cin8 ? (CI) + 4 : (CI);                                       \
-    WR = wp[(size_t)nx * kWave];                                                            \
-    if (last) {                                                                             \
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, wc.x, acc, 0, 0, 0);                  \
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, wc.y, acc, 0, 0, 0);                  \
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, wc.z, acc, 0, 0, 0);                  \
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, wc.w, acc, 0, 0, 0);                  \
-    } else {                                                                                \
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wc.x, a.x, acc, 0, 0, 0);                  \
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wc.y, a.y, acc, 0, 0, 0);                  \
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wc.z, a.z, acc, 0, 0, 0);                  \
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wc.w, a.w, acc, 0, 0, 0);                  \
-    }                                                                                       \
-  }
-          PN2_MLP_STEP(w0, c)
-          PN2_MLP_STEP(w1, c + 1)
-          PN2_MLP_STEP(w2, c + 2)
-          PN2_MLP_STEP(w3, c + 3)
-#undef PN2_MLP_STEP
-        }
-        if (!last) {
-          // rows = features 32*to + 8q + 4h + e (e = reg & 3), column = point 32*rt + col
-          float* op = outb + (32 * rt + col) * Sout + 32 * to + 4 * h;
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const int fb = 32 * to + 8 * q + 4 * h;
-            const float4 s = *reinterpret_cast<const float4*>(Ld.scale + fb);
-            const float4 t = *reinterpret_cast<const float4*>(Ld.shift + fb);
-            float4 y;
-            y.x = act(acc[4 * q + 0] * s.x + t.x, Ld.relu);
-            y.y = act(acc[4 * q + 1] * s.y + t.y, Ld.relu);
-            y.z = act(acc[4 * q + 2] * s.z + t.z, Ld.relu);
-            y.w = act(acc[4 * q + 3] * s.w + t.w, Ld.relu);
-            *reinterpret_cast<float4*>(op + 8 * q) = y;
-          }
-        } else {
-          // rows = points 32*rt + (r&3) + 8(r>>2) + 4h, column = feature fo
-          const int fo = 32 * to + col;
-          const float s = Ld.scale[fo], t = Ld.shift[fo];
-          float y[16];
-#pragma unroll
-          for (int r = 0; r < 16; ++r) y[r] = act(acc[r] * s + t, Ld.relu);
-          if (!pooled) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-              const int p = 32 * rt + (r & 3) + 8 * (r >> 2) + 4 * h;
-              if (s_src[p] < 0 || fo >= Ld.cout) continue;
-              long long orow;
-              if (SRC == kSrcGroup) {
-                // per-point output of the group's k-th neighbour (no pooling)
-                int k = (prm.passes == 1) ? (p & (ns_pad - 1)) : pass * P + p;
-                if (k >= prm.ns) continue;
-                orow = (long long)s_aux[p] * prm.ns + k;
-              } else {
-                orow = (long long)blockIdx.x * P + p;
-              }
-              prm.out[orow * Ld.cout + fo] = y[r];
-            }
-          } else {
-            // per local group u of this row tile: u = r >> (lg-1) for ns_pad 8/16, else 0
-            const int lg = prm.lg_ns_pad;
-            const int gpt = lg >= 5 ? 1 : (32 >> lg);
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-              if (u >= gpt) break;
-              float mx = -__builtin_inff(), sm = 0.f;
-#pragma unroll
-              for (int r = 0; r < 16; ++r) {
-                const int ur = lg >= 5 ? 0 : (r >> (lg - 1));
-                if (ur != u) continue;
-                const int p = 32 * rt + (r & 3) + 8 * (r >> 2) + 4 * h;
-                mx = fmaxf(mx, y[r]);
-                sm = sm + y[r] * s_pw[p];
-              }
-              mx = fmaxf(mx, __shfl_xor(mx, 32, kWave));
-              sm = sm + __shfl_xor(sm, 32, kWave);
-              if (h == 0) {
-                float* pp = part + ((size_t)(rt * 4 + u) * 2) * coutp + fo;
-                pp[0] = mx;
-                pp[coutp] = sm;
-              }
-            }
-          }
-        }
+        const int to = item / nsplit;
+        const int rt0 = (item - to * nsplit) * rg_tiles;
+        if (rg_tiles == 1) layer_item<SRC, R, 1>(ctx, l, last, to, rt0, pass);
+        else layer_item<SRC, R, (R >= 2 ? 2 : 1)>(ctx, l, last, to, rt0, pass);
       }
       __syncthreads();
+      PN2_STAMP(3 + l);
     }
 
     // ---- 4. pooling: combine the row-tile partials of each group, store -----------------
@@ -395,6 +611,7 @@ __global__ __launch_bounds__(kBlock) void mlp_kernel(const Params prm) {
       __syncthreads();
     }
   }
+  PN2_STAMP(15);
 }
 
 // Packed layer: Wp [cout32][cin8][2][32][4] then scale [cout32*32] then shift [cout32*32].
@@ -466,7 +683,6 @@ size_t plan(Params& prm, int nl, const pn2_mlp_layer* layers, int cin0, int R, b
   }
   prm.nl = nl;
   prm.width0 = ((cin0 + 7) / 8) * 8;
-  prm.div_w0 = make_fastdiv((uint32_t)prm.width0);
   // row strides = 4 (mod 32) floats: the 16-byte reads/writes of 8 consecutive rows hit
   // distinct bank quads
   prm.stride0 = ((w0 + 31) / 32) * 32 + 4;
@@ -484,6 +700,22 @@ size_t plan(Params& prm, int nl, const pn2_mlp_layer* layers, int cin0, int R, b
   return off * sizeof(float);
 }
 
+// Input segments of the three sources (see Params).
+void set_segments(Params& prm, int nA, bool vecA, int offA, int nB, bool vecB, int offB,
+                  int cin_total) {
+  prm.vecA = vecA;
+  prm.nA = vecA ? nA / 4 : nA;
+  prm.offA = offA;
+  prm.vecB = vecB;
+  prm.nB = vecB ? nB / 4 : nB;
+  prm.offB = offB;
+  prm.divA = make_fastdiv((uint32_t)(prm.nA > 0 ? prm.nA : 1));
+  prm.divB = make_fastdiv((uint32_t)(prm.nB > 0 ? prm.nB : 1));
+  prm.cin_total = cin_total;
+  const int npad = prm.width0 - cin_total;
+  prm.div_pad = make_fastdiv((uint32_t)(npad > 0 ? npad : 1));
+}
+
 int check_layers(int nl, const pn2_mlp_layer* layers, int cin0) {
   if (nl < 1 || nl > PN2_MLP_MAX_LAYERS || !layers) return PN2_EINVAL;
   int cin = cin0;
@@ -497,7 +729,10 @@ int check_layers(int nl, const pn2_mlp_layer* layers, int cin0) {
 
 // Dynamic LDS beyond the 64 KiB default is opted into once per instantiation.
 template <int SRC, int R>
-int launch_one(const Params& prm, long long nblocks, size_t lds, hipStream_t s) {
+int launch_one(Params prm, long long nblocks, size_t lds, hipStream_t s) {
+#ifdef PN2_MLP_STAMP
+  prm.stamp = g_stamp;
+#endif
   static const hipError_t attr = hipFuncSetAttribute(
       reinterpret_cast<const void*>(&mlp_kernel<SRC, R>),
       hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsLimit);
@@ -515,34 +750,50 @@ int launch_rows_R(Params& prm, int R, long long nblocks, size_t lds, hipStream_t
   return launch_one<SRC, 4>(prm, nblocks, lds, s);
 }
 
-// Row tiles per workgroup: enough (row tile, output tile) items that the four waves all work
-// on the narrowest layer, within the LDS limit, and not fewer workgroups than CUs when the
-// work allows it.
+// Row tiles per workgroup: prefer the cheapest R whose LDS lets two
+// workgroups share a CU (one wave per SIMD leaves every stall exposed), then any that fits.
 int choose_R(Params& prm, int nl, const pn2_mlp_layer* layers, int cin0, bool pooled,
              long long tiles32, int min_R, size_t* lds_out) {
-  int min_c32 = 1 << 30;
-  for (int l = 0; l < nl; ++l) {
-    const int c32 = (layers[l].cout + 31) / 32;
-    min_c32 = c32 < min_c32 ? c32 : min_c32;
-  }
-  int want = min_c32 >= 4 ? 1 : (min_c32 >= 2 ? 2 : 4);
-  while (want > min_R && tiles32 / want < 256) want >>= 1;
-  if (want < min_R) want = min_R;
-  for (int R = want; R >= min_R; R >>= 1) {
+  int best = 0, best_occ = 0;
+  double best_cost = 0;
+  size_t best_lds = 0;
+  for (int R = 4; R >= min_R; R >>= 1) {
     const size_t lds = plan(prm, nl, layers, cin0, R, pooled);
-    if (lds <= kLdsLimit) {
-      *lds_out = lds;
-      return R;
+    if (lds > kLdsLimit) continue;
+    if (R > 1 && tiles32 < 256LL * R) continue;  // too few workgroups to fill the chip
+    // per row tile: items per wave x (RG row tiles x cin8 chunks + ~4 chunks of exposed
+    // weight-load latency per item), the kernel's item split (see mlp_kernel, section 3)
+    double cost = 0;
+    for (int l = 0; l < nl; ++l) {
+      const int c32 = (layers[l].cout + 31) / 32, cin8 = (layers[l].cin + 7) / 8;
+      const int nsplit = item_split(R, c32);
+      const int items = nsplit * c32, rg = R / nsplit;
+      cost += (double)((items + kWaves - 1) / kWaves) * (rg * cin8 + 4) / R;
     }
-    if (R == 1) break;
+    const int occ = lds * 2 <= kLdsLimit ? 2 : 1;
+    if (!best || occ > best_occ || (occ == best_occ && cost < best_cost)) {
+      best = R;
+      best_occ = occ;
+      best_cost = cost;
+      best_lds = lds;
+    }
   }
-  return 0;
+  if (best) {
+    *lds_out = plan(prm, nl, layers, cin0, best, pooled);
+    (void)best_lds;
+  }
+  return best;
 }
 
 }  // namespace
 }  // namespace pn2
 
 extern "C" {
+
+#ifdef PN2_MLP_STAMP
+// diagnostic builds only (tools/stamp_mlp.py): device buffer of kStampWG x 16 u64, or NULL
+void pn2_mlp_set_stamp(void* buf) { pn2::g_stamp = static_cast<unsigned long long*>(buf); }
+#endif
 
 size_t pn2_mlp_packed_size(int cin, int cout) {
   if (cin <= 0 || cout <= 0) return 0;
@@ -604,6 +855,10 @@ int pn2_group_mlp(const float* xyz, const float* points, const float* new_xyz,
   prm.ns = nsample;
   prm.lg_ns_pad = ilog2(ns_pad);
   prm.layout = layout;
+  if (layout == kXyzOnly) set_segments(prm, 0, false, 0, 3, false, 0, 3);
+  else if (layout == kPointsOnly) set_segments(prm, C, C % 4 == 0, 0, 0, false, 0, C);
+  else if (layout == kXyzFirst) set_segments(prm, C, C % 4 == 0, 3, 3, false, 0, C + 3);
+  else set_segments(prm, C, C % 4 == 0, 0, 3, false, C, C + 3);
   prm.ngroups = (int)ngroups;
   prm.pool = pool;
   prm.out = out;
@@ -646,6 +901,7 @@ int pn2_fp_mlp(const float* dist, const int32_t* nn_idx, const float* points1, i
   prm.n = n;
   prm.m = m;
   prm.rows = rows;
+  set_segments(prm, C2, C2 % 4 == 0, 0, C1, C1 % 4 == 0 && C2 % 4 == 0, C2, C1 + C2);
   prm.passes = 1;
   prm.pool = PN2_POOL_NONE;
   prm.out = out;
@@ -668,6 +924,7 @@ int pn2_shared_mlp(const float* x, long long rows, int cin, int nlayers,
   prm.x = x;
   prm.cin = cin;
   prm.rows = rows;
+  set_segments(prm, cin, cin % 4 == 0, 0, 0, false, 0, cin);
   prm.passes = 1;
   prm.pool = PN2_POOL_NONE;
   prm.out = out;

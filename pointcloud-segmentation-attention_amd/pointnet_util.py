@@ -315,11 +315,22 @@ def pointnet_fp_module(xyz1, xyz2, points1, points2, mlp, is_training, bn_decay,
         return tf_util.mlp_torch(x, layers, is_training, bn_decay)
     fused = tf_util.packed_mlp(store, scopes, C1 + C2, mlp, bn=bn)
     dist, idx = tf_interpolate.three_nn(xyz1, xyz2, known_grid, unknown_grid)
-    B, n, m = int(xyz1.shape[0]), int(xyz1.shape[1]), int(xyz2.shape[1])
+    return fp_mlp(dist, idx, points1, points2, fused)
+
+
+def fp_mlp(dist, idx, points1, points2, mlp):
+    """pointnet_fp_module after three_nn: IDW weights of dist (B,n,3), interpolation of
+    points2 (B,m,C2) at idx, concat [interp, points1 (B,n,C1) or None], then the fused MLP
+    `mlp` (tf_util.SharedMLP) -> (B, n, mlp.cout) (pn2_fp_mlp, one kernel)."""
+    dist = device_tensor(dist, "dist", torch.float32)
+    idx = device_tensor(idx, "idx", torch.int32)
+    points2 = device_tensor(points2, "points2", torch.float32)
+    B, n, m, C2 = int(dist.shape[0]), int(dist.shape[1]), int(points2.shape[1]), int(points2.shape[2])
     if points1 is not None:
         points1 = device_tensor(points1, "points1", torch.float32)
-    out = torch.empty((B, n, fused.cout), dtype=torch.float32, device=xyz1.device)
-    tab, nl = fused.table()
+    C1 = 0 if points1 is None else int(points1.shape[2])
+    out = torch.empty((B, n, mlp.cout), dtype=torch.float32, device=dist.device)
+    tab, nl = mlp.table()
     check(lib().pn2_fp_mlp(ptr(dist), ptr(idx), ptr(points1), C1, ptr(points2), C2, B, n, m, nl,
-                           tab, ptr(out), stream_of(xyz1)), "fp_mlp")
+                           tab, ptr(out), stream_of(dist)), "fp_mlp")
     return out

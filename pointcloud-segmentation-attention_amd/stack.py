@@ -12,15 +12,27 @@ outputs are replaced by fixed synthetic U[-1,1) tensors of the right shapes, pre
 the timed region. One "step" runs every geometric op of every layer for the whole batch:
 FPS (+gather), ball query, fused group/centre/concat, the attention reduction (cfg3), and
 three_nn + IDW + three_interpolate + concat of every FP layer.
+
+With model=True (make_inputs) the step is instead the whole inference forward pass of
+pointnet2_sem_seg.py:19-61 (= pointnet2_sem_seg_features.py with rgb+normals for cfg3): every
+SA layer as one fused group + MLP + max-pool kernel fed by the previous layer's real output,
+every FP layer as one fused interpolation + MLP kernel, and the conv1d head (fc1 with batch
+norm, dropout = identity at inference, fc2 to 21 classes) fused into FP4's MLP. Weights are
+the reference initialisers (tf_util.ParamStore, fixed seed).
 """
 import torch
 
-from . import attention_layer, pointnet_util, synth, tf_grouping, tf_sampling
+from . import attention_layer, pointnet_util, synth, tf_grouping, tf_interpolate, tf_sampling, \
+    tf_util
 
 SSG_SA = ((1024, 0.1, 32, 64), (256, 0.2, 32, 128), (64, 0.4, 32, 256), (16, 0.8, 32, 512))
 SSG_FP_OUT = (256, 256, 128, 128)
 MSG_SA = ((512, (0.1, 0.2, 0.4), (16, 32, 128), (64, 128, 128)),
           (128, (0.2, 0.4, 0.8), (32, 64, 128), (128, 256, 256)))
+# the full model's MLP widths (pointnet2_sem_seg.py:29-60)
+SSG_SA_MLP = ((32, 32, 64), (64, 64, 128), (128, 128, 256), (256, 256, 512))
+SSG_FP_MLP = ((256, 256), (256, 256), (256, 128), (128, 128, 128))
+NUM_CLASSES = 21  # ScanNet (pointnet2_sem_seg_attention.py:17)
 
 NSIDE = 4  # side streams of the overlapped step (SSG)
 
@@ -44,14 +56,49 @@ def _rand_per_cloud(cloud_ids, shape, device, seed, slot):
     return torch.stack(rows) * 2.0 - 1.0
 
 
-def make_inputs(config, cloud_ids, device, seed=1234):
-    """Resident inputs of one step: the synthetic ScanNet crops and the stand-in MLP outputs."""
+class SemSegModel:
+    """The packed MLPs of pointnet2_sem_seg(_features) (pointnet2_sem_seg.py:29-60) under the
+    reference's variable scopes: layer1..4/conv<j>, fa_layer1..4/conv_<j>, fc1, fc2. FP4's
+    MLP carries the head: fa_layer4's three layers, then fc1 (128, batch norm, relu) and fc2
+    (NUM_CLASSES, no batch norm, no activation) as the 4th and 5th layers of ONE kernel."""
+
+    def __init__(self, in_channels, params=None, device="cuda"):
+        self.store = params if params is not None else tf_util.ParamStore(seed=7, device=device)
+        st = self.store
+        self.sa, c = [], in_channels
+        for i, widths in enumerate(SSG_SA_MLP):
+            self.sa.append(tf_util.packed_mlp(st, [f"layer{i + 1}/conv{j}" for j in range(3)],
+                                              c + 3, widths))
+            c = widths[-1]
+        levels_c = [in_channels] + [w[-1] for w in SSG_SA_MLP]
+        self.fp, c2 = [], SSG_SA_MLP[3][-1]
+        for k, widths in enumerate(SSG_FP_MLP):
+            cin = c2 + levels_c[3 - k]
+            scopes = [f"fa_layer{k + 1}/conv_{j}" for j in range(len(widths))]
+            layers = tf_util.packed_mlp(st, scopes, cin, widths).layers
+            if k == 3:  # + the conv1d head (pointnet2_sem_seg.py:57-60)
+                head1 = tf_util.packed_mlp(st, ["fc1"], widths[-1], [128]).layers
+                head2 = tf_util.packed_mlp(st, ["fc2"], 128, [NUM_CLASSES], bn=False,
+                                           relu=False).layers
+                layers = layers + head1 + head2
+            self.fp.append(tf_util.SharedMLP(layers))
+            c2 = widths[-1]
+
+
+def make_inputs(config, cloud_ids, device, seed=1234, model=False):
+    """Resident inputs of one step: the synthetic ScanNet crops and the stand-in MLP outputs
+    (or, with model=True, the packed weights of the whole segmentation model)."""
     N, kind, with_feat, attn = CONFIGS[config]
     B = len(cloud_ids)
     xyz, feats = synth.batch(cloud_ids, N, "scannet", with_features=with_feat)
     inp = {"config": config, "B": B, "N": N,
            "xyz": torch.from_numpy(xyz).to(device),
            "feats": torch.from_numpy(feats).to(device) if feats is not None else None}
+    if model:
+        if kind != "ssg":
+            raise NotImplementedError("model=True: the SSG segmentation model (cfg2 / cfg3)")
+        inp["model"] = SemSegModel(6 if with_feat else 0, device=device)
+        return inp
     r = lambda shape, slot: _rand_per_cloud(cloud_ids, shape, device, seed, slot)  # noqa: E731
     if kind == "ssg":
         inp["sa_out"] = [r((npt, c), i) for i, (npt, _, _, c) in enumerate(SSG_SA)]
@@ -115,7 +162,10 @@ class Step:
         self.kind = CONFIGS[inp["config"]][1]
         self.overlap = overlap and inp["xyz"].is_cuda
         self.v = {}  # intermediates by name
-        self.tasks = self._tasks_ssg() if self.kind == "ssg" else self._tasks_msg()
+        if "model" in inp:
+            self.tasks = self._tasks_ssg_model()
+        else:
+            self.tasks = self._tasks_ssg() if self.kind == "ssg" else self._tasks_msg()
         self.ran = False
         self.synced_inputs = False
         self.nlanes = 1 + max(t.lane for t in self.tasks)
@@ -203,6 +253,73 @@ class Step:
         tasks.append(Task("fp1", 3, (sampled[3],), fp(3)))
         return tasks
 
+    def _tasks_ssg_model(self):
+        """The whole inference forward of the SSG segmentation model. Lane 0: SA1's sampler;
+        lane 4: SA2..SA4's samplers; lanes 2-3: the FP layers' neighbour searches (they need
+        only the sampled coordinates); lane 1: the data-dependent chain SA1 -> SA4 -> FP1 ->
+        FP4+head, each layer one fused kernel (plus the ball query before each SA)."""
+        inp, v, mdl = self.inp, self.v, self.inp["model"]
+        xyz0 = inp["xyz"]
+        B = int(xyz0.shape[0])
+        npoints = [sa_[0] for sa_ in SSG_SA]
+        if not tf_sampling.chain_supported(int(xyz0.shape[1]), npoints):
+            raise NotImplementedError("model step: the fused sampler chain's cloud sizes")
+        big = int(xyz0.shape[1]) >= tf_grouping.GRID_MIN_POINTS
+        v["chain"] = [(torch.empty((B, m), dtype=torch.int32, device=xyz0.device),
+                       torch.empty((B, m, 3), dtype=torch.float32, device=xyz0.device))
+                      for m in npoints]
+        v["xyz"] = [xyz0] + [nx for _, nx in v["chain"]]
+        v["pts"] = [inp["feats"], None, None, None, None]
+        v["nn"], v["fp"] = [None] * 4, [None] * 4
+        tasks = []
+        if big:
+            tasks.append(Task("grid1", 1, (), lambda: v.__setitem__(
+                "grid1", tf_grouping.BallGrid(xyz0, SSG_SA[0][1]))))
+        tasks.append(Task("fps1", 0, (), lambda: tf_sampling.farthest_point_sample_chain(
+            npoints[:1], xyz0, out=v["chain"][:1]), direct=True))
+        tasks.append(Task("fps234", 4, ("fps1",), lambda: tf_sampling.farthest_point_sample_chain(
+            npoints[1:], v["xyz"][1], out=v["chain"][1:]), direct=True))
+        sampled = ("fps1", "fps234", "fps234", "fps234")
+
+        def nn(k):  # FP layer k interpolates level 4-k onto level 3-k
+            def f():
+                lvl = 3 - k
+                v["nn"][k] = tf_interpolate.three_nn(
+                    v["xyz"][lvl], v["xyz"][lvl + 1],
+                    unknown_grid=v.get("grid1") if lvl == 0 else None)
+            return f
+
+        def sa(i):
+            def f():
+                _, radius, nsample, _ = SSG_SA[i]
+                xyz, new_xyz = v["xyz"][i], v["xyz"][i + 1]
+                idx, _ = tf_grouping.query_ball_point(radius, nsample, xyz, new_xyz,
+                                                      grid=v.get("grid1") if i == 0 else None)
+                v["pts"][i + 1] = pointnet_util.group_mlp(xyz, v["pts"][i], new_xyz, idx,
+                                                          mdl.sa[i], "max")
+            return f
+
+        def fp(k):
+            def f():
+                lvl = 3 - k
+                p2 = v["pts"][4] if k == 0 else v["fp"][k - 1]
+                dist, idx = v["nn"][k]
+                v["fp"][k] = pointnet_util.fp_mlp(dist, idx, v["pts"][lvl], p2, mdl.fp[k])
+            return f
+
+        grid_dep = ("grid1",) if big else ()
+        # task "nn<k+1>" = FP layer k+1's search (fa_layer<k+1>)
+        tasks.append(Task("nn4", 2, (sampled[0],) + grid_dep, nn(3)))
+        tasks.append(Task("nn3", 2, (sampled[1],), nn(2)))
+        tasks.append(Task("nn2", 3, (sampled[2],), nn(1)))
+        tasks.append(Task("nn1", 3, (sampled[3],), nn(0)))
+        tasks.append(Task("sa1", 1, (sampled[0],), sa(0)))
+        for i in (1, 2, 3):
+            tasks.append(Task(f"sa{i + 1}", 1, (sampled[i],), sa(i)))
+        for k in range(4):
+            tasks.append(Task(f"fp{k + 1}", 1, (f"nn{k + 1}",), fp(k)))
+        return tasks
+
     def _tasks_msg(self):
         inp, v = self.inp, self.v
         v["xyz"] = [inp["xyz"], None, None]
@@ -248,6 +365,8 @@ class Step:
 
     def outputs(self):
         v = self.v
+        if "model" in self.inp:  # logits (B, N, 21), then the SA levels' features
+            return [v["fp"][3]] + v["pts"][1:]
         if self.kind == "ssg":
             return [t for o in v["sa"] for t in o] + list(v["fp"])
         return [v["gp"][k] for k in sorted(v["gp"])]
@@ -330,8 +449,8 @@ class GraphStep:
     on its lane's stream; replay() relaunches them with the same cross-stream events as the
     eager step. Inputs stay resident, outputs are overwritten in place at every replay."""
 
-    def __init__(self, inp, warmup=2, overlap=True):
-        self.step = Step(inp, overlap=overlap)
+    def __init__(self, inp, warmup=2, overlap=True, streams=None):
+        self.step = Step(inp, overlap=overlap, streams=streams)
         dev = inp["xyz"].device
         warm = side_stream(dev, "warm")
         warm.wait_stream(torch.cuda.current_stream(dev))
@@ -385,10 +504,20 @@ class Pipeline:
     samplers; with 3 sets the side work of a step has two sampler periods to finish. Every
     step still does all of its work; run(k) returns after enqueueing, join() waits."""
 
-    def __init__(self, inp, graphs=True, overlap=True, nsets=3):
-        mk = (lambda: GraphStep(inp, overlap=overlap)) if graphs else \
-            (lambda: Step(inp, overlap=overlap))
-        self.sets = [mk() for _ in range(max(2, nsets))]
+    def __init__(self, inp, graphs=True, overlap=True, nsets=3, private_streams=False):
+        # private_streams: every buffer set gets its own side streams, so the side lanes of
+        # consecutive steps overlap each other too (the whole-model step, whose lane-1 chain
+        # of SA/FP layers is longer than a sampler period); otherwise the sets share them
+        dev = inp["xyz"].device
+
+        def streams(i):  # set 0 keeps the process-wide side streams
+            if i == 0 or not (private_streams and overlap and inp["xyz"].is_cuda):
+                return None
+            return [None] + [side_stream(dev, (i, lane)) for lane in range(1, NSIDE + 1)]
+
+        mk = (lambda i: GraphStep(inp, overlap=overlap, streams=streams(i))) if graphs else \
+            (lambda i: Step(inp, overlap=overlap, streams=streams(i)))
+        self.sets = [mk(i) for i in range(max(2, nsets))]
         self.k = 0
 
     def run(self, sampler_events=None):
