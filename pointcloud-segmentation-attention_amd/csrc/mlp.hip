@@ -44,6 +44,7 @@ struct LayerDev {
   const float* scale;  // [cout32*32]
   const float* shift;  // [cout32*32]
   int cin8, cout32, cout, relu;
+  int lofs;  // float offset of this layer's packed block in the LDS weight copy (WL kernels)
 };
 
 struct Params {
@@ -52,6 +53,8 @@ struct Params {
   int width0;            // layer-0 input width in LDS (cin8*8)
   int stride0, stride1;  // LDS row strides (floats) of the activation buffers
   int off1, off_part, off_run, off_meta;  // float offsets into dynamic LDS
+  int off_w, wfloats;  // WL kernels: LDS copy of every layer's packed block (wfloats floats)
+  int direct_pool;     // one pass, ns_pad <= 32: a row tile's pooled values are final
   // input row = segment A (+ segment B) (+ zero padding up to width0); nA/nB = units per row
   // (float4 chunks when vecA/vecB, else floats), offA/offB = LDS column of the segment
   int nA, nB, offA, offB, vecA, vecB, cin_total;
@@ -190,11 +193,9 @@ PN2_DEV void gather_segment(int n, FastDiv div_n, int off, float* act, int strid
     T vals[kGatherUnroll];
 #pragma unroll
     for (int u = 0; u < kGatherUnroll; ++u) {
-      const int e = e0 + u * kBlock;
-      if (e < total) {
-        const int p = (int)fdiv((uint32_t)e, div_n);
-        vals[u] = fetch(p, e - p * n);
-      }
+      const int e = min(e0 + u * kBlock, total - 1);  // branch-free: every load in flight
+      const int p = (int)fdiv((uint32_t)e, div_n);
+      vals[u] = fetch(p, e - p * n);
     }
 #pragma unroll
     for (int u = 0; u < kGatherUnroll; ++u) {
@@ -322,9 +323,22 @@ __host__ __device__ inline int item_split(int R, int c32) {
   return nsplit;
 }
 
+// pooled output of group g, feature fo (pointnet_util.py:130-145)
+PN2_DEV void store_pooled(const Params& prm, int g, int fo, int cout, float mx, float sm) {
+  const float avg = sm / (float)prm.ns;
+  if (prm.pool == PN2_POOL_MAX) prm.out[(size_t)g * cout + fo] = mx;
+  else if (prm.pool == PN2_POOL_AVG) prm.out[(size_t)g * cout + fo] = avg;
+  else if (prm.pool == PN2_POOL_WEIGHTED_AVG) prm.out[(size_t)g * cout + fo] = sm;
+  else {  // max_and_avg: concat [avg, max] (pointnet_util.py:145)
+    prm.out[(size_t)g * 2 * cout + fo] = avg;
+    prm.out[(size_t)g * 2 * cout + cout + fo] = mx;
+  }
+}
+
 // What a layer item needs from the kernel (LDS carve, lane coordinates, pooling state).
 struct Ctx {
   const Params* prm;
+  const float* wl;  // LDS weight copy (WL kernels) or nullptr
   float* act0;
   float* act1;
   float* part;
@@ -338,15 +352,23 @@ struct Ctx {
 // One item of layer l: the MFMA product, then either the intermediate epilogue (scale,
 // shift, activation, 16-byte writes into the other LDS buffer) or the last layer's (per-point
 // stores, or per-group pooling partials in LDS).
-template <int SRC, int R, int RG>
+template <int SRC, int R, int RG, bool WL>
 PN2_DEV void layer_item(const Ctx& cx, int l, bool last, int to, int rt0, int pass) {
   constexpr int P = 32 * R;
   const Params& prm = *cx.prm;
   const LayerDev& Ld = prm.L[l];
+  const float4* wbase = Ld.w;
+  const float* scale = Ld.scale;
+  const float* shift = Ld.shift;
+  if (WL) {  // the workgroup's LDS copy of the packed block
+    wbase = reinterpret_cast<const float4*>(cx.wl + Ld.lofs);
+    scale = cx.wl + Ld.lofs + Ld.cout32 * Ld.cin8 * 256;
+    shift = scale + Ld.cout32 * 32;
+  }
   const float* in = (l & 1) ? cx.act1 : cx.act0;
   const int Sin = (l & 1) ? prm.stride1 : prm.stride0;
   const int lane = cx.lane, col = cx.col, h = cx.h;
-  const float4* wp = Ld.w + (size_t)to * Ld.cin8 * kWave + lane;
+  const float4* wp = wbase + (size_t)to * Ld.cin8 * kWave + lane;
   const float* ap = in + (32 * rt0 + col) * Sin + 4 * h;
   f32x16 acc[RG];
   if (!last) {
@@ -357,8 +379,8 @@ PN2_DEV void layer_item(const Ctx& cx, int l, bool last, int to, int rt0, int pa
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int fb = 32 * to + 8 * q + 4 * h;
-      sc[q] = *reinterpret_cast<const float4*>(Ld.scale + fb);
-      sh[q] = *reinterpret_cast<const float4*>(Ld.shift + fb);
+      sc[q] = *reinterpret_cast<const float4*>(scale + fb);
+      sh[q] = *reinterpret_cast<const float4*>(shift + fb);
     }
     mma_item<false, RG>(wp, ap, 32 * Sin, Ld.cin8, acc);
 #pragma unroll
@@ -378,8 +400,18 @@ PN2_DEV void layer_item(const Ctx& cx, int l, bool last, int to, int rt0, int pa
     return;
   }
   const int fo = 32 * to + col;
-  const float s = Ld.scale[fo], t = Ld.shift[fo];
+  const float s = scale[fo], t = shift[fo];
+#ifdef PN2_MLP_STAMP
+  const bool st = prm.stamp && blockIdx.x < kStampWG && threadIdx.x == 0 && to == 0;
+  if (st) prm.stamp[blockIdx.x * 16 + 10] = __builtin_amdgcn_s_memtime();
+#endif
   mma_item<true, RG>(wp, ap, 32 * Sin, Ld.cin8, acc);
+#ifdef PN2_MLP_STAMP
+  if (st) {
+    __builtin_amdgcn_s_waitcnt(0);
+    prm.stamp[blockIdx.x * 16 + 11] = __builtin_amdgcn_s_memtime();
+  }
+#endif
 #pragma unroll
   for (int r = 0; r < RG; ++r) {
     const int rt = rt0 + r;
@@ -404,34 +436,67 @@ PN2_DEV void layer_item(const Ctx& cx, int l, bool last, int to, int rt0, int pa
         prm.out[orow * Ld.cout + fo] = y[i];
       }
     } else {
-      // per local group u of this row tile: u = i >> (lg-1) for ns_pad 8/16, else 0
+      // rows of register i: (i&3) + 8(i>>2) + 4h, so register quad q = i>>2 holds rows
+      // 8q..8q+7 (both lane halves). Per-quad partials, then groups of 1, 2 or 4 quads
+      // (ns_pad 8, 16, >= 32), then the two lane halves (v_permlane32_swap).
+      const bool wsum = prm.pool != PN2_POOL_MAX;
+      float mq[4], sq[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        mq[q] = fmaxf(fmaxf(y[4 * q], y[4 * q + 1]), fmaxf(y[4 * q + 2], y[4 * q + 3]));
+        sq[q] = 0.f;
+        if (wsum) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            sq[q] = sq[q] + y[4 * q + e] * cx.s_pw[32 * rt + e + 8 * q + 4 * h];
+        }
+      }
       const int lg = prm.lg_ns_pad;
-      const int gpt = lg >= 5 ? 1 : (32 >> lg);
+      int gpt;
+      if (lg >= 5) {
+        mq[0] = fmaxf(fmaxf(mq[0], mq[1]), fmaxf(mq[2], mq[3]));
+        sq[0] = (sq[0] + sq[1]) + (sq[2] + sq[3]);
+        gpt = 1;
+      } else if (lg == 4) {
+        mq[0] = fmaxf(mq[0], mq[1]);
+        sq[0] = sq[0] + sq[1];
+        mq[1] = fmaxf(mq[2], mq[3]);
+        sq[1] = sq[2] + sq[3];
+        gpt = 2;
+      } else {
+        gpt = 4;
+      }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        if (u >= gpt) break;
-        float mx = -__builtin_inff(), sm = 0.f;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int ui = lg >= 5 ? 0 : (i >> (lg - 1));
-          if (ui != u) continue;
-          const int p = 32 * rt + (i & 3) + 8 * (i >> 2) + 4 * h;
-          mx = fmaxf(mx, y[i]);
-          sm = sm + y[i] * cx.s_pw[p];
-        }
-        mx = fmaxf(mx, __shfl_xor(mx, 32, kWave));
-        sm = sm + __shfl_xor(sm, 32, kWave);
-        if (h == 0) {
-          float* pp = cx.part + ((size_t)(rt * 4 + u) * 2) * cx.coutp + fo;
-          pp[0] = mx;
-          pp[cx.coutp] = sm;
+        if (u < gpt) {
+          auto xm = __builtin_amdgcn_permlane32_swap(__float_as_uint(mq[u]),
+                                                     __float_as_uint(mq[u]), false, false);
+          const float mx = fmaxf(__uint_as_float(xm[0]), __uint_as_float(xm[1]));
+          float sm = 0.f;
+          if (wsum) {
+            auto xs = __builtin_amdgcn_permlane32_swap(__float_as_uint(sq[u]),
+                                                       __float_as_uint(sq[u]), false, false);
+            sm = __uint_as_float(xs[0]) + __uint_as_float(xs[1]);
+          }
+          if (prm.direct_pool) {  // this row tile holds whole groups: store the final value
+            const int g = blockIdx.x * prm.gpw + rt * gpt + u;
+            if (h == 0 && g < prm.ngroups && fo < Ld.cout)
+              store_pooled(prm, g, fo, Ld.cout, mx, sm);
+#ifdef PN2_MLP_STAMP
+            if (st) prm.stamp[blockIdx.x * 16 + 12] = __builtin_amdgcn_s_memtime();
+#endif
+          } else if (h == 0) {
+            float* pp = cx.part + ((size_t)(rt * 4 + u) * 2) * cx.coutp + fo;
+            pp[0] = mx;
+            pp[cx.coutp] = sm;
+          }
         }
       }
     }
   }
 }
 
-template <int SRC, int R>
+template <int SRC, int R, bool WL>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2, 2))) void mlp_kernel(const Params prm) {
   constexpr int P = 32 * R;
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -455,7 +520,29 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2, 2))) 
   const bool pooled = (SRC == kSrcGroup) && prm.pool >= 0;
   const LayerDev& LL = prm.L[prm.nl - 1];
   const int coutp = LL.cout32 * 32;
-  const Ctx ctx{&prm, act0, act1, part, s_src, s_aux, s_pw, lane, col, h, ns_pad, coutp, pooled};
+  const float* wl = WL ? smem + prm.off_w : nullptr;
+  const Ctx ctx{&prm, wl, act0, act1, part, s_src, s_aux, s_pw, lane, col, h, ns_pad, coutp,
+                pooled};
+  if (WL) {
+    // every layer's packed block into LDS once; the loads overlap the metadata phase and
+    // the first barrier publishes them
+    const float4* src0 = reinterpret_cast<const float4*>(prm.L[0].w);
+    (void)src0;
+    for (int l = 0; l < prm.nl; ++l) {
+      const LayerDev& Ld = prm.L[l];
+      const int n4 = (Ld.cout32 * Ld.cin8 * 256 + Ld.cout32 * 64) / 4;
+      const float4* src = Ld.w;
+      float4* dst = reinterpret_cast<float4*>(smem + prm.off_w + Ld.lofs);
+      for (int i0 = tid; i0 < n4; i0 += kBlock * 4) {
+        float4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = src[min(i0 + u * kBlock, n4 - 1)];  // branch-free
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (i0 + u * kBlock < n4) dst[i0 + u * kBlock] = v[u];
+      }
+    }
+  }
 
   PN2_STAMP(0);
   for (int pass = 0; pass < prm.passes; ++pass) {
@@ -563,15 +650,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2, 2))) 
       for (int item = wave; item < nitems; item += kWaves) {
         const int to = item / nsplit;
         const int rt0 = (item - to * nsplit) * rg_tiles;
-        if (rg_tiles == 1) layer_item<SRC, R, 1>(ctx, l, last, to, rt0, pass);
-        else layer_item<SRC, R, (R >= 2 ? 2 : 1)>(ctx, l, last, to, rt0, pass);
+        if (rg_tiles == 1) layer_item<SRC, R, 1, WL>(ctx, l, last, to, rt0, pass);
+        else layer_item<SRC, R, (R >= 2 ? 2 : 1), WL>(ctx, l, last, to, rt0, pass);
       }
       __syncthreads();
       PN2_STAMP(3 + l);
     }
 
     // ---- 4. pooling: combine the row-tile partials of each group, store -----------------
-    if (pooled) {
+    if (pooled && !prm.direct_pool) {
       const int cout = LL.cout;
       const bool first = pass == 0, final = pass == prm.passes - 1;
       const int ngr = prm.passes == 1 ? prm.gpw : 1;
@@ -595,17 +682,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2, 2))) 
             run[fo] = mx;
             run[coutp + fo] = sm;
           }
-          if (final) {
-            const int pool = prm.pool;
-            const float avg = sm / (float)prm.ns;
-            if (pool == PN2_POOL_MAX) prm.out[(size_t)g * cout + fo] = mx;
-            else if (pool == PN2_POOL_AVG) prm.out[(size_t)g * cout + fo] = avg;
-            else if (pool == PN2_POOL_WEIGHTED_AVG) prm.out[(size_t)g * cout + fo] = sm;
-            else {  // max_and_avg: concat [avg, max] (pointnet_util.py:145)
-              prm.out[(size_t)g * 2 * cout + fo] = avg;
-              prm.out[(size_t)g * 2 * cout + cout + fo] = mx;
-            }
-          }
+          if (final) store_pooled(prm, g, fo, cout, mx, sm);
         }
       }
       __syncthreads();
@@ -662,8 +739,10 @@ int ilog2(int v) {
 constexpr size_t kLdsLimit = 160 * 1024;
 
 // Fill the layer table and LDS layout for R row tiles; returns LDS bytes (0 = invalid).
-size_t plan(Params& prm, int nl, const pn2_mlp_layer* layers, int cin0, int R, bool pooled) {
+size_t plan(Params& prm, int nl, const pn2_mlp_layer* layers, int cin0, int R, bool pooled,
+            bool wl = false) {
   const int P = 32 * R;
+  int wfloats = 0;
   int w0 = ((cin0 + 7) / 8) * 8, w1 = 0;
   for (int l = 0; l < nl; ++l) {
     const pn2_mlp_layer& L = layers[l];
@@ -676,6 +755,8 @@ size_t plan(Params& prm, int nl, const pn2_mlp_layer* layers, int cin0, int R, b
     prm.L[l].cout32 = cout32;
     prm.L[l].cout = L.cout;
     prm.L[l].relu = (L.flags & PN2_MLP_RELU) ? 1 : 0;
+    prm.L[l].lofs = wfloats;
+    wfloats += cout32 * cin8 * 256 + cout32 * 64;
     if (l < nl - 1) {  // layer l writes buffer (l+1)&1
       if ((l + 1) & 1) w1 = w1 > cout32 * 32 ? w1 : cout32 * 32;
       else w0 = w0 > cout32 * 32 ? w0 : cout32 * 32;
@@ -697,6 +778,10 @@ size_t plan(Params& prm, int nl, const pn2_mlp_layer* layers, int cin0, int R, b
   if (pooled) off += 2 * (size_t)coutp;
   prm.off_meta = (int)off;
   off += (size_t)P * 9 + kMaxGroupsPerWG;
+  off = (off + 3) & ~(size_t)3;
+  prm.off_w = (int)off;
+  prm.wfloats = wl ? wfloats : 0;
+  off += prm.wfloats;
   return off * sizeof(float);
 }
 
@@ -728,16 +813,17 @@ int check_layers(int nl, const pn2_mlp_layer* layers, int cin0) {
 }
 
 // Dynamic LDS beyond the 64 KiB default is opted into once per instantiation.
-template <int SRC, int R>
+template <int SRC, int R, bool WL>
 int launch_one(Params prm, long long nblocks, size_t lds, hipStream_t s) {
 #ifdef PN2_MLP_STAMP
   prm.stamp = g_stamp;
 #endif
   static const hipError_t attr = hipFuncSetAttribute(
-      reinterpret_cast<const void*>(&mlp_kernel<SRC, R>),
+      reinterpret_cast<const void*>(&mlp_kernel<SRC, R, WL>),
       hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsLimit);
   if (attr != hipSuccess) return (int)attr;
-  hipLaunchKernelGGL((mlp_kernel<SRC, R>), dim3((unsigned)nblocks), dim3(kBlock), lds, s, prm);
+  hipLaunchKernelGGL((mlp_kernel<SRC, R, WL>), dim3((unsigned)nblocks), dim3(kBlock), lds, s,
+                     prm);
   PN2_RETURN_LAUNCH();
 }
 
@@ -745,9 +831,15 @@ template <int SRC>
 int launch_rows_R(Params& prm, int R, long long nblocks, size_t lds, hipStream_t s) {
   if (nblocks <= 0) return PN2_OK;
   if (nblocks > 0x7fffffffLL) return PN2_EINVAL;
-  if (R == 1) return launch_one<SRC, 1>(prm, nblocks, lds, s);
-  if (R == 2) return launch_one<SRC, 2>(prm, nblocks, lds, s);
-  return launch_one<SRC, 4>(prm, nblocks, lds, s);
+  if (prm.wfloats) {  // weights staged in LDS (small MLPs of the SA layers)
+    if (SRC != kSrcGroup) return PN2_EINVAL;
+    if (R == 1) return launch_one<kSrcGroup, 1, true>(prm, nblocks, lds, s);
+    if (R == 2) return launch_one<kSrcGroup, 2, true>(prm, nblocks, lds, s);
+    return launch_one<kSrcGroup, 4, true>(prm, nblocks, lds, s);
+  }
+  if (R == 1) return launch_one<SRC, 1, false>(prm, nblocks, lds, s);
+  if (R == 2) return launch_one<SRC, 2, false>(prm, nblocks, lds, s);
+  return launch_one<SRC, 4, false>(prm, nblocks, lds, s);
 }
 
 // Row tiles per workgroup: prefer the cheapest R whose LDS lets two
@@ -873,6 +965,16 @@ int pn2_group_mlp(const float* xyz, const float* points, const float* new_xyz,
     nblocks = ngroups;
   }
   if (pooled && prm.gpw > kMaxGroupsPerWG) return PN2_EINVAL;
+  prm.direct_pool = pooled && prm.passes == 1 && ns_pad <= 32;
+  {
+    // small MLPs: stage every layer's weights in LDS when two workgroups still fit a CU
+    Params p2 = prm;
+    const size_t lds_wl = plan(p2, nlayers, layers, cin0, R, pooled, true);
+    if (lds_wl * 2 <= kLdsLimit) {
+      prm = p2;
+      lds = lds_wl;
+    }
+  }
   return launch_rows_R<kSrcGroup>(prm, R, nblocks, lds, (hipStream_t)stream);
 }
 

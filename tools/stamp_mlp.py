@@ -27,7 +27,7 @@ lib = pkg.lib()
 lib.pn2_mlp_set_stamp.argtypes = [ctypes.c_void_p]
 lib.pn2_mlp_set_stamp.restype = None
 dev = torch.device("cuda:0")
-B = int(sys.argv[1]) if len(sys.argv) > 1 else 16
+B = 16
 inp = S.make_inputs("cfg2", list(range(B)), dev, model=True)
 mdl = inp["model"]
 xyz = [inp["xyz"]]
@@ -65,6 +65,10 @@ def run(name, fn, nl):
         ph[f"L{l + 1}"] = t[:, 3 + l] - t[:, prev]
         prev = 3 + l
     ph["pool"] = t[:, 15] - t[:, prev]
+    sub = t[(t[:, 10] > 0) & (t[:, 11] > 0) & (t[:, 12] > 0)]
+    if len(sub):  # the last layer's first item of wave 0 (stamped builds): MMA, epilogue
+        ph["last_item_mma"] = sub[:, 11] - sub[:, 10]
+        ph["last_item_epi"] = sub[:, 12] - sub[:, 11]
     span = t[:, 15].max() - t[:, 0].min()
     # workgroups alive at a time (sampled at 200 points of the span)
     ts = np.linspace(t[:, 0].min(), t[:, 15].max(), 200)
@@ -84,7 +88,7 @@ for i, (m, r, ns, _) in enumerate(S.SSG_SA):
     run(f"SA{i + 1}", lambda: pu.group_mlp(xyz[i], pts[i], xyz[i + 1], idx, mdl.sa[i], "max"),
         len(mdl.sa[i].layers))
 p2 = pts[4]
-for k in range(4):
+for k in range(4 if "--fp" in sys.argv else 0):
     lvl = 3 - k
     dist, nidx = pkg.tf_interpolate.three_nn(xyz[lvl], xyz[lvl + 1])
     p1 = pts[lvl]
