@@ -200,10 +200,12 @@ def main():
         e2e = {"value": world * B * args.e2e_steps / e_el, "unit": "clouds/s",
                "ms_per_step": e_el / args.e2e_steps * 1e3, "steps": args.e2e_steps,
                "sa1_sampler_ms": e_fps, "checksum": float(e_sums.sum().item()),
-               "model": "pointnet2_sem_seg" + ("_features" if args.config == "cfg3" else "")
-                        + " inference forward: SA x4 (fused group + MLP + max pool), "
-                          "FP x4 (fused interpolation + MLP), fc1+fc2 head fused into FP4; "
-                          "fp32 matrix cores; reference initialisers, fixed seed"}
+               "model": ("pointnet2_sem_seg_attention with rgb+normal inputs, inference "
+                         "forward: SA x4 (fused group + MLP, Dense q/k/v on the matrix cores, "
+                         "attention reduction + batch norm)" if args.config == "cfg3" else
+                         "pointnet2_sem_seg inference forward: SA x4 (fused group + MLP + max "
+                         "pool)") + ", FP x4 (fused interpolation + MLP), fc1+fc2 head fused "
+                        "into FP4; fp32 matrix cores; reference initialisers, fixed seed"}
 
     if rank == 0:
         clouds = world * B * args.steps

@@ -8,6 +8,7 @@ num_heads = C/4 (:256-258, :313-315); that is the configuration the kernel imple
 """
 import torch
 
+from . import pointnet_util, tf_grouping, tf_sampling, tf_util
 from ._lib import InvalidArgumentError, check, device_tensor, lib, ptr, stream_of
 
 
@@ -90,3 +91,91 @@ class AttentionLayer(torch.nn.Module):
         K = self.key_net(x).contiguous()
         V = self.value_net(x).contiguous()
         return attention_reduce(Q.reshape(Q.shape[0], Q.shape[1], -1).contiguous(), K, V)
+
+
+def _attention_scopes(scope):
+    # tf.layers.Dense names inside the Keras layer, in build order (:24-26)
+    base = f"{scope}/ScannetAttentionLayer"
+    return f"{base}/dense", f"{base}/dense_1", f"{base}/dense_2"
+
+
+def pointnet_sa_module_attention(xyz, points, npoint, radius, nsample, mlp, mlp2, group_all,
+                                 is_training, bn_decay, scope, bn=True, pooling='max', knn=False,
+                                 use_xyz=True, use_nchw=False, params=None, and_pooling=False):
+    """attention_layer.py:229-276 (and_pooling=True: :279-338, attention + max pool).
+
+    Returns (new_xyz, new_points (B, npoint, mlp[-1] or mlp2[-1]), idx). Variables:
+    '<scope>/conv<i>/...' (the MLP), '<scope>/ScannetAttentionLayer/dense{,_1,_2}/{kernel,bias}'
+    (query, key, value), '<scope>/<scope>/{gamma,beta,moving_mean,moving_variance}' (the batch
+    norm after the attention, :261), '<scope>/conv_post_<i>/...' (mlp2)."""
+    store = params if params is not None else tf_util.default_store()
+    pu = pointnet_util
+    xyz = device_tensor(xyz, "xyz", torch.float32)
+    C = int(mlp[-1])
+    if C % 4:
+        raise InvalidArgumentError("attention SA needs mlp[-1] % 4 == 0 (heads of 4)")
+    scopes = [f"{scope}/conv{i}" for i in range(len(mlp))]
+    qs, ks, vs = _attention_scopes(scope)
+    empty = pu._is_empty_points(points)
+    cin = (0 if empty else int(points.shape[2])) + (3 if (use_xyz or empty) else 0)
+    training = is_training or pu._needs_grad(xyz, points)
+    if group_all:
+        new_xyz, grouped, idx, _ = pu.sample_and_group_all(xyz, points, use_xyz)
+    elif training or knn:
+        new_xyz, grouped, idx, _ = pu.sample_and_group(npoint, radius, nsample, xyz, points, knn,
+                                                       use_xyz)
+    else:
+        _, new_xyz = tf_sampling.farthest_point_sample_and_gather(npoint, xyz)
+        idx, _ = tf_grouping.query_ball_point(radius, nsample, xyz, new_xyz)
+    if training:
+        X = tf_util.mlp_torch(grouped, tf_util.torch_layers(store, scopes, cin, mlp, bn=bn),
+                              is_training, bn_decay)
+        dense = lambda sc, x: x @ store.dense(sc, C, C)["weights"].to(x.device) + \
+            store.dense(sc, C, C)["biases"].to(x.device)  # noqa: E731
+        Q = dense(qs, X[:, :, 0])
+        out = attention_reduce(Q.contiguous(), dense(ks, X).contiguous(), dense(vs, X).contiguous())
+        p = store.bn(f"{scope}/{scope}", C)
+        layer = tf_util.TorchLayer({"weights": torch.eye(C), "biases": None, **p}, relu=False)
+        out = tf_util.mlp_torch(out, [layer], is_training, bn_decay)
+        if and_pooling:
+            out = out + X.max(dim=2).values
+    else:
+        fused = tf_util.packed_mlp(store, scopes, cin, mlp, bn=bn)
+        X = pu.group_mlp(xyz, points, new_xyz, idx, fused, None, use_xyz=use_xyz)  # (B,M,ns,C)
+        out = sa_attention_tail(X, store, scope, C, and_pooling)
+    if mlp2:
+        post = [f"{scope}/conv_post_{i}" for i in range(len(mlp2))]
+        if training:
+            out = tf_util.mlp_torch(out, tf_util.torch_layers(store, post, C, mlp2, bn=bn),
+                                    is_training, bn_decay)
+        else:
+            out = tf_util.packed_mlp(store, post, C, mlp2, bn=bn)(out)
+    return new_xyz, out, idx
+
+
+def sa_attention_tail(X, store, scope, C, and_pooling=False):
+    """Inference tail of the attention SA layers on the per-point MLP output X (B,M,ns,C):
+    the Dense query (first neighbour, :259), key and value projections on the matrix cores,
+    the reduction kernel, the batch norm (:261) and, for _and_pooling, + max over ns (:303)."""
+    qs, ks, vs = _attention_scopes(scope)
+    K = tf_util.packed_dense(store, ks, C, C)(X)
+    V = tf_util.packed_dense(store, vs, C, C)(X)
+    Q = tf_util.packed_dense(store, qs, C, C)(X[:, :, 0].contiguous())
+    out = attention_reduce(Q, K, V)
+    scale, shift = tf_util.bn_affine(store, f"{scope}/{scope}", C, X.device)
+    out = out * scale + shift
+    if and_pooling:  # pooling='max' only (:296-299)
+        out = out + pointnet_util.group_pool(X, "max").squeeze(2)
+    return out
+
+
+def pointnet_sa_module_attention_and_pooling(xyz, points, npoint, radius, nsample, mlp, mlp2,
+                                             group_all, is_training, bn_decay, scope, bn=True,
+                                             pooling='max', knn=False, use_xyz=True,
+                                             use_nchw=False, params=None):
+    """attention_layer.py:279-338: attention output (after its batch norm) + max pool."""
+    if pooling != 'max':
+        raise ValueError("Pooling must be max for this implementation")
+    return pointnet_sa_module_attention(xyz, points, npoint, radius, nsample, mlp, mlp2,
+                                        group_all, is_training, bn_decay, scope, bn, pooling, knn,
+                                        use_xyz, use_nchw, params, and_pooling=True)

@@ -14,7 +14,8 @@ FPS (+gather), ball query, fused group/centre/concat, the attention reduction (c
 three_nn + IDW + three_interpolate + concat of every FP layer.
 
 With model=True (make_inputs) the step is instead the whole inference forward pass of
-pointnet2_sem_seg.py:19-61 (= pointnet2_sem_seg_features.py with rgb+normals for cfg3): every
+pointnet2_sem_seg.py:19-61 (cfg3: with rgb+normals and the attention SA layers of
+pointnet2_sem_seg_attention.py): every
 SA layer as one fused group + MLP + max-pool kernel fed by the previous layer's real output,
 every FP layer as one fused interpolation + MLP kernel, and the conv1d head (fc1 with batch
 norm, dropout = identity at inference, fc2 to 21 classes) fused into FP4's MLP. Weights are
@@ -60,9 +61,12 @@ class SemSegModel:
     """The packed MLPs of pointnet2_sem_seg(_features) (pointnet2_sem_seg.py:29-60) under the
     reference's variable scopes: layer1..4/conv<j>, fa_layer1..4/conv_<j>, fc1, fc2. FP4's
     MLP carries the head: fa_layer4's three layers, then fc1 (128, batch norm, relu) and fc2
-    (NUM_CLASSES, no batch norm, no activation) as the 4th and 5th layers of ONE kernel."""
+    (NUM_CLASSES, no batch norm, no activation) as the 4th and 5th layers of ONE kernel.
+    attention=True: the SA layers of pointnet2_sem_seg_attention.py:27-42
+    (pointnet_sa_module_attention: attention + batch norm instead of max pooling)."""
 
-    def __init__(self, in_channels, params=None, device="cuda"):
+    def __init__(self, in_channels, params=None, device="cuda", attention=False):
+        self.attention = attention
         self.store = params if params is not None else tf_util.ParamStore(seed=7, device=device)
         st = self.store
         self.sa, c = [], in_channels
@@ -83,6 +87,12 @@ class SemSegModel:
                 layers = layers + head1 + head2
             self.fp.append(tf_util.SharedMLP(layers))
             c2 = widths[-1]
+        if attention:  # pack the Dense / batch-norm variables up front (not inside a capture)
+            for i, widths in enumerate(SSG_SA_MLP):
+                C, sc = widths[-1], f"layer{i + 1}"
+                for d in attention_layer._attention_scopes(sc):
+                    tf_util.packed_dense(st, d, C, C)
+                tf_util.bn_affine(st, f"{sc}/{sc}", C, device)
 
 
 def make_inputs(config, cloud_ids, device, seed=1234, model=False):
@@ -97,7 +107,7 @@ def make_inputs(config, cloud_ids, device, seed=1234, model=False):
     if model:
         if kind != "ssg":
             raise NotImplementedError("model=True: the SSG segmentation model (cfg2 / cfg3)")
-        inp["model"] = SemSegModel(6 if with_feat else 0, device=device)
+        inp["model"] = SemSegModel(6 if with_feat else 0, device=device, attention=attn)
         return inp
     r = lambda shape, slot: _rand_per_cloud(cloud_ids, shape, device, seed, slot)  # noqa: E731
     if kind == "ssg":
@@ -295,8 +305,13 @@ class Step:
                 xyz, new_xyz = v["xyz"][i], v["xyz"][i + 1]
                 idx, _ = tf_grouping.query_ball_point(radius, nsample, xyz, new_xyz,
                                                       grid=v.get("grid1") if i == 0 else None)
-                v["pts"][i + 1] = pointnet_util.group_mlp(xyz, v["pts"][i], new_xyz, idx,
-                                                          mdl.sa[i], "max")
+                if mdl.attention:  # attention + batch norm (attention_layer.py:229-276)
+                    X = pointnet_util.group_mlp(xyz, v["pts"][i], new_xyz, idx, mdl.sa[i], None)
+                    v["pts"][i + 1] = attention_layer.sa_attention_tail(
+                        X, mdl.store, f"layer{i + 1}", SSG_SA_MLP[i][-1])
+                else:
+                    v["pts"][i + 1] = pointnet_util.group_mlp(xyz, v["pts"][i], new_xyz, idx,
+                                                              mdl.sa[i], "max")
             return f
 
         def fp(k):

@@ -65,6 +65,19 @@ class ParamStore(dict):
             p["moving_variance"] = self.get(f"{scope}/bn/moving_variance", (cout,), "ones")
         return p
 
+    def dense(self, scope, cin, cout):
+        """The variables of a tf.layers.Dense(cout) built under `scope` (glorot-uniform kernel,
+        zero bias: the Keras defaults)."""
+        return {"weights": self.get(f"{scope}/kernel", (cin, cout), "xavier"),
+                "biases": self.get(f"{scope}/bias", (cout,), "zeros")}
+
+    def bn(self, scope, c):
+        """The variables of a standalone batch_norm_template(scope) (tf_util.py:512-531)."""
+        return {"gamma": self.get(f"{scope}/gamma", (c,), "ones"),
+                "beta": self.get(f"{scope}/beta", (c,), "zeros"),
+                "moving_mean": self.get(f"{scope}/moving_mean", (c,), "zeros"),
+                "moving_variance": self.get(f"{scope}/moving_variance", (c,), "ones")}
+
     def invalidate(self):
         """Drop packed copies (call after changing parameters in place)."""
         self._packed.clear()
@@ -165,6 +178,30 @@ def packed_mlp(store, scopes, cin, widths, bn=True, relu=True):
     mlp = SharedMLP(layers)
     store._packed[key] = mlp
     return mlp
+
+
+def packed_dense(store, scope, cin, cout):
+    """SharedMLP of one tf.layers.Dense (no activation) over the store's variables, cached."""
+    key = ("dense", scope, cin, cout)
+    hit = store._packed.get(key)
+    if hit is None:
+        p = store.dense(scope, cin, cout)
+        hit = SharedMLP([PackedLayer(p["weights"], p["biases"], relu=False, device=store.device)])
+        store._packed[key] = hit
+    return hit
+
+
+def bn_affine(store, scope, c, device):
+    """Inference batch norm as (scale, shift) device tensors: x * scale + shift."""
+    key = ("bn", scope, c)
+    hit = store._packed.get(key)
+    if hit is None:
+        p = store.bn(scope, c)
+        s64 = p["gamma"].double() / torch.sqrt(p["moving_variance"].double() + BN_EPSILON)
+        shift = p["beta"].double() - p["moving_mean"].double() * s64
+        hit = (s64.float().to(device), shift.float().to(device))
+        store._packed[key] = hit
+    return hit
 
 
 def conv2d(inputs, num_output_channels, kernel_size, scope, stride=[1, 1], padding='SAME',

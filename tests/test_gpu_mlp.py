@@ -240,3 +240,30 @@ def test_group_all_and_mlp2(env):
     y = O.mlp_f64(x, layers).max(axis=1, keepdims=True)
     ref = O.mlp_f64(y, [cv("ga/conv_post_0", 128, 96)])
     np.testing.assert_allclose(got.cpu().numpy(), ref, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("and_pooling", [False, True])
+def test_attention_sa_module_matches_torch_composition(env, and_pooling):
+    """pointnet_sa_module_attention(_and_pooling) (attention_layer.py:229-338): the fused
+    inference path (group + MLP kernel, packed Dense layers, reduction kernel, batch norm)
+    against its differentiable torch composition on the same variables (grad-enabled inputs
+    take that path; is_training=False keeps the moving statistics)."""
+    pkg, O, torch, dev = env
+    al, tu = pkg.attention_layer, pkg.tf_util
+    xyz_np, feats_np = pkg.synth.batch([2, 3], 2048, "scannet", with_features=True)
+    xyz, feats = torch.from_numpy(xyz_np).to(dev), torch.from_numpy(feats_np).to(dev)
+    store = tu.ParamStore(seed=11)
+    g = np.random.default_rng(2)
+    for k in ("moving_mean", "moving_variance", "gamma", "beta"):
+        lo, hi = {"moving_mean": (-.1, .1), "moving_variance": (.5, 2), "gamma": (.5, 1.5),
+                  "beta": (-.2, .2)}[k]
+        store[f"att/att/{k}"] = torch.from_numpy(g.uniform(lo, hi, 64).astype(np.float32))
+    fn = al.pointnet_sa_module_attention_and_pooling if and_pooling else \
+        al.pointnet_sa_module_attention
+    with torch.no_grad():
+        nx, got, idx = fn(xyz, feats, 256, 0.2, 32, [32, 64], None, False, False, None, "att",
+                          params=store)
+    assert got.shape == (2, 256, 64)
+    ref = fn(xyz.clone().requires_grad_(True), feats, 256, 0.2, 32, [32, 64], None, False,
+             False, None, "att", params=store)[1].detach()
+    np.testing.assert_allclose(got.cpu().numpy(), ref.cpu().numpy(), rtol=1e-4, atol=2e-5)

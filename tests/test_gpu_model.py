@@ -44,6 +44,7 @@ def pipeline(O, pkg, xyz, feats, store, dt):
         levels.append(O.gather_point(levels[-1], O.fps(levels[-1], m)))
     pts = [None if feats is None else feats.astype(dt)]
     c = 0 if feats is None else feats.shape[2]
+    attention = store._packed and any(k[0] == "dense" for k in store._packed)
     for i, (m, r, ns, _) in enumerate(S.SSG_SA):
         idx, _ = O.ball_query(levels[i], levels[i + 1], r, ns)
         b = np.arange(xyz.shape[0])[:, None, None]
@@ -51,8 +52,29 @@ def pipeline(O, pkg, xyz, feats, store, dt):
         g = gx if pts[i] is None else np.concatenate([gx, pts[i][b, idx]], axis=-1)
         layers = [conv(f"layer{i + 1}/conv{j}", c + 3 if j == 0 else S.SSG_SA_MLP[i][j - 1], w)
                   for j, w in enumerate(S.SSG_SA_MLP[i])]
-        pts.append(_mlp(g, layers, dt).max(axis=2))
+        X = _mlp(g, layers, dt)
         c = S.SSG_SA_MLP[i][-1]
+        if attention:  # attention_layer.py:29-45 + the batch norm of :261
+            sc = f"layer{i + 1}"
+            dq, dk, dv = [{**{k: v.cpu().numpy() for k, v in store.dense(d, c, c).items()},
+                           "relu": False} for d in pkg.attention_layer._attention_scopes(sc)]
+            Q = _mlp(X[:, :, 0], [dq], dt)
+            K, V = _mlp(X, [dk], dt), _mlp(X, [dv], dt)
+            Bm, Mm, nsm = X.shape[:3]
+            H = c // 4
+            Qh = Q.reshape(Bm, Mm, H, 1, 4)
+            Kh = K.reshape(Bm, Mm, H, nsm, 4)  # the reference's reshape of (ns, C)
+            Vh = V.reshape(Bm, Mm, H, nsm, 4)
+            w = (Qh @ np.swapaxes(Kh, -1, -2)) / dt(2.0)
+            w = np.exp(w - w.max(-1, keepdims=True))
+            w = w / w.sum(-1, keepdims=True)
+            out = (w @ Vh).reshape(Bm, Mm, c)
+            bnp = {k: v.cpu().numpy() for k, v in store.bn(f"{sc}/{sc}", c).items()}
+            s_ = bnp["gamma"].astype(np.float64) / np.sqrt(bnp["moving_variance"].astype(np.float64) + 1e-3)
+            t_ = bnp["beta"].astype(np.float64) - bnp["moving_mean"].astype(np.float64) * s_
+            pts.append((out * s_.astype(dt) + t_.astype(dt)).astype(dt))
+        else:
+            pts.append(X.max(axis=2))
     p2 = pts[4]
     for k, widths in enumerate(S.SSG_FP_MLP):
         lvl = 3 - k
