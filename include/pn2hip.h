@@ -28,6 +28,8 @@
  *   SA pooling           pointnet_util.py:130-145, :200          → pn2_group_pool
  *   pointnet_sa_module   pointnet_util.py:106-145 (group, conv2d  → pn2_group_mlp
  *     MLP, pooling; tf_util.py:120-185 conv2d + batch_norm)
+ *   pointnet_sa_module_attention(_and_pooling)                   → pn2_group_mlp_attention
+ *                        attention_layer.py:229-338
  *   pointnet_fp_module   pointnet_util.py:218-238 (interp + MLP)  → pn2_fp_mlp
  *   conv1d head          tf_util.py:52-117, pointnet2_sem_seg.py  → pn2_shared_mlp
  *                        :57-60 (fc1, fc2)
@@ -267,6 +269,22 @@ int pn2_group_mlp(const float* xyz, const float* points, const float* new_xyz,
                   const int32_t* idx, int B, int N, int C, int M, int nsample, int flags,
                   int nlayers, const pn2_mlp_layer* layers, int pool, float* out,
                   pn2_stream_t stream);
+/* pointnet_sa_module_attention (attention_layer.py:229-276) after sampling and ball query:
+ * group + MLP as pn2_group_mlp, then — without the per-point features leaving the chip — the
+ * AttentionLayer (attention_layer.py:10-45, output_dim = key_dim = 4, heads = C/4):
+ * qkv[0..2] = the packed Dense query / key / value layers (C -> C, no activation;
+ * pn2_mlp_pack with the Dense kernel and bias), query = the group's first neighbour (:259),
+ * head h = the flat block [4*ns*h, 4*ns*(h+1)) of the group's (ns, C) keys and values (the
+ * tf.reshape of :35-36), softmax((K_h q_h)/2) V_h; then the inference batch norm
+ * out = att * bn_scale + bn_shift (:261; NULL = none) and, with add_max, + the max over nsample
+ * of the MLP output (pointnet_sa_module_attention_and_pooling, :296-303). out (B,M,C).
+ * nsample <= 128; C = layers[nlayers-1].cout, a multiple of 32. */
+int pn2_group_mlp_attention(const float* xyz, const float* points, const float* new_xyz,
+                            const int32_t* idx, int B, int N, int C, int M, int nsample,
+                            int flags, int nlayers, const pn2_mlp_layer* layers,
+                            const pn2_mlp_layer* qkv, const float* bn_scale,
+                            const float* bn_shift, int add_max, float* out,
+                            pn2_stream_t stream);
 /* pointnet_fp_module (pointnet_util.py:218-238): IDW weights of dist (B,n,3) + interpolation
  * of points2 (B,m,C2) at nn_idx (B,n,3) + concat [interp, points1 (B,n,C1)] (bit-identical to
  * pn2_fp_apply's output) fed to the packed layers → out (B,n,cout). points1 may be NULL

@@ -79,6 +79,8 @@ SIGNATURES = {
     "pn2_mlp_packed_size": (_S, [_I, _I]),
     "pn2_mlp_pack": (_I, [_P, _P, _P, _P, _I, _I, _P, _S, _P]),
     "pn2_group_mlp": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _I, _P, _P]),
+    "pn2_group_mlp_attention": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P,
+                                     _I, _P, _P]),
     "pn2_fp_mlp": (_I, [_P, _P, _P, _I, _P, _I, _I, _I, _I, _I, _P, _P, _P]),
     "pn2_shared_mlp": (_I, [_P, _LL, _I, _I, _P, _P, _P]),
 }

@@ -141,8 +141,8 @@ def pointnet_sa_module_attention(xyz, points, npoint, radius, nsample, mlp, mlp2
             out = out + X.max(dim=2).values
     else:
         fused = tf_util.packed_mlp(store, scopes, cin, mlp, bn=bn)
-        X = pu.group_mlp(xyz, points, new_xyz, idx, fused, None, use_xyz=use_xyz)  # (B,M,ns,C)
-        out = sa_attention_tail(X, store, scope, C, and_pooling)
+        out = group_mlp_attention(xyz, points, new_xyz, idx, fused, store, scope, and_pooling,
+                                  use_xyz=use_xyz)
     if mlp2:
         post = [f"{scope}/conv_post_{i}" for i in range(len(mlp2))]
         if training:
@@ -151,6 +151,37 @@ def pointnet_sa_module_attention(xyz, points, npoint, radius, nsample, mlp, mlp2
         else:
             out = tf_util.packed_mlp(store, post, C, mlp2, bn=bn)(out)
     return new_xyz, out, idx
+
+
+def group_mlp_attention(xyz, points, new_xyz, idx, mlp, store, scope, and_pooling=False,
+                        use_xyz=True):
+    """The whole inference SA-attention layer after sampling and ball query in ONE kernel
+    (pn2_group_mlp_attention): group + MLP `mlp`, Dense q/k/v, the reduction per head, the
+    batch norm '<scope>/<scope>' and (and_pooling) + max pool; the per-point features never
+    leave the chip. -> (B, M, C)."""
+    pu = pointnet_util
+    xyz = device_tensor(xyz, "xyz", torch.float32)
+    new_xyz = device_tensor(new_xyz, "new_xyz", torch.float32)
+    idx = device_tensor(idx, "idx", torch.int32)
+    B, N = int(xyz.shape[0]), int(xyz.shape[1])
+    M, ns = int(idx.shape[1]), int(idx.shape[2])
+    if pu._is_empty_points(points):
+        points, Cin = None, 0
+    else:
+        points = device_tensor(points, "points", torch.float32)
+        Cin = int(points.shape[2])
+    C = mlp.cout
+    qkv = [tf_util.packed_dense(store, d, C, C) for d in _attention_scopes(scope)]
+    table = (type(mlp.table()[0][0]) * 3)(*[d.layers[0].struct() for d in qkv])
+    scale, shift = tf_util.bn_affine(store, f"{scope}/{scope}", C, xyz.device)
+    out = torch.empty((B, M, C), dtype=torch.float32, device=xyz.device)
+    flags = pu.PN2_USE_XYZ if use_xyz else 0
+    tab, n = mlp.table()
+    check(lib().pn2_group_mlp_attention(ptr(xyz), ptr(points), ptr(new_xyz), ptr(idx), B, N, Cin,
+                                        M, ns, flags, n, tab, table, ptr(scale), ptr(shift),
+                                        1 if and_pooling else 0, ptr(out), stream_of(xyz)),
+          "group_mlp_attention")
+    return out
 
 
 def sa_attention_tail(X, store, scope, C, and_pooling=False):

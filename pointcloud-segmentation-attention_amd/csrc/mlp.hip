@@ -78,6 +78,14 @@ struct Params {
   int pool;
   float* out;
   unsigned long long* stamp;  // PN2_MLP_STAMP builds: per-workgroup phase timestamps
+  // attention tail (pn2_group_mlp_attention): the MLP's last layer stays in LDS (X), then the
+  // Dense query (first neighbour of each group) / key / value layers, the reduction per head
+  // and the batch norm (+ max pool of X), column segment by column segment of K and V
+  int attn, att_wseg, att_nseg, att_add_max;
+  LayerDev qkv[3];
+  const float* att_scale;
+  const float* att_shift;
+  int off_k, off_v, off_q, stride_kv, stride_q;
 };
 
 #ifdef PN2_MLP_STAMP
@@ -332,6 +340,149 @@ PN2_DEV void store_pooled(const Params& prm, int g, int fo, int cout, float mx, 
   else {  // max_and_avg: concat [avg, max] (pointnet_util.py:145)
     prm.out[(size_t)g * 2 * cout + fo] = avg;
     prm.out[(size_t)g * 2 * cout + cout + fo] = mx;
+  }
+}
+
+// One Dense layer item (no activation) of the attention tail: output tile `to` of layer D
+// over row tile rt of X, written (scale/shift epilogue = bias) into dst at column
+// (to - to0)*32, rows 32*rt + col. For the query, row_of_lane maps lane col to X row
+// col*ns_pad (the first neighbour of group col) and only rows < nrows are written.
+PN2_DEV void dense_item(const LayerDev& D, const float* X, int Sx, int xrow, int to, int to0,
+                        float* dst, int Sd, int drow, bool write, int lane, int h) {
+  float4 sc[4], sh[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int fb = 32 * to + 8 * q + 4 * h;
+    sc[q] = *reinterpret_cast<const float4*>(D.scale + fb);
+    sh[q] = *reinterpret_cast<const float4*>(D.shift + fb);
+  }
+  f32x16 acc[1];
+  mma_item<false, 1>(D.w + (size_t)to * D.cin8 * kWave + lane, X + xrow * Sx + 4 * h, 0, D.cin8,
+                     acc);
+  if (!write) return;
+  float* op = dst + drow * Sd + 32 * (to - to0) + 4 * h;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    float4 y;
+    y.x = acc[0][4 * q + 0] * sc[q].x + sh[q].x;
+    y.y = acc[0][4 * q + 1] * sc[q].y + sh[q].y;
+    y.z = acc[0][4 * q + 2] * sc[q].z + sh[q].z;
+    y.w = acc[0][4 * q + 3] * sc[q].w + sh[q].w;
+    *reinterpret_cast<float4*>(op + 8 * q) = y;
+  }
+}
+
+// (1x4)·(4x1) of tf.matmul, summed left to right (as attn.hip)
+PN2_DEV float dot4q(float4 q, float4 k) {
+  float s = q.x * k.x;
+  s = s + q.y * k.y;
+  s = s + q.z * k.z;
+  s = s + q.w * k.w;
+  return s;
+}
+
+// AttentionLayer.call (attention_layer.py:29-45) + batch_norm_for_conv2d (:261) [+ the max pool
+// of :296-303] on the workgroup's groups, from the MLP output X (P rows x C) in LDS.
+// Head h of a group reads the flat block [4*ns*h, 4*ns*(h+1)) of the group's row-major (ns, C)
+// K and V (the tf.reshape quirk of :35-36): with C <= 4*ns that block spans whole rows (K and V
+// are computed whole, one segment); with C = k*4*ns it is the column block h % k of row h / k,
+// so K and V are computed k column segments at a time and each segment completes its heads.
+template <int R>
+PN2_DEV void attention_tail(const Params& prm, float* smem, const float* X, int Sx) {
+  const int tid = threadIdx.x, lane = lane_id(), wave = tid / kWave;
+  const int col = lane & 31, h = lane >> 5;
+  const int C = prm.L[prm.nl - 1].cout;
+  const int C32 = C / 32;
+  const int ns = prm.ns, ns_pad = 1 << prm.lg_ns_pad;
+  const int G = prm.gpw;
+  float* Kb = smem + prm.off_k;
+  float* Vb = smem + prm.off_v;
+  float* Qb = smem + prm.off_q;
+  const int Skv = prm.stride_kv, Sq = prm.stride_q;
+  // query of every group: Dense_q(X[first neighbour]) (:259, :31)
+  for (int to = wave; to < C32; to += kWaves)
+    dense_item(prm.qkv[0], X, Sx, col < G ? col * ns_pad : 0, to, 0, Qb, Sq, col, col < G,
+               lane, h);
+  const int wseg = prm.att_wseg, t_seg = wseg / 32;
+  const bool whole = wseg == C;
+  const int hs_per_group = whole ? C / 4 : ns;  // heads completed by one segment
+  for (int sgi = 0; sgi < prm.att_nseg; ++sgi) {
+    // K and V of this column segment (:32-33)
+    const int nitems = 2 * R * t_seg;
+    for (int item = wave; item < nitems; item += kWaves) {
+      const int which = item / (R * t_seg);
+      const int rem = item - which * (R * t_seg);
+      const int to = sgi * t_seg + rem / R, rt = rem % R;
+      dense_item(prm.qkv[1 + which], X, Sx, 32 * rt + col, to, sgi * t_seg, which ? Vb : Kb, Skv,
+                 32 * rt + col, true, lane, h);
+    }
+    __syncthreads();
+    // one half-wave per (group, head): scores, softmax over the ns pseudo-keys, weighted V
+    const int units = G * hs_per_group;
+    for (int u = wave * 2 + h; u < units; u += 2 * kWaves) {
+      const int gi = u / hs_per_group, hs = u - gi * hs_per_group;
+      const int g = blockIdx.x * G + gi;
+      const int hg = whole ? hs : (C / wseg) * hs + sgi;  // the head's index in [0, C/4)
+      const float4 q = *reinterpret_cast<const float4*>(Qb + gi * Sq + 4 * hg);
+      const int r0 = gi * ns_pad;
+      auto key_at = [&](int j, const float* B) {
+        int row, c;
+        if (whole) {
+          const int f = 4 * ns * hs + 4 * j;  // flat index in the group's (ns, C) matrix
+          row = f / C;
+          c = f - row * C;
+        } else {
+          row = hs;
+          c = 4 * j;
+        }
+        return *reinterpret_cast<const float4*>(B + (r0 + row) * Skv + c);
+      };
+      float mx = -__builtin_inff();
+      for (int j = col; j < ns; j += 32) mx = fmaxf(mx, dot4q(q, key_at(j, Kb)) / 2.0f);
+      mx = seg_max<32>(mx);  // softmax (:39)
+      float sum = 0.f;
+      float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int j = col; j < ns; j += 32) {
+        const float e = expf(dot4q(q, key_at(j, Kb)) / 2.0f - mx);
+        sum = sum + e;
+        const float4 v = key_at(j, Vb);
+        o.x = o.x + e * v.x;
+        o.y = o.y + e * v.y;
+        o.z = o.z + e * v.z;
+        o.w = o.w + e * v.w;
+      }
+      sum = seg_sum<32>(sum);
+      o.x = seg_sum<32>(o.x) / sum;  // aᵀ·V_h (:40), a = e / sum
+      o.y = seg_sum<32>(o.y) / sum;
+      o.z = seg_sum<32>(o.z) / sum;
+      o.w = seg_sum<32>(o.w) / sum;
+      float4 pm = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (prm.att_add_max) {  // + reduce_max over ns of X (:296-303)
+        float4 m4 = make_float4(-__builtin_inff(), -__builtin_inff(), -__builtin_inff(),
+                                -__builtin_inff());
+        for (int j = col; j < ns; j += 32) {
+          const float4 x = *reinterpret_cast<const float4*>(X + (r0 + j) * Sx + 4 * hg);
+          m4.x = fmaxf(m4.x, x.x);
+          m4.y = fmaxf(m4.y, x.y);
+          m4.z = fmaxf(m4.z, x.z);
+          m4.w = fmaxf(m4.w, x.w);
+        }
+        pm = make_float4(seg_max<32>(m4.x), seg_max<32>(m4.y), seg_max<32>(m4.z),
+                         seg_max<32>(m4.w));
+      }
+      if (col == 0 && g < prm.ngroups) {
+        float4 y = o;
+        if (prm.att_scale) {  // batch_norm_for_conv2d, inference (:261)
+          const float4 s4 = *reinterpret_cast<const float4*>(prm.att_scale + 4 * hg);
+          const float4 t4 = *reinterpret_cast<const float4*>(prm.att_shift + 4 * hg);
+          y = make_float4(y.x * s4.x + t4.x, y.y * s4.y + t4.y, y.z * s4.z + t4.z,
+                          y.w * s4.w + t4.w);
+        }
+        if (prm.att_add_max) y = make_float4(y.x + pm.x, y.y + pm.y, y.z + pm.z, y.w + pm.w);
+        *reinterpret_cast<float4*>(prm.out + (size_t)g * C + 4 * hg) = y;
+      }
+    }
+    __syncthreads();  // the next segment overwrites K and V
   }
 }
 
@@ -642,7 +793,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     // the 4 waves split the row tiles so every wave works (nsplit row groups).
     for (int l = 0; l < prm.nl; ++l) {
       const LayerDev& Ld = prm.L[l];
-      const bool last = l == prm.nl - 1;
+      const bool last = l == prm.nl - 1 && !prm.attn;
       const int c32 = Ld.cout32;
       const int nsplit = item_split(R, c32);
       const int rg_tiles = R / nsplit;
@@ -655,6 +806,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2, 2))) 
       }
       __syncthreads();
       PN2_STAMP(3 + l);
+    }
+
+    if constexpr (SRC == kSrcGroup) {
+      if (prm.attn) attention_tail<R>(prm, smem, (prm.nl & 1) ? act1 : act0,
+                                      (prm.nl & 1) ? prm.stride1 : prm.stride0);
     }
 
     // ---- 4. pooling: combine the row-tile partials of each group, store -----------------
@@ -757,7 +913,7 @@ size_t plan(Params& prm, int nl, const pn2_mlp_layer* layers, int cin0, int R, b
     prm.L[l].relu = (L.flags & PN2_MLP_RELU) ? 1 : 0;
     prm.L[l].lofs = wfloats;
     wfloats += cout32 * cin8 * 256 + cout32 * 64;
-    if (l < nl - 1) {  // layer l writes buffer (l+1)&1
+    if (l < nl - 1 || prm.attn) {  // layer l writes buffer (l+1)&1
       if ((l + 1) & 1) w1 = w1 > cout32 * 32 ? w1 : cout32 * 32;
       else w0 = w0 > cout32 * 32 ? w0 : cout32 * 32;
     }
@@ -779,6 +935,16 @@ size_t plan(Params& prm, int nl, const pn2_mlp_layer* layers, int cin0, int R, b
   prm.off_meta = (int)off;
   off += (size_t)P * 9 + kMaxGroupsPerWG;
   off = (off + 3) & ~(size_t)3;
+  if (prm.attn) {  // K and V column segments (P rows), queries (one row per group)
+    prm.stride_kv = prm.att_wseg + 4;
+    prm.stride_q = coutp + 4;
+    prm.off_k = (int)off;
+    off += (size_t)P * prm.stride_kv;
+    prm.off_v = (int)off;
+    off += (size_t)P * prm.stride_kv;
+    prm.off_q = (int)off;
+    off += (size_t)(P >> prm.lg_ns_pad > 0 ? P >> prm.lg_ns_pad : 1) * prm.stride_q;
+  }
   prm.off_w = (int)off;
   prm.wfloats = wl ? wfloats : 0;
   off += prm.wfloats;
@@ -910,10 +1076,11 @@ int pn2_mlp_pack(const float* weight, const float* bias, const float* bn_scale,
   PN2_RETURN_LAUNCH();
 }
 
-int pn2_group_mlp(const float* xyz, const float* points, const float* new_xyz,
-                  const int32_t* idx, int B, int N, int C, int M, int nsample, int flags,
-                  int nlayers, const pn2_mlp_layer* layers, int pool, float* out,
-                  pn2_stream_t stream) {
+static int group_mlp_impl(const float* xyz, const float* points, const float* new_xyz,
+                          const int32_t* idx, int B, int N, int C, int M, int nsample, int flags,
+                          int nlayers, const pn2_mlp_layer* layers, int pool,
+                          const pn2_mlp_layer* qkv, const float* bn_scale, const float* bn_shift,
+                          int add_max, float* out, hipStream_t stream) {
   using namespace pn2;
   if (B < 0 || N < 0 || C < 0 || M < 0 || nsample <= 0) return PN2_EINVAL;
   if (pool < PN2_POOL_NONE || pool > PN2_POOL_MAX_AND_AVG) return PN2_EINVAL;
@@ -923,20 +1090,56 @@ int pn2_group_mlp(const float* xyz, const float* points, const float* new_xyz,
   else { layout = (flags & PN2_XYZ_LAST) ? kXyzLast : kXyzFirst; cin0 = C + 3; }
   int rc = check_layers(nlayers, layers, cin0);
   if (rc) return rc;
+  const int ns_pad = nsample < 8 ? 8 : next_pow2(nsample);
+  Params prm = {};
+  prm.lg_ns_pad = ilog2(ns_pad);
+  int min_R = 1;
+  if (qkv) {
+    const int Ca = layers[nlayers - 1].cout;
+    if (Ca % 32 || (!bn_scale) != (!bn_shift)) return PN2_EINVAL;
+    for (int i = 0; i < 3; ++i) {
+      if (!qkv[i].packed || qkv[i].cin != Ca || qkv[i].cout != Ca || (qkv[i].flags & PN2_MLP_RELU))
+        return PN2_EINVAL;
+      if ((reinterpret_cast<uintptr_t>(qkv[i].packed) & 15) != 0) return PN2_EINVAL;
+    }
+    if (ns_pad > 128) return PN2_EINVAL;  // one pass: the group's rows all in one workgroup
+    prm.attn = 1;
+    // column segments of K and V: whole rows when a head spans rows (C <= 4 ns), else blocks
+    // of 4 ns columns (each completes the heads of its column block)
+    prm.att_wseg = (Ca <= 4 * nsample || Ca % (4 * nsample) || (4 * nsample) % 32) ? Ca
+                                                                                    : 4 * nsample;
+    prm.att_nseg = Ca / prm.att_wseg;
+    prm.att_add_max = add_max ? 1 : 0;
+    prm.att_scale = bn_scale;
+    prm.att_shift = bn_shift;
+    pool = PN2_POOL_NONE;
+    min_R = ns_pad > 32 ? ns_pad / 32 : 1;
+  }
   const long long ngroups = (long long)B * M;
   if (ngroups == 0) return PN2_OK;
   if (!xyz || !new_xyz || !idx || !out || ngroups > 0x7fffffffLL) return PN2_EINVAL;
   if ((long long)B * N > 0x7fffffffLL || ngroups * nsample > 0x7fffffffLL) return PN2_EINVAL;
-  const int ns_pad = nsample < 8 ? 8 : next_pow2(nsample);
   const bool pooled = pool >= 0;
-  Params prm = {};
   size_t lds = 0;
   // a single-pass workgroup holds whole groups: P = 32R must be a multiple of ns_pad, or
   // the group is processed in ns_pad / P passes of one workgroup
   const long long tiles32 = (ngroups * ns_pad + 31) / 32;
-  const int R = choose_R(prm, nlayers, layers, cin0, pooled, tiles32, 1, &lds);
+  const int R = choose_R(prm, nlayers, layers, cin0, pooled, tiles32, min_R, &lds);
   if (!R) return PN2_EINVAL;
   const int P = 32 * R;
+  if (qkv) {
+    for (int i = 0; i < 3; ++i) {
+      const int cin8 = (qkv[i].cin + 7) / 8, cout32 = qkv[i].cout / 32;
+      const float* base = static_cast<const float*>(qkv[i].packed);
+      prm.qkv[i].w = reinterpret_cast<const float4*>(base);
+      prm.qkv[i].scale = base + (size_t)cout32 * cin8 * 256;
+      prm.qkv[i].shift = prm.qkv[i].scale + cout32 * 32;
+      prm.qkv[i].cin8 = cin8;
+      prm.qkv[i].cout32 = cout32;
+      prm.qkv[i].cout = qkv[i].cout;
+      prm.qkv[i].relu = 0;
+    }
+  }
   prm.xyz = xyz;
   prm.points = points;
   prm.new_xyz = new_xyz;
@@ -945,7 +1148,6 @@ int pn2_group_mlp(const float* xyz, const float* points, const float* new_xyz,
   prm.C = C;
   prm.M = M;
   prm.ns = nsample;
-  prm.lg_ns_pad = ilog2(ns_pad);
   prm.layout = layout;
   if (layout == kXyzOnly) set_segments(prm, 0, false, 0, 3, false, 0, 3);
   else if (layout == kPointsOnly) set_segments(prm, C, C % 4 == 0, 0, 0, false, 0, C);
@@ -975,7 +1177,27 @@ int pn2_group_mlp(const float* xyz, const float* points, const float* new_xyz,
       lds = lds_wl;
     }
   }
-  return launch_rows_R<kSrcGroup>(prm, R, nblocks, lds, (hipStream_t)stream);
+  return launch_rows_R<kSrcGroup>(prm, R, nblocks, lds, stream);
+}
+
+int pn2_group_mlp(const float* xyz, const float* points, const float* new_xyz,
+                  const int32_t* idx, int B, int N, int C, int M, int nsample, int flags,
+                  int nlayers, const pn2_mlp_layer* layers, int pool, float* out,
+                  pn2_stream_t stream) {
+  return group_mlp_impl(xyz, points, new_xyz, idx, B, N, C, M, nsample, flags, nlayers, layers,
+                        pool, nullptr, nullptr, nullptr, 0, out, (hipStream_t)stream);
+}
+
+int pn2_group_mlp_attention(const float* xyz, const float* points, const float* new_xyz,
+                            const int32_t* idx, int B, int N, int C, int M, int nsample,
+                            int flags, int nlayers, const pn2_mlp_layer* layers,
+                            const pn2_mlp_layer* qkv, const float* bn_scale,
+                            const float* bn_shift, int add_max, float* out,
+                            pn2_stream_t stream) {
+  if (!qkv) return PN2_EINVAL;
+  return group_mlp_impl(xyz, points, new_xyz, idx, B, N, C, M, nsample, flags, nlayers, layers,
+                        PN2_POOL_NONE, qkv, bn_scale, bn_shift, add_max, out,
+                        (hipStream_t)stream);
 }
 
 int pn2_fp_mlp(const float* dist, const int32_t* nn_idx, const float* points1, int C1,

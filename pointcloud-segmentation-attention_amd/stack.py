@@ -306,9 +306,8 @@ class Step:
                 idx, _ = tf_grouping.query_ball_point(radius, nsample, xyz, new_xyz,
                                                       grid=v.get("grid1") if i == 0 else None)
                 if mdl.attention:  # attention + batch norm (attention_layer.py:229-276)
-                    X = pointnet_util.group_mlp(xyz, v["pts"][i], new_xyz, idx, mdl.sa[i], None)
-                    v["pts"][i + 1] = attention_layer.sa_attention_tail(
-                        X, mdl.store, f"layer{i + 1}", SSG_SA_MLP[i][-1])
+                    v["pts"][i + 1] = attention_layer.group_mlp_attention(
+                        xyz, v["pts"][i], new_xyz, idx, mdl.sa[i], mdl.store, f"layer{i + 1}")
                 else:
                     v["pts"][i + 1] = pointnet_util.group_mlp(xyz, v["pts"][i], new_xyz, idx,
                                                               mdl.sa[i], "max")

@@ -267,3 +267,39 @@ def test_attention_sa_module_matches_torch_composition(env, and_pooling):
     ref = fn(xyz.clone().requires_grad_(True), feats, 256, 0.2, 32, [32, 64], None, False,
              False, None, "att", params=store)[1].detach()
     np.testing.assert_allclose(got.cpu().numpy(), ref.cpu().numpy(), rtol=1e-4, atol=2e-5)
+
+
+@pytest.mark.parametrize("widths,ns,add_max", [
+    ([32, 64], 32, False),     # C = 64 < 4 ns: heads span whole rows (one segment)
+    ([64, 128], 32, True),     # C = 4 ns
+    ([128, 256], 32, False),   # C = 8 ns: 2 column segments
+    ([256, 512], 32, True),    # SA4 widths: 4 column segments
+    ([32, 64], 16, False),     # 2 groups per row tile
+    ([64, 128], 64, True),     # a group spans 2 row tiles
+])
+def test_fused_attention_matches_unfused(env, widths, ns, add_max):
+    """pn2_group_mlp_attention (one kernel: group + MLP + Dense q/k/v + heads + batch norm
+    [+ max pool]) against the same layer run unfused (per-point group_mlp output, packed Dense
+    layers, attention_reduce kernel, batch norm, group_pool), rtol 1e-4 / atol 2e-5."""
+    pkg, O, torch, dev = env
+    al, tu, pu = pkg.attention_layer, pkg.tf_util, pkg.pointnet_util
+    xyz_np, _ = pkg.synth.batch([5, 6], 2048, "scannet")
+    pts_np = np.random.default_rng(ns).uniform(-1, 1, (2, 2048, 16)).astype(np.float32)
+    xyz, pts = torch.from_numpy(xyz_np).to(dev), torch.from_numpy(pts_np).to(dev)
+    store = tu.ParamStore(seed=ns + widths[-1])
+    C = widths[-1]
+    g = np.random.default_rng(C)
+    for k, (lo, hi) in {"moving_mean": (-.1, .1), "moving_variance": (.5, 2), "gamma": (.5, 1.5),
+                        "beta": (-.2, .2)}.items():
+        store[f"s/s/{k}"] = torch.from_numpy(g.uniform(lo, hi, C).astype(np.float32))
+    for d in al._attention_scopes("s"):  # non-zero Dense biases
+        store[f"{d}/bias"] = torch.from_numpy(g.uniform(-.1, .1, C).astype(np.float32))
+    with torch.no_grad():
+        new_xyz = pkg.tf_sampling.farthest_point_sample_and_gather(128, xyz)[1]
+        idx, _ = pkg.tf_grouping.query_ball_point(0.2, ns, xyz, new_xyz)
+        mlp = tu.packed_mlp(store, [f"s/conv{i}" for i in range(len(widths))], 19, widths)
+        got = al.group_mlp_attention(xyz, pts, new_xyz, idx, mlp, store, "s", add_max)
+        X = pu.group_mlp(xyz, pts, new_xyz, idx, mlp, None)
+        ref = al.sa_attention_tail(X, store, "s", C, add_max)
+    assert got.shape == (2, 128, C)
+    np.testing.assert_allclose(got.cpu().numpy(), ref.cpu().numpy(), rtol=1e-4, atol=2e-5)

@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--batch", type=int, default=16)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--lib", default=None)
+    ap.add_argument("--config", default="cfg2", choices=["cfg2", "cfg3"])
     args = ap.parse_args()
     if args.lib:
         os.environ["PN2HIP_LIB"] = args.lib
@@ -32,7 +33,7 @@ def main():
     S, pu = pkg.stack, pkg.pointnet_util
     dev = torch.device("cuda:0")
     B = args.batch
-    inp = S.make_inputs("cfg2", list(range(B)), dev, model=True)
+    inp = S.make_inputs(args.config, list(range(B)), dev, model=True)
     mdl = inp["model"]
     xyz = [inp["xyz"]]
     for (m, _, _, _) in S.SSG_SA:
@@ -62,19 +63,24 @@ def main():
         return e0.elapsed_time(e1) / args.iters * 1e3  # us
 
     rows_out = []
-    pts = [None] + [feats(m, c) for (m, _, _, c) in S.SSG_SA]
-    for i, (m, r, ns, _) in enumerate(S.SSG_SA):
+    pts = [inp["feats"]] + [feats(m, c) for (m, _, _, c) in S.SSG_SA]
+    for i, (m, r, ns, c) in enumerate(S.SSG_SA):
         idx, _ = pkg.tf_grouping.query_ball_point(r, ns, xyz[i], xyz[i + 1])
         mlp = mdl.sa[i]
-        us = timeit(lambda: pu.group_mlp(xyz[i], pts[i], xyz[i + 1], idx, mlp, "max"))
-        rows_out.append((f"SA{i + 1}", us, flops(mlp, B * m * ns)))
-    levels_c = [0] + [c for (_, _, _, c) in S.SSG_SA]
+        if mdl.attention:
+            us = timeit(lambda: pkg.attention_layer.group_mlp_attention(
+                xyz[i], pts[i], xyz[i + 1], idx, mlp, mdl.store, f"layer{i + 1}"))
+            fl = flops(mlp, B * m * ns) + 2 * 2 * B * m * ns * c * c + 2 * B * m * 32 * c * c
+        else:
+            us = timeit(lambda: pu.group_mlp(xyz[i], pts[i], xyz[i + 1], idx, mlp, "max"))
+            fl = flops(mlp, B * m * ns)
+        rows_out.append((f"SA{i + 1}", us, fl))
     p2 = pts[4]
     for k in range(4):
         lvl = 3 - k
         dist, nidx = pkg.tf_interpolate.three_nn(xyz[lvl], xyz[lvl + 1])
         mlp = mdl.fp[k]
-        p1 = pts[lvl]
+        p1 = pts[lvl] if lvl > 0 else inp["feats"]
         us = timeit(lambda: pu.fp_mlp(dist, nidx, p1, p2, mlp))
         rows_out.append((f"FP{k + 1}", us, flops(mlp, B * int(xyz[lvl].shape[1]))))
         p2 = feats(int(xyz[lvl].shape[1]), mlp.cout if k < 3 else 128)
