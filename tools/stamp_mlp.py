@@ -4,8 +4,7 @@ stamped build csrc/build/libpn2hip_stamp.so, `make -C .../csrc stamp`).
 
 For the whole-model layer shapes (SA1..SA4 group + MLP + pool, FP1..FP4 interpolation + MLP)
 prints, averaged over the first 4096 workgroups: metadata, gather, each layer, pooling (in
-s_memtime ticks and as a share of the workgroup's life), the number of workgroups alive at
-once, and the kernel's span."""
+s_memtime ticks and as a share of the workgroup's life)."""
 import ctypes
 import importlib
 import json
@@ -69,16 +68,12 @@ def run(name, fn, nl):
     if len(sub):  # the last layer's first item of wave 0 (stamped builds): MMA, epilogue
         ph["last_item_mma"] = sub[:, 11] - sub[:, 10]
         ph["last_item_epi"] = sub[:, 12] - sub[:, 11]
-    span = t[:, 15].max() - t[:, 0].min()
-    # workgroups alive at a time (sampled at 200 points of the span)
-    ts = np.linspace(t[:, 0].min(), t[:, 15].max(), 200)
-    alive = [int(((t[:, 0] <= x) & (t[:, 15] > x)).sum()) for x in ts]
+    # (s_memtime counters of different XCDs are not synchronised: only durations within one
+    # workgroup are compared)
     print(json.dumps({"layer": name, "event_us": round(us, 1), "wgs_stamped": int(len(t)),
-                      "ticks_per_us": round(span / us, 1) if us else None,
                       "mean_life_ticks": int(life.mean()),
                       "phase_share": {k: round(float(v.mean() / life.mean()), 3) for k, v in ph.items()},
-                      "phase_ticks": {k: int(v.mean()) for k, v in ph.items()},
-                      "alive_median": int(np.median(alive)), "alive_max": int(max(alive))}),
+                      "phase_ticks": {k: int(v.mean()) for k, v in ph.items()}}),
           flush=True)
 
 
