@@ -30,10 +30,16 @@ class ParamStore(dict):
     """TF variable name -> float32 tensor, with the reference's initialisers for misses."""
 
     def __init__(self, *args, seed=0, device="cuda", **kw):
-        super().__init__(*args, **kw)
+        super().__init__()
         self.seed = seed
         self.device = device
         self._packed = {}
+        for k, v in dict(*args, **kw).items():
+            self[k] = v
+
+    def __setitem__(self, name, value):
+        # checkpoint arrays (numpy or torch) are kept as float32 CPU tensors
+        super().__setitem__(name, torch.as_tensor(value, dtype=torch.float32).detach().cpu())
 
     def _init(self, name, shape, kind):
         if kind == "xavier":  # tf.contrib.layers.xavier_initializer(): glorot uniform

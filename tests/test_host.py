@@ -91,3 +91,23 @@ def test_oracle_step_shapes(pn2, orc):
     assert shapes == [(1, 1024, 32, 3), (1, 256, 32, 67), (1, 64, 32, 131), (1, 16, 32, 259),
                       (1, 64, 768), (1, 256, 384), (1, 1024, 320), (1, 8192, 128)]
     assert all(np.isfinite(o).all() for o in outs)
+
+
+def test_param_store_names_and_initialisers(pn2):
+    """tf_util.ParamStore: the reference's TF variable names, its initialisers for misses
+    (xavier weights, zero biases, BN gamma 1 / beta 0 / mean 0 / variance 1), checkpoint
+    arrays accepted as numpy and reshaped from the TF [1,1,cin,cout] kernel layout."""
+    import numpy as np
+    st = pn2.tf_util.ParamStore({"l/conv0/weights": np.ones((1, 1, 3, 8), np.float32)}, seed=1)
+    p = st.conv("l/conv0", 3, 8)
+    assert tuple(p["weights"].shape) == (3, 8) and float(p["weights"].sum()) == 24.0
+    q = st.conv("l/conv1", 8, 16)
+    assert set(st) >= {"l/conv1/weights", "l/conv1/biases", "l/conv1/bn/gamma",
+                       "l/conv1/bn/beta", "l/conv1/bn/moving_mean", "l/conv1/bn/moving_variance"}
+    lim = np.sqrt(6.0 / (8 + 16))
+    w = q["weights"].numpy()
+    assert np.abs(w).max() <= lim and w.std() > 0
+    assert float(q["biases"].abs().sum()) == 0 and float(q["gamma"].sum()) == 16
+    assert np.array_equal(st.conv("l/conv1", 8, 16)["weights"].numpy(), w)  # cached
+    d = st.dense("s/ScannetAttentionLayer/dense", 4, 4)
+    assert tuple(d["weights"].shape) == (4, 4)
