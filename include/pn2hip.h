@@ -33,6 +33,10 @@
  *   pointnet_fp_module   pointnet_util.py:218-238 (interp + MLP)  → pn2_fp_mlp
  *   conv1d head          tf_util.py:52-117, pointnet2_sem_seg.py  → pn2_shared_mlp
  *                        :57-60 (fc1, fc2)
+ *   get_subset           scannet_dataset/data_transformation.py  → pn2_scene_bbox,
+ *                        :70-154 (training crop sampler)           pn2_crop_sample
+ *   whole-scene chunker  scannet_dataset/complete_scene_loader.py → pn2_subvolume_select,
+ *                        :4-117 (subvolume selection, gathers)     pn2_gather_rows
  *
  * (reference paths are under pointnet2_tensorflow/tf_ops/{sampling,grouping,interpolation_3d},
  *  pointnet2_tensorflow/utils and attention_points/attention_scannet.)
@@ -296,6 +300,46 @@ int pn2_fp_mlp(const float* dist, const int32_t* nn_idx, const float* points1, i
  * e.g. the fc1/fc2 head of pointnet2_sem_seg.py:57-60). */
 int pn2_shared_mlp(const float* x, long long rows, int cin, int nlayers,
                    const pn2_mlp_layer* layers, float* out, pn2_stream_t stream);
+
+/* ---------------------------------------------------------------- scene crops ---------- */
+
+/* Scene bounding box: bbox = [min x, min y, min z, max x, max y, max z] of points (N,3)
+ * (reduce_min / reduce_max, data_transformation.py:90-91). workspace:
+ * pn2_scene_workspace_size(N) bytes of device memory. */
+size_t pn2_scene_workspace_size(int N);
+int pn2_scene_bbox(const float* points, int N, float* bbox, void* workspace,
+                   size_t workspace_bytes, pn2_stream_t stream);
+/* get_subset (data_transformation.py:70-154) for B crops of one scene, with the reference's
+ * random draws supplied by the caller: centres (B,T) = the point index each try is centred on
+ * (:95-97, T = 10 in the reference), u (B,K) = the uniform [0,1) draws of the final choice
+ * (:146). Try t's area: x, y within the centre -+ 0.75, z over the scene (:98-103); points
+ * inside it +0.2 (>= lo, < hi) in index order; valid if labelled / (3 n) >= 0.7 (the
+ * reference divides by reduce_sum(ones_like((n,3) points)), :113) and the occupied voxel keys
+ * / 31 / 31 / 62 >= 0.02 (:119-126); the first valid try is kept, else the last (:138-141).
+ * Outputs (B,K[,3]): points, labels, colors (int32, may be NULL with out_colors NULL),
+ * normals (may be NULL likewise), weights = label_weights[label] * mask, mask = inside the
+ * area +0.01 (:114-117, :150-153). bbox from pn2_scene_bbox. workspace:
+ * pn2_crop_workspace_size(B, N, T) bytes. */
+size_t pn2_crop_workspace_size(int B, int N, int T);
+int pn2_crop_sample(const float* points, const int32_t* labels, const int32_t* colors,
+                    const float* normals, int N, const float* bbox, const int32_t* centres,
+                    int B, int T, const float* u, int K, const float* label_weights, int nlw,
+                    void* workspace, size_t workspace_bytes, float* out_points,
+                    int32_t* out_labels, int32_t* out_colors, float* out_normals,
+                    float* out_weights, pn2_stream_t stream);
+/* Whole-scene chunker, selection part (complete_scene_loader.py:33-40): for each of S boxes
+ * bounds (S,6) = [lo xyz, hi xyz] in FLOAT64 (the reference's float32 points compare against
+ * float64 bounds), the indices of the points with lo - margin <= p <= hi + margin on all axes,
+ * ascending, in sel[s*N ...], inner[s*N + k] = 1 if that point is also within [lo, hi], and the
+ * per-slice counts in counts (S, pn2_subvolume_slices(N)) — their row sums are the subvolume
+ * sizes. The random shuffle / fill-up of the chunks is drawn by the caller. */
+int pn2_subvolume_slices(int N);
+int pn2_subvolume_select(const float* points, int N, const double* bounds, int S, double margin,
+                         int32_t* counts, int32_t* sel, uint8_t* inner, pn2_stream_t stream);
+/* dst[r] = src[idx[r]] for n rows of row_bytes bytes (a multiple of 4); idx outside
+ * [0, nsrc) reads row 0. */
+int pn2_gather_rows(const void* src, long long nsrc, int row_bytes, const int32_t* idx,
+                    long long n, void* dst, pn2_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -415,3 +415,68 @@ def run_stack_cpu(inp_np, config):
                 outs.append(group_concat(xyz, points, new_xyz, gidx, xyz_last=True)[0])
             xyz, points = new_xyz, inp_np["sa_out"][0]
     return outs
+
+
+# ---------------------------------------------------------------- scene crops (numpy)
+# data_transformation.py:70-154 (get_subset) restated in numpy with TF's float32 semantics, for
+# caller-supplied random draws (test infrastructure: the crop sampler kernels' bar). TensorFlow
+# is not importable here, so this restatement is "parity unpinned" beyond its own reading of the
+# reference text; the scene CHUNKER (complete_scene_loader.py) is pinned to the reference
+# function itself through tests/golden/scene_chunks_*.npz.
+
+GET_SUBSET_LABEL_WEIGHTS = [0, 2.743064592944318, 3.0830506790927132, 4.785754459526457,
+                            4.9963745147506184, 4.372710774561782, 5.039124880965811,
+                            4.86451825464344, 4.717751595568025, 4.809412839311939,
+                            5.052097251455304, 5.389129668645318, 5.390614085649042,
+                            5.127458225110977, 5.086056870814752, 5.3831185190895265,
+                            5.422684124268539, 5.422955391988761, 5.433705358072363,
+                            5.417426773812747, 4.870172044153657]  # data_transformation.py:82-86
+
+
+def crop_sample(points, labels, colors, normals, centres, u, label_weights=None):
+    """One crop: centres (T,) point indices of the tries, u (K,) uniform draws.
+    Returns points, labels, colors, normals, sample_weight, chosen try, stats (T,3)."""
+    f32 = np.float32
+    p = np.asarray(points, f32)
+    lw = np.asarray(GET_SUBSET_LABEL_WEIGHTS if label_weights is None else label_weights, f32)
+    mn, mx = p.min(0), p.max(0)  # :90-91
+    T = len(centres)
+    chosen, stats = T - 1, []
+
+    def area(t):
+        c = p[centres[t]]
+        lo = np.array([c[0] - f32(0.75), c[1] - f32(0.75), mn[2]], f32)  # :98-103
+        hi = np.array([c[0] + f32(0.75), c[1] + f32(0.75), mx[2]], f32)
+        return lo, hi
+
+    for t in range(T):
+        lo, hi = area(t)
+        inarea = np.all((p >= lo - f32(0.2)) & (hi + f32(0.2) > p), axis=1)  # :105-106
+        cur = p[inarea]
+        n = len(cur)
+        lab = int((np.asarray(labels)[inarea] > 0).sum())
+        m = np.all((cur >= lo - f32(0.01)) & (hi + f32(0.01) > cur), axis=1)  # :114-117
+        v = np.ceil(((cur[m] - lo) / (hi - lo)) * np.array([31, 31, 62], f32))  # :119-120
+        key = (v[:, 0] * f32(31.0)) * f32(62.0) + v[:, 1] * f32(62) + v[:, 2]   # :121
+        occ = len(np.unique(key))
+        stats.append((n, lab, occ))
+        cur_len = f32(3 * n)  # reduce_sum(ones_like((n,3) cur_points)) (:113)
+        with np.errstate(invalid="ignore", divide="ignore"):
+            valid = (f32(lab) / cur_len >= f32(0.7)) and \
+                (f32(f32(f32(f32(occ) / f32(31.0)) / f32(31.0)) / f32(62.0)) >= f32(0.02))
+        if valid:
+            chosen = t
+            break
+    lo, hi = area(chosen)
+    inarea = np.all((p >= lo - f32(0.2)) & (hi + f32(0.2) > p), axis=1)
+    sel = np.nonzero(inarea)[0]
+    n = len(sel)
+    mask = np.all((p[sel] >= lo - f32(0.01)) & (hi + f32(0.01) > p[sel]), axis=1)
+    k = (np.asarray(u, f32) * f32(n)).astype(np.int64)  # random_uniform(0, cur_len) -> int32
+    k = np.clip(k, 0, n - 1)
+    idx = sel[k]
+    lab = np.asarray(labels)[idx]
+    w = lw[lab] * mask[k].astype(f32)  # :152-153
+    return (p[idx], lab, None if colors is None else np.asarray(colors)[idx],
+            None if normals is None else np.asarray(normals)[idx], w, chosen,
+            np.array(stats + [(0, 0, 0)] * (T - len(stats)), np.int64))

@@ -83,6 +83,14 @@ SIGNATURES = {
                                      _I, _P, _P]),
     "pn2_fp_mlp": (_I, [_P, _P, _P, _I, _P, _I, _I, _I, _I, _I, _P, _P, _P]),
     "pn2_shared_mlp": (_I, [_P, _LL, _I, _I, _P, _P, _P]),
+    "pn2_scene_workspace_size": (_S, [_I]),
+    "pn2_scene_bbox": (_I, [_P, _I, _P, _P, _S, _P]),
+    "pn2_crop_workspace_size": (_S, [_I, _I, _I]),
+    "pn2_crop_sample": (_I, [_P, _P, _P, _P, _I, _P, _P, _I, _I, _P, _I, _P, _I, _P, _S, _P, _P,
+                             _P, _P, _P, _P]),
+    "pn2_subvolume_slices": (_I, [_I]),
+    "pn2_subvolume_select": (_I, [_P, _I, _P, _I, ctypes.c_double, _P, _P, _P, _P]),
+    "pn2_gather_rows": (_I, [_P, _LL, _I, _P, _LL, _P, _P]),
 }
 
 _lib = None

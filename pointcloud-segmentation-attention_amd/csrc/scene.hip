@@ -1,0 +1,440 @@
+// The step before the hot path: crops of a ScanNet scene on the GPU, gfx950.
+//
+// Replaces attention_points/scannet_dataset/data_transformation.py:70-154 (get_subset: the
+// training crop sampler, TF graph ops) and the O(N x subvolumes) part of
+// complete_scene_loader.py:4-117 (the whole-scene chunker of evaluation / test, numpy).
+// The random draws stay with the caller (TF's random_uniform / numpy's RandomState in the
+// reference), so for the same draws the results are the reference's exactly:
+//  - pn2_crop_sample takes each crop's try centres (point indices, :95-97) and the npoints
+//    uniform draws of the final choice (:146);
+//  - the chunker's shuffles and fill-up choices are drawn on the host in the reference's call
+//    order from the counts pn2_subvolume_select returns.
+// Layout: one workgroup per (crop, try) for the validity statistics (the voxel-occupancy set
+// of a try lives in a 63,552-bit LDS bitmap); the in-area compaction is split over slices of
+// the scene (count pass, then a pass that writes indices at its slice's exclusive prefix), so
+// the order is the reference's tf.where / boolean-mask order (ascending point index).
+#include "common.h"
+
+namespace pn2 {
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kSlice = 4096;  // points per compaction slice
+// The reference's voxel key v0*31*62 + v1*62 + v2 (:121) with v = ceil(frac * [31, 31, 62]);
+// the 0.01 margin lets v0, v1 reach 32, so keys lie in [0, 32*1922 + 32*62 + 62]. The key is
+// not injective (v1*62 + v2 can exceed 1922); tf.unique counts KEYS, and so does the bitmap.
+constexpr int kVoxKeys = 32 * 1922 + 32 * 62 + 62 + 1;
+constexpr int kVoxWords = (kVoxKeys + 31) / 32;
+
+// ---- scene bounding box (reduce_min / reduce_max over the points, :90-91) ----------------
+__global__ __launch_bounds__(kBlock) void bbox_partial_kernel(const float* __restrict__ p, int N,
+                                                              float* __restrict__ part) {
+  __shared__ float s[6][kBlock / kWave];
+  float mn[3] = {__builtin_inff(), __builtin_inff(), __builtin_inff()};
+  float mx[3] = {-__builtin_inff(), -__builtin_inff(), -__builtin_inff()};
+  for (int i = blockIdx.x * kBlock + threadIdx.x; i < N; i += gridDim.x * kBlock)
+    for (int c = 0; c < 3; ++c) {
+      const float v = p[(size_t)i * 3 + c];
+      mn[c] = fminf(mn[c], v);
+      mx[c] = fmaxf(mx[c], v);
+    }
+  const int w = threadIdx.x / kWave;
+  for (int c = 0; c < 3; ++c) {
+    float a = mn[c], b = mx[c];
+    for (int o = kWave / 2; o > 0; o >>= 1) {
+      a = fminf(a, __shfl_xor(a, o, kWave));
+      b = fmaxf(b, __shfl_xor(b, o, kWave));
+    }
+    if (lane_id() == 0) {
+      s[c][w] = a;
+      s[3 + c][w] = b;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 6) {
+    float v = s[threadIdx.x][0];
+    for (int i = 1; i < kBlock / kWave; ++i)
+      v = threadIdx.x < 3 ? fminf(v, s[threadIdx.x][i]) : fmaxf(v, s[threadIdx.x][i]);
+    part[blockIdx.x * 6 + threadIdx.x] = v;
+  }
+}
+
+__global__ void bbox_final_kernel(const float* __restrict__ part, int nparts,
+                                  float* __restrict__ bbox) {
+  const int c = threadIdx.x;
+  if (c >= 6) return;
+  float v = part[c];
+  for (int i = 1; i < nparts; ++i) v = c < 3 ? fminf(v, part[i * 6 + c]) : fmaxf(v, part[i * 6 + c]);
+  bbox[c] = v;
+}
+
+// ---- crop sampler (get_subset) -----------------------------------------------------------
+// One try's area (:98-103): x, y = centre -+ 0.75, z = the scene's z range; all fp32.
+struct Area {
+  float lo[3], hi[3];
+};
+PN2_DEV Area try_area(const float* p, const float* bbox, int centre) {
+  Area a;
+  const float* c = p + (size_t)centre * 3;
+  a.lo[0] = c[0] - 0.75f;
+  a.lo[1] = c[1] - 0.75f;
+  a.lo[2] = bbox[2];
+  a.hi[0] = c[0] + 0.75f;
+  a.hi[1] = c[1] + 0.75f;
+  a.hi[2] = bbox[5];
+  return a;
+}
+// points >= (current_min - m) and (current_max + m) > points, all three axes (:105-106, :116)
+PN2_DEV bool in_box(const float* q, const Area& a, float m) {
+  bool ok = true;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) ok = ok && (q[c] >= a.lo[c] - m) && (a.hi[c] + m > q[c]);
+  return ok;
+}
+
+// stats[b][t] = {n (in the 0.2-margin area), labelled (label > 0), voxels occupied by the
+// 0.01-margin points}; validity (:124-126) is evaluated by the consumers.
+__global__ __launch_bounds__(kBlock) void crop_try_kernel(const float* __restrict__ p,
+                                                          const int32_t* __restrict__ labels,
+                                                          int N, const float* __restrict__ bbox,
+                                                          const int32_t* __restrict__ centres,
+                                                          int T, int32_t* __restrict__ stats) {
+  __shared__ uint32_t vox[kVoxWords];
+  __shared__ int s_cnt[3];
+  const int bt = blockIdx.x;  // b * T + t
+  for (int i = threadIdx.x; i < kVoxWords; i += kBlock) vox[i] = 0;
+  if (threadIdx.x < 3) s_cnt[threadIdx.x] = 0;
+  __syncthreads();
+  const Area a = try_area(p, bbox, centres[bt]);
+  float ext[3];
+  const float scale[3] = {31.0f, 31.0f, 62.0f};
+  for (int c = 0; c < 3; ++c) ext[c] = a.hi[c] - a.lo[c];
+  int n = 0, lab = 0;
+  for (int i = threadIdx.x; i < N; i += kBlock) {
+    const float* q = p + (size_t)i * 3;
+    if (!in_box(q, a, 0.2f)) continue;
+    ++n;
+    lab += labels[i] > 0;
+    if (in_box(q, a, 0.01f)) {
+      // vidx = ceil((p - current_min) / (current_max - current_min) * [31, 31, 62]) (:119-120)
+      int v[3];
+      for (int c = 0; c < 3; ++c) v[c] = (int)ceilf(((q[c] - a.lo[c]) / ext[c]) * scale[c]);
+      const int key = v[0] * 1922 + v[1] * 62 + v[2];  // vidx_0*31*62 + vidx_1*62 + vidx_2
+      if (key >= 0 && key < kVoxKeys) atomicOr(&vox[key >> 5], 1u << (key & 31));
+    }
+  }
+  atomicAdd(&s_cnt[0], n);
+  atomicAdd(&s_cnt[1], lab);
+  __syncthreads();
+  int occ = 0;
+  for (int i = threadIdx.x; i < kVoxWords; i += kBlock) occ += __popc(vox[i]);
+  atomicAdd(&s_cnt[2], occ);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    stats[bt * 3 + 0] = s_cnt[0];
+    stats[bt * 3 + 1] = s_cnt[1];
+    stats[bt * 3 + 2] = s_cnt[2];
+  }
+}
+
+// The try the reference keeps: the first valid one, else the last (:138-141).
+// isvalid = labelled / cur_len >= 0.7 and occupied / 31 / 31 / 62 >= 0.02, all fp32, with
+// cur_len = reduce_sum(ones_like(cur_points)) = 3 n (the (n, 3) point tensor, :113).
+PN2_DEV int chosen_try(const int32_t* stats, int b, int T) {
+  for (int t = 0; t < T; ++t) {
+    const int32_t* s = stats + (b * T + t) * 3;
+    const float cur_len = (float)(3 * s[0]);
+    const float frac = (float)s[1] / cur_len;
+    const float occ = (((float)s[2] / 31.0f) / 31.0f) / 62.0f;
+    if (frac >= 0.7f && occ >= 0.02f) return t;
+  }
+  return T - 1;
+}
+
+// Slice counts of the chosen try's area: cnt[b][slice].
+__global__ __launch_bounds__(kBlock) void crop_count_kernel(const float* __restrict__ p, int N,
+                                                            const float* __restrict__ bbox,
+                                                            const int32_t* __restrict__ centres,
+                                                            const int32_t* __restrict__ stats,
+                                                            int T, int nslices,
+                                                            int32_t* __restrict__ cnt) {
+  const int b = blockIdx.y, sl = blockIdx.x;
+  const int t = chosen_try(stats, b, T);
+  const Area a = try_area(p, bbox, centres[b * T + t]);
+  const int i0 = sl * kSlice, i1 = min(N, i0 + kSlice);
+  int n = 0;
+  for (int i = i0 + threadIdx.x; i < i1; i += kBlock) n += in_box(p + (size_t)i * 3, a, 0.2f);
+  __shared__ int s;
+  if (threadIdx.x == 0) s = 0;
+  __syncthreads();
+  atomicAdd(&s, n);
+  __syncthreads();
+  if (threadIdx.x == 0) cnt[b * nslices + sl] = s;
+}
+
+// Ordered compaction of one slice: in-area point indices at the slice's exclusive prefix
+// (tf.where order, :107), and the 0.01-margin mask of each (:114-117).
+__global__ __launch_bounds__(kBlock) void crop_compact_kernel(
+    const float* __restrict__ p, int N, const float* __restrict__ bbox,
+    const int32_t* __restrict__ centres, const int32_t* __restrict__ stats, int T, int nslices,
+    const int32_t* __restrict__ cnt, int32_t* __restrict__ sel, uint8_t* __restrict__ inner) {
+  const int b = blockIdx.y, sl = blockIdx.x;
+  const int t = chosen_try(stats, b, T);
+  const Area a = try_area(p, bbox, centres[b * T + t]);
+  __shared__ int s_base, s_wave[kBlock / kWave];
+  if (threadIdx.x == 0) {
+    int base = 0;
+    for (int k = 0; k < sl; ++k) base += cnt[b * nslices + k];
+    s_base = base;
+  }
+  __syncthreads();
+  int base = s_base;
+  const int w = threadIdx.x / kWave, lane = lane_id();
+  const int i0 = sl * kSlice, i1 = min(N, i0 + kSlice);
+  int32_t* out = sel + (size_t)b * N;
+  uint8_t* inn = inner + (size_t)b * N;
+  for (int c0 = i0; c0 < i1; c0 += kBlock) {
+    const int i = c0 + threadIdx.x;
+    const bool in = i < i1 && in_box(p + (size_t)i * 3, a, 0.2f);
+    const uint64_t bal = __ballot(in);
+    const int rank = __popcll(bal & ((1ull << lane) - 1));
+    if (lane == 0) s_wave[w] = __popcll(bal);
+    __syncthreads();
+    int off = base;
+    for (int k = 0; k < w; ++k) off += s_wave[k];
+    if (in) {
+      out[off + rank] = i;
+      inn[off + rank] = in_box(p + (size_t)i * 3, a, 0.01f) ? 1 : 0;
+    }
+    int tot = 0;
+    for (int k = 0; k < kBlock / kWave; ++k) tot += s_wave[k];
+    base += tot;
+    __syncthreads();
+  }
+}
+
+// The final draw (:145-153): choice = int(u * n) over the chosen area's n points, gathered
+// points / labels / colours / normals, mask, sample weight = label_weights[label] * mask.
+__global__ __launch_bounds__(kBlock) void crop_gather_kernel(
+    const float* __restrict__ p, const int32_t* __restrict__ labels,
+    const int32_t* __restrict__ colors, const float* __restrict__ normals, int N,
+    const int32_t* __restrict__ cnt, int nslices, const int32_t* __restrict__ sel,
+    const uint8_t* __restrict__ inner, const float* __restrict__ u, int K,
+    const float* __restrict__ label_weights, int nlw, float* __restrict__ op,
+    int32_t* __restrict__ ol, int32_t* __restrict__ oc, float* __restrict__ on,
+    float* __restrict__ ow) {
+  const int b = blockIdx.y;
+  const int j = blockIdx.x * kBlock + threadIdx.x;
+  __shared__ int s_n;
+  if (threadIdx.x == 0) {
+    int n = 0;
+    for (int k = 0; k < nslices; ++k) n += cnt[b * nslices + k];
+    s_n = n;
+  }
+  __syncthreads();
+  if (j >= K) return;
+  const int n = s_n;
+  // tf.random_uniform((npoints,), 0, cur_len) = u * (cur_len - 0) + 0 in fp32, then int32 cast
+  int k = (int)(u[(size_t)b * K + j] * (float)n);
+  k = min(max(k, 0), n - 1);
+  const int i = sel[(size_t)b * N + k];
+  const size_t o = (size_t)b * K + j;
+  for (int c = 0; c < 3; ++c) {
+    op[o * 3 + c] = p[(size_t)i * 3 + c];
+    if (colors) oc[o * 3 + c] = colors[(size_t)i * 3 + c];
+    if (normals) on[o * 3 + c] = normals[(size_t)i * 3 + c];
+  }
+  const int lab = labels[i];
+  ol[o] = lab;
+  const float m = inner[(size_t)b * N + k] ? 1.0f : 0.0f;
+  ow[o] = (lab >= 0 && lab < nlw ? label_weights[lab] : 0.0f) * m;
+}
+
+// ---- whole-scene chunker: subvolume selection (complete_scene_loader.py:33-40) ----------
+// bounds (S, 6) in float64 (lo xyz, hi xyz): the reference compares its float32 points with
+// float64 bounds (coordmin + [i*1.5, j*1.5, 0] promotes to float64).
+PN2_DEV bool in_box_d(const float* q, const double* bd, double m) {
+  bool ok = true;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const double v = (double)q[c];
+    ok = ok && (v >= bd[c] - m) && (v <= bd[3 + c] + m);
+  }
+  return ok;
+}
+
+__global__ __launch_bounds__(kBlock) void subvol_count_kernel(const float* __restrict__ p, int N,
+                                                              const double* __restrict__ bounds,
+                                                              double margin, int nslices,
+                                                              int32_t* __restrict__ cnt) {
+  const int s = blockIdx.y, sl = blockIdx.x;
+  double bd[6];
+  for (int c = 0; c < 6; ++c) bd[c] = bounds[s * 6 + c];
+  const int i0 = sl * kSlice, i1 = min(N, i0 + kSlice);
+  int n = 0;
+  for (int i = i0 + threadIdx.x; i < i1; i += kBlock) n += in_box_d(p + (size_t)i * 3, bd, margin);
+  __shared__ int sh;
+  if (threadIdx.x == 0) sh = 0;
+  __syncthreads();
+  atomicAdd(&sh, n);
+  __syncthreads();
+  if (threadIdx.x == 0) cnt[s * nslices + sl] = sh;
+}
+
+__global__ __launch_bounds__(kBlock) void subvol_compact_kernel(
+    const float* __restrict__ p, int N, const double* __restrict__ bounds, double margin,
+    int nslices, const int32_t* __restrict__ cnt, int32_t* __restrict__ sel,
+    uint8_t* __restrict__ inner) {
+  const int s = blockIdx.y, sl = blockIdx.x;
+  double bd[6];
+  for (int c = 0; c < 6; ++c) bd[c] = bounds[s * 6 + c];
+  __shared__ int s_base, s_wave[kBlock / kWave];
+  if (threadIdx.x == 0) {
+    int base = 0;
+    for (int k = 0; k < sl; ++k) base += cnt[s * nslices + k];
+    s_base = base;
+  }
+  __syncthreads();
+  int base = s_base;
+  const int w = threadIdx.x / kWave, lane = lane_id();
+  const int i0 = sl * kSlice, i1 = min(N, i0 + kSlice);
+  for (int c0 = i0; c0 < i1; c0 += kBlock) {
+    const int i = c0 + threadIdx.x;
+    const bool in = i < i1 && in_box_d(p + (size_t)i * 3, bd, margin);
+    const uint64_t bal = __ballot(in);
+    const int rank = __popcll(bal & ((1ull << lane) - 1));
+    if (lane == 0) s_wave[w] = __popcll(bal);
+    __syncthreads();
+    int off = base;
+    for (int k = 0; k < w; ++k) off += s_wave[k];
+    if (in) {
+      sel[(size_t)s * N + off + rank] = i;
+      // mask = (cur >= curmin) * (cur <= curmax), no margin (:40)
+      inner[(size_t)s * N + off + rank] = in_box_d(p + (size_t)i * 3, bd, 0.0) ? 1 : 0;
+    }
+    int tot = 0;
+    for (int k = 0; k < kBlock / kWave; ++k) tot += s_wave[k];
+    base += tot;
+    __syncthreads();
+  }
+}
+
+// out[r] = src[idx[r]] for rows of row_bytes bytes (16-byte units when aligned).
+__global__ __launch_bounds__(kBlock) void gather_rows_kernel(const uint8_t* __restrict__ src,
+                                                             long long nsrc, int row_bytes,
+                                                             const int32_t* __restrict__ idx,
+                                                             long long n, uint8_t* __restrict__ dst) {
+  const bool v16 = (row_bytes & 15) == 0 && ((uintptr_t)src & 15) == 0 && ((uintptr_t)dst & 15) == 0;
+  const int units = v16 ? row_bytes / 16 : row_bytes / 4;
+  const long long total = n * units;
+  for (long long e = (long long)blockIdx.x * kBlock + threadIdx.x; e < total;
+       e += (long long)gridDim.x * kBlock) {
+    const long long r = e / units;
+    const int u = (int)(e - r * units);
+    long long s = idx[r];
+    if (s < 0 || s >= nsrc) s = 0;
+    if (v16)
+      reinterpret_cast<uint4*>(dst + r * row_bytes)[u] =
+          reinterpret_cast<const uint4*>(src + s * row_bytes)[u];
+    else
+      reinterpret_cast<uint32_t*>(dst + r * row_bytes)[u] =
+          reinterpret_cast<const uint32_t*>(src + s * row_bytes)[u];
+  }
+}
+
+unsigned nslices_of(int N) { return (unsigned)((N + kSlice - 1) / kSlice); }
+
+}  // namespace
+}  // namespace pn2
+
+extern "C" {
+
+size_t pn2_scene_workspace_size(int N) {
+  // bbox partials (64 x 6 floats) + bbox
+  (void)N;
+  return (64 * 6 + 8) * sizeof(float);
+}
+
+int pn2_scene_bbox(const float* points, int N, float* bbox, void* workspace,
+                   size_t workspace_bytes, pn2_stream_t stream) {
+  if (N <= 0 || !points || !bbox || !workspace) return PN2_EINVAL;
+  if (workspace_bytes < pn2_scene_workspace_size(N)) return PN2_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  int parts = (N + pn2::kBlock * 16 - 1) / (pn2::kBlock * 16);
+  parts = parts < 1 ? 1 : (parts > 64 ? 64 : parts);
+  float* part = static_cast<float*>(workspace);
+  hipLaunchKernelGGL(pn2::bbox_partial_kernel, dim3(parts), dim3(pn2::kBlock), 0, s, points, N,
+                     part);
+  hipLaunchKernelGGL(pn2::bbox_final_kernel, dim3(1), dim3(64), 0, s, part, parts, bbox);
+  PN2_RETURN_LAUNCH();
+}
+
+size_t pn2_crop_workspace_size(int B, int N, int T) {
+  const size_t ns = pn2::nslices_of(N);
+  return (size_t)B * T * 3 * 4 + (size_t)B * ns * 4 + (size_t)B * N * 4 + (size_t)B * N + 64;
+}
+
+int pn2_crop_sample(const float* points, const int32_t* labels, const int32_t* colors,
+                    const float* normals, int N, const float* bbox, const int32_t* centres,
+                    int B, int T, const float* u, int K, const float* label_weights, int nlw,
+                    void* workspace, size_t workspace_bytes, float* out_points,
+                    int32_t* out_labels, int32_t* out_colors, float* out_normals,
+                    float* out_weights, pn2_stream_t stream) {
+  if (B < 0 || N <= 0 || T <= 0 || K < 0 || nlw < 0) return PN2_EINVAL;
+  if (B == 0 || K == 0) return PN2_OK;
+  if (!points || !labels || !bbox || !centres || !u || !out_points || !out_labels ||
+      !out_weights || !workspace || (nlw && !label_weights))
+    return PN2_EINVAL;
+  if ((colors && !out_colors) || (normals && !out_normals)) return PN2_EINVAL;
+  if ((long long)B * N > 0x7fffffffLL) return PN2_EINVAL;
+  if (workspace_bytes < pn2_crop_workspace_size(B, N, T)) return PN2_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  const unsigned ns = pn2::nslices_of(N);
+  int32_t* stats = static_cast<int32_t*>(workspace);
+  int32_t* cnt = stats + (size_t)B * T * 3;
+  int32_t* sel = cnt + (size_t)B * ns;
+  uint8_t* inner = reinterpret_cast<uint8_t*>(sel + (size_t)B * N);
+  hipLaunchKernelGGL(pn2::crop_try_kernel, dim3((unsigned)(B * T)), dim3(pn2::kBlock), 0, s,
+                     points, labels, N, bbox, centres, T, stats);
+  hipLaunchKernelGGL(pn2::crop_count_kernel, dim3(ns, (unsigned)B), dim3(pn2::kBlock), 0, s,
+                     points, N, bbox, centres, stats, T, (int)ns, cnt);
+  hipLaunchKernelGGL(pn2::crop_compact_kernel, dim3(ns, (unsigned)B), dim3(pn2::kBlock), 0, s,
+                     points, N, bbox, centres, stats, T, (int)ns, cnt, sel, inner);
+  hipLaunchKernelGGL(pn2::crop_gather_kernel,
+                     dim3((unsigned)((K + pn2::kBlock - 1) / pn2::kBlock), (unsigned)B),
+                     dim3(pn2::kBlock), 0, s, points, labels, colors, normals, N, cnt, (int)ns,
+                     sel, inner, u, K, label_weights, nlw, out_points, out_labels, out_colors,
+                     out_normals, out_weights);
+  PN2_RETURN_LAUNCH();
+}
+
+int pn2_subvolume_select(const float* points, int N, const double* bounds, int S, double margin,
+                         int32_t* counts, int32_t* sel, uint8_t* inner, pn2_stream_t stream) {
+  if (N < 0 || S < 0) return PN2_EINVAL;
+  if ((long long)N * S == 0) return PN2_OK;
+  if (!points || !bounds || !counts || !sel || !inner) return PN2_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  const unsigned ns = pn2::nslices_of(N);
+  hipLaunchKernelGGL(pn2::subvol_count_kernel, dim3(ns, (unsigned)S), dim3(pn2::kBlock), 0, s,
+                     points, N, bounds, margin, (int)ns, counts);
+  hipLaunchKernelGGL(pn2::subvol_compact_kernel, dim3(ns, (unsigned)S), dim3(pn2::kBlock), 0, s,
+                     points, N, bounds, margin, (int)ns, counts, sel, inner);
+  PN2_RETURN_LAUNCH();
+}
+
+int pn2_subvolume_slices(int N) { return (int)pn2::nslices_of(N); }
+
+int pn2_gather_rows(const void* src, long long nsrc, int row_bytes, const int32_t* idx,
+                    long long n, void* dst, pn2_stream_t stream) {
+  if (nsrc < 0 || n < 0 || row_bytes <= 0 || (row_bytes & 3)) return PN2_EINVAL;
+  if (n == 0) return PN2_OK;
+  if (!src || !idx || !dst || nsrc == 0) return PN2_EINVAL;
+  long long blocks = (n * (row_bytes / 4) + pn2::kBlock - 1) / pn2::kBlock;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(pn2::gather_rows_kernel, dim3((unsigned)blocks), dim3(pn2::kBlock), 0,
+                     (hipStream_t)stream, static_cast<const uint8_t*>(src), nsrc, row_bytes,
+                     idx, n, static_cast<uint8_t*>(dst));
+  PN2_RETURN_LAUNCH();
+}
+
+}  // extern "C"

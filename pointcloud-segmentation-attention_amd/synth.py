@@ -119,3 +119,51 @@ def features_uniform(seed, shape):
     """U[-1,1) float32 tensor standing in for an MLP output."""
     n = int(np.prod(shape))
     return (uniform(seed, n) * 2.0 - 1.0).astype(np.float32).reshape(shape)
+
+
+def scannet_scene(scene_id, n_points=60000, size=(6.0, 4.5, 2.6)):
+    """A synthetic ScanNet-like room (the input of the crop sampler / scene chunker,
+    scannet_dataset/data_transformation.py:70, complete_scene_loader.py:4): floor, four walls
+    and a few boxes, points (n,3) float32 with the room's corner at a random offset, labels
+    (n,) int32 in [0, 20] (0 = unannotated, ~15 %), colours (n,3) int32 in [0, 255], unit
+    normals (n,3) float32. Deterministic in scene_id."""
+    import numpy as np
+    g = np.random.default_rng(0xC0FFEE + scene_id)
+    sx, sy, sz = size
+    kind = g.choice(3, n_points, p=[0.35, 0.35, 0.30])
+    pts = np.empty((n_points, 3), np.float64)
+    nrm = np.zeros((n_points, 3), np.float64)
+    lab = np.empty(n_points, np.int64)
+    f = kind == 0  # floor
+    pts[f] = np.stack([g.uniform(0, sx, f.sum()), g.uniform(0, sy, f.sum()), np.zeros(f.sum())], 1)
+    nrm[f, 2] = 1
+    lab[f] = 2
+    w = kind == 1  # walls
+    side = g.integers(0, 4, w.sum())
+    t = g.uniform(0, 1, w.sum())
+    z = g.uniform(0, sz, w.sum())
+    wx = np.where(side == 0, t * sx, np.where(side == 1, t * sx, np.where(side == 2, 0.0, sx)))
+    wy = np.where(side == 0, 0.0, np.where(side == 1, sy, t * sy))
+    pts[w] = np.stack([wx, wy, z], 1)
+    nrm[w] = np.stack([(side == 2) * 1.0 - (side == 3) * 1.0, (side == 0) * 1.0 - (side == 1) * 1.0,
+                       np.zeros(w.sum())], 1)
+    lab[w] = 1
+    b = kind == 2  # boxes (furniture)
+    nb = 6
+    cx, cy = g.uniform(0.5, sx - 0.5, nb), g.uniform(0.5, sy - 0.5, nb)
+    hx, hy, hz = g.uniform(0.2, 0.6, nb), g.uniform(0.2, 0.6, nb), g.uniform(0.4, 1.2, nb)
+    bi = g.integers(0, nb, b.sum())
+    u, v = g.uniform(-1, 1, b.sum()), g.uniform(-1, 1, b.sum())
+    face = g.integers(0, 3, b.sum())
+    px = np.where(face == 0, cx[bi] + np.sign(u) * hx[bi], cx[bi] + u * hx[bi])
+    py = np.where(face == 1, cy[bi] + np.sign(v) * hy[bi], cy[bi] + v * hy[bi])
+    pz = np.where(face == 2, 2 * hz[bi], g.uniform(0, 1, b.sum()) * 2 * hz[bi])
+    pts[b] = np.stack([px, py, pz], 1)
+    nrm[b, 2] = 1
+    lab[b] = 3 + bi % 18
+    pts += g.normal(0, 0.005, pts.shape)
+    pts += g.uniform(-3, 3, 3) * np.array([1, 1, 0.1])
+    lab[g.uniform(0, 1, n_points) < 0.15] = 0
+    col = g.integers(0, 256, (n_points, 3)).astype(np.int32)
+    return (pts.astype(np.float32), lab.astype(np.int32), col,
+            (nrm / np.maximum(np.linalg.norm(nrm, axis=1, keepdims=True), 1e-9)).astype(np.float32))

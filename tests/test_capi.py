@@ -162,3 +162,21 @@ def test_mlp_contract(pn2):
     assert lib.pn2_group_mlp(None, None, None, None, 0, 10, 6, 4, 8, 1, 2, good, 0, None,
                              None) == E                     # points NULL: the width is 3
     assert lib.pn2_fp_mlp(fake, fake, None, 3, fake, 6, 1, 4, 4, 2, good, fake, None) == E
+
+
+def test_scene_contract(pn2):
+    lib, E = pn2.lib(), -22
+    fake = 1 << 20
+    assert lib.pn2_scene_bbox(None, 0, None, None, 0, None) == E
+    assert lib.pn2_scene_bbox(fake, 10, fake, fake, 0, None) == E           # workspace too small
+    assert lib.pn2_crop_sample(fake, fake, None, None, 100, fake, fake, 2, 0, fake, 16, None, 0,
+                               fake, 1 << 30, fake, fake, None, None, fake, None) == E  # T = 0
+    assert lib.pn2_crop_sample(None, None, None, None, 100, None, None, 0, 10, None, 16, None, 0,
+                               None, 0, None, None, None, None, None, None) == 0     # no crops
+    assert lib.pn2_crop_sample(fake, fake, fake, None, 100, fake, fake, 2, 10, fake, 16, None, 0,
+                               fake, 1 << 30, fake, fake, None, None, fake, None) == E  # colors w/o out
+    assert lib.pn2_subvolume_select(None, 0, None, 4, 0.2, None, None, None, None) == 0
+    assert lib.pn2_subvolume_select(None, 10, None, 4, 0.2, None, None, None, None) == E
+    assert lib.pn2_subvolume_slices(4096) == 1 and lib.pn2_subvolume_slices(4097) == 2
+    assert lib.pn2_gather_rows(fake, 10, 6, fake, 4, fake, None) == E        # row bytes % 4
+    assert lib.pn2_gather_rows(None, 10, 8, None, 0, None, None) == 0
