@@ -19,12 +19,12 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-# The step runs on 4 streams (sampler chain + 3 side lanes) plus 2 setup streams; HIP maps
-# streams to hardware queues round-robin, and with its default of 4 queues a side lane
-# would share the chain's queue and sit in front of the next step's sampler. 8 <= 32.
-# The whole-model step gives each of its 3 buffer sets 4 private side streams: 16 queues keep
-# every stream on its own queue (the pool allows <= 32).
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "16")
+# HIP hardware queues per process (GPU_MAX_HW_QUEUES, set from --hw-queues before HIP starts;
+# the GPU box exports 4). Streams map onto them round-robin. Measured on one box
+# (scripts/ab_queues.sh): with 4 queues the geometric step runs 21.7k
+# clouds/s, with 8 or 16 the side lanes run fully beside the SA1 sampler and slow it from
+# 0.72 to 0.81 ms (18.7k clouds/s) -- while the whole-model step gains (11.2k -> 14.5k).
+DEFAULT_HW_QUEUES = 4
 
 PKG = "pointcloud-segmentation-attention_amd"
 METRIC = "8192-pt clouds/sec through SA+FP layers, 1/2/4/8 MI355X; HBM GB/s vs peak"
@@ -119,10 +119,17 @@ def main():
     ap.add_argument("--model", action="store_true",
                     help="the step is the whole segmentation model's inference forward "
                          "(SA/FP geometry + fused MLPs + head) instead of the geometry alone")
+    ap.add_argument("--hw-queues", type=int, default=None,
+                    help="GPU_MAX_HW_QUEUES for this process (default: the environment's, else "
+                         f"{DEFAULT_HW_QUEUES}; <= 32)")
     ap.add_argument("--e2e-steps", type=int, default=20,
                     help="after the geometric measurement, time this many whole-model steps "
                          "(reported as 'e2e'; 0 = skip)")
     args = ap.parse_args()
+    if args.hw_queues is not None:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, max(1, args.hw_queues)))
+    else:
+        os.environ.setdefault("GPU_MAX_HW_QUEUES", str(DEFAULT_HW_QUEUES))
 
     import torch
     import torch.distributed as dist
@@ -233,6 +240,7 @@ def main():
                        "parallelism": f"dp{world} (batch split)",
                        "launch": "eager" if args.eager else
                        "samplers: direct launches; side lanes: hipGraph replay",
+                       "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "0")),
                        "streams": ("SA1 sampler + 4 side streams" if overlap else "one stream")
                        + (f", steps software-pipelined over {args.sets} buffer sets" if pipelined else "")},
             "roofline": {"kernel": f"SA1 sampler (FPS + gather fused): {B} clouds x {N} pts -> "
