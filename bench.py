@@ -122,6 +122,9 @@ def main():
     ap.add_argument("--hw-queues", type=int, default=None,
                     help="GPU_MAX_HW_QUEUES for this process (default: the environment's, else "
                          f"{DEFAULT_HW_QUEUES}; <= 32)")
+    ap.add_argument("--lane0-priority", choices=["auto", "default", "high"], default="auto",
+                    help="stream priority of lane 0 (the SA1 sampler chain); auto = default "
+                         "for the geometric step, high for the whole model")
     ap.add_argument("--e2e-steps", type=int, default=20,
                     help="after the geometric measurement, time this many whole-model steps "
                          "(reported as 'e2e'; 0 = skip)")
@@ -153,7 +156,23 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
+    # Lane 0 (the SA1 sampler chain) runs on the current stream. "high" makes it a
+    # high-priority stream (HIP keeps a separate queue pool per priority, so the sampler never
+    # waits behind side-lane work in a shared queue). Measured (scripts/ab_prio.sh,
+    # DESIGN.md §3.6): the geometric step is faster with the default priority (21.8k vs 18.9k
+    # clouds/s: with its side lanes fully concurrent the latency-bound sampler slows 0.715 ->
+    # 0.80 ms), the whole model with high (its side lanes carry most of the work). "auto" =
+    # default for the geometric step, high for the whole model.
+    hi_lane0 = torch.cuda.Stream(device=dev, priority=-1)
+
     def measure(model, steps, warmup):
+        prio = args.lane0_priority
+        if prio == "auto":
+            prio = "high" if model else "default"
+        with torch.cuda.stream(hi_lane0 if prio == "high" else torch.cuda.current_stream(dev)):
+            return _measure(model, steps, warmup) + (prio,)
+
+    def _measure(model, steps, warmup):
         """W warm-up steps, then K timed steps between barrier + synchronize; returns
         (max-over-ranks elapsed seconds, mean SA1-sampler ms, last outputs)."""
         inp = pkg.stack.make_inputs(args.config, ids, dev, model=model)
@@ -197,16 +216,19 @@ def main():
 
     overlap = not args.no_overlap
     pipelined = overlap and not args.no_pipeline
-    elapsed, fps_ms, outs = measure(args.model, args.steps, args.warmup)
+    elapsed, fps_ms, outs, prio0 = measure(args.model, args.steps, args.warmup)
     # per-cloud output checksums, gathered (outside the timed region) so ranks can be compared
     sums = pkg.shard.gather_checksums(pkg.shard.cloud_checksums(outs, B))
     e2e = None
     if not args.model and args.e2e_steps > 0 and pkg.stack.CONFIGS[args.config][1] == "ssg":
-        e_el, e_fps, e_outs = measure(True, args.e2e_steps, min(args.warmup, 5))
+        # after the geometric step: the stream-to-queue mapping is round-robin in creation
+        # order, and creating the model's streams first cost the geometric step 29 %
+        e_el, e_fps, e_outs, e_prio = measure(True, args.e2e_steps, min(args.warmup, 5))
         e_sums = pkg.shard.gather_checksums(pkg.shard.cloud_checksums(e_outs, B))
         e2e = {"value": world * B * args.e2e_steps / e_el, "unit": "clouds/s",
                "ms_per_step": e_el / args.e2e_steps * 1e3, "steps": args.e2e_steps,
                "sa1_sampler_ms": e_fps, "checksum": float(e_sums.sum().item()),
+               "lane0_priority": e_prio,
                "model": ("pointnet2_sem_seg_attention with rgb+normal inputs, inference "
                          "forward: SA x4 (fused group + MLP, Dense q/k/v on the matrix cores, "
                          "attention reduction + batch norm)" if args.config == "cfg3" else
@@ -241,6 +263,7 @@ def main():
                        "launch": "eager" if args.eager else
                        "samplers: direct launches; side lanes: hipGraph replay",
                        "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "0")),
+                       "lane0_priority": prio0,
                        "streams": ("SA1 sampler + 4 side streams" if overlap else "one stream")
                        + (f", steps software-pipelined over {args.sets} buffer sets" if pipelined else "")},
             "roofline": {"kernel": f"SA1 sampler (FPS + gather fused): {B} clouds x {N} pts -> "
