@@ -28,7 +28,7 @@ fi
 
 if [ "${SKIP_PROF:-0}" != "1" ]; then
   echo "== rocprofv3 kernel trace"
-  timeout -k 10 ${PROF_TIMEOUT:-600} rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o run -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline ${BENCH_ARGS:-} > $OUT/prof_$TAG.log 2>&1
+  timeout -k 10 ${PROF_TIMEOUT:-600} rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o run -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --e2e-steps 0 ${BENCH_ARGS:-} > $OUT/prof_$TAG.log 2>&1
   rc=$?; tail -5 $OUT/prof_$TAG.log; echo "rocprof rc=$rc"
   find $OUT/prof_$TAG -name "*stats*" | head
   [ $rc -eq 0 ] || exit $rc
