@@ -25,6 +25,9 @@
 // Both orientations read the operands through the same lane maps, so one packed weight format
 // serves every layer: Wp[to][c][h][i][s] = W[8c + 4h + s][32*to + i] (pn2_mlp_pack), one
 // float4 per lane per 4 MFMAs, and activations are read as act[p][8c + 4h .. +3].
+#include <cstdio>
+#include <cstdlib>
+
 #include "common.h"
 
 namespace pn2 {
@@ -82,6 +85,8 @@ struct Params {
   // Dense query (first neighbour of each group) / key / value layers, the reduction per head
   // and the batch norm (+ max pool of X), column segment by column segment of K and V
   int attn, att_wseg, att_nseg, att_add_max;
+  int ntiles;  // tiles of P rows
+  int tpw;     // consecutive tiles per workgroup (grid = ceil(ntiles / tpw))
   LayerDev qkv[3];
   const float* att_scale;
   const float* att_shift;
@@ -381,6 +386,130 @@ PN2_DEV float dot4q(float4 q, float4 k) {
   return s;
 }
 
+// The query of every group, Dense_q(X[first neighbour]) (attention_layer.py:31, :259), on the
+// VALU: only G rows are needed, so a 32-row MFMA tile would waste (32 - G)/32 of its work
+// (31/32 at SA3/SA4, where one group fills the workgroup). Thread -> (group, output feature);
+// the packed weights are read as one float4 over 4 consecutive input features, the row of X
+// as LDS broadcasts. Four partial sums (one per feature residue mod 4), then the epilogue.
+PN2_DEV void attn_query(const LayerDev& D, const float* X, int Sx, int G, int ns_pad, float* Qb,
+                        int Sq, int C) {
+  for (int o = threadIdx.x; o < G * C; o += kBlock) {
+    const int gi = o / C, f = o - gi * C;
+    const float4* wp = D.w + (size_t)(f >> 5) * D.cin8 * kWave + (f & 31);
+    const float* x = X + gi * ns_pad * Sx;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+#pragma unroll 4
+    for (int c = 0; c < D.cin8; ++c) {
+      const float4 w0 = wp[c * kWave], w1 = wp[c * kWave + 32];
+      const float4 x0 = *reinterpret_cast<const float4*>(x + 8 * c);
+      const float4 x1 = *reinterpret_cast<const float4*>(x + 8 * c + 4);
+      a0 = fmaf(x0.x, w0.x, a0);
+      a1 = fmaf(x0.y, w0.y, a1);
+      a2 = fmaf(x0.z, w0.z, a2);
+      a3 = fmaf(x0.w, w0.w, a3);
+      a0 = fmaf(x1.x, w1.x, a0);
+      a1 = fmaf(x1.y, w1.y, a1);
+      a2 = fmaf(x1.z, w1.z, a2);
+      a3 = fmaf(x1.w, w1.w, a3);
+    }
+    Qb[gi * Sq + f] = ((a0 + a1) + (a2 + a3)) * D.scale[f] + D.shift[f];
+  }
+}
+
+template <int L>
+PN2_DEV float lane_sum(float v) {
+#pragma unroll
+  for (int o = L / 2; o > 0; o >>= 1) v = v + __shfl_xor(v, o, kWave);
+  return v;
+}
+template <int L>
+PN2_DEV float lane_max(float v) {
+#pragma unroll
+  for (int o = L / 2; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, kWave));
+  return v;
+}
+
+// Scores, softmax over the ns pseudo-keys and the weighted V of every (group, head) unit of
+// one K/V column segment (attention_layer.py:37-40) [+ the batch norm of :261 and the max pool
+// of :296-303], L lanes per unit: each lane takes every L-th pseudo-key, so the per-unit sums
+// are register sums plus log2(L) lane exchanges (L is picked so the units fill the block).
+template <int L>
+PN2_DEV void attn_scores(const Params& prm, const float* X, int Sx, const float* Kb,
+                         const float* Vb, const float* Qb, int sgi, int tile) {
+  const int C = prm.L[prm.nl - 1].cout;
+  const int ns = prm.ns, ns_pad = 1 << prm.lg_ns_pad;
+  const int G = prm.gpw;
+  const int Skv = prm.stride_kv, Sq = prm.stride_q;
+  const int wseg = prm.att_wseg;
+  const bool whole = wseg == C;
+  const int hs_per_group = whole ? C / 4 : ns;  // heads completed by one segment
+  const int units = G * hs_per_group;
+  const int sub = threadIdx.x & (L - 1);
+  for (int u = threadIdx.x / L; u < units; u += kBlock / L) {
+    const int gi = u / hs_per_group, hs = u - gi * hs_per_group;
+    const int g = tile * G + gi;
+    const int hg = whole ? hs : (C / wseg) * hs + sgi;  // the head's index in [0, C/4)
+    const float4 q = *reinterpret_cast<const float4*>(Qb + gi * Sq + 4 * hg);
+    const int r0 = gi * ns_pad;
+    auto key_at = [&](int j, const float* B) {
+      int row, c;
+      if (whole) {
+        const int f = 4 * ns * hs + 4 * j;  // flat index in the group's (ns, C) matrix
+        row = f / C;
+        c = f - row * C;
+      } else {
+        row = hs;
+        c = 4 * j;
+      }
+      return *reinterpret_cast<const float4*>(B + (r0 + row) * Skv + c);
+    };
+    float mx = -__builtin_inff();
+    for (int j = sub; j < ns; j += L) mx = fmaxf(mx, dot4q(q, key_at(j, Kb)) / 2.0f);
+    mx = lane_max<L>(mx);  // softmax (:39)
+    float sum = 0.f;
+    float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int j = sub; j < ns; j += L) {
+      const float e = expf(dot4q(q, key_at(j, Kb)) / 2.0f - mx);
+      sum = sum + e;
+      const float4 v = key_at(j, Vb);
+      o.x = o.x + e * v.x;
+      o.y = o.y + e * v.y;
+      o.z = o.z + e * v.z;
+      o.w = o.w + e * v.w;
+    }
+    sum = lane_sum<L>(sum);
+    o.x = lane_sum<L>(o.x) / sum;  // aᵀ·V_h (:40), a = e / sum
+    o.y = lane_sum<L>(o.y) / sum;
+    o.z = lane_sum<L>(o.z) / sum;
+    o.w = lane_sum<L>(o.w) / sum;
+    float4 pm = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (prm.att_add_max) {  // + reduce_max over ns of X (:296-303)
+      float4 m4 = make_float4(-__builtin_inff(), -__builtin_inff(), -__builtin_inff(),
+                              -__builtin_inff());
+      for (int j = sub; j < ns; j += L) {
+        const float4 x = *reinterpret_cast<const float4*>(X + (r0 + j) * Sx + 4 * hg);
+        m4.x = fmaxf(m4.x, x.x);
+        m4.y = fmaxf(m4.y, x.y);
+        m4.z = fmaxf(m4.z, x.z);
+        m4.w = fmaxf(m4.w, x.w);
+      }
+      pm = make_float4(lane_max<L>(m4.x), lane_max<L>(m4.y), lane_max<L>(m4.z),
+                       lane_max<L>(m4.w));
+    }
+    if (sub == 0 && g < prm.ngroups) {
+      float4 y = o;
+      if (prm.att_scale) {  // batch_norm_for_conv2d, inference (:261)
+        const float4 s4 = *reinterpret_cast<const float4*>(prm.att_scale + 4 * hg);
+        const float4 t4 = *reinterpret_cast<const float4*>(prm.att_shift + 4 * hg);
+        y = make_float4(y.x * s4.x + t4.x, y.y * s4.y + t4.y, y.z * s4.z + t4.z,
+                        y.w * s4.w + t4.w);
+      }
+      if (prm.att_add_max) y = make_float4(y.x + pm.x, y.y + pm.y, y.z + pm.z, y.w + pm.w);
+      *reinterpret_cast<float4*>(prm.out + (size_t)g * C + 4 * hg) = y;
+    }
+  }
+}
+
 // AttentionLayer.call (attention_layer.py:29-45) + batch_norm_for_conv2d (:261) [+ the max pool
 // of :296-303] on the workgroup's groups, from the MLP output X (P rows x C) in LDS.
 // Head h of a group reads the flat block [4*ns*h, 4*ns*(h+1)) of the group's row-major (ns, C)
@@ -388,24 +517,22 @@ PN2_DEV float dot4q(float4 q, float4 k) {
 // are computed whole, one segment); with C = k*4*ns it is the column block h % k of row h / k,
 // so K and V are computed k column segments at a time and each segment completes its heads.
 template <int R>
-PN2_DEV void attention_tail(const Params& prm, float* smem, const float* X, int Sx) {
+PN2_DEV void attention_tail(const Params& prm, float* smem, const float* X, int Sx, int tile) {
   const int tid = threadIdx.x, lane = lane_id(), wave = tid / kWave;
   const int col = lane & 31, h = lane >> 5;
   const int C = prm.L[prm.nl - 1].cout;
-  const int C32 = C / 32;
-  const int ns = prm.ns, ns_pad = 1 << prm.lg_ns_pad;
   const int G = prm.gpw;
   float* Kb = smem + prm.off_k;
   float* Vb = smem + prm.off_v;
   float* Qb = smem + prm.off_q;
-  const int Skv = prm.stride_kv, Sq = prm.stride_q;
-  // query of every group: Dense_q(X[first neighbour]) (:259, :31)
-  for (int to = wave; to < C32; to += kWaves)
-    dense_item(prm.qkv[0], X, Sx, col < G ? col * ns_pad : 0, to, 0, Qb, Sq, col, col < G,
-               lane, h);
-  const int wseg = prm.att_wseg, t_seg = wseg / 32;
-  const bool whole = wseg == C;
-  const int hs_per_group = whole ? C / 4 : ns;  // heads completed by one segment
+  const int Skv = prm.stride_kv;
+  attn_query(prm.qkv[0], X, Sx, G, 1 << prm.lg_ns_pad, Qb, prm.stride_q, C);
+  PN2_STAMP(9);
+  const int t_seg = prm.att_wseg / 32;
+  const int units = G * (prm.att_wseg == C ? C / 4 : prm.ns);
+  int L = 32;  // lanes per unit: the largest power of two <= 32 that keeps the units in one pass
+  while (L > 1 && units * L > kBlock) L >>= 1;
+  while (L > 1 && L > prm.ns) L >>= 1;
   for (int sgi = 0; sgi < prm.att_nseg; ++sgi) {
     // K and V of this column segment (:32-33)
     const int nitems = 2 * R * t_seg;
@@ -417,72 +544,17 @@ PN2_DEV void attention_tail(const Params& prm, float* smem, const float* X, int 
                  32 * rt + col, true, lane, h);
     }
     __syncthreads();
-    // one half-wave per (group, head): scores, softmax over the ns pseudo-keys, weighted V
-    const int units = G * hs_per_group;
-    for (int u = wave * 2 + h; u < units; u += 2 * kWaves) {
-      const int gi = u / hs_per_group, hs = u - gi * hs_per_group;
-      const int g = blockIdx.x * G + gi;
-      const int hg = whole ? hs : (C / wseg) * hs + sgi;  // the head's index in [0, C/4)
-      const float4 q = *reinterpret_cast<const float4*>(Qb + gi * Sq + 4 * hg);
-      const int r0 = gi * ns_pad;
-      auto key_at = [&](int j, const float* B) {
-        int row, c;
-        if (whole) {
-          const int f = 4 * ns * hs + 4 * j;  // flat index in the group's (ns, C) matrix
-          row = f / C;
-          c = f - row * C;
-        } else {
-          row = hs;
-          c = 4 * j;
-        }
-        return *reinterpret_cast<const float4*>(B + (r0 + row) * Skv + c);
-      };
-      float mx = -__builtin_inff();
-      for (int j = col; j < ns; j += 32) mx = fmaxf(mx, dot4q(q, key_at(j, Kb)) / 2.0f);
-      mx = seg_max<32>(mx);  // softmax (:39)
-      float sum = 0.f;
-      float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
-      for (int j = col; j < ns; j += 32) {
-        const float e = expf(dot4q(q, key_at(j, Kb)) / 2.0f - mx);
-        sum = sum + e;
-        const float4 v = key_at(j, Vb);
-        o.x = o.x + e * v.x;
-        o.y = o.y + e * v.y;
-        o.z = o.z + e * v.z;
-        o.w = o.w + e * v.w;
-      }
-      sum = seg_sum<32>(sum);
-      o.x = seg_sum<32>(o.x) / sum;  // aᵀ·V_h (:40), a = e / sum
-      o.y = seg_sum<32>(o.y) / sum;
-      o.z = seg_sum<32>(o.z) / sum;
-      o.w = seg_sum<32>(o.w) / sum;
-      float4 pm = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (prm.att_add_max) {  // + reduce_max over ns of X (:296-303)
-        float4 m4 = make_float4(-__builtin_inff(), -__builtin_inff(), -__builtin_inff(),
-                                -__builtin_inff());
-        for (int j = col; j < ns; j += 32) {
-          const float4 x = *reinterpret_cast<const float4*>(X + (r0 + j) * Sx + 4 * hg);
-          m4.x = fmaxf(m4.x, x.x);
-          m4.y = fmaxf(m4.y, x.y);
-          m4.z = fmaxf(m4.z, x.z);
-          m4.w = fmaxf(m4.w, x.w);
-        }
-        pm = make_float4(seg_max<32>(m4.x), seg_max<32>(m4.y), seg_max<32>(m4.z),
-                         seg_max<32>(m4.w));
-      }
-      if (col == 0 && g < prm.ngroups) {
-        float4 y = o;
-        if (prm.att_scale) {  // batch_norm_for_conv2d, inference (:261)
-          const float4 s4 = *reinterpret_cast<const float4*>(prm.att_scale + 4 * hg);
-          const float4 t4 = *reinterpret_cast<const float4*>(prm.att_shift + 4 * hg);
-          y = make_float4(y.x * s4.x + t4.x, y.y * s4.y + t4.y, y.z * s4.z + t4.z,
-                          y.w * s4.w + t4.w);
-        }
-        if (prm.att_add_max) y = make_float4(y.x + pm.x, y.y + pm.y, y.z + pm.z, y.w + pm.w);
-        *reinterpret_cast<float4*>(prm.out + (size_t)g * C + 4 * hg) = y;
-      }
+    if (sgi == 0) PN2_STAMP(13);
+    switch (L) {
+      case 32: attn_scores<32>(prm, X, Sx, Kb, Vb, Qb, sgi, tile); break;
+      case 16: attn_scores<16>(prm, X, Sx, Kb, Vb, Qb, sgi, tile); break;
+      case 8: attn_scores<8>(prm, X, Sx, Kb, Vb, Qb, sgi, tile); break;
+      case 4: attn_scores<4>(prm, X, Sx, Kb, Vb, Qb, sgi, tile); break;
+      case 2: attn_scores<2>(prm, X, Sx, Kb, Vb, Qb, sgi, tile); break;
+      default: attn_scores<1>(prm, X, Sx, Kb, Vb, Qb, sgi, tile); break;
     }
     __syncthreads();  // the next segment overwrites K and V
+    if (sgi == 0) PN2_STAMP(14);
   }
 }
 
@@ -498,6 +570,7 @@ struct Ctx {
   const float* s_pw;
   int lane, col, h, ns_pad, coutp;
   bool pooled;
+  int tile;  // the workgroup's current tile (a workgroup loops over prm.tpw tiles)
 };
 
 // One item of layer l: the MFMA product, then either the intermediate epilogue (scale,
@@ -582,7 +655,7 @@ PN2_DEV void layer_item(const Ctx& cx, int l, bool last, int to, int rt0, int pa
           if (k >= prm.ns) continue;
           orow = (long long)cx.s_aux[p] * prm.ns + k;
         } else {
-          orow = (long long)blockIdx.x * P + p;
+          orow = (long long)cx.tile * P + p;
         }
         prm.out[orow * Ld.cout + fo] = y[i];
       }
@@ -630,7 +703,7 @@ PN2_DEV void layer_item(const Ctx& cx, int l, bool last, int to, int rt0, int pa
             sm = __uint_as_float(xs[0]) + __uint_as_float(xs[1]);
           }
           if (prm.direct_pool) {  // this row tile holds whole groups: store the final value
-            const int g = blockIdx.x * prm.gpw + rt * gpt + u;
+            const int g = cx.tile * prm.gpw + rt * gpt + u;
             if (h == 0 && g < prm.ngroups && fo < Ld.cout)
               store_pooled(prm, g, fo, Ld.cout, mx, sm);
 #ifdef PN2_MLP_STAMP
@@ -645,6 +718,87 @@ PN2_DEV void layer_item(const Ctx& cx, int l, bool last, int to, int rt0, int pa
       }
     }
   }
+}
+
+// Per-slot metadata in two steps so a multi-tile workgroup can issue the next unit's global
+// loads (neighbour index, or three_nn distances and indices) while the current unit's layers
+// run: fetch_meta only loads, commit_meta computes and writes the slot tables into LDS.
+struct MetaPf {
+  int i0, i1, i2;
+  float d0, d1, d2;
+};
+
+template <int SRC, int P>
+PN2_DEV MetaPf fetch_meta(const Params& prm, int tile, int pass, int p) {
+  MetaPf f{-1, 0, 0, 0.f, 0.f, 0.f};
+  if (SRC == kSrcGroup) {
+    const int ns_pad = 1 << prm.lg_ns_pad;
+    const int g = prm.passes == 1 ? tile * prm.gpw + (p >> prm.lg_ns_pad) : tile;
+    const int k = prm.passes == 1 ? (p & (ns_pad - 1)) : pass * P + p;
+    if (g < prm.ngroups) {
+      const int kk = k < prm.ns ? k : 0;  // padding slots repeat the first neighbour
+      f.i0 = prm.idx[(size_t)g * prm.ns + kk];
+    }
+  } else if (SRC == kSrcFP) {
+    const long long row = (long long)tile * P + p;
+    if (row < prm.rows) {
+      const float* d = prm.dist + row * 3;
+      const int32_t* ii = prm.nn + row * 3;
+      f.d0 = d[0];
+      f.d1 = d[1];
+      f.d2 = d[2];
+      f.i0 = ii[0];
+      f.i1 = ii[1];
+      f.i2 = ii[2];
+    }
+  }
+  return f;
+}
+
+template <int SRC, int P>
+PN2_DEV void commit_meta(const Params& prm, int tile, int pass, int p, const MetaPf& f,
+                         int* s_src, int* s_aux, float* s_pw, float* s_fw, int* s_fi) {
+  int src = -1, aux = 0;
+  float pw = 0.f;
+  if (SRC == kSrcGroup) {
+    const int ns_pad = 1 << prm.lg_ns_pad;
+    const int g = prm.passes == 1 ? tile * prm.gpw + (p >> prm.lg_ns_pad) : tile;
+    const int k = prm.passes == 1 ? (p & (ns_pad - 1)) : pass * P + p;
+    if (g < prm.ngroups) {
+      const int b = g / prm.M;
+      src = b * prm.N + f.i0;
+      aux = g;
+      if (k < prm.ns) {
+        pw = 1.f;
+        if (prm.pool == PN2_POOL_WEIGHTED_AVG) {
+          // exp(-5 |grouped_xyz|) (pointnet_util.py:136-137)
+          const float* q = prm.xyz + (size_t)src * 3;
+          const float* c = prm.new_xyz + (size_t)g * 3;
+          const float dx = q[0] - c[0], dy = q[1] - c[1], dz = q[2] - c[2];
+          pw = expf(-sqrtf((dx * dx + dy * dy) + dz * dz) * 5.0f);
+        }
+      }
+    }
+  } else {
+    const long long row = (long long)tile * P + p;
+    if (row < prm.rows) {
+      src = (int)row;
+      if (SRC == kSrcFP) {
+        const int b = (int)(row / prm.n);
+        float w1, w2, w3;
+        idw3(f.d0, f.d1, f.d2, w1, w2, w3);
+        s_fw[3 * p] = w1;
+        s_fw[3 * p + 1] = w2;
+        s_fw[3 * p + 2] = w3;
+        s_fi[3 * p] = b * prm.m + f.i0;
+        s_fi[3 * p + 1] = b * prm.m + f.i1;
+        s_fi[3 * p + 2] = b * prm.m + f.i2;
+      }
+    }
+  }
+  s_src[p] = src;
+  s_aux[p] = aux;
+  s_pw[p] = pw;
 }
 
 template <int SRC, int R, bool WL>
@@ -672,8 +826,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2, 2))) 
   const LayerDev& LL = prm.L[prm.nl - 1];
   const int coutp = LL.cout32 * 32;
   const float* wl = WL ? smem + prm.off_w : nullptr;
-  const Ctx ctx{&prm, wl, act0, act1, part, s_src, s_aux, s_pw, lane, col, h, ns_pad, coutp,
-                pooled};
+  Ctx ctx{&prm, wl, act0, act1, part, s_src, s_aux, s_pw, lane, col, h, ns_pad, coutp,
+          pooled, 0};
   if (WL) {
     // every layer's packed block into LDS once; the loads overlap the metadata phase and
     // the first barrier publishes them
@@ -695,61 +849,20 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     }
   }
 
+  // Tiles of this workgroup: prm.tpw consecutive tiles (adjacent groups share cached
+  // points; weights staged in LDS are loaded once for all of them).
+  const int t_begin = (int)blockIdx.x * prm.tpw;
+  const int t_end = min(t_begin + prm.tpw, prm.ntiles);
+  // metadata of the first unit; later units' loads are issued one unit ahead (below)
+  MetaPf pf{};
+  if (t_begin < t_end && tid < P) pf = fetch_meta<SRC, P>(prm, t_begin, 0, tid);
+
   PN2_STAMP(0);
+  for (int tile = t_begin; tile < t_end; ++tile)
   for (int pass = 0; pass < prm.passes; ++pass) {
+    ctx.tile = tile;
     // ---- 1. per-slot metadata -----------------------------------------------------------
-    if (tid < P) {
-      const int p = tid;
-      int src = -1, aux = 0;
-      float pw = 0.f;
-      if (SRC == kSrcGroup) {
-        int g, k;
-        if (prm.passes == 1) {
-          g = blockIdx.x * prm.gpw + (p >> prm.lg_ns_pad);
-          k = p & (ns_pad - 1);
-        } else {
-          g = blockIdx.x;
-          k = pass * P + p;
-        }
-        if (g < prm.ngroups) {
-          const int b = g / prm.M;
-          const int kk = k < prm.ns ? k : 0;  // padding slots repeat the first neighbour
-          src = b * prm.N + prm.idx[(size_t)g * prm.ns + kk];
-          aux = g;
-          if (k < prm.ns) {
-            pw = 1.f;
-            if (prm.pool == PN2_POOL_WEIGHTED_AVG) {
-              // exp(-5 |grouped_xyz|) (pointnet_util.py:136-137)
-              const float* q = prm.xyz + (size_t)src * 3;
-              const float* c = prm.new_xyz + (size_t)g * 3;
-              const float dx = q[0] - c[0], dy = q[1] - c[1], dz = q[2] - c[2];
-              pw = expf(-sqrtf((dx * dx + dy * dy) + dz * dz) * 5.0f);
-            }
-          }
-        }
-      } else {
-        const long long row = (long long)blockIdx.x * P + p;
-        if (row < prm.rows) {
-          src = (int)row;
-          if (SRC == kSrcFP) {
-            const int b = (int)(row / prm.n);
-            const float* d = prm.dist + row * 3;
-            const int32_t* ii = prm.nn + row * 3;
-            float w1, w2, w3;
-            idw3(d[0], d[1], d[2], w1, w2, w3);
-            s_fw[3 * p] = w1;
-            s_fw[3 * p + 1] = w2;
-            s_fw[3 * p + 2] = w3;
-            s_fi[3 * p] = b * prm.m + ii[0];
-            s_fi[3 * p + 1] = b * prm.m + ii[1];
-            s_fi[3 * p + 2] = b * prm.m + ii[2];
-          }
-        }
-      }
-      s_src[p] = src;
-      s_aux[p] = aux;
-      s_pw[p] = pw;
-    }
+    if (tid < P) commit_meta<SRC, P>(prm, tile, pass, tid, pf, s_src, s_aux, s_pw, s_fw, s_fi);
     if (pooled && prm.pool == PN2_POOL_WEIGHTED_AVG && pass == 0) {
       // normaliser sum(exp(-5|grouped_xyz|)) over the group's ns entries (:138-139)
       if (prm.passes == 1) {
@@ -761,7 +874,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2, 2))) 
           if (lane == 0) s_norm[gi] = v;
         }
       } else {
-        const int g = blockIdx.x;
+        const int g = tile;
         const int b = g / prm.M;
         const float* c = prm.new_xyz + (size_t)g * 3;
         float v = 0.f;
@@ -787,6 +900,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     gather_rows<SRC, P>(prm, act0, s_src, s_aux, s_fw, s_fi);
     __syncthreads();
     PN2_STAMP(2);
+    // the next unit's metadata loads, in flight while this unit's layers run
+    {
+      const bool more_passes = pass + 1 < prm.passes;
+      const int nt = more_passes ? tile : tile + 1, np = more_passes ? pass + 1 : 0;
+      if (nt < t_end && tid < P) pf = fetch_meta<SRC, P>(prm, nt, np, tid);
+    }
 
     // ---- 3. the layers ------------------------------------------------------------------
     // An item = one 32-column output tile over RG of the R row tiles; layers narrower than
@@ -810,7 +929,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2, 2))) 
 
     if constexpr (SRC == kSrcGroup) {
       if (prm.attn) attention_tail<R>(prm, smem, (prm.nl & 1) ? act1 : act0,
-                                      (prm.nl & 1) ? prm.stride1 : prm.stride0);
+                                      (prm.nl & 1) ? prm.stride1 : prm.stride0, tile);
     }
 
     // ---- 4. pooling: combine the row-tile partials of each group, store -----------------
@@ -820,7 +939,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2, 2))) 
       const int ngr = prm.passes == 1 ? prm.gpw : 1;
       const int lg = prm.lg_ns_pad;
       for (int gi = 0; gi < ngr; ++gi) {
-        const int g = prm.passes == 1 ? blockIdx.x * prm.gpw + gi : blockIdx.x;
+        const int g = prm.passes == 1 ? tile * prm.gpw + gi : tile;
         if (g >= prm.ngroups) break;
         int rt0, nrt, u;
         if (prm.passes > 1) { rt0 = 0; nrt = R; u = 0; }
@@ -978,23 +1097,62 @@ int check_layers(int nl, const pn2_mlp_layer* layers, int cin0) {
   return PN2_OK;
 }
 
+// Compute units of the current device (cached per device id).
+int device_cus() {
+  static int cache[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  if (!cache[dev]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 0;
+    cache[dev] = n;
+  }
+  return cache[dev];
+}
+
 // Dynamic LDS beyond the 64 KiB default is opted into once per instantiation.
 template <int SRC, int R, bool WL>
 int launch_one(Params prm, long long nblocks, size_t lds, hipStream_t s) {
-#ifdef PN2_MLP_STAMP
-  prm.stamp = g_stamp;
-#endif
   static const hipError_t attr = hipFuncSetAttribute(
       reinterpret_cast<const void*>(&mlp_kernel<SRC, R, WL>),
       hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsLimit);
   if (attr != hipSuccess) return (int)attr;
-  hipLaunchKernelGGL((mlp_kernel<SRC, R, WL>), dim3((unsigned)nblocks), dim3(kBlock), lds, s,
-                     prm);
+  prm.ntiles = (int)nblocks;
+  // Several consecutive tiles per workgroup (weights staged once, the next tile's metadata
+  // loads overlapping the current tile's layers), but only as many as keep >= 4 rounds of
+  // workgroups: the dispatcher then still balances around CUs that other streams' kernels
+  // hold (a grid of exactly the co-resident slots with static tile ranges waited for the SA1
+  // sampler's CUs in the whole-model pipeline).
+  prm.tpw = 1;
+  static const int max_tpw = [] {  // tuning overrides (scripts/ab_tpw.sh)
+    const char* e = std::getenv("PN2_MLP_TPW");
+    return e ? std::atoi(e) : 8;
+  }();
+  static const int rounds = [] {
+    const char* e = std::getenv("PN2_MLP_ROUNDS");
+    return e ? std::atoi(e) : 4;
+  }();
+  const long long slots = (long long)device_cus() * (lds * 2 <= kLdsLimit ? 2 : 1);
+  while (slots > 0 && prm.tpw * 2 <= max_tpw && nblocks >= slots * rounds * prm.tpw * 2)
+    prm.tpw *= 2;
+  long long grid = (nblocks + prm.tpw - 1) / prm.tpw;
+#ifdef PN2_MLP_STAMP
+  prm.stamp = g_stamp;
+  prm.tpw = 1;  // one tile per workgroup: the stamps are per tile
+  grid = nblocks;
+#endif
+  hipLaunchKernelGGL((mlp_kernel<SRC, R, WL>), dim3((unsigned)grid), dim3(kBlock), lds, s, prm);
   PN2_RETURN_LAUNCH();
 }
 
 template <int SRC>
 int launch_rows_R(Params& prm, int R, long long nblocks, size_t lds, hipStream_t s) {
+  static const bool trace = std::getenv("PN2_MLP_TRACE") != nullptr;  // tuning diagnostics
+  if (trace)
+    std::fprintf(stderr, "pn2_mlp: src %d R %d wl %d blocks %lld lds %zu gpw %d passes %d "
+                 "attn %d nseg %d\n", SRC, R, prm.wfloats ? 1 : 0, nblocks, lds, prm.gpw,
+                 prm.passes, prm.attn, prm.att_nseg);
   if (nblocks <= 0) return PN2_OK;
   if (nblocks > 0x7fffffffLL) return PN2_EINVAL;
   if (prm.wfloats) {  // weights staged in LDS (small MLPs of the SA layers)

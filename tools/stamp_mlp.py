@@ -4,7 +4,8 @@ stamped build csrc/build/libpn2hip_stamp.so, `make -C .../csrc stamp`).
 
 For the whole-model layer shapes (SA1..SA4 group + MLP + pool, FP1..FP4 interpolation + MLP)
 prints, averaged over the first 4096 workgroups: metadata, gather, each layer, pooling (in
-s_memtime ticks and as a share of the workgroup's life)."""
+s_memtime ticks and as a share of the workgroup's life). --attention: the cfg3 model's
+attention SA layers, with the tail split into query, K/V products and scores/softmax."""
 import ctypes
 import importlib
 import json
@@ -27,7 +28,8 @@ lib.pn2_mlp_set_stamp.argtypes = [ctypes.c_void_p]
 lib.pn2_mlp_set_stamp.restype = None
 dev = torch.device("cuda:0")
 B = 16
-inp = S.make_inputs("cfg2", list(range(B)), dev, model=True)
+ATTN = "--attention" in sys.argv  # cfg3: rgb+normals, attention pooling in every SA
+inp = S.make_inputs("cfg3" if ATTN else "cfg2", list(range(B)), dev, model=True)
 mdl = inp["model"]
 xyz = [inp["xyz"]]
 for (m, _, _, _) in S.SSG_SA:
@@ -63,7 +65,13 @@ def run(name, fn, nl):
     for l in range(nl):
         ph[f"L{l + 1}"] = t[:, 3 + l] - t[:, prev]
         prev = 3 + l
-    ph["pool"] = t[:, 15] - t[:, prev]
+    if ATTN and name.startswith("SA"):  # attention tail: query, K/V (segment 0), scores
+        ph["attn_q"] = t[:, 9] - t[:, prev]
+        ph["attn_kv"] = t[:, 13] - t[:, 9]
+        ph["attn_scores"] = t[:, 14] - t[:, 13]
+        ph["attn_rest"] = t[:, 15] - t[:, 14]
+    else:
+        ph["pool"] = t[:, 15] - t[:, prev]
     sub = t[(t[:, 10] > 0) & (t[:, 11] > 0) & (t[:, 12] > 0)]
     if len(sub):  # the last layer's first item of wave 0 (stamped builds): MMA, epilogue
         ph["last_item_mma"] = sub[:, 11] - sub[:, 10]
@@ -77,11 +85,15 @@ def run(name, fn, nl):
           flush=True)
 
 
-pts = [None] + [feats(m, c) for (m, _, _, c) in S.SSG_SA]
+pts = [inp["feats"]] + [feats(m, c) for (m, _, _, c) in S.SSG_SA]
 for i, (m, r, ns, _) in enumerate(S.SSG_SA):
     idx, _ = pkg.tf_grouping.query_ball_point(r, ns, xyz[i], xyz[i + 1])
-    run(f"SA{i + 1}", lambda: pu.group_mlp(xyz[i], pts[i], xyz[i + 1], idx, mdl.sa[i], "max"),
-        len(mdl.sa[i].layers))
+    if ATTN:
+        fn = lambda: pkg.attention_layer.group_mlp_attention(  # noqa: E731
+            xyz[i], pts[i], xyz[i + 1], idx, mdl.sa[i], mdl.store, f"layer{i + 1}")
+    else:
+        fn = lambda: pu.group_mlp(xyz[i], pts[i], xyz[i + 1], idx, mdl.sa[i], "max")  # noqa: E731
+    run(f"SA{i + 1}", fn, len(mdl.sa[i].layers))
 p2 = pts[4]
 for k in range(4 if "--fp" in sys.argv else 0):
     lvl = 3 - k
