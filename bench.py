@@ -109,8 +109,10 @@ def main():
                     help="launch every op from Python instead of replaying the captured hipGraphs")
     ap.add_argument("--no-overlap", action="store_true",
                     help="run the whole step on one stream (no side stream beside the sampler chain)")
-    ap.add_argument("--time-every", type=int, default=1,
-                    help="bracket every Nth timed step's SA1 sampler with HIP events (diagnostic)")
+    ap.add_argument("--time-every", type=int, default=10,
+                    help="bracket every Nth timed step's SA1 sampler with HIP events (the "
+                         "roofline's launch time is their mean; two event packets on lane 0 "
+                         "per bracketed step cost ~10 us of step time, DESIGN.md §5)")
     ap.add_argument("--sets", type=int, default=3,
                     help="buffer sets the pipelined steps rotate over (>= 2)")
     ap.add_argument("--no-pipeline", action="store_true",
