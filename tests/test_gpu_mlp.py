@@ -303,3 +303,52 @@ def test_fused_attention_matches_unfused(env, widths, ns, add_max):
         ref = al.sa_attention_tail(X, store, "s", C, add_max)
     assert got.shape == (2, 128, C)
     np.testing.assert_allclose(got.cpu().numpy(), ref.cpu().numpy(), rtol=1e-4, atol=2e-5)
+
+
+def test_multi_tile_workgroups_full_batch(env):
+    """The whole-batch launches of the model (B = 16 clouds of 8,192 points) are the only ones
+    large enough for several tiles per workgroup (csrc/mlp.hip launch_one: tpw doubles while
+    the grid keeps >= 4 rounds of 2 workgroups on each of the 256 CUs): SA1 (4,096 tiles of
+    128 rows -> 2 tiles per workgroup, weights staged in LDS) and SA2 (4,096 tiles of 32 rows).
+    Same f64 bar as above."""
+    pkg, O, torch, dev = env
+    B, N = 16, 8192
+    xyz, _ = pkg.synth.batch(range(40, 40 + B), N, "scannet")
+    rng = np.random.default_rng(16)
+    T = lambda a: None if a is None else torch.from_numpy(a).to(dev)  # noqa: E731
+    x1 = O.gather_point(xyz, O.fps(xyz, 1024))
+    for (src, nxt, M, r, C, widths) in [(xyz, x1, 1024, 0.1, 0, [32, 32, 64]),
+                                        (x1, None, 256, 0.2, 64, [64, 64, 128])]:
+        new_xyz = nxt if nxt is not None else O.gather_point(src, O.fps(src, M))
+        idx, _ = O.ball_query(src, new_xyz, r, 32)
+        points = rng.uniform(-1, 1, (B, src.shape[1], C)).astype(np.float32) if C else None
+        grouped, gxyz = O.group_concat(src, points, new_xyz, idx)
+        layers = make_layers(rng, grouped.shape[-1], widths)
+        got = pkg.pointnet_util.group_mlp(T(src), T(points), T(new_xyz), T(idx),
+                                          fused(pkg, layers), "max").cpu().numpy()
+        ref64 = O.pool_f64(O.mlp_f64(grouped, layers), gxyz, "max")
+        ref32 = O.pool_f64(mlp_f32(grouped, layers), gxyz, "max")
+        assert_close(got, ref64, ref32, f"group_mlp B=16 M={M}")
+
+
+def test_multi_tile_attention_full_batch(env):
+    """The cfg3 SA1 attention launch (B = 16, 8,192 tiles of 64 rows -> 4 tiles per workgroup)
+    against the unfused composition, as test_fused_attention_matches_unfused."""
+    pkg, O, torch, dev = env
+    al, tu, pu = pkg.attention_layer, pkg.tf_util, pkg.pointnet_util
+    xyz_np, feats_np = pkg.synth.batch(range(60, 76), 8192, "scannet", with_features=True)
+    xyz, pts = torch.from_numpy(xyz_np).to(dev), torch.from_numpy(feats_np).to(dev)
+    store = tu.ParamStore(seed=23)
+    g = np.random.default_rng(64)
+    for k, (lo, hi) in {"moving_mean": (-.1, .1), "moving_variance": (.5, 2), "gamma": (.5, 1.5),
+                        "beta": (-.2, .2)}.items():
+        store[f"s/s/{k}"] = torch.from_numpy(g.uniform(lo, hi, 64).astype(np.float32))
+    with torch.no_grad():
+        new_xyz = pkg.tf_sampling.farthest_point_sample_and_gather(1024, xyz)[1]
+        idx, _ = pkg.tf_grouping.query_ball_point(0.1, 32, xyz, new_xyz)
+        mlp = tu.packed_mlp(store, [f"s/conv{i}" for i in range(3)], 9, [32, 32, 64])
+        got = al.group_mlp_attention(xyz, pts, new_xyz, idx, mlp, store, "s", False)
+        X = pu.group_mlp(xyz, pts, new_xyz, idx, mlp, None)
+        ref = al.sa_attention_tail(X, store, "s", 64, False)
+    assert got.shape == (16, 1024, 64)
+    np.testing.assert_allclose(got.cpu().numpy(), ref.cpu().numpy(), rtol=1e-4, atol=2e-5)
