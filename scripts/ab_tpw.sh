@@ -4,8 +4,6 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_gpu_mlp.py tests/test_gpu_model.py -x -q --timeout 200 --timeout-method thread > gpurun_out/tpw_tests.log 2>&1
-rc=$?; tail -2 gpurun_out/tpw_tests.log; [ $rc -eq 0 ] || exit $rc
 for v in "1 4" "8 4" "8 2" "8 1"; do
   set -- $v
   for cfg in cfg2 cfg3; do
