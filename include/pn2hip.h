@@ -8,6 +8,7 @@
  *   FarthestPointSample  tf_sampling.cpp:94-123, .cu:105-170     → pn2_fps (+_gather, _chain)
  *   GatherPoint          tf_sampling.cpp:125-148, .cu:172-181    → pn2_gather_point
  *   GatherPointGrad      tf_sampling.cpp:150-178, .cu:183-192    → pn2_gather_point_grad
+ *   ProbSample           tf_sampling.cpp:66-92, .cu:7-104,197-201 → pn2_prob_sample
  *   QueryBallPoint       tf_grouping.cpp:66-106, _g.cu:3-36      → pn2_ball_query,
  *                                                                  pn2_ball_query_grid
  *   SelectionSort        tf_grouping.cpp:108-137, _g.cu:83-123   → pn2_select_top_k
@@ -122,6 +123,15 @@ int pn2_gather_point(const float* inp, const int32_t* idx, int B, int N, int M, 
  * (tf_sampling.cpp:174). Float atomics: summation order is not fixed. */
 int pn2_gather_point_grad(const float* out_g, const int32_t* idx, int B, int N, int M,
                           float* inp_g, pn2_stream_t stream);
+/* Categorical sampling (ProbSample). inp (B,N) weights, inpr (B,M) uniform draws in [0,1) →
+ * out (B,M): per row, the first index whose inclusive prefix sum of inp reaches
+ * inpr * (the row total), found by the reference's binary search (tf_sampling_g.cu:90-104).
+ * The prefix sum repeats cumsumKernel's fp32 addition order (:7-88), so the indices equal
+ * the reference's. workspace: pn2_prob_sample_workspace_size(B, N) bytes (the prefix sums,
+ * tf_sampling.cpp:85-88). N = 0 with M > 0 is rejected (the reference reads cum[-1]). */
+size_t pn2_prob_sample_workspace_size(int B, int N);
+int pn2_prob_sample(const float* inp, const float* inpr, int B, int N, int M, float* workspace,
+                    size_t workspace_bytes, int32_t* out, pn2_stream_t stream);
 
 /* ---------------------------------------------------------------- grouping -------------- */
 

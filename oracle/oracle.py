@@ -25,6 +25,7 @@ _P, _I, _F = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
 _ORACLE_SIGS = {
     "pn2o_selection_sort": [_P, _I, _I, _I, _I, _P, _P],
     "pn2o_knn_point": [_P, _P, _I, _I, _I, _I, _I, _P, _P],
+    "pn2o_prob_sample": [_P, _P, _I, _I, _I, _P],
     "pn2o_set_threads": [_I],
     "pn2o_fps": [_P, _I, _I, _I, _P],
     "pn2o_gather_point": [_P, _P, _I, _I, _I, _P],
@@ -52,6 +53,7 @@ _REF_CPU_SIGS = {
 _REF_GPU_SIGS = {
     "pn2ref_selection_sort": [_P, _I, _I, _I, _I, _P, _P],
     "pn2ref_fps": [_P, _I, _I, _I, _P],
+    "pn2ref_prob_sample": [_P, _P, _I, _I, _I, _P],
     "pn2ref_gather_point": [_P, _P, _I, _I, _I, _P],
     "pn2ref_query_ball_point": [_P, _P, _I, _I, _I, _F, _I, _P, _P],
     "pn2ref_group_point": [_P, _P, _I, _I, _I, _I, _I, _P],
@@ -380,6 +382,17 @@ def knn_point(k, xyz1, xyz2):
     idx = np.zeros((B, m, k), np.int32)
     olib().pn2o_knn_point(_p(xyz1), _p(xyz2), B, n, m, c, int(k), _p(val), _p(idx))
     return val, idx
+
+
+def prob_sample(inp, inpr):
+    """prob_sample(inp (B,n), inpr (B,m)) -> (B,m) int32 (tf_sampling.py:14-23)."""
+    inp, inpr = _f32(inp), _f32(inpr)
+    B, n = inp.shape
+    m = inpr.shape[1]
+    out = np.zeros((B, m), np.int32)
+    if B and m:
+        olib().pn2o_prob_sample(_p(inp), _p(inpr), B, n, m, _p(out))
+    return out
 
 
 def run_stack_cpu(inp_np, config):

@@ -426,3 +426,76 @@ void pn2o_knn_point(const float* xyz1, const float* xyz2, int B, int n, int m, i
     free(p);
   }
 }
+
+/* ------------------------------------------------------------- prob_sample ------------- */
+/* ProbSample (tf_sampling.py:14-23 -> ProbSampleGpuOp tf_sampling.cpp:66-92 ->
+ * probsampleLauncher tf_sampling_g.cu:197-201): cumsumKernel (:7-88) then
+ * binarysearchKernel (:90-104). The cumsum's fp32 addition order is a fixed function of n,
+ * restated here sequentially:
+ *  - chunks of 8192 (BlockSize*4, :8, :13); per chunk, 4-element prefixes
+ *    v2+=v1, v4+=v3, v3+=v2, v4+=v2 (:18-25), a trailing partial quad summed left to right
+ *    and repeated into the padding (:32-40);
+ *  - the quad totals scanned by the tree of :43-64 (pairs ((2k+2)<<u)-1 += ((2k+1)<<u)-1 up,
+ *    then ((2k+3)<<u)-1 += ((2k+2)<<u)-1 down; the pairs of one level are independent);
+ *  - each quad's values += the previous quad's inclusive total (:66-74), out = value +
+ *    running sum (:77-79), and the chunk total carried with Kahan compensation (:80-83).
+ * binarysearchKernel: q = r * cum[n-1]; r0 = n-1, steps k = base..1 (base = the smallest
+ * power of two >= n): if (r0 >= k && cum[r0-k] >= q) r0 -= k. */
+#define PS_CHUNK 8192
+void pn2o_prob_sample(const float* inp, const float* inpr, int B, int N, int M, int32_t* out) {
+  RFOR
+  for (int b = 0; b < B; ++b) {
+    const float* x = inp + (size_t)b * N;
+    float* cum = (float*)malloc(sizeof(float) * (N > 0 ? N : 1));
+    float* quad = (float*)malloc(sizeof(float) * PS_CHUNK);
+    float* tot = (float*)malloc(sizeof(float) * (PS_CHUNK / 4));
+    float run = 0.f, comp = 0.f;
+    for (int j = 0; j < N; j += PS_CHUNK) {
+      const int len = N - j < PS_CHUNK ? N - j : PS_CHUNK;
+      const int len4 = (len + 3) & ~3;
+      const int nq = len4 >> 2;
+      for (int k = 0; k < len; k += 4) {
+        if (k + 3 < len) {
+          float v1 = x[j + k], v2 = x[j + k + 1], v3 = x[j + k + 2], v4 = x[j + k + 3];
+          v2 += v1;
+          v4 += v3;
+          v3 += v2;
+          v4 += v2;
+          quad[k] = v1; quad[k + 1] = v2; quad[k + 2] = v3; quad[k + 3] = v4;
+          tot[k >> 2] = v4;
+        } else {
+          float v = 0.f;
+          for (int k2 = k; k2 < len; ++k2) { v += x[j + k2]; quad[k2] = v; }
+          for (int k2 = len; k2 < len4; ++k2) quad[k2] = v;
+          tot[k >> 2] = v;
+        }
+      }
+      int u = 0;
+      for (; (2 << u) <= nq; ++u)
+        for (int k = 0; k < (nq >> (u + 1)); ++k)
+          tot[(((k << 1) + 2) << u) - 1] += tot[(((k << 1) + 1) << u) - 1];
+      for (--u; u >= 0; --u)
+        for (int k = 0; k < ((nq - (1 << u)) >> (u + 1)); ++k)
+          tot[(((k << 1) + 3) << u) - 1] += tot[(((k << 1) + 2) << u) - 1];
+      for (int q = 1; q < nq; ++q)
+        for (int e = 0; e < 4; ++e) quad[4 * q + e] += tot[q - 1];
+      for (int k = 0; k < len; ++k) cum[j + k] = quad[k] + run;
+      const float t = tot[nq - 1] + comp;
+      const float r2 = run + t;
+      comp = t - (r2 - run);
+      run = r2;
+    }
+    int base = 1;
+    while (base < N) base <<= 1;
+    for (int i = 0; i < M; ++i) {
+      const float q = inpr[(size_t)b * M + i] * cum[N - 1];
+      int r = N - 1;
+      for (int k = base; k >= 1; k >>= 1)
+        if (r >= k && cum[r - k] >= q) r -= k;
+      out[(size_t)b * M + i] = r;
+    }
+    free(cum);
+    free(quad);
+    free(tot);
+  }
+}

@@ -16,6 +16,8 @@ void queryBallPointLauncher(int b, int n, int m, float radius, int nsample, cons
 void groupPointLauncher(int b, int n, int c, int m, int nsample, const float* points,
                         const int* idx, float* out);
 void selectionSortLauncher(int b, int n, int m, int k, const float* dist, int* outi, float* out);
+void probsampleLauncher(int b, int n, int m, const float* inp_p, const float* inp_r, float* temp,
+                        int* out);
 
 extern "C" {
 // tf_sampling.cpp:114-118: temp workspace of 32 x n floats
@@ -24,6 +26,16 @@ int pn2ref_fps(const float* xyz, int b, int n, int m, int32_t* out) {
   hipError_t e = hipMalloc(&temp, sizeof(float) * 32 * (size_t)(n > 0 ? n : 1));
   if (e != hipSuccess) return (int)e;
   farthestpointsamplingLauncher(b, n, m, xyz, temp, out);
+  e = hipDeviceSynchronize();
+  (void)hipFree(temp);
+  return (int)e;
+}
+// tf_sampling.cpp:85-89: temp workspace of b x n floats (the cumsum)
+int pn2ref_prob_sample(const float* inp, const float* inpr, int b, int n, int m, int32_t* out) {
+  float* temp = nullptr;
+  hipError_t e = hipMalloc(&temp, sizeof(float) * (size_t)(b > 0 ? b : 1) * (n > 0 ? n : 1));
+  if (e != hipSuccess) return (int)e;
+  probsampleLauncher(b, n, m, inp, inpr, temp, out);
   e = hipDeviceSynchronize();
   (void)hipFree(temp);
   return (int)e;

@@ -1,9 +1,6 @@
-"""Farthest point sampling and gather_point — drop-in for
+"""Farthest point sampling, gather_point and prob_sample — drop-in for
 pointnet2_tensorflow/tf_ops/sampling/tf_sampling.py (same names, argument order, shapes,
 dtypes and error messages), running the gfx950 kernels of libpn2hip.so.
-
-prob_sample is not provided: no model of the reference calls it (only the __main__ demo of
-tf_sampling.py:61-90).
 """
 import ctypes
 
@@ -33,6 +30,31 @@ def _fps(npoint, inp, want_xyz):
         rc = L.pn2_fps_gather(ptr(inp), B, N, npoint, ptr(idx), ptr(new_xyz), stream_of(inp))
     check(rc, "FarthestPointSample")
     return idx, new_xyz
+
+
+def prob_sample(inp, inpr):
+    """tf_sampling.py:14-23 (ProbSample, no gradient).
+
+    input: (batch_size, ncategory) float32 weights, (batch_size, npoints) float32 uniform draws
+    returns: (batch_size, npoints) int32 — per draw r, the first category whose inclusive
+    prefix sum reaches r * (the row total), with the reference's fp32 prefix-sum order
+    """
+    if inp.dim() != 2:  # tf_sampling.cpp:76
+        raise InvalidArgumentError("ProbSample expects (batch_size,num_choices) inp shape")
+    if inpr.dim() != 2 or inpr.shape[0] != inp.shape[0]:  # tf_sampling.cpp:79
+        raise InvalidArgumentError("ProbSample expects (batch_size,num_points) inpr shape")
+    inp = device_tensor(inp, "inp", torch.float32)
+    inpr = device_tensor(inpr, "inpr", torch.float32)
+    B, N, M = int(inp.shape[0]), int(inp.shape[1]), int(inpr.shape[1])
+    out = torch.empty((B, M), dtype=torch.int32, device=inp.device)
+    if B == 0 or M == 0:
+        return out
+    L = lib()
+    ws_bytes = L.pn2_prob_sample_workspace_size(B, N)
+    ws = torch.empty(max(1, ws_bytes // 4), dtype=torch.float32, device=inp.device)
+    check(L.pn2_prob_sample(ptr(inp), ptr(inpr), B, N, M, ptr(ws), ws_bytes, ptr(out),
+                            stream_of(inp)), "ProbSample")
+    return out
 
 
 def farthest_point_sample(npoint, inp):

@@ -5,10 +5,11 @@ The reference kernels (pointnet2_tensorflow/tf_ops/sampling/tf_sampling_g.cu:105
 grouping/tf_grouping_g.cu:3-57) are compiled UNCHANGED for gfx950 into oracle/_ref/libref_gpu.so
 (oracle/Makefile target `ref`, built in the container that has /root/reference; the .so then
 travels to the GPU box with the repo snapshot). Run on the MI355X:
-    python tests/golden/make_golden_gpu.py [out_dir]   (default: tests/golden)
+    python tests/golden/make_golden_gpu.py [out_dir] [--prob-only]   (default: tests/golden)
 Nothing here reads /root/reference. Outputs:
     fps_*.npz   farthest_point_sample + gather_point of the reference kernels
     bqg_*.npz   query_ball_point of the reference kernel WITH its pts_cnt output
+    prob_*.npz  prob_sample (cumsumKernel + binarysearchKernel, tf_sampling_g.cu:7-104)
 Inputs are deterministic (synth.py SplitMix64 / fixed lattices). Cases follow SURVEY.md §8(c):
 cfg1, one SA1 crop with duplicates, the N>3072 global-memory branch of the reference FPS
 (tf_sampling_g.cu:133-141), N<512, N=1, npoint > #unique points, all-duplicate clouds and a
@@ -32,7 +33,8 @@ from oracle import oracle as O  # noqa: E402
 pkg = importlib.import_module("pointcloud-segmentation-attention_amd")
 synth = pkg.synth
 DEV = torch.device("cuda:0")
-OUT = sys.argv[1] if len(sys.argv) > 1 else HERE  # the GPU box merges back only gpurun_out/
+_ARGS = [a for a in sys.argv[1:] if not a.startswith("--")]
+OUT = _ARGS[0] if _ARGS else HERE  # the GPU box merges back only gpurun_out/
 
 
 def save(name, meta, **arrays):
@@ -89,9 +91,43 @@ def sel_case(name, d, k, src):
          dist=d, outi=outi.cpu().numpy(), out=out.cpu().numpy())
 
 
+def prob_case(name, w, r, src):
+    B, n = w.shape
+    m = r.shape[1]
+    wt, rt = torch.from_numpy(w).to(DEV), torch.from_numpy(r).to(DEV)
+    out = torch.full((B, m), -1, dtype=torch.int32, device=DEV)
+    assert O.ref_gpu().pn2ref_prob_sample(wt.data_ptr(), rt.data_ptr(), B, n, m,
+                                          out.data_ptr()) == 0
+    save(name, {"op": "prob_sample", "inputs": src,
+                "ref": "tf_sampling_g.cu:7-104,197-201 (cumsumKernel, binarysearchKernel) "
+                       "compiled for gfx950"},
+         inp=w, inpr=r, out=out.cpu().numpy())
+
+
+def prob_cases():
+    rng = np.random.default_rng(13)
+    f32 = lambda a: np.ascontiguousarray(a, np.float32)  # noqa: E731
+    prob_case("prob_uniform", f32(rng.random((3, 1003))), f32(rng.random((3, 200))),
+              "U[0,1) weights (3,1003): a partial last quad; 200 draws")
+    prob_case("prob_chunks", f32(rng.random((2, 20001))), f32(rng.random((2, 300))),
+              "U[0,1) weights (2,20001): 3 chunks of 8192, Kahan carry, partial quad")
+    w = rng.exponential(1.0, (2, 8192)) ** 6  # wide dynamic range: rounding decides
+    w[:, ::7] = 0.0
+    r = rng.random((2, 256))
+    r[:, :4] = [0.0, np.nextafter(np.float32(1), np.float32(0)), 0.5, 1e-7]
+    prob_case("prob_skewed", f32(w), f32(r), "exp(1)^6 weights with zeros (2,8192); "
+              "draws incl. 0, 1-ulp, 0.5, 1e-7")
+    prob_case("prob_small", f32([[0.0, 0.0, 1.0, 0.0, 2.0], [1.0, 1.0, 1.0, 1.0, 1.0]]),
+              f32(rng.random((2, 64))), "(2,5) with zero weights and ties")
+    prob_case("prob_n1", f32([[3.0]]), f32([[0.0, 0.3, 0.99]]), "one category")
+
+
 def main():
     if not O.have_ref_gpu():
         raise SystemExit("oracle/_ref/libref_gpu.so missing: build it with `make -C oracle ref`")
+    prob_cases()
+    if "--prob-only" in sys.argv:
+        return
     fps_case("fps_uniform_cfg1", synth.batch([0], 1024, "uniform")[0], 256,
              "uniform U[0,1)^3 (1,1024) -> 256 (cfg1)")
     fps_case("fps_scannet_sa1", synth.batch([1], 8192, "scannet")[0], 1024,

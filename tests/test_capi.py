@@ -70,7 +70,11 @@ def test_argument_checks_return_einval_without_launching(pn2):
                                     None) == E  # null buffers
     assert lib.pn2_group_pool(None, None, 1, 1, 4, 8, 7, None, None) == E       # mode
     assert lib.pn2_fp_fused(None, None, None, 3, None, 4, 1, 4, 4, None, None) == E  # C1 w/o points1
+    assert lib.pn2_prob_sample(None, None, 1, 0, 4, None, 0, None, None) == E  # n = 0
+    assert lib.pn2_prob_sample(None, None, 2, 10, 4, None, 0, None, None) == E  # workspace
+    assert lib.pn2_prob_sample_workspace_size(3, 100) == 1200
     # empty work is a no-op, not an error (nothing is launched)
+    assert lib.pn2_prob_sample(None, None, 2, 10, 0, None, 0, None, None) == 0
     assert lib.pn2_gather_point(None, None, 0, 10, 10, None, None) == 0
     assert lib.pn2_three_nn(None, None, 0, 10, 10, None, None, None) == 0
 

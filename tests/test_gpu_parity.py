@@ -100,6 +100,58 @@ def test_fps_vs_reference_kernel(env, kind, B, N, M):
     assert np.array_equal(got, ref), f"{(got != ref).sum()} FPS indices differ from reference"
 
 
+PROB_CASES = [  # (B, n, m, weights)
+    (3, 1003, 200, "uniform"),
+    (2, 8192, 512, "skewed"),      # exactly one chunk
+    (2, 50001, 1000, "uniform"),   # 7 chunks, Kahan carry, partial last quad
+    (4, 37, 300, "zeros"),         # zero weights: flat prefix sums, ties
+    (1, 1, 5, "uniform"),
+]
+
+
+def _prob_inputs(B, n, m, kind, seed):
+    rng = np.random.default_rng(seed)
+    if kind == "skewed":
+        w = rng.exponential(1.0, (B, n)) ** 6
+    else:
+        w = rng.random((B, n))
+    if kind == "zeros":
+        w[:, rng.random(n) < 0.5] = 0.0
+        w[:, 0] = 0.0
+    r = rng.random((B, m))
+    r[:, 0] = 0.0
+    return np.ascontiguousarray(w, np.float32), np.ascontiguousarray(r, np.float32)
+
+
+@pytest.mark.parametrize("B,n,m,kind", PROB_CASES)
+def test_prob_sample_vs_oracle_and_reference(env, B, n, m, kind):
+    """ProbSample (tf_sampling_g.cu:7-104): indices bit-exact against the oracle and against the
+    reference's own cumsumKernel + binarysearchKernel run on this GPU."""
+    pkg, O, torch, dev = env
+    w, r = _prob_inputs(B, n, m, kind, seed=n + m)
+    got = pkg.tf_sampling.prob_sample(torch.from_numpy(w).to(dev),
+                                      torch.from_numpy(r).to(dev)).cpu().numpy()
+    assert np.array_equal(got, O.prob_sample(w, r)), "prob_sample differs from the oracle"
+    if O.have_ref_gpu():
+        out = torch.full((B, m), -1, dtype=torch.int32, device=dev)
+        wt, rt = torch.from_numpy(w).to(dev), torch.from_numpy(r).to(dev)
+        assert O.ref_gpu().pn2ref_prob_sample(wt.data_ptr(), rt.data_ptr(), B, n, m,
+                                              out.data_ptr()) == 0
+        assert np.array_equal(got, out.cpu().numpy()), "prob_sample differs from the reference"
+
+
+def test_prob_sample_errors(env):
+    pkg, O, torch, dev = env
+    ts = pkg.tf_sampling
+    with pytest.raises(pkg._lib.InvalidArgumentError, match="num_choices"):
+        ts.prob_sample(torch.zeros(2, 3, 4, device=dev), torch.zeros(2, 5, device=dev))
+    with pytest.raises(pkg._lib.InvalidArgumentError, match="num_points"):
+        ts.prob_sample(torch.zeros(2, 3, device=dev), torch.zeros(3, 5, device=dev))
+    with pytest.raises(pkg._lib.InvalidArgumentError):  # n = 0 (the reference reads cum[-1])
+        ts.prob_sample(torch.zeros(2, 0, device=dev), torch.zeros(2, 5, device=dev))
+    assert ts.prob_sample(torch.ones(2, 3, device=dev), torch.zeros(2, 0, device=dev)).shape == (2, 0)
+
+
 def test_gather_point(env):
     pkg, O, torch, dev = env
     x = _cloud(pkg, "scannet", 3, 2048)
@@ -547,6 +599,9 @@ def test_hip_reproduces_golden(env, path):
                                                                         T(d["xyz"]))
         assert np.array_equal(idx.cpu().numpy(), d["idx"])
         assert np.array_equal(_bits(new_xyz.cpu().numpy()), _bits(d["new_xyz"]))
+    elif op == "prob_sample":
+        got = pkg.tf_sampling.prob_sample(T(d["inp"]), T(d["inpr"]))
+        assert np.array_equal(got.cpu().numpy(), d["out"])
     else:
         pytest.fail(f"unknown golden op {op}")
 

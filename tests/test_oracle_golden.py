@@ -32,7 +32,7 @@ def test_golden_vectors_exist():
     names = {os.path.basename(p)[:-4] for p in GOLDEN}
     for need in ("bq_uniform_cfg1", "bq_scannet_sa1", "bq_scannet_msg128", "bq_boundary",
                  "group_tf_op_test", "nn_uniform_demo", "nn_lattice_ties", "interp_tf_op_test",
-                 "interp_fp4"):
+                 "interp_fp4", "prob_chunks", "prob_skewed"):
         assert need in names, need
 
 
@@ -76,6 +76,8 @@ def test_oracle_reproduces_golden(orc, path):
         oi, oo = orc.selection_sort(d["dist"], int(meta["k"]))
         assert np.array_equal(oi, d["outi"])
         assert np.array_equal(_bits(oo), _bits(d["out"]))
+    elif op == "prob_sample":
+        assert np.array_equal(orc.prob_sample(d["inp"], d["inpr"]), d["out"])
     elif op == "farthest_point_sample":
         idx = orc.fps(d["xyz"], int(meta["npoint"]))
         assert np.array_equal(idx, d["idx"]), f"{(idx != d['idx']).sum()} FPS indices differ"
