@@ -85,6 +85,8 @@ struct Params {
   // Dense query (first neighbour of each group) / key / value layers, the reduction per head
   // and the batch norm (+ max pool of X), column segment by column segment of K and V
   int attn, att_wseg, att_nseg, att_add_max;
+  int stage_out;  // rows / fp sources: the last layer goes to LDS, then whole rows to HBM
+  int out_vec;    // stage_out with cout % 4 == 0 and a 16-byte aligned out: float4 stores
   int ntiles;  // tiles of P rows
   int tpw;     // consecutive tiles per workgroup (grid = ceil(ntiles / tpw))
   LayerDev qkv[3];
@@ -912,7 +914,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     // the 4 waves split the row tiles so every wave works (nsplit row groups).
     for (int l = 0; l < prm.nl; ++l) {
       const LayerDev& Ld = prm.L[l];
-      const bool last = l == prm.nl - 1 && !prm.attn;
+      const bool last = l == prm.nl - 1 && !prm.attn && !prm.stage_out;
       const int c32 = Ld.cout32;
       const int nsplit = item_split(R, c32);
       const int rg_tiles = R / nsplit;
@@ -930,6 +932,26 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     if constexpr (SRC == kSrcGroup) {
       if (prm.attn) attention_tail<R>(prm, smem, (prm.nl & 1) ? act1 : act0,
                                       (prm.nl & 1) ? prm.stride1 : prm.stride0, tile);
+    } else if (prm.stage_out) {
+      // the tile's output rows are contiguous in HBM: one wave per row, whole rows stored
+      // coalesced (the next tile's gather writes LDS only after the metadata barrier)
+      const int ll = prm.nl - 1;
+      const float* src = (ll & 1) ? act0 : act1;
+      const int S = (ll & 1) ? prm.stride0 : prm.stride1;
+      const int cout = prm.L[ll].cout;
+      const long long row0 = (long long)tile * P;
+      const int nrows = (int)min((long long)P, prm.rows - row0);
+      float* dst = prm.out + row0 * cout;
+      if (prm.out_vec) {
+        const int c4 = cout >> 2;
+        for (int p = wave; p < nrows; p += kWaves)
+          for (int c = lane; c < c4; c += kWave)
+            reinterpret_cast<float4*>(dst + (size_t)p * cout)[c] =
+                *reinterpret_cast<const float4*>(src + p * S + 4 * c);
+      } else {
+        for (int p = wave; p < nrows; p += kWaves)
+          for (int c = lane; c < cout; c += kWave) dst[(size_t)p * cout + c] = src[p * S + c];
+      }
     }
 
     // ---- 4. pooling: combine the row-tile partials of each group, store -----------------
@@ -1032,7 +1054,7 @@ size_t plan(Params& prm, int nl, const pn2_mlp_layer* layers, int cin0, int R, b
     prm.L[l].relu = (L.flags & PN2_MLP_RELU) ? 1 : 0;
     prm.L[l].lofs = wfloats;
     wfloats += cout32 * cin8 * 256 + cout32 * 64;
-    if (l < nl - 1 || prm.attn) {  // layer l writes buffer (l+1)&1
+    if (l < nl - 1 || prm.attn || prm.stage_out) {  // layer l writes buffer (l+1)&1
       if ((l + 1) & 1) w1 = w1 > cout32 * 32 ? w1 : cout32 * 32;
       else w0 = w0 > cout32 * 32 ? w0 : cout32 * 32;
     }
@@ -1199,6 +1221,36 @@ int choose_R(Params& prm, int nl, const pn2_mlp_layer* layers, int cin0, bool po
     (void)best_lds;
   }
   return best;
+}
+
+// Per-point outputs (fp / rows sources): stage the last layer through LDS when that fits the
+// same occupancy, else store it from the registers.
+int choose_R_staged(Params& prm, int nl, const pn2_mlp_layer* layers, int cin0, long long tiles32,
+                    const float* out, size_t* lds_out) {
+  Params plain = prm;
+  size_t lds_plain = 0;
+  const int R_plain = choose_R(plain, nl, layers, cin0, false, tiles32, 1, &lds_plain);
+  static const bool off = [] {  // A/B override (scripts)
+    const char* e = std::getenv("PN2_MLP_STAGE_OUT");
+    return e && e[0] == '0';
+  }();
+  if (!off) {
+    Params staged = prm;
+    staged.stage_out = 1;
+    size_t lds = 0;
+    const int R = choose_R(staged, nl, layers, cin0, false, tiles32, 1, &lds);
+    const int occ = lds * 2 <= kLdsLimit ? 2 : 1, occ_plain = lds_plain * 2 <= kLdsLimit ? 2 : 1;
+    if (R && (!R_plain || (R == R_plain && occ == occ_plain))) {
+      const int cout = layers[nl - 1].cout;
+      staged.out_vec = (cout % 4 == 0) && ((reinterpret_cast<uintptr_t>(out) & 15) == 0);
+      prm = staged;
+      *lds_out = lds;
+      return R;
+    }
+  }
+  prm = plain;
+  *lds_out = lds_plain;
+  return R_plain;
 }
 
 }  // namespace
@@ -1372,7 +1424,7 @@ int pn2_fp_mlp(const float* dist, const int32_t* nn_idx, const float* points1, i
   if (rows > 0x7fffffffLL || (long long)B * m > 0x7fffffffLL) return PN2_EINVAL;
   Params prm = {};
   size_t lds = 0;
-  const int R = choose_R(prm, nlayers, layers, C1 + C2, false, (rows + 31) / 32, 1, &lds);
+  const int R = choose_R_staged(prm, nlayers, layers, C1 + C2, (rows + 31) / 32, out, &lds);
   if (!R) return PN2_EINVAL;
   prm.dist = dist;
   prm.nn = nn_idx;
@@ -1401,7 +1453,7 @@ int pn2_shared_mlp(const float* x, long long rows, int cin, int nlayers,
   if (!x || !out || rows > 0x7fffffffLL) return PN2_EINVAL;
   Params prm = {};
   size_t lds = 0;
-  const int R = choose_R(prm, nlayers, layers, cin, false, (rows + 31) / 32, 1, &lds);
+  const int R = choose_R_staged(prm, nlayers, layers, cin, (rows + 31) / 32, out, &lds);
   if (!R) return PN2_EINVAL;
   prm.x = x;
   prm.cin = cin;
