@@ -95,6 +95,36 @@ def pmc_traffic(config, B):
     return e["fetch_bytes_x2"] + e["write_bytes"], os.path.relpath(files[-1], ROOT) + f" [{k}]"
 
 
+def _e2e_child(args, e2e):
+    """The whole-model measurement in a child process (`bench.py --model`, same config, queues
+    and steps). HIP maps streams to hardware queues round-robin in creation order, so in the
+    geometric step's process the model's streams land on other queues than in a standalone
+    run (12.7-13.1k vs 16.2-16.4k clouds/s). Fills e2e and returns True, or
+    returns False (the caller then measures in process)."""
+    import subprocess
+    cmd = [sys.executable, os.path.abspath(__file__), "--model", "--config", args.config,
+           "--steps", str(args.e2e_steps), "--warmup", str(min(args.warmup, 5)),
+           "--no-cpu-baseline", "--time-every", str(args.time_every), "--sets", str(args.sets),
+           "--lane0-priority", args.lane0_priority]
+    if args.batch:
+        cmd += ["--batch", str(args.batch)]
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=dict(os.environ))
+        line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1] \
+            if r.returncode == 0 else None
+    except (subprocess.TimeoutExpired, IndexError):
+        line = None
+    if not line:
+        log("e2e child failed; measuring in process")
+        return False
+    d = json.loads(line)
+    e2e.update({"value": d["value"], "unit": d["unit"], "ms_per_step": d["ms_per_step"],
+                "steps": d["steps"], "sa1_sampler_ms": d["roofline"]["avg_launch_ms"],
+                "checksum": d["checksum"], "lane0_priority": d["config"]["lane0_priority"],
+                "process": "child (bench.py --model)"})
+    return True
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -127,6 +157,10 @@ def main():
     ap.add_argument("--lane0-priority", choices=["auto", "default", "high"], default="auto",
                     help="stream priority of lane 0 (the SA1 sampler chain); auto = default "
                          "for the geometric step, high for the whole model")
+    ap.add_argument("--e2e-in-process", action="store_true",
+                    help="measure the e2e field in this process after the geometric step "
+                         "(default at N = 1: a fresh child process, `bench.py --model`, whose "
+                         "streams get the hardware-queue mapping of a standalone run)")
     ap.add_argument("--e2e-steps", type=int, default=20,
                     help="after the geometric measurement, time this many whole-model steps "
                          "(reported as 'e2e'; 0 = skip)")
@@ -223,20 +257,24 @@ def main():
     sums = pkg.shard.gather_checksums(pkg.shard.cloud_checksums(outs, B))
     e2e = None
     if not args.model and args.e2e_steps > 0 and pkg.stack.CONFIGS[args.config][1] == "ssg":
-        # after the geometric step: the stream-to-queue mapping is round-robin in creation
-        # order, and creating the model's streams first cost the geometric step 29 %
-        e_el, e_fps, e_outs, e_prio = measure(True, args.e2e_steps, min(args.warmup, 5))
-        e_sums = pkg.shard.gather_checksums(pkg.shard.cloud_checksums(e_outs, B))
-        e2e = {"value": world * B * args.e2e_steps / e_el, "unit": "clouds/s",
-               "ms_per_step": e_el / args.e2e_steps * 1e3, "steps": args.e2e_steps,
-               "sa1_sampler_ms": e_fps, "checksum": float(e_sums.sum().item()),
-               "lane0_priority": e_prio,
+        e2e = {}
+        child = world == 1 and not args.e2e_in_process and _e2e_child(args, e2e)
+        if not child:
+            # after the geometric step: the stream-to-queue mapping is round-robin in creation
+            # order, and creating the model's streams first cost the geometric step 29 %
+            e_el, e_fps, e_outs, e_prio = measure(True, args.e2e_steps, min(args.warmup, 5))
+            e_sums = pkg.shard.gather_checksums(pkg.shard.cloud_checksums(e_outs, B))
+            e2e.update({"value": world * B * args.e2e_steps / e_el, "unit": "clouds/s",
+                        "ms_per_step": e_el / args.e2e_steps * 1e3, "steps": args.e2e_steps,
+                        "sa1_sampler_ms": e_fps, "checksum": float(e_sums.sum().item()),
+                        "lane0_priority": e_prio, "process": "same as the geometric step"})
+        e2e.update({
                "model": ("pointnet2_sem_seg_attention with rgb+normal inputs, inference "
                          "forward: SA x4 (fused group + MLP, Dense q/k/v on the matrix cores, "
                          "attention reduction + batch norm)" if args.config == "cfg3" else
                          "pointnet2_sem_seg inference forward: SA x4 (fused group + MLP + max "
                          "pool)") + ", FP x4 (fused interpolation + MLP), fc1+fc2 head fused "
-                        "into FP4; fp32 matrix cores; reference initialisers, fixed seed"}
+                        "into FP4; fp32 matrix cores; reference initialisers, fixed seed"})
 
     if rank == 0:
         clouds = world * B * args.steps
