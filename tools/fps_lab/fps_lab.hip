@@ -1379,6 +1379,233 @@ void launch_reg(const float* xyz, int B, int N, int M, int32_t* idx, float* nx, 
                        M, idx, nx);
 }
 
+// Variant 12 (cells): work skipping that keeps every wave equally busy. The cloud is sorted by
+// a coarse Morton code (4 bits per axis, counting sort in LDS) and dealt round-robin to the 256
+// threads, so slot s of EVERY thread holds one compact cell of 256 points (cell s). Per
+// iteration the new centre c and the current global maximum D (the previous winner's
+// distance: every running min is <= D) decide per cell, uniformly: if the cell's bounding box
+// is at least D away from c (with a 2^-16 relative margin against fp32 rounding), no point of
+// the cell can lower its running min, and the slot is skipped by all threads at once. Points
+// are no longer in the reference's tie order, so each slot carries its tie key
+// (k mod 512, k div 512) explicitly; the argmax is (max d, then min key). The lane maximum is
+// kept per group of 4 slots and only groups with a scanned slot are re-reduced.
+constexpr int kV12Cells = 32;
+constexpr int kV12Buckets = 4096;
+
+PN2_DEV uint32_t v12_ord(float f) {  // order-preserving float -> uint map
+  const uint32_t b = __float_as_uint(f);
+  return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+PN2_DEV float v12_unord(uint32_t u) {
+  return __uint_as_float((u & 0x80000000u) ? (u & 0x7FFFFFFFu) : ~u);
+}
+PN2_DEV float v12_wave_max(float v) { return v12_unord(wave_max_u32(v12_ord(v))); }
+PN2_DEV float v12_wave_min(float v) { return v12_unord(~wave_max_u32(~v12_ord(v))); }
+PN2_DEV uint32_t v12_spread4(uint32_t v) {  // 4 bits -> every third bit
+  v &= 15u;
+  return (v & 1u) | ((v & 2u) << 2) | ((v & 4u) << 4) | ((v & 8u) << 6);
+}
+
+__global__ __launch_bounds__(256) void fps_v12_kernel(const float* __restrict__ xyz, int N, int M,
+                                                      int32_t* __restrict__ idx,
+                                                      float* __restrict__ new_xyz) {
+  constexpr int BLOCK = 256, PPT = kV12Cells, NP = BLOCK * PPT, NW = BLOCK / kWave;
+  constexpr int NG = PPT / 4;
+  __shared__ float sxyz[3 * NP];
+  __shared__ int hist[kV12Buckets + 1];
+  __shared__ unsigned short order[NP];
+  __shared__ unsigned short code[NP];
+  __shared__ float wbox[NW][PPT][6];
+  __shared__ float sbb[NW][6];
+  __shared__ int wsum[NW];
+  __shared__ uint2 red[2][8];
+  const int t = threadIdx.x, lane = t & (kWave - 1), w = t / kWave;
+  const float* __restrict__ P = xyz + (size_t)blockIdx.x * N * 3;
+  int32_t* I = idx + (size_t)blockIdx.x * M;
+  float* NX = new_xyz ? new_xyz + (size_t)blockIdx.x * M * 3 : nullptr;
+
+  for (int e = t; e < 3 * N; e += BLOCK) sxyz[e] = P[e];
+  for (int e = t; e <= kV12Buckets; e += BLOCK) hist[e] = 0;
+  __syncthreads();
+  // bounding box of the cloud
+  float lo[3] = {3e38f, 3e38f, 3e38f}, hi[3] = {-3e38f, -3e38f, -3e38f};
+  for (int k = t; k < N; k += BLOCK)
+    for (int a = 0; a < 3; ++a) {
+      lo[a] = fminf(lo[a], sxyz[3 * k + a]);
+      hi[a] = fmaxf(hi[a], sxyz[3 * k + a]);
+    }
+  for (int a = 0; a < 3; ++a) {
+    lo[a] = v12_wave_min(lo[a]);
+    hi[a] = v12_wave_max(hi[a]);
+  }
+  if (lane == 0)
+    for (int a = 0; a < 3; ++a) { sbb[w][a] = lo[a]; sbb[w][3 + a] = hi[a]; }
+  __syncthreads();
+  float sc[3];
+  for (int a = 0; a < 3; ++a) {
+    float l = sbb[0][a], h = sbb[0][3 + a];
+    for (int q = 1; q < NW; ++q) { l = fminf(l, sbb[q][a]); h = fmaxf(h, sbb[q][3 + a]); }
+    lo[a] = l;
+    sc[a] = 16.f / fmaxf(h - l, 1e-30f);
+  }
+  // coarse Morton codes, counting sort: order[] = point indices by cell-major position
+  for (int k = t; k < NP; k += BLOCK) {
+    uint32_t m = kV12Buckets;  // padding slots sort last
+    if (k < N) {
+      m = 0;
+      for (int a = 0; a < 3; ++a) {
+        const int q = min(15, max(0, (int)((sxyz[3 * k + a] - lo[a]) * sc[a])));
+        m |= v12_spread4((uint32_t)q) << a;
+      }
+    }
+    code[k] = (unsigned short)m;
+    atomicAdd(&hist[m], 1);
+  }
+  __syncthreads();
+  {  // exclusive scan of hist[0..4096]: 16 buckets per thread, the last one by thread 255
+    int loc[16], sum = 0;
+    for (int i = 0; i < 16; ++i) { loc[i] = hist[16 * t + i]; sum += loc[i]; }
+    int incl = sum;
+    for (int o = 1; o < kWave; o <<= 1) {
+      const int v = __shfl_up(incl, o, kWave);
+      if (lane >= o) incl += v;
+    }
+    if (lane == kWave - 1) wsum[w] = incl;
+    __syncthreads();
+    int base = 0;
+    for (int q = 0; q < w; ++q) base += wsum[q];
+    int run = base + incl - sum;
+    for (int i = 0; i < 16; ++i) { hist[16 * t + i] = run; run += loc[i]; }
+    if (t == BLOCK - 1) hist[kV12Buckets] = run;
+  }
+  __syncthreads();
+  for (int k = t; k < NP; k += BLOCK) order[atomicAdd(&hist[code[k]], 1)] = (unsigned short)k;
+  __syncthreads();
+
+  // slot s of thread t: the point at cell-major position s * 256 + t
+  float px[PPT], py[PPT], pz[PPT];
+  int tb[PPT], tk[PPT];
+#pragma unroll
+  for (int s = 0; s < PPT; ++s) {
+    const int k = order[s * BLOCK + t];
+    const bool in = k < N;
+    const int kk = in ? k : 0;
+    px[s] = sxyz[3 * kk];
+    py[s] = sxyz[3 * kk + 1];
+    pz[s] = sxyz[3 * kk + 2];
+    tb[s] = in ? __float_as_int(kInitTemp) : -1;
+    tk[s] = in ? (((k & 511) << 4) | (k >> 9)) : 0x7FFFFFFF;
+  }
+  // cell boxes: lane c (and c + 32) of every wave keeps cell c's box
+#pragma unroll
+  for (int s = 0; s < PPT; ++s) {
+    const float a0 = v12_wave_min(px[s]), a1 = v12_wave_min(py[s]), a2 = v12_wave_min(pz[s]);
+    const float b0 = v12_wave_max(px[s]), b1 = v12_wave_max(py[s]), b2 = v12_wave_max(pz[s]);
+    if (lane == 0) {
+      wbox[w][s][0] = a0; wbox[w][s][1] = a1; wbox[w][s][2] = a2;
+      wbox[w][s][3] = b0; wbox[w][s][4] = b1; wbox[w][s][5] = b2;
+    }
+  }
+  __syncthreads();
+  float blo[3], bhi[3];
+  {
+    const int c = lane & (PPT - 1);
+    for (int a = 0; a < 3; ++a) {
+      float l = wbox[0][c][a], h = wbox[0][c][3 + a];
+      for (int q = 1; q < NW; ++q) { l = fminf(l, wbox[q][c][a]); h = fmaxf(h, wbox[q][c][3 + a]); }
+      blo[a] = l;
+      bhi[a] = h;
+    }
+  }
+  // per-group cache of the lane's (max, min key among the max)
+  int gm[NG], gk[NG];
+  auto regroup = [&](int g) {
+    const int m = max(max(tb[4 * g], tb[4 * g + 1]), max(tb[4 * g + 2], tb[4 * g + 3]));
+    int key = 0x7FFFFFFF;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) key = (tb[4 * g + q] == m) ? min(key, tk[4 * g + q]) : key;
+    gm[g] = m;
+    gk[g] = key;
+  };
+#pragma unroll
+  for (int g = 0; g < NG; ++g) regroup(g);
+
+  float cx = sxyz[0], cy = sxyz[1], cz = sxyz[2];
+  float D = kInitTemp;
+  if (t == 0) {
+    I[0] = 0;
+    if (NX) { NX[0] = cx; NX[1] = cy; NX[2] = cz; }
+  }
+  constexpr float kMargin = 1.0f - 1.0f / 65536.0f;
+  for (int j = 1; j < M; ++j) {
+    // which cells can change: box distance below the global max D (lanes 0..31 = cells)
+    float lb2;
+    {
+      const float gx = fmaxf(fmaxf(blo[0] - cx, cx - bhi[0]), 0.f);
+      const float gy = fmaxf(fmaxf(blo[1] - cy, cy - bhi[1]), 0.f);
+      const float gz = fmaxf(fmaxf(blo[2] - cz, cz - bhi[2]), 0.f);
+      lb2 = (gx * gx + gy * gy) + gz * gz;
+    }
+    const uint32_t mask = (uint32_t)__builtin_amdgcn_ballot_w64(!(lb2 * kMargin >= D));
+#pragma unroll
+    for (int s = 0; s < PPT; ++s) {
+      if (mask & (1u << s)) {
+        const float dx = px[s] - cx, dy = py[s] - cy, dz = pz[s] - cz;
+        const float d = (dx * dx + dy * dy) + dz * dz;
+        tb[s] = min(tb[s], __float_as_int(d));
+      }
+    }
+#pragma unroll
+    for (int g = 0; g < NG; ++g)
+      if (mask & (0xFu << (4 * g))) regroup(g);
+    int bd = gm[0];
+#pragma unroll
+    for (int g = 1; g < NG; ++g) bd = max(bd, gm[g]);
+    int bk = 0x7FFFFFFF;
+#pragma unroll
+    for (int g = 0; g < NG; ++g) bk = (gm[g] == bd) ? min(bk, gk[g]) : bk;
+    // wave: max distance, then the smallest key among the lanes holding it
+    const uint32_t hv = (uint32_t)(bd + 1);
+    const uint32_t km = wave_max_u32(hv);
+    const uint64_t cand = __builtin_amdgcn_ballot_w64(hv == km);
+    uint32_t key;
+    if (__builtin_popcountll(cand) == 1) {
+      key = (uint32_t)__builtin_amdgcn_readlane(bk, (int)__builtin_ctzll(cand));
+    } else {
+      const uint32_t kk = (hv == km) ? (uint32_t)bk : 0xFFFFFFFFu;
+      key = ~wave_max_u32(~kk);
+    }
+    if (lane == 0) red[j & 1][w] = make_uint2(km, key);
+    __syncthreads();
+    const bool inw = (lane & 7) < NW;
+    const uint2 r = inw ? red[j & 1][lane & 7] : make_uint2(0u, 0xFFFFFFFFu);
+    uint32_t bm = max_dpp_u32<kDppXor1>(r.x);
+    bm = max_dpp_u32<kDppXor2>(bm);
+    bm = max_dpp_u32<kDppHalfMirror>(bm);
+    const uint64_t wins = __builtin_amdgcn_ballot_w64(r.x == bm) & 0xFFull;
+    uint32_t bkey;
+    if (__builtin_popcountll(wins) == 1) {
+      bkey = (uint32_t)__builtin_amdgcn_readlane((int)r.y, (int)__builtin_ctzll(wins));
+    } else {
+      uint32_t kk = ~((r.x == bm) ? r.y : 0xFFFFFFFFu);
+      kk = max_dpp_u32<kDppXor1>(kk);
+      kk = max_dpp_u32<kDppXor2>(kk);
+      kk = max_dpp_u32<kDppHalfMirror>(kk);
+      bkey = ~(uint32_t)__builtin_amdgcn_readfirstlane((int)kk);
+    }
+    const int old = (int)((bkey & 15u) * 512u + (bkey >> 4));
+    D = __int_as_float((int)bm - 1);
+    cx = sxyz[3 * old];
+    cy = sxyz[3 * old + 1];
+    cz = sxyz[3 * old + 2];
+    if (t == 0) {
+      I[j] = old;
+      if (NX) { NX[3 * j] = cx; NX[3 * j + 1] = cy; NX[3 * j + 2] = cz; }
+    }
+  }
+}
+
+
 // (variant, block, points-per-thread) launch table used by the tuner (pn2_fps_tune)
 #define PN2_FPS_CONFIGS(X)                                                                      \
   X(64, 1) X(64, 2) X(64, 4) X(64, 8) X(64, 16) X(128, 4) X(128, 8) X(128, 16) X(256, 1)      \
@@ -1429,6 +1656,11 @@ int fps_tune_impl(const float* xyz, int B, int N, int M, int32_t* idx, float* nx
   }
   PN2_FPS_CONFIGS(PN2_X)
 #undef PN2_X
+  if (variant == 120) {  // v12 cells: 256 threads x 32 slots, N <= 8192
+    if (block != 256 || ppt != 32 || N > 8192) return PN2_EINVAL;
+    hipLaunchKernelGGL(fps_v12_kernel, dim3(B), dim3(256), 0, s, xyz, N, M, idx, nx);
+    PN2_RETURN_LAUNCH();
+  }
   if (variant >= 111 && variant <= 114) {  // v11, variant = 110 + G
     const int G = variant - 110;
 #define PN2_V11(BL, PP, GG)                                                    \
@@ -1555,6 +1787,7 @@ int fps_tune_impl(const float* xyz, int B, int N, int M, int32_t* idx, float* nx
   }
   return PN2_EINVAL;
 }
+
 
 }  // namespace
 }  // namespace pn2

@@ -55,6 +55,7 @@ def _candidates(N, slack):
     c += [(97 if g == 4 else 98, bl, pp) for bl, pp, g in V9A if N <= bl * pp <= max(slack * N, 64)]
     c += [(110 + g, bl, pp) for bl, pp, g in V11 if N <= bl * pp <= max(slack * N, 64)]
     c += [(90 + g, bl, pp) for bl, pp, g in V9 if N <= bl * pp <= max(slack * N, 64)]
+    c += [(120, 256, 32)] if N <= 8192 <= max(slack * N, 64) else []  # v12 cells
     return c
 
 
