@@ -95,6 +95,31 @@ def pmc_traffic(config, B):
     return e["fetch_bytes_x2"] + e["write_bytes"], os.path.relpath(files[-1], ROOT) + f" [{k}]"
 
 
+MAX_CLOCK_GHZ = 2.4  # MI355X_MICROARCH.md, chip-level parameters
+
+
+def sa1_valu_bound(config, ns_per_iteration):
+    """Per-CU VALU bound of the SA1 sampler (one workgroup = one CU per cloud): the loop's
+    VALU instructions per iteration (static count of the built kernel,
+    profiles/<round>/sa1_loop_isa.json from tools/sa1_loop_isa.py) x 4 cycles (wave64, one wave
+    per SIMD) against the measured iteration at the max clock (a lower clock under load only
+    raises the fraction). Only for the 8192-point sampler that file describes."""
+    import glob
+    if config not in ("cfg2", "cfg3"):
+        return None
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "sa1_loop_isa.json")))
+    if not files:
+        return None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    cycles = ns_per_iteration * MAX_CLOCK_GHZ
+    return {"valu_instr_per_iteration": d["mix"]["valu"],
+            "floor_cycles_per_iteration": d["valu_issue_floor_cycles"],
+            "cycles_per_iteration_at_max_clock": cycles,
+            "frac": d["valu_issue_floor_cycles"] / cycles,
+            "source": os.path.relpath(files[-1], ROOT)}
+
+
 def _e2e_child(args, e2e):
     """The whole-model measurement in a child process (`bench.py --model`, same config, queues
     and steps). HIP maps streams to hardware queues round-robin in creation order, so in the
@@ -313,8 +338,10 @@ def main():
                          "traffic": traffic, "traffic_source": traffic_src,
                          "avg_launch_ms": fps_ms, "algorithmic_bytes_per_launch": fps_bytes,
                          "ns_per_iteration": fps_ms * 1e6 / max(1, M1 - 1),
+                         "valu": sa1_valu_bound(args.config, fps_ms * 1e6 / max(1, M1 - 1)),
                          "note": "latency-bound serial argmax (M-1 dependent block-wide "
-                                 "reductions); the HBM fraction is structurally low"},
+                                 "reductions); the HBM fraction is structurally low, the "
+                                 "per-CU VALU-issue fraction ('valu') is the bound that applies"},
             "step_hbm": {"algorithmic_bytes": step_bytes,
                          "achieved_GBps": step_bytes * world / (elapsed / args.steps) / 1e9,
                          "frac": step_bytes * world / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBPS},
