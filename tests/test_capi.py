@@ -117,6 +117,24 @@ def test_ball_threshold_equals_sqrt_predicate(pn2, r):
     assert lib.pn2_ball_threshold(0.0) == 0.0
 
 
+def test_sa1_loop_isa_matches_built_library():
+    """profiles/r1/sa1_loop_isa.json (the VALU count behind bench.py's roofline.valu) describes
+    the SA1 sampler loop of the library as built."""
+    import json
+    import sys
+    import tempfile
+    if not os.path.exists("/opt/rocm/lib/llvm/bin/llvm-objdump"):
+        pytest.skip("llvm-objdump not available")
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import place_sa1_loop
+    with tempfile.TemporaryDirectory() as t:
+        _, body = place_sa1_loop.loop_body(
+            os.path.join(ROOT, "pointcloud-segmentation-attention_amd", "libpn2hip.so"), t)
+    valu = sum(1 for ln in body if ln.split()[0].startswith("v_"))
+    with open(os.path.join(ROOT, "profiles", "r1", "sa1_loop_isa.json")) as f:
+        assert json.load(f)["mix"]["valu"] == valu
+
+
 def test_sa1_sampler_loop_placement():
     """The SA1 sampler's iteration loop sits at a code offset = 4 mod 8 in the built library
     (the placement measured ~6 % faster than 0 mod 8; tools/place_sa1_loop.py chooses it)."""
