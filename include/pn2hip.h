@@ -326,6 +326,8 @@ int pn2_scene_bbox(const float* points, int N, float* bbox, void* workspace,
  * inside it +0.2 (>= lo, < hi) in index order; valid if labelled / (3 n) >= 0.7 (the
  * reference divides by reduce_sum(ones_like((n,3) points)), :113) and the occupied voxel keys
  * / 31 / 31 / 62 >= 0.02 (:119-126); the first valid try is kept, else the last (:138-141).
+ * With the 3 n denominator no try can be valid (labelled / 3n <= 1/3), so the last try is
+ * used without evaluating the others; the earlier centres only mirror the reference's draws.
  * Outputs (B,K[,3]): points, labels, colors (int32, may be NULL with out_colors NULL),
  * normals (may be NULL likewise), weights = label_weights[label] * mask, mask = inside the
  * area +0.01 (:114-117, :150-153). bbox from pn2_scene_bbox. workspace:

@@ -20,11 +20,6 @@ namespace {
 
 constexpr int kBlock = 256;
 constexpr int kSlice = 4096;  // points per compaction slice
-// The reference's voxel key v0*31*62 + v1*62 + v2 (:121) with v = ceil(frac * [31, 31, 62]);
-// the 0.01 margin lets v0, v1 reach 32, so keys lie in [0, 32*1922 + 32*62 + 62]. The key is
-// not injective (v1*62 + v2 can exceed 1922); tf.unique counts KEYS, and so does the bitmap.
-constexpr int kVoxKeys = 32 * 1922 + 32 * 62 + 62 + 1;
-constexpr int kVoxWords = (kVoxKeys + 31) / 32;
 
 // ---- scene bounding box (reduce_min / reduce_max over the points, :90-91) ----------------
 __global__ __launch_bounds__(kBlock) void bbox_partial_kernel(const float* __restrict__ p, int N,
@@ -92,74 +87,24 @@ PN2_DEV bool in_box(const float* q, const Area& a, float m) {
   return ok;
 }
 
-// stats[b][t] = {n (in the 0.2-margin area), labelled (label > 0), voxels occupied by the
-// 0.01-margin points}; validity (:124-126) is evaluated by the consumers.
-__global__ __launch_bounds__(kBlock) void crop_try_kernel(const float* __restrict__ p,
-                                                          const int32_t* __restrict__ labels,
-                                                          int N, const float* __restrict__ bbox,
-                                                          const int32_t* __restrict__ centres,
-                                                          int T, int32_t* __restrict__ stats) {
-  __shared__ uint32_t vox[kVoxWords];
-  __shared__ int s_cnt[3];
-  const int bt = blockIdx.x;  // b * T + t
-  for (int i = threadIdx.x; i < kVoxWords; i += kBlock) vox[i] = 0;
-  if (threadIdx.x < 3) s_cnt[threadIdx.x] = 0;
-  __syncthreads();
-  const Area a = try_area(p, bbox, centres[bt]);
-  float ext[3];
-  const float scale[3] = {31.0f, 31.0f, 62.0f};
-  for (int c = 0; c < 3; ++c) ext[c] = a.hi[c] - a.lo[c];
-  int n = 0, lab = 0;
-  for (int i = threadIdx.x; i < N; i += kBlock) {
-    const float* q = p + (size_t)i * 3;
-    if (!in_box(q, a, 0.2f)) continue;
-    ++n;
-    lab += labels[i] > 0;
-    if (in_box(q, a, 0.01f)) {
-      // vidx = ceil((p - current_min) / (current_max - current_min) * [31, 31, 62]) (:119-120)
-      int v[3];
-      for (int c = 0; c < 3; ++c) v[c] = (int)ceilf(((q[c] - a.lo[c]) / ext[c]) * scale[c]);
-      const int key = v[0] * 1922 + v[1] * 62 + v[2];  // vidx_0*31*62 + vidx_1*62 + vidx_2
-      if (key >= 0 && key < kVoxKeys) atomicOr(&vox[key >> 5], 1u << (key & 31));
-    }
-  }
-  atomicAdd(&s_cnt[0], n);
-  atomicAdd(&s_cnt[1], lab);
-  __syncthreads();
-  int occ = 0;
-  for (int i = threadIdx.x; i < kVoxWords; i += kBlock) occ += __popc(vox[i]);
-  atomicAdd(&s_cnt[2], occ);
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    stats[bt * 3 + 0] = s_cnt[0];
-    stats[bt * 3 + 1] = s_cnt[1];
-    stats[bt * 3 + 2] = s_cnt[2];
-  }
-}
-
-// The try the reference keeps: the first valid one, else the last (:138-141).
-// isvalid = labelled / cur_len >= 0.7 and occupied / 31 / 31 / 62 >= 0.02, all fp32, with
-// cur_len = reduce_sum(ones_like(cur_points)) = 3 n (the (n, 3) point tensor, :113).
-PN2_DEV int chosen_try(const int32_t* stats, int b, int T) {
-  for (int t = 0; t < T; ++t) {
-    const int32_t* s = stats + (b * T + t) * 3;
-    const float cur_len = (float)(3 * s[0]);
-    const float frac = (float)s[1] / cur_len;
-    const float occ = (((float)s[2] / 31.0f) / 31.0f) / 62.0f;
-    if (frac >= 0.7f && occ >= 0.02f) return t;
-  }
-  return T - 1;
-}
+// The try the reference keeps (:138-141): the first valid one, else the last. No try is ever
+// valid: isvalid needs labelled / cur_len >= 0.7 (:124), and cur_len =
+// reduce_sum(ones_like(cur_points)) over the (n, 3) point tensor is 3 n (:113), so the
+// fraction is at most n / 3n = 1/3 (fp32 division of integers <= 2^24: <= 0.33334), and
+// NaN for n = 0. The kernels therefore use the last try directly; the reference's per-try
+// statistics (points in the area, labelled points, occupied voxels) have no effect on the
+// output and are not computed (tests/test_oracle_golden.py checks the bound over every
+// (labelled, n) pair up to 2^20 and that the oracle, which does compute them, keeps the last).
+PN2_DEV int chosen_try(int T) { return T - 1; }
 
 // Slice counts of the chosen try's area: cnt[b][slice].
 __global__ __launch_bounds__(kBlock) void crop_count_kernel(const float* __restrict__ p, int N,
                                                             const float* __restrict__ bbox,
                                                             const int32_t* __restrict__ centres,
-                                                            const int32_t* __restrict__ stats,
                                                             int T, int nslices,
                                                             int32_t* __restrict__ cnt) {
   const int b = blockIdx.y, sl = blockIdx.x;
-  const int t = chosen_try(stats, b, T);
+  const int t = chosen_try(T);
   const Area a = try_area(p, bbox, centres[b * T + t]);
   const int i0 = sl * kSlice, i1 = min(N, i0 + kSlice);
   int n = 0;
@@ -176,10 +121,10 @@ __global__ __launch_bounds__(kBlock) void crop_count_kernel(const float* __restr
 // (tf.where order, :107), and the 0.01-margin mask of each (:114-117).
 __global__ __launch_bounds__(kBlock) void crop_compact_kernel(
     const float* __restrict__ p, int N, const float* __restrict__ bbox,
-    const int32_t* __restrict__ centres, const int32_t* __restrict__ stats, int T, int nslices,
+    const int32_t* __restrict__ centres, int T, int nslices,
     const int32_t* __restrict__ cnt, int32_t* __restrict__ sel, uint8_t* __restrict__ inner) {
   const int b = blockIdx.y, sl = blockIdx.x;
-  const int t = chosen_try(stats, b, T);
+  const int t = chosen_try(T);
   const Area a = try_area(p, bbox, centres[b * T + t]);
   __shared__ int s_base, s_wave[kBlock / kWave];
   if (threadIdx.x == 0) {
@@ -394,12 +339,10 @@ int pn2_crop_sample(const float* points, const int32_t* labels, const int32_t* c
   int32_t* cnt = stats + (size_t)B * T * 3;
   int32_t* sel = cnt + (size_t)B * ns;
   uint8_t* inner = reinterpret_cast<uint8_t*>(sel + (size_t)B * N);
-  hipLaunchKernelGGL(pn2::crop_try_kernel, dim3((unsigned)(B * T)), dim3(pn2::kBlock), 0, s,
-                     points, labels, N, bbox, centres, T, stats);
   hipLaunchKernelGGL(pn2::crop_count_kernel, dim3(ns, (unsigned)B), dim3(pn2::kBlock), 0, s,
-                     points, N, bbox, centres, stats, T, (int)ns, cnt);
+                     points, N, bbox, centres, T, (int)ns, cnt);
   hipLaunchKernelGGL(pn2::crop_compact_kernel, dim3(ns, (unsigned)B), dim3(pn2::kBlock), 0, s,
-                     points, N, bbox, centres, stats, T, (int)ns, cnt, sel, inner);
+                     points, N, bbox, centres, T, (int)ns, cnt, sel, inner);
   hipLaunchKernelGGL(pn2::crop_gather_kernel,
                      dim3((unsigned)((K + pn2::kBlock - 1) / pn2::kBlock), (unsigned)B),
                      dim3(pn2::kBlock), 0, s, points, labels, colors, normals, N, cnt, (int)ns,

@@ -68,11 +68,9 @@ def test_crop_sample_vs_oracle(env, scene_id, n, B, K):
                              ow.data_ptr(), None)
     assert rc == 0
     torch.cuda.synchronize()
-    stats = ws[:B * T * 3].cpu().numpy().reshape(B, T, 3)
     for b in range(B):
         rp, rl, rcol, rn, rw, chosen, rstats = O.crop_sample(pts, lab, col, nrm, centres[b], u[b])
         assert chosen == T - 1  # the reference's 3n denominator: no try is ever valid
-        assert np.array_equal(stats[b], rstats), (stats[b], rstats)
         assert np.array_equal(op[b].cpu().numpy(), rp)
         assert np.array_equal(ol[b].cpu().numpy(), rl)
         assert np.array_equal(oc[b].cpu().numpy(), rcol)

@@ -182,6 +182,18 @@ def test_crop_sample_oracle_reference_quirks():
     assert np.all((w == 0) | (w == lw[l]))
 
 
+def test_crop_validity_can_never_hold():
+    """pn2_crop_sample keeps the last try without evaluating any (csrc/scene.hip chosen_try):
+    the reference's fraction labelled / reduce_sum(ones_like((n,3) points)) is computed in fp32
+    as float(labelled) / float(3 n), labelled <= n, so it is largest at labelled = n; over every
+    n up to 2^20 it stays below the 0.7 threshold (and n = 0 gives NaN, also not >= 0.7)."""
+    n = np.arange(1, 1 << 20, dtype=np.int64)
+    frac = n.astype(np.float32) / (3 * n).astype(np.float32)
+    assert frac.max() < 0.34
+    with np.errstate(invalid="ignore"):
+        assert not (np.float32(0) / np.float32(0) >= np.float32(0.7))
+
+
 def test_scene_chunk_golden_file():
     import json
     import os
