@@ -75,3 +75,45 @@ def test_random_sa_fp_layer_vs_oracle(env, seed):
     p2 = rng.uniform(-1, 1, (B, M, C2)).astype(np.float32)
     out = pkg.pointnet_util.fp_interpolate(T(xyz), new_xyz, T(pts), T(p2))
     assert np.array_equal(_bits(out.cpu().numpy()), _bits(O.fp_fused(xyz, ref_new, pts, p2))), what
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_random_knn_and_grads_vs_oracle(env, seed):
+    """knn_point / select_top_k bit-exact; gather / group / interpolate gradients (float
+    atomics: summation order not fixed) within 1e-5 of the oracle's sequential sums."""
+    pkg, O, torch, dev = env
+    rng = np.random.default_rng(5000 + seed)
+    kind = ["uniform", "scannet", "lattice"][seed % 3]
+    B = int(rng.integers(1, 4))
+    n = int(rng.choice([16, 100, 513, 1024, 2048]))
+    m = int(rng.choice([1, 7, 64, 256]))
+    k = int(min(n, rng.choice([1, 3, 8, 16, 32])))
+    xyz1 = _cloud(pkg, rng, kind, B, n)
+    xyz2 = _cloud(pkg, rng, kind, B, m)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    what = f"seed {seed}: {kind} B={B} n={n} m={m} k={k}"
+    val, idx = pkg.tf_grouping.knn_point(k, T(xyz1), T(xyz2))
+    rval, ridx = O.knn_point(k, xyz1, xyz2)
+    assert np.array_equal(idx.cpu().numpy(), ridx), what
+    assert np.array_equal(_bits(val.cpu().numpy()), _bits(rval)), what
+
+    C = int(rng.choice([3, 8, 64]))
+    pts = T(rng.uniform(-1, 1, (B, n, C)).astype(np.float32))
+    gidx = T(ridx.astype(np.int32))
+    go = rng.uniform(-1, 1, (B, m, k, C)).astype(np.float32)
+    g = pkg.tf_grouping.group_point_grad(pts, gidx, T(go)).cpu().numpy()
+    np.testing.assert_allclose(g, O.group_point_grad(n, ridx, go), rtol=1e-5, atol=1e-5,
+                               err_msg=what)
+    fidx = O.fps(xyz1, min(n, m))
+    gog = rng.uniform(-1, 1, (B, fidx.shape[1], 3)).astype(np.float32)
+    g = pkg.tf_sampling.gather_point_grad(T(xyz1), T(fidx), T(gog)).cpu().numpy()
+    np.testing.assert_allclose(g, O.gather_point_grad(n, fidx, gog), rtol=1e-5, atol=1e-5,
+                               err_msg=what)
+    if m >= 3:
+        dist, nidx = O.three_nn(xyz1, xyz2)
+        w = O.idw_weights(dist)
+        p2 = T(rng.uniform(-1, 1, (B, m, C)).astype(np.float32))
+        goi = rng.uniform(-1, 1, (B, n, C)).astype(np.float32)
+        g = pkg.tf_interpolate.three_interpolate_grad(p2, T(nidx), T(w), T(goi)).cpu().numpy()
+        np.testing.assert_allclose(g, O.three_interpolate_grad(m, nidx, w, goi), rtol=1e-5,
+                                   atol=1e-5, err_msg=what)
