@@ -38,7 +38,7 @@ if [ "${SKIP_PMC:-0}" != "1" ]; then
   # TCC pass on gfx950), kernel trace only -- never combined with runtime/sys tracing.
   for C in FETCH_SIZE WRITE_SIZE; do
     echo "== rocprofv3 --pmc $C"
-    timeout -k 10 ${PROF_TIMEOUT:-600} rocprofv3 --pmc $C --kernel-trace --output-format csv -d $OUT/pmc_${C}_$TAG -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline ${BENCH_ARGS:-} > $OUT/pmc_${C}_$TAG.log 2>&1
+    timeout -k 10 ${PROF_TIMEOUT:-600} rocprofv3 --pmc $C --kernel-trace --output-format csv -d $OUT/pmc_${C}_$TAG -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --e2e-steps 0 ${BENCH_ARGS:-} > $OUT/pmc_${C}_$TAG.log 2>&1
     rc=$?; tail -3 $OUT/pmc_${C}_$TAG.log; echo "pmc $C rc=$rc"
     [ $rc -eq 0 ] || exit $rc
   done
