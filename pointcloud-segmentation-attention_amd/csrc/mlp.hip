@@ -354,8 +354,9 @@ PN2_DEV void store_pooled(const Params& prm, int g, int fo, int cout, float mx, 
 // over row tile rt of X, written (scale/shift epilogue = bias) into dst at column
 // (to - to0)*32, rows 32*rt + col. For the query, row_of_lane maps lane col to X row
 // col*ns_pad (the first neighbour of group col) and only rows < nrows are written.
+template <int RG>
 PN2_DEV void dense_item(const LayerDev& D, const float* X, int Sx, int xrow, int to, int to0,
-                        float* dst, int Sd, int drow, bool write, int lane, int h) {
+                        float* dst, int Sd, int drow, int lane, int h) {
   float4 sc[4], sh[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
@@ -363,19 +364,21 @@ PN2_DEV void dense_item(const LayerDev& D, const float* X, int Sx, int xrow, int
     sc[q] = *reinterpret_cast<const float4*>(D.scale + fb);
     sh[q] = *reinterpret_cast<const float4*>(D.shift + fb);
   }
-  f32x16 acc[1];
-  mma_item<false, 1>(D.w + (size_t)to * D.cin8 * kWave + lane, X + xrow * Sx + 4 * h, 0, D.cin8,
-                     acc);
-  if (!write) return;
-  float* op = dst + drow * Sd + 32 * (to - to0) + 4 * h;
+  f32x16 acc[RG];
+  mma_item<false, RG>(D.w + (size_t)to * D.cin8 * kWave + lane, X + xrow * Sx + 4 * h, 32 * Sx,
+                      D.cin8, acc);
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    float4 y;
-    y.x = acc[0][4 * q + 0] * sc[q].x + sh[q].x;
-    y.y = acc[0][4 * q + 1] * sc[q].y + sh[q].y;
-    y.z = acc[0][4 * q + 2] * sc[q].z + sh[q].z;
-    y.w = acc[0][4 * q + 3] * sc[q].w + sh[q].w;
-    *reinterpret_cast<float4*>(op + 8 * q) = y;
+  for (int r = 0; r < RG; ++r) {
+    float* op = dst + (drow + 32 * r) * Sd + 32 * (to - to0) + 4 * h;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float4 y;
+      y.x = acc[r][4 * q + 0] * sc[q].x + sh[q].x;
+      y.y = acc[r][4 * q + 1] * sc[q].y + sh[q].y;
+      y.z = acc[r][4 * q + 2] * sc[q].z + sh[q].z;
+      y.w = acc[r][4 * q + 3] * sc[q].w + sh[q].w;
+      *reinterpret_cast<float4*>(op + 8 * q) = y;
+    }
   }
 }
 
@@ -537,13 +540,16 @@ PN2_DEV void attention_tail(const Params& prm, float* smem, const float* X, int 
   while (L > 1 && L > prm.ns) L >>= 1;
   for (int sgi = 0; sgi < prm.att_nseg; ++sgi) {
     // K and V of this column segment (:32-33)
-    const int nitems = 2 * R * t_seg;
+    // items of two row tiles (R >= 2): each weight fragment serves both tiles
+    constexpr int RGk = R >= 2 ? 2 : 1;
+    constexpr int npair = R / RGk;
+    const int nitems = 2 * npair * t_seg;
     for (int item = wave; item < nitems; item += kWaves) {
-      const int which = item / (R * t_seg);
-      const int rem = item - which * (R * t_seg);
-      const int to = sgi * t_seg + rem / R, rt = rem % R;
-      dense_item(prm.qkv[1 + which], X, Sx, 32 * rt + col, to, sgi * t_seg, which ? Vb : Kb, Skv,
-                 32 * rt + col, true, lane, h);
+      const int which = item / (npair * t_seg);
+      const int rem = item - which * (npair * t_seg);
+      const int to = sgi * t_seg + rem / npair, rt = (rem % npair) * RGk;
+      dense_item<RGk>(prm.qkv[1 + which], X, Sx, 32 * rt + col, to, sgi * t_seg,
+                      which ? Vb : Kb, Skv, 32 * rt + col, lane, h);
     }
     __syncthreads();
     if (sgi == 0) PN2_STAMP(13);
