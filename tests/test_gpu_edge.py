@@ -53,6 +53,23 @@ def test_empty_interpolation(env):
     assert out.shape == (2, 0, 4)
 
 
+def test_empty_gradients(env):
+    """No index points at any input row, so every gradient is zero in the input's shape."""
+    pkg, torch, dev = env
+    pts = torch.rand(2, 10, 4, device=dev)
+    g = pkg.tf_grouping.group_point_grad(pts, torch.zeros(2, 0, 8, dtype=torch.int32, device=dev),
+                                         torch.zeros(2, 0, 8, 4, device=dev))
+    assert g.shape == (2, 10, 4) and not g.any()
+    xyz = torch.rand(2, 10, 3, device=dev)
+    g = pkg.tf_sampling.gather_point_grad(xyz, torch.zeros(2, 0, dtype=torch.int32, device=dev),
+                                          torch.zeros(2, 0, 3, device=dev))
+    assert g.shape == (2, 10, 3) and not g.any()
+    g = pkg.tf_interpolate.three_interpolate_grad(pts, torch.zeros(2, 0, 3, dtype=torch.int32, device=dev),
+                                                  torch.zeros(2, 0, 3, device=dev),
+                                                  torch.zeros(2, 0, 4, device=dev))
+    assert g.shape == (2, 10, 4) and not g.any()
+
+
 def test_empty_layers(env):
     pkg, torch, dev = env
     pu = pkg.pointnet_util
