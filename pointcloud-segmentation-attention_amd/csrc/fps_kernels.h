@@ -10,6 +10,11 @@ namespace {
 
 constexpr float kInitTemp = 1e38f;  // tf_sampling_g.cu:118
 
+// Wave issue priority (s_setprio) of the samplers' iteration loops; 0 = the hardware default.
+#ifndef PN2_FPS_PRIO
+#define PN2_FPS_PRIO 0
+#endif
+
 // Low word of the argmax key: larger = earlier in the reference's tie order.
 PN2_DEV uint32_t tie_low(int k) {
   const uint32_t tk = (((uint32_t)k & 511u) << 20) | ((uint32_t)k >> 9);
@@ -158,6 +163,7 @@ PN2_DEV void fps_v9_body(const float* P, int N, int M, const float* CXYZ, int32_
   if constexpr (STAMP) {
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_prev)::"memory");
   }
+  if constexpr (PN2_FPS_PRIO > 0) __builtin_amdgcn_s_setprio(PN2_FPS_PRIO);
   if constexpr (PAD > 0) asm volatile(".rept %0\n\ts_nop 0\n\t.endr" ::"n"(PAD));
   for (int j = 1; j < M; ++j) {
     int dv[PPT];  // this iteration's squared distances as int bits
