@@ -1,9 +1,9 @@
 #!/bin/bash
 # A/B of s_setprio 3 on the samplers' loops (csrc/build_prio/libpn2hip.so, built with
+# -DPN2_FPS_PRIO=3 at its own loop placement) against the product library, in-step.
 # Build the variant first: place_sa1_loop.py --flags "<Makefile FLAGS> -DPN2_FPS_PRIO=3" --out
 # csrc/build_prio/sa1_pad.h, then hipcc -DPN2_FPS_PRIO=3 -DPN2_SA1_PAD=<k> -c fps.hip and link
 # it with the other build/*.o into csrc/build_prio/libpn2hip.so.
-# -DPN2_FPS_PRIO=3 at its own loop placement) against the product library, in-step.
 set -e
 P=pointcloud-segmentation-attention_amd
 mkdir -p gpurun_out
