@@ -42,35 +42,73 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
+def _cpu_share():
+    """Host threads this process may use: the box's CPU share (OMP_NUM_THREADS, 16 on the
+    GPU box), bounded by the affinity mask."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    env = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(aff, int(env))) if env and env.isdigit() else aff
+
+
 def cpu_baseline(config, B_per_step, seconds, threads):
     """The oracle (C restatement of the reference's CPU loops, oracle/pn2_oracle.c) timed on
-    this host over a bounded sample of the same workload."""
-    import numpy as np
-
+    this host over a bounded sample of the same workload, twice: single-threaded (the
+    reference's loops are serial) and on `threads` threads (OpenMP over clouds; default: the
+    box's CPU share). The machine's full core count and CPU model are stated, and the
+    all-cores rate is extrapolated linearly from the measured per-thread rate (an upper
+    bound for the CPU, so the GPU ratio against it is the conservative one)."""
     from oracle import oracle as O
     pkg = importlib.import_module(PKG)
-    O.set_threads(threads)
-    N, kind, with_feat, attn = pkg.stack.CONFIGS[config]
-    B = max(threads, 1)
-    inp = pkg.stack.make_inputs(config, list(range(B)), "cpu")
-    np_inp = {k: v for k, v in inp.items()}
-    np_inp["xyz"] = inp["xyz"].numpy()
-    np_inp["feats"] = None if inp["feats"] is None else inp["feats"].numpy()
-    for k in ("sa_out", "fp_out"):
-        if k in inp:
-            np_inp[k] = [t.numpy() for t in inp[k]]
-    if "attn" in inp:
-        np_inp["attn"] = [tuple(t.numpy() for t in qkv) for qkv in inp["attn"]]
-    clouds, t0 = 0, time.perf_counter()
-    while True:
-        O.run_stack_cpu(np_inp, config)
-        clouds += B
-        el = time.perf_counter() - t0
-        if el >= seconds:
-            break
-    return {"value": clouds / el, "unit": "clouds/s", "cores": threads, "kind": "port",
-            "sample": f"{clouds} clouds ({config} step, {B} per call, OpenMP over clouds) in "
-                      f"{el:.1f} s on {threads} host threads; C restatement oracle/pn2_oracle.c"}
+
+    def timed(nthreads, budget):
+        O.set_threads(nthreads)
+        B = max(nthreads, 1)
+        inp = pkg.stack.make_inputs(config, list(range(B)), "cpu")
+        np_inp = dict(inp)
+        np_inp["xyz"] = inp["xyz"].numpy()
+        np_inp["feats"] = None if inp["feats"] is None else inp["feats"].numpy()
+        for k in ("sa_out", "fp_out"):
+            if k in inp:
+                np_inp[k] = [t.numpy() for t in inp[k]]
+        if "attn" in inp:
+            np_inp["attn"] = [tuple(t.numpy() for t in qkv) for qkv in inp["attn"]]
+        O.run_stack_cpu(np_inp, config)  # warm-up (page-in, OpenMP pool)
+        clouds, t0 = 0, time.perf_counter()
+        while True:
+            O.run_stack_cpu(np_inp, config)
+            clouds += B
+            el = time.perf_counter() - t0
+            if el >= budget:
+                return clouds / el, clouds, el
+
+    nproc = os.cpu_count() or 1
+    v1, c1, e1 = timed(1, seconds / 2)
+    vt, ct, et = timed(threads, seconds / 2)
+    est_all = v1 * nproc
+    return {"value": vt, "unit": "clouds/s", "cores": threads, "kind": "port",
+            "value_1core": v1, "value_threads": vt, "threads": threads,
+            "cores_all": nproc, "value_all_cores_extrapolated": est_all,
+            "cpu_model": _cpu_model(),
+            "sample": f"{config} steps of the C restatement oracle/pn2_oracle.c: {c1} clouds "
+                      f"(1 per call) in {e1:.1f} s on 1 thread; {ct} clouds ({threads} per call, "
+                      f"OpenMP over clouds) in {et:.1f} s on {threads} threads (the box's CPU "
+                      f"share); all-cores figure = 1-core rate x {nproc} (nproc), extrapolated, "
+                      "not run (the box allows its CPU share only)"}
 
 
 def pmc_traffic(config, B):
@@ -150,6 +188,60 @@ def _e2e_child(args, e2e):
     return True
 
 
+def launch_ranks(ngpus, argv):
+    """`bench.py --gpus N` outside torch.distributed.run: launch N ranks of this script on one
+    node (torch.distributed.run, rendezvous on 127.0.0.1) as a child process and return its
+    exit status. Rank 0 prints the JSON line. The reference's only parallelism is this batch
+    split (pointnet2_tensorflow/train_multi_gpu.py:181-190)."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={ngpus}", "--master-addr=127.0.0.1", f"--master-port={port}",
+           os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC (RCCL between ranks)
+    env.setdefault("OMP_NUM_THREADS", "1")
+    log(f"launching {ngpus} ranks: {' '.join(cmd)}")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def dry_run(args):
+    """The multi-rank plumbing without kernels (CPU, gloo): shard ids, per-rank synthetic
+    inputs, barrier-bracketed timing with the max over ranks, per-cloud checksum gather."""
+    import torch.distributed as dist
+    pkg = importlib.import_module(PKG)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo")
+    B = args.batch or (8 if args.config == "cfg5" else 16)
+    ids = pkg.shard.shard_ids(rank, world, B)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    inp = pkg.stack.make_inputs(args.config, ids, "cpu")
+    outs = [inp["xyz"]] + ([inp["feats"]] if inp["feats"] is not None else []) \
+        + list(inp["sa_out"]) + list(inp.get("fp_out", []))
+    if world > 1:
+        dist.barrier()
+    elapsed = pkg.shard.max_over_ranks(time.perf_counter() - t0)
+    sums = pkg.shard.gather_checksums(pkg.shard.cloud_checksums(outs, B))
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "clouds/s", "n_gpus": world,
+                          "dry_run": True, "clouds": world * B, "clouds_per_rank": B,
+                          "elapsed_max_over_ranks": elapsed,
+                          "checksum": float(sums.sum().item()),
+                          "per_cloud_checksums": [float(x) for x in sums.tolist()],
+                          "config": {"config": args.config, "clouds_per_gpu": B,
+                                     "global_batch": world * B,
+                                     "parallelism": f"dp{world} (batch split)"}}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -158,7 +250,9 @@ def main():
     ap.add_argument("--config", default="cfg2", choices=sorted(WORKLOADS))
     ap.add_argument("--batch", type=int, default=None, help="clouds per GPU (default: config's)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=None,
+                    help="threads of the multi-threaded CPU baseline leg (default: the box's "
+                         "CPU share, OMP_NUM_THREADS / affinity)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--eager", action="store_true",
                     help="launch every op from Python instead of replaying the captured hipGraphs")
@@ -189,7 +283,18 @@ def main():
     ap.add_argument("--e2e-steps", type=int, default=20,
                     help="after the geometric measurement, time this many whole-model steps "
                          "(reported as 'e2e'; 0 = skip)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher / rank plumbing only, on the CPU over gloo: every rank builds "
+                         "its shard's synthetic inputs and checksums them per cloud; max-over-"
+                         "ranks timing and the checksum gather run as in the real bench; no "
+                         "kernels, value = null (tests/test_bench_launcher.py)")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # one process per GPU: start the ranks as children BEFORE anything touches the GPU
+        # (this process never initialises HIP), and exit with the launcher's status
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if args.dry_run:
+        return dry_run(args)
     if args.hw_queues is not None:
         os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, max(1, args.hw_queues)))
     else:
@@ -352,7 +457,14 @@ def main():
         if world == 1 and not args.no_cpu_baseline and not args.model:
             try:
                 result["cpu_baseline"] = cpu_baseline(args.config, B, args.cpu_seconds,
-                                                      args.cpu_threads)
+                                                      args.cpu_threads or _cpu_share())
+                cb = result["cpu_baseline"]
+                # vs_baseline stays null (BASELINE.md publishes no number for this metric);
+                # the GPU/CPU ratios against the measured and extrapolated CPU rates:
+                cb["gpu_over_cpu"] = {"1core": value / cb["value_1core"],
+                                      f"{cb['threads']}threads": value / cb["value_threads"],
+                                      "all_cores_extrapolated":
+                                          value / cb["value_all_cores_extrapolated"]}
             except Exception as e:  # the baseline is reported, never the product
                 log(f"cpu baseline failed: {e!r}")
                 result["cpu_baseline"] = None
