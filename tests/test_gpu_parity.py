@@ -513,13 +513,7 @@ def test_gradients(env):
     np.testing.assert_allclose(p.grad.cpu().numpy(), np.repeat(counts[..., None], 16, -1), **TOL)
 
 
-@pytest.mark.parametrize("config,B", [("cfg2", 16), ("cfg3", 4), ("cfg5", 2)])
-def test_stack_full_size(env, config, B):
-    """The benchmark step at full size, every output against the CPU restatement."""
-    pkg, O, torch, dev = env
-    inp = pkg.stack.make_inputs(config, list(range(B)), dev)
-    outs = pkg.stack.run(inp)
-    torch.cuda.synchronize()
+def _np_inputs(inp):
     np_inp = {k: v for k, v in inp.items()}
     for k in ("xyz", "feats"):
         np_inp[k] = None if inp[k] is None else inp[k].cpu().numpy()
@@ -528,12 +522,62 @@ def test_stack_full_size(env, config, B):
             np_inp[k] = [t.cpu().numpy() for t in inp[k]]
     if "attn" in inp:
         np_inp["attn"] = [tuple(t.cpu().numpy() for t in qkv) for qkv in inp["attn"]]
-    ref = O.run_stack_cpu(np_inp, config)
+    return np_inp
+
+
+def _check_outputs(outs, ref):
     assert len(ref) == len(outs)
     for k, (g, r) in enumerate(zip(outs, ref)):
         g = g.cpu().numpy()
         assert g.shape == r.shape, (k, g.shape, r.shape)
         np.testing.assert_allclose(g, r, err_msg=f"output {k}", **TOL)
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("config,B", [("cfg2", 16), ("cfg3", 16), ("cfg5", 8)])
+def test_stack_full_size(env, config, B):
+    """The benchmark step at its BASELINE.json batch (cfg2/cfg3 B = 16, cfg5 B = 8: the launch
+    geometry of ball query and grouping depends on it), every output against the CPU
+    restatement."""
+    pkg, O, torch, dev = env
+    inp = pkg.stack.make_inputs(config, list(range(B)), dev)
+    outs = pkg.stack.run(inp)
+    torch.cuda.synchronize()
+    _check_outputs(outs, O.run_stack_cpu(_np_inputs(inp), config))
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("config,B", [("cfg2", 16), ("cfg3", 16), ("cfg5", 8)])
+def test_pipeline_full_size(env, config, B):
+    """What bench.py times: the software-pipelined hipGraph steps over 3 buffer sets, at the
+    BASELINE batch, after several rotations; the last step's outputs against the oracle."""
+    pkg, O, torch, dev = env
+    inp = pkg.stack.make_inputs(config, list(range(100, 100 + B)), dev)
+    pipe = pkg.stack.Pipeline(inp, graphs=True, nsets=3)
+    for _ in range(7):
+        pipe.run()
+    outs = pipe.join()
+    torch.cuda.synchronize()
+    _check_outputs(outs, O.run_stack_cpu(_np_inputs(inp), config))
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("rank", [1, 7])
+def test_cfg4_rank_shard(env, rank):
+    """cfg4 (B = 128 over 8 GPUs, 16 per rank): the shard a rank owns (global cloud ids from
+    shard.shard_ids, 16-31 for rank 1, 112-127 for rank 7) run on this GPU; outputs and the
+    per-cloud checksums that bench.py gathers equal the oracle's for the same global clouds."""
+    pkg, O, torch, dev = env
+    ids = pkg.shard.shard_ids(rank, 8, 16)
+    assert ids == list(range(16 * rank, 16 * rank + 16))
+    inp = pkg.stack.make_inputs("cfg2", ids, dev)
+    outs = pkg.stack.run(inp)
+    torch.cuda.synchronize()
+    ref = O.run_stack_cpu(_np_inputs(inp), "cfg2")
+    _check_outputs(outs, ref)
+    got = pkg.shard.cloud_checksums([o.cpu() for o in outs], 16)
+    want = pkg.shard.cloud_checksums([torch.from_numpy(r) for r in ref], 16)
+    np.testing.assert_allclose(got.numpy(), want.numpy(), rtol=1e-6, atol=1e-3)
 
 
 @pytest.mark.parametrize("config,B", [("cfg2", 4), ("cfg3", 2), ("cfg5", 2)])
