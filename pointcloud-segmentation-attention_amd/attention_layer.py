@@ -10,6 +10,7 @@ import torch
 
 from . import pointnet_util, tf_grouping, tf_sampling, tf_util
 from ._lib import InvalidArgumentError, check, device_tensor, lib, ptr, stream_of
+from ._torch_ops import ops
 
 
 def attention_reduce(Q, K, V):
@@ -26,46 +27,19 @@ def attention_reduce(Q, K, V):
     B, M, ns, C = (int(s) for s in K.shape)
     if tuple(Q.shape) != (B, M, C) or C % 4 != 0:
         raise InvalidArgumentError("attention_reduce expects Q (B,M,C) with C a multiple of 4")
-    Q = device_tensor(Q, "Q", torch.float32)
-    K = device_tensor(K, "K", torch.float32)
-    V = device_tensor(V, "V", torch.float32)
-    if torch.is_grad_enabled() and (Q.requires_grad or K.requires_grad or V.requires_grad):
-        return _AttentionReduce.apply(Q, K, V)
-    return _attn_fwd(Q, K, V)
-
-
-def _attn_fwd(Q, K, V):
-    B, M, ns, C = (int(s) for s in K.shape)
-    out = torch.empty((B, M, C), dtype=torch.float32, device=Q.device)
-    check(lib().pn2_attn_reduce(ptr(Q), ptr(K), ptr(V), B, M, ns, C, ptr(out), stream_of(Q)),
-          "attention_reduce")
-    return out
+    # torch.ops.pn2.attn_reduce (autograd: pn2_attn_reduce_grad, _torch_ops.py)
+    return ops().attn_reduce(device_tensor(Q, "Q", torch.float32),
+                             device_tensor(K, "K", torch.float32),
+                             device_tensor(V, "V", torch.float32))
 
 
 def attention_reduce_grad(Q, K, V, grad_out):
     """(dQ, dK, dV) of attention_reduce for the incoming gradient grad_out (B,M,C): the
     gradient TF's autodiff takes through attention_layer.py:35-42 (pn2_attn_reduce_grad)."""
-    B, M, ns, C = (int(s) for s in K.shape)
-    grad_out = device_tensor(grad_out, "grad_out", torch.float32)
-    dQ = torch.empty_like(Q)
-    dK = torch.empty_like(K)
-    dV = torch.empty_like(V)
-    check(lib().pn2_attn_reduce_grad(ptr(Q), ptr(K), ptr(V), ptr(grad_out), B, M, ns, C,
-                                     ptr(dQ), ptr(dK), ptr(dV), stream_of(Q)),
-          "attention_reduce_grad")
-    return dQ, dK, dV
-
-
-class _AttentionReduce(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, Q, K, V):
-        ctx.save_for_backward(Q, K, V)
-        return _attn_fwd(Q, K, V)
-
-    @staticmethod
-    def backward(ctx, grad_out):
-        Q, K, V = ctx.saved_tensors
-        return attention_reduce_grad(Q, K, V, grad_out.contiguous())
+    return tuple(ops().attn_reduce_grad(device_tensor(Q, "Q", torch.float32),
+                                        device_tensor(K, "K", torch.float32),
+                                        device_tensor(V, "V", torch.float32),
+                                        device_tensor(grad_out, "grad_out", torch.float32)))
 
 
 class AttentionLayer(torch.nn.Module):

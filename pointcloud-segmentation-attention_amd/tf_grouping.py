@@ -6,10 +6,15 @@ select_top_k / knn_point (tf_grouping.py:22-31,48-73) run knn.hip: one wavefront
 row, radix select + the reference's selection-sort swaps replayed on at most 3k candidates,
 so ties come out in exactly the reference's order; knn_point never builds the (b,m,n)
 distance matrix.
+
+Every reference-signature call goes through the torch.ops.pn2 operators (csrc/torch_ops.cpp;
+autograd for group_point in _torch_ops.py); query_ball_point with a caller-built grid (the
+benchmark step's early grid) calls the C ABI directly.
 """
 import torch
 
 from ._lib import InvalidArgumentError, check, device_tensor, lib, ptr, stream_of
+from ._torch_ops import ops
 from .grid import PointGrid
 
 
@@ -54,20 +59,16 @@ def query_ball_point(radius, nsample, xyz1, xyz2, grid=None):
         raise InvalidArgumentError("QueryBallPoint expects (batch_size, npoint, 3) xyz2 shape.")
     xyz1 = device_tensor(xyz1, "xyz1", torch.float32)
     xyz2 = device_tensor(xyz2, "xyz2", torch.float32)
+    if grid is None:  # the op builds the grid itself when the cloud is large (same switch)
+        return tuple(ops().query_ball_point(float(radius), int(nsample), xyz1, xyz2))
+    if not grid.matches(xyz1):
+        raise InvalidArgumentError("QueryBallPoint grid was built over a different xyz1")
     B, N = int(xyz1.shape[0]), int(xyz1.shape[1])
     M, ns = int(xyz2.shape[1]), int(nsample)
     idx = torch.empty((B, M, ns), dtype=torch.int32, device=xyz1.device)
     pts_cnt = torch.empty((B, M), dtype=torch.int32, device=xyz1.device)
-    if grid is None and N >= GRID_MIN_POINTS and B * M >= GRID_MIN_QUERIES:
-        grid = BallGrid(xyz1, radius)
-    if grid is not None:
-        if not grid.matches(xyz1):
-            raise InvalidArgumentError("QueryBallPoint grid was built over a different xyz1")
-        check(lib().pn2_ball_query_grid(ptr(grid.buf), ptr(xyz2), B, N, M, float(radius), ns,
-                                        ptr(idx), ptr(pts_cnt), stream_of(xyz1)), "QueryBallPoint")
-    else:
-        check(lib().pn2_ball_query(ptr(xyz1), ptr(xyz2), B, N, M, float(radius), ns, ptr(idx),
-                                   ptr(pts_cnt), stream_of(xyz1)), "QueryBallPoint")
+    check(lib().pn2_ball_query_grid(ptr(grid.buf), ptr(xyz2), B, N, M, float(radius), ns,
+                                    ptr(idx), ptr(pts_cnt), stream_of(xyz1)), "QueryBallPoint")
     return idx, pts_cnt
 
 
@@ -86,17 +87,9 @@ def select_top_k(k, dist):
     if dist.dim() != 3:  # tf_grouping.cpp:118
         raise InvalidArgumentError("SelectionSort expects (b,m,n) dist shape.")
     dist = device_tensor(dist, "dist", torch.float32)
-    B, m, n = (int(s) for s in dist.shape)
-    k = int(k)
-    if k > n:
+    if int(k) > int(dist.shape[2]):
         raise InvalidArgumentError("SelectionSort expects k <= n")
-    outi = torch.empty((B, m, n), dtype=torch.int32, device=dist.device)
-    out = torch.empty((B, m, n), dtype=torch.float32, device=dist.device)
-    ws = torch.empty((max(lib().pn2_select_top_k_workspace_size(B, m, k), 16),),
-                     dtype=torch.uint8, device=dist.device)
-    check(lib().pn2_select_top_k(ptr(dist), B, m, n, k, ptr(outi), ptr(out), ptr(ws),
-                                 stream_of(dist)), "SelectionSort")
-    return outi, out
+    return tuple(ops().select_top_k(int(k), dist))
 
 
 def knn_point(k, xyz1, xyz2):
@@ -116,15 +109,9 @@ def knn_point(k, xyz1, xyz2):
         raise InvalidArgumentError("knn_point expects (b,n,c) xyz1 and (b,m,c) xyz2")
     xyz1 = device_tensor(xyz1, "xyz1", torch.float32)
     xyz2 = device_tensor(xyz2, "xyz2", torch.float32)
-    B, n, c = (int(s) for s in xyz1.shape)
-    m, k = int(xyz2.shape[1]), int(k)
-    if not 0 < k <= n:
+    if not 0 < int(k) <= int(xyz1.shape[1]):
         raise InvalidArgumentError("SelectionSort expects positive k")
-    val = torch.empty((B, m, k), dtype=torch.float32, device=xyz1.device)
-    idx = torch.empty((B, m, k), dtype=torch.int32, device=xyz1.device)
-    check(lib().pn2_knn_point(ptr(xyz1), ptr(xyz2), B, n, m, c, k, ptr(val), ptr(idx),
-                              stream_of(xyz1)), "knn_point")
-    return val, idx
+    return tuple(ops().knn_point(int(k), xyz1, xyz2))
 
 
 def _check_group(points, idx, name="GroupPoint"):
@@ -132,24 +119,6 @@ def _check_group(points, idx, name="GroupPoint"):
         raise InvalidArgumentError(f"{name} expects (batch_size, num_points, channel) points shape")
     if idx.dim() != 3 or idx.shape[0] != points.shape[0]:  # tf_grouping.cpp:155
         raise InvalidArgumentError(f"{name} expects (batch_size, npoints, nsample) idx shape")
-
-
-def _group_fwd(points, idx):
-    B, N, C = (int(s) for s in points.shape)
-    M, ns = int(idx.shape[1]), int(idx.shape[2])
-    out = torch.empty((B, M, ns, C), dtype=torch.float32, device=points.device)
-    check(lib().pn2_group_point(ptr(points), ptr(idx), B, N, C, M, ns, ptr(out),
-                                stream_of(points)), "GroupPoint")
-    return out
-
-
-def _group_grad(B, N, C, idx, grad_out):
-    M, ns = int(idx.shape[1]), int(idx.shape[2])
-    grad_out = device_tensor(grad_out, "grad_out", torch.float32)
-    gp = torch.empty((B, N, C), dtype=torch.float32, device=grad_out.device)
-    check(lib().pn2_group_point_grad(ptr(grad_out), ptr(idx), B, N, C, M, ns, ptr(gp),
-                                     stream_of(grad_out)), "GroupPointGrad")
-    return gp
 
 
 def group_point_grad(points, idx, grad_out):
@@ -160,20 +129,8 @@ def group_point_grad(points, idx, grad_out):
     if tuple(grad_out.shape) != (B, M, ns, C):  # tf_grouping.cpp:191
         raise InvalidArgumentError(
             "GroupPointGrad expects (batch_size, npoints, nsample, channel) grad_out shape")
-    return _group_grad(B, N, C, device_tensor(idx, "idx", torch.int32), grad_out)
-
-
-class _GroupPoint(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, points, idx):
-        ctx.save_for_backward(idx)
-        ctx.bnc = tuple(int(s) for s in points.shape)
-        return _group_fwd(points, idx)
-
-    @staticmethod
-    def backward(ctx, grad_out):  # tf_grouping.py:42-46 (no gradient for idx)
-        (idx,) = ctx.saved_tensors
-        return _group_grad(*ctx.bnc, idx, grad_out), None
+    return ops().group_point_grad(points, device_tensor(idx, "idx", torch.int32),
+                                  device_tensor(grad_out, "grad_out", torch.float32))
 
 
 def group_point(points, idx):
@@ -186,8 +143,5 @@ def group_point(points, idx):
         out: (batch_size, npoint, nsample, channel) float32 array — differentiable w.r.t. points
     """
     _check_group(points, idx)
-    points = device_tensor(points, "points", torch.float32)
-    idx = device_tensor(idx, "idx", torch.int32)
-    if torch.is_grad_enabled() and points.requires_grad:
-        return _GroupPoint.apply(points, idx)
-    return _group_fwd(points, idx)
+    return ops().group_point(device_tensor(points, "points", torch.float32),
+                             device_tensor(idx, "idx", torch.int32))

@@ -1,11 +1,14 @@
 """three_nn / three_interpolate — drop-in for
 pointnet2_tensorflow/tf_ops/interpolation_3d/tf_interpolate.py (same names, argument order,
 shapes, dtypes and error messages). The reference registers these ops for DEVICE_CPU only
-(tf_interpolate.cpp:187,222,262); here they are gfx950 kernels and the data never leaves HBM.
+(tf_interpolate.cpp:187,222,262); here they are gfx950 kernels and the data never leaves HBM. Reference-signature calls go
+through the torch.ops.pn2 operators (csrc/torch_ops.cpp; autograd for three_interpolate in
+_torch_ops.py); three_nn with caller-built grids calls the C ABI directly.
 """
 import torch
 
 from ._lib import InvalidArgumentError, check, device_tensor, lib, ptr, stream_of
+from ._torch_ops import ops
 from .grid import PointGrid
 
 
@@ -38,6 +41,8 @@ def three_nn(xyz1, xyz2, known_grid=None, unknown_grid=None):
         raise InvalidArgumentError("ThreeNN expects (b,m,3) xyz2 shape.")
     xyz1 = device_tensor(xyz1, "xyz1", torch.float32)
     xyz2 = device_tensor(xyz2, "xyz2", torch.float32)
+    if known_grid is None and unknown_grid is None:  # the op picks the grid search itself
+        return tuple(ops().three_nn(xyz1, xyz2))
     B, n, m = int(xyz1.shape[0]), int(xyz1.shape[1]), int(xyz2.shape[1])
     dist = torch.empty((B, n, 3), dtype=torch.float32, device=xyz1.device)
     idx = torch.empty((B, n, 3), dtype=torch.int32, device=xyz1.device)
@@ -66,45 +71,15 @@ def _check_interp(points, idx, weight, name="ThreeInterpolate"):
         raise InvalidArgumentError(f"{name} expects (b,n,3) weight shape")
 
 
-def _interp_fwd(points, idx, weight):
-    B, m, C = (int(s) for s in points.shape)
-    n = int(idx.shape[1])
-    out = torch.empty((B, n, C), dtype=torch.float32, device=points.device)
-    check(lib().pn2_three_interpolate(ptr(points), ptr(idx), ptr(weight), B, m, C, n, ptr(out),
-                                      stream_of(points)), "ThreeInterpolate")
-    return out
-
-
-def _interp_grad(B, m, C, idx, weight, grad_out):
-    n = int(idx.shape[1])
-    grad_out = device_tensor(grad_out, "grad_out", torch.float32)
-    gp = torch.empty((B, m, C), dtype=torch.float32, device=grad_out.device)
-    check(lib().pn2_three_interpolate_grad(ptr(grad_out), ptr(idx), ptr(weight), B, n, C, m,
-                                           ptr(gp), stream_of(grad_out)), "ThreeInterpolateGrad")
-    return gp
-
-
 def three_interpolate_grad(points, idx, weight, grad_out):
     """ThreeInterpolateGrad (tf_interpolate.cpp:225-262)."""
     _check_interp(points, idx, weight, "ThreeInterpolateGrad")
     B, m, C = (int(s) for s in points.shape)
     if tuple(grad_out.shape) != (B, idx.shape[1], C):  # :243
         raise InvalidArgumentError("ThreeInterpolateGrad expects (b,n,c) grad_out shape")
-    return _interp_grad(B, m, C, device_tensor(idx, "idx", torch.int32),
-                        device_tensor(weight, "weight", torch.float32), grad_out)
-
-
-class _ThreeInterpolate(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, points, idx, weight):
-        ctx.save_for_backward(idx, weight)
-        ctx.bmc = tuple(int(s) for s in points.shape)
-        return _interp_fwd(points, idx, weight)
-
-    @staticmethod
-    def backward(ctx, grad_out):  # tf_interpolate.py:29-34 (points only)
-        idx, weight = ctx.saved_tensors
-        return _interp_grad(*ctx.bmc, idx, weight, grad_out), None, None
+    return ops().three_interpolate_grad(points, device_tensor(idx, "idx", torch.int32),
+                                        device_tensor(weight, "weight", torch.float32),
+                                        device_tensor(grad_out, "grad_out", torch.float32))
 
 
 def three_interpolate(points, idx, weight):
@@ -118,12 +93,9 @@ def three_interpolate(points, idx, weight):
         out: (b,n,c) float32 array, interpolated point values — differentiable w.r.t. points
     """
     _check_interp(points, idx, weight)
-    points = device_tensor(points, "points", torch.float32)
-    idx = device_tensor(idx, "idx", torch.int32)
-    weight = device_tensor(weight, "weight", torch.float32)
-    if torch.is_grad_enabled() and points.requires_grad:
-        return _ThreeInterpolate.apply(points, idx, weight)
-    return _interp_fwd(points, idx, weight)
+    return ops().three_interpolate(device_tensor(points, "points", torch.float32),
+                                   device_tensor(idx, "idx", torch.int32),
+                                   device_tensor(weight, "weight", torch.float32))
 
 
 def idw_weights(dist):
@@ -131,8 +103,4 @@ def idw_weights(dist):
     d = max(dist, 1e-10); weight = (1/d) / sum_3(1/d)."""
     if dist.dim() != 3 or dist.shape[2] != 3:
         raise InvalidArgumentError("idw_weights expects (b,n,3) dist shape")
-    dist = device_tensor(dist, "dist", torch.float32)
-    B, n = int(dist.shape[0]), int(dist.shape[1])
-    w = torch.empty_like(dist)
-    check(lib().pn2_idw_weights(ptr(dist), B, n, ptr(w), stream_of(dist)), "idw_weights")
-    return w
+    return ops().idw_weights(device_tensor(dist, "dist", torch.float32))

@@ -1,12 +1,15 @@
 """Farthest point sampling, gather_point and prob_sample — drop-in for
 pointnet2_tensorflow/tf_ops/sampling/tf_sampling.py (same names, argument order, shapes,
-dtypes and error messages), running the gfx950 kernels of libpn2hip.so.
+dtypes and error messages), running the gfx950 kernels of libpn2hip.so through the
+torch.ops.pn2 operators (csrc/torch_ops.cpp; autograd for gather_point in _torch_ops.py).
+The fused sampler chain (farthest_point_sample_chain) calls the C ABI directly.
 """
 import ctypes
 
 import torch
 
 from ._lib import InvalidArgumentError, check, device_tensor, lib, ptr, stream_of
+from ._torch_ops import ops
 
 
 def _fps(npoint, inp, want_xyz):
@@ -16,20 +19,9 @@ def _fps(npoint, inp, want_xyz):
         raise InvalidArgumentError(
             "FarthestPointSample expects (batch_size,num_points,3) inp shape")
     inp = device_tensor(inp, "inp", torch.float32)
-    B, N = int(inp.shape[0]), int(inp.shape[1])
-    idx = torch.empty((B, npoint), dtype=torch.int32, device=inp.device)
-    new_xyz = torch.empty((B, npoint, 3), dtype=torch.float32, device=inp.device) if want_xyz \
-        else None
-    L = lib()
-    ws_bytes = L.pn2_fps_workspace_size(B, N)
-    if ws_bytes:
-        ws = torch.empty((ws_bytes + 3) // 4, dtype=torch.float32, device=inp.device)
-        rc = L.pn2_fps_ws(ptr(inp), B, N, npoint, ptr(idx), ptr(new_xyz), ptr(ws), ws_bytes,
-                          stream_of(inp))
-    else:
-        rc = L.pn2_fps_gather(ptr(inp), B, N, npoint, ptr(idx), ptr(new_xyz), stream_of(inp))
-    check(rc, "FarthestPointSample")
-    return idx, new_xyz
+    if want_xyz:
+        return tuple(ops().farthest_point_sample_and_gather(npoint, inp))
+    return ops().farthest_point_sample(npoint, inp), None
 
 
 def prob_sample(inp, inpr):
@@ -43,18 +35,8 @@ def prob_sample(inp, inpr):
         raise InvalidArgumentError("ProbSample expects (batch_size,num_choices) inp shape")
     if inpr.dim() != 2 or inpr.shape[0] != inp.shape[0]:  # tf_sampling.cpp:79
         raise InvalidArgumentError("ProbSample expects (batch_size,num_points) inpr shape")
-    inp = device_tensor(inp, "inp", torch.float32)
-    inpr = device_tensor(inpr, "inpr", torch.float32)
-    B, N, M = int(inp.shape[0]), int(inp.shape[1]), int(inpr.shape[1])
-    out = torch.empty((B, M), dtype=torch.int32, device=inp.device)
-    if B == 0 or M == 0:
-        return out
-    L = lib()
-    ws_bytes = L.pn2_prob_sample_workspace_size(B, N)
-    ws = torch.empty(max(1, ws_bytes // 4), dtype=torch.float32, device=inp.device)
-    check(L.pn2_prob_sample(ptr(inp), ptr(inpr), B, N, M, ptr(ws), ws_bytes, ptr(out),
-                            stream_of(inp)), "ProbSample")
-    return out
+    return ops().prob_sample(device_tensor(inp, "inp", torch.float32),
+                             device_tensor(inpr, "inpr", torch.float32))
 
 
 def farthest_point_sample(npoint, inp):
@@ -128,23 +110,6 @@ def _check_gather(inp, idx, name="GatherPoint"):
         raise InvalidArgumentError(f"{name} expects (batch_size,num_result) idx shape")
 
 
-def _gather_fwd(inp, idx):
-    B, N, M = int(inp.shape[0]), int(inp.shape[1]), int(idx.shape[1])
-    out = torch.empty((B, M, 3), dtype=torch.float32, device=inp.device)
-    check(lib().pn2_gather_point(ptr(inp), ptr(idx), B, N, M, ptr(out), stream_of(inp)),
-          "GatherPoint")
-    return out
-
-
-def _scatter_add(B, N, idx, out_g):
-    M = int(idx.shape[1])
-    out_g = device_tensor(out_g, "out_g", torch.float32)
-    inp_g = torch.empty((B, N, 3), dtype=torch.float32, device=out_g.device)
-    check(lib().pn2_gather_point_grad(ptr(out_g), ptr(idx), B, N, M, ptr(inp_g),
-                                      stream_of(out_g)), "GatherPointGrad")
-    return inp_g
-
-
 def gather_point_grad(inp, idx, out_g):
     """GatherPointGrad (tf_sampling.cpp:150-178): scatter-add of out_g into inp's shape."""
     if inp.dim() != 3 or inp.shape[2] != 3:
@@ -156,20 +121,8 @@ def gather_point_grad(inp, idx, out_g):
     if tuple(out_g.shape) != (B, M, 3):
         raise InvalidArgumentError(
             "GatherPointGradGpuOp expects (batch_size,num_result,3) out_g shape")
-    return _scatter_add(B, N, device_tensor(idx, "idx", torch.int32), out_g)
-
-
-class _GatherPoint(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, inp, idx):
-        ctx.save_for_backward(idx)
-        ctx.bn = (int(inp.shape[0]), int(inp.shape[1]))
-        return _gather_fwd(inp, idx)
-
-    @staticmethod
-    def backward(ctx, out_g):  # tf_sampling.py:44-48 (no gradient for idx)
-        (idx,) = ctx.saved_tensors
-        return _scatter_add(ctx.bn[0], ctx.bn[1], idx, out_g), None
+    return ops().gather_point_grad(inp, device_tensor(idx, "idx", torch.int32),
+                                   device_tensor(out_g, "out_g", torch.float32))
 
 
 def gather_point(inp, idx):
@@ -179,8 +132,5 @@ def gather_point(inp, idx):
     returns: (batch_size, npoints, 3) float32 — differentiable w.r.t. inp
     """
     _check_gather(inp, idx)
-    inp = device_tensor(inp, "inp", torch.float32)
-    idx = device_tensor(idx, "idx", torch.int32)
-    if torch.is_grad_enabled() and inp.requires_grad:
-        return _GatherPoint.apply(inp, idx)
-    return _gather_fwd(inp, idx)
+    return ops().gather_point(device_tensor(inp, "inp", torch.float32),
+                              device_tensor(idx, "idx", torch.int32))
