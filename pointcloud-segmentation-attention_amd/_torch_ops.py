@@ -13,7 +13,7 @@ import os
 
 import torch
 
-from ._lib import _HERE
+from ._lib import _HERE, InvalidArgumentError
 
 TORCH_LIB_PATH = os.environ.get("PN2TORCH_LIB") or os.path.join(_HERE, "libpn2torch.so")
 _loaded = False
@@ -31,6 +31,18 @@ def ops():
         _register_autograd()
         _loaded = True
     return torch.ops.pn2
+
+
+def call(name, *args):
+    """torch.ops.pn2.<name>(*args) for the mirror modules: the op's reference-text ValueError
+    (TORCH_CHECK_VALUE, or PN2_EINVAL from the C ABI) surfaces as InvalidArgumentError, the
+    mirror's stand-in for tf.errors.InvalidArgumentError (a ValueError too)."""
+    try:
+        return getattr(ops(), name)(*args)
+    except InvalidArgumentError:
+        raise
+    except ValueError as e:
+        raise InvalidArgumentError(str(e).splitlines()[0]) from e
 
 
 def _register_autograd():

@@ -10,7 +10,7 @@ import torch
 
 from . import pointnet_util, tf_grouping, tf_sampling, tf_util
 from ._lib import InvalidArgumentError, check, device_tensor, lib, ptr, stream_of
-from ._torch_ops import ops
+from ._torch_ops import call
 
 
 def attention_reduce(Q, K, V):
@@ -28,7 +28,7 @@ def attention_reduce(Q, K, V):
     if tuple(Q.shape) != (B, M, C) or C % 4 != 0:
         raise InvalidArgumentError("attention_reduce expects Q (B,M,C) with C a multiple of 4")
     # torch.ops.pn2.attn_reduce (autograd: pn2_attn_reduce_grad, _torch_ops.py)
-    return ops().attn_reduce(device_tensor(Q, "Q", torch.float32),
+    return call("attn_reduce", device_tensor(Q, "Q", torch.float32),
                              device_tensor(K, "K", torch.float32),
                              device_tensor(V, "V", torch.float32))
 
@@ -36,7 +36,7 @@ def attention_reduce(Q, K, V):
 def attention_reduce_grad(Q, K, V, grad_out):
     """(dQ, dK, dV) of attention_reduce for the incoming gradient grad_out (B,M,C): the
     gradient TF's autodiff takes through attention_layer.py:35-42 (pn2_attn_reduce_grad)."""
-    return tuple(ops().attn_reduce_grad(device_tensor(Q, "Q", torch.float32),
+    return tuple(call("attn_reduce_grad", device_tensor(Q, "Q", torch.float32),
                                         device_tensor(K, "K", torch.float32),
                                         device_tensor(V, "V", torch.float32),
                                         device_tensor(grad_out, "grad_out", torch.float32)))

@@ -14,7 +14,7 @@ benchmark step's early grid) calls the C ABI directly.
 import torch
 
 from ._lib import InvalidArgumentError, check, device_tensor, lib, ptr, stream_of
-from ._torch_ops import ops
+from ._torch_ops import call
 from .grid import PointGrid
 
 
@@ -60,7 +60,7 @@ def query_ball_point(radius, nsample, xyz1, xyz2, grid=None):
     xyz1 = device_tensor(xyz1, "xyz1", torch.float32)
     xyz2 = device_tensor(xyz2, "xyz2", torch.float32)
     if grid is None:  # the op builds the grid itself when the cloud is large (same switch)
-        return tuple(ops().query_ball_point(float(radius), int(nsample), xyz1, xyz2))
+        return tuple(call("query_ball_point", float(radius), int(nsample), xyz1, xyz2))
     if not grid.matches(xyz1):
         raise InvalidArgumentError("QueryBallPoint grid was built over a different xyz1")
     B, N = int(xyz1.shape[0]), int(xyz1.shape[1])
@@ -89,7 +89,7 @@ def select_top_k(k, dist):
     dist = device_tensor(dist, "dist", torch.float32)
     if int(k) > int(dist.shape[2]):
         raise InvalidArgumentError("SelectionSort expects k <= n")
-    return tuple(ops().select_top_k(int(k), dist))
+    return tuple(call("select_top_k", int(k), dist))
 
 
 def knn_point(k, xyz1, xyz2):
@@ -111,7 +111,7 @@ def knn_point(k, xyz1, xyz2):
     xyz2 = device_tensor(xyz2, "xyz2", torch.float32)
     if not 0 < int(k) <= int(xyz1.shape[1]):
         raise InvalidArgumentError("SelectionSort expects positive k")
-    return tuple(ops().knn_point(int(k), xyz1, xyz2))
+    return tuple(call("knn_point", int(k), xyz1, xyz2))
 
 
 def _check_group(points, idx, name="GroupPoint"):
@@ -129,7 +129,7 @@ def group_point_grad(points, idx, grad_out):
     if tuple(grad_out.shape) != (B, M, ns, C):  # tf_grouping.cpp:191
         raise InvalidArgumentError(
             "GroupPointGrad expects (batch_size, npoints, nsample, channel) grad_out shape")
-    return ops().group_point_grad(points, device_tensor(idx, "idx", torch.int32),
+    return call("group_point_grad", points, device_tensor(idx, "idx", torch.int32),
                                   device_tensor(grad_out, "grad_out", torch.float32))
 
 
@@ -143,5 +143,5 @@ def group_point(points, idx):
         out: (batch_size, npoint, nsample, channel) float32 array — differentiable w.r.t. points
     """
     _check_group(points, idx)
-    return ops().group_point(device_tensor(points, "points", torch.float32),
+    return call("group_point", device_tensor(points, "points", torch.float32),
                              device_tensor(idx, "idx", torch.int32))

@@ -8,7 +8,7 @@ _torch_ops.py); three_nn with caller-built grids calls the C ABI directly.
 import torch
 
 from ._lib import InvalidArgumentError, check, device_tensor, lib, ptr, stream_of
-from ._torch_ops import ops
+from ._torch_ops import call
 from .grid import PointGrid
 
 
@@ -42,7 +42,7 @@ def three_nn(xyz1, xyz2, known_grid=None, unknown_grid=None):
     xyz1 = device_tensor(xyz1, "xyz1", torch.float32)
     xyz2 = device_tensor(xyz2, "xyz2", torch.float32)
     if known_grid is None and unknown_grid is None:  # the op picks the grid search itself
-        return tuple(ops().three_nn(xyz1, xyz2))
+        return tuple(call("three_nn", xyz1, xyz2))
     B, n, m = int(xyz1.shape[0]), int(xyz1.shape[1]), int(xyz2.shape[1])
     dist = torch.empty((B, n, 3), dtype=torch.float32, device=xyz1.device)
     idx = torch.empty((B, n, 3), dtype=torch.int32, device=xyz1.device)
@@ -77,7 +77,7 @@ def three_interpolate_grad(points, idx, weight, grad_out):
     B, m, C = (int(s) for s in points.shape)
     if tuple(grad_out.shape) != (B, idx.shape[1], C):  # :243
         raise InvalidArgumentError("ThreeInterpolateGrad expects (b,n,c) grad_out shape")
-    return ops().three_interpolate_grad(points, device_tensor(idx, "idx", torch.int32),
+    return call("three_interpolate_grad", points, device_tensor(idx, "idx", torch.int32),
                                         device_tensor(weight, "weight", torch.float32),
                                         device_tensor(grad_out, "grad_out", torch.float32))
 
@@ -93,7 +93,7 @@ def three_interpolate(points, idx, weight):
         out: (b,n,c) float32 array, interpolated point values — differentiable w.r.t. points
     """
     _check_interp(points, idx, weight)
-    return ops().three_interpolate(device_tensor(points, "points", torch.float32),
+    return call("three_interpolate", device_tensor(points, "points", torch.float32),
                                    device_tensor(idx, "idx", torch.int32),
                                    device_tensor(weight, "weight", torch.float32))
 
@@ -103,4 +103,4 @@ def idw_weights(dist):
     d = max(dist, 1e-10); weight = (1/d) / sum_3(1/d)."""
     if dist.dim() != 3 or dist.shape[2] != 3:
         raise InvalidArgumentError("idw_weights expects (b,n,3) dist shape")
-    return ops().idw_weights(device_tensor(dist, "dist", torch.float32))
+    return call("idw_weights", device_tensor(dist, "dist", torch.float32))

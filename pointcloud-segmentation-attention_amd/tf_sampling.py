@@ -9,7 +9,7 @@ import ctypes
 import torch
 
 from ._lib import InvalidArgumentError, check, device_tensor, lib, ptr, stream_of
-from ._torch_ops import ops
+from ._torch_ops import call
 
 
 def _fps(npoint, inp, want_xyz):
@@ -20,8 +20,8 @@ def _fps(npoint, inp, want_xyz):
             "FarthestPointSample expects (batch_size,num_points,3) inp shape")
     inp = device_tensor(inp, "inp", torch.float32)
     if want_xyz:
-        return tuple(ops().farthest_point_sample_and_gather(npoint, inp))
-    return ops().farthest_point_sample(npoint, inp), None
+        return tuple(call("farthest_point_sample_and_gather", npoint, inp))
+    return call("farthest_point_sample", npoint, inp), None
 
 
 def prob_sample(inp, inpr):
@@ -35,7 +35,7 @@ def prob_sample(inp, inpr):
         raise InvalidArgumentError("ProbSample expects (batch_size,num_choices) inp shape")
     if inpr.dim() != 2 or inpr.shape[0] != inp.shape[0]:  # tf_sampling.cpp:79
         raise InvalidArgumentError("ProbSample expects (batch_size,num_points) inpr shape")
-    return ops().prob_sample(device_tensor(inp, "inp", torch.float32),
+    return call("prob_sample", device_tensor(inp, "inp", torch.float32),
                              device_tensor(inpr, "inpr", torch.float32))
 
 
@@ -121,7 +121,7 @@ def gather_point_grad(inp, idx, out_g):
     if tuple(out_g.shape) != (B, M, 3):
         raise InvalidArgumentError(
             "GatherPointGradGpuOp expects (batch_size,num_result,3) out_g shape")
-    return ops().gather_point_grad(inp, device_tensor(idx, "idx", torch.int32),
+    return call("gather_point_grad", inp, device_tensor(idx, "idx", torch.int32),
                                    device_tensor(out_g, "out_g", torch.float32))
 
 
@@ -132,5 +132,5 @@ def gather_point(inp, idx):
     returns: (batch_size, npoints, 3) float32 — differentiable w.r.t. inp
     """
     _check_gather(inp, idx)
-    return ops().gather_point(device_tensor(inp, "inp", torch.float32),
+    return call("gather_point", device_tensor(inp, "inp", torch.float32),
                               device_tensor(idx, "idx", torch.int32))
