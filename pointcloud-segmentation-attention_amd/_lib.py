@@ -48,6 +48,7 @@ SIGNATURES = {
     "pn2_fps": (_I, [_P, _I, _I, _I, _P, _P]),
     "pn2_fps_gather": (_I, [_P, _I, _I, _I, _P, _P, _P]),
     "pn2_fps_max_points": (_I, []),
+    "pn2_fps_set_algo": (_I, [_I]),
     "pn2_prob_sample_workspace_size": (_S, [_I, _I]),
     "pn2_prob_sample": (_I, [_P, _P, _I, _I, _I, _P, _S, _P, _P]),
     "pn2_fps_workspace_size": (_S, [_I, _I]),

@@ -11,6 +11,7 @@
 // pointnet_util.py:34). Clouds beyond kMaxRegPoints keep the running min in a caller-provided
 // workspace (fps_ws_kernel). Measured variants live in tools/fps_lab.
 #include "fps_kernels.h"
+#include "fps_hot.h"
 
 // Code placement of the SA1 (256 x 32) sampler's iteration loop. The loop runs ~6 % slower
 // when it starts at an address = 0 mod 8 than at 4 mod 8 (tools/pad_fps.py,
@@ -108,6 +109,9 @@ __global__ void gather_point_grad_kernel(const float* __restrict__ out_g,
 
 constexpr int kMaxRegPoints = 1024 * 16;
 
+// Sampler selection for large clouds: 0 = measured default, 1 = v9 block scan, 2 = hot set.
+int g_fps_algo = 0;
+
 // ---- sampler chain: SA1..SAk's samplers of one cloud, stage 2.. in ONE workgroup -----------
 // The SSG stack samples 8192 -> 1024 -> 256 -> 64 -> 16, each stage from the previous stage's
 // output. pn2_fps_chain runs a big first stage (N > kChainNext) as the ordinary sampler
@@ -178,7 +182,11 @@ int fps_impl(const float* xyz, int B, int N, int M, int32_t* idx, float* nx, voi
   else if (N <= 1024) launch_v9<256, 4, 2, true>(xyz, B, N, M, idx, nx, s);
   else if (N <= 2048) launch_v9<256, 8, 2, true>(xyz, B, N, M, idx, nx, s);
   else if (N <= 4096) launch_v9<256, 16, 4, true>(xyz, B, N, M, idx, nx, s);
-  else if (N <= 8192) launch_v9<256, 32, 4, true, false, PN2_SA1_PAD>(xyz, B, N, M, idx, nx, s);
+  else if (N <= 8192) {
+    if (g_fps_algo >= 2) launch_hot<256, 32>(xyz, B, N, M, idx, nx, s, g_fps_algo == 3 || g_fps_algo == 5,
+                                             g_fps_algo >= 4);
+    else launch_v9<256, 32, 4, true, false, PN2_SA1_PAD>(xyz, B, N, M, idx, nx, s);
+  }
   else if (N <= kMaxRegPoints) launch_v9<512, 32, 4>(xyz, B, N, M, idx, nx, s);
   else {
     if (!ws || ws_bytes < (size_t)B * N * sizeof(float)) return PN2_EINVAL;
@@ -193,6 +201,12 @@ int fps_impl(const float* xyz, int B, int N, int M, int32_t* idx, float* nx, voi
 extern "C" {
 
 int pn2_fps_max_points(void) { return pn2::kMaxRegPoints; }
+
+int pn2_fps_set_algo(int algo) {
+  const int old = pn2::g_fps_algo;
+  if (algo >= 0 && algo <= 5) pn2::g_fps_algo = algo;
+  return old;
+}
 
 int pn2_fps_chain(const float* xyz, int B, int N, int nstages, const int* npoint,
                   int32_t* const* idx, float* const* new_xyz, pn2_stream_t stream) {

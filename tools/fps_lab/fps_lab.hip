@@ -3,6 +3,7 @@
 // and tools/stamp_fps.py. NOT part of libpn2hip.so: built into tools/fps_lab/libpn2fpslab.so
 // by tools/fps_lab/Makefile. DESIGN.md records what each variant taught.
 #include "../../pointcloud-segmentation-attention_amd/csrc/fps_kernels.h"
+#include "../../pointcloud-segmentation-attention_amd/csrc/fps_hot.h"
 
 namespace pn2 {
 namespace {
@@ -1789,10 +1790,114 @@ int fps_tune_impl(const float* xyz, int B, int N, int M, int32_t* idx, float* nx
 }
 
 
+
+// Hot-loop micro-benchmark (lab only): wave 0 of one workgroup runs the fps_hot.h hot-phase
+// pick loop over the first 128 points of a cloud with no certification bound, `iters` picks,
+// and reports s_memtime cycles per pick. VAR bits switch pieces off to price them:
+// 1 = no ring write, 2 = no tie check, 4 = no readfirstlane (ballot on the DPP result).
+template <int VAR>
+__global__ __launch_bounds__(64) void hot_loop_bench(const float* __restrict__ xyz, int iters,
+                                                     int32_t* __restrict__ out,
+                                                     unsigned long long* __restrict__ cyc) {
+  using f2 = float __attribute__((ext_vector_type(2)));
+  __shared__ float4 scl[256];
+  const int lane = threadIdx.x;
+  int hv[2], hk[2];
+  f2 hx, hy, hz;
+  for (int q = 0; q < 2; ++q) {
+    hk[q] = lane * 2 + q;
+    hx[q] = xyz[3 * hk[q]]; hy[q] = xyz[3 * hk[q] + 1]; hz[q] = xyz[3 * hk[q] + 2];
+    hv[q] = __float_as_int(kInitTemp);
+  }
+  const uint32_t hkey0 = hot_key(hk[0]), hkey1 = hot_key(hk[1]);
+  int acc = 0;
+  unsigned long long c0, c1;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(c0)::"memory");
+  for (int jj = 0; jj < iters; ++jj) {
+    const bool b1 = hv[1] > hv[0] || (hv[1] == hv[0] && hkey1 < hkey0);
+    const int cv = b1 ? hv[1] : hv[0];
+    const uint32_t ck = b1 ? hkey1 : hkey0;
+    const uint32_t enc = hot_enc(cv);
+    const uint32_t wmv = wave_max_u32(enc);
+    const uint32_t wm = (VAR & 4) ? wmv : uniform_u32(wmv);
+    const uint64_t hold = __builtin_amdgcn_ballot_w64(enc == wm);
+    int L;
+    if ((VAR & 2) || __builtin_popcountll(hold) == 1) {
+      L = (int)__builtin_ctzll(hold);
+    } else {
+      const uint32_t km = ~uniform_u32(wave_max_u32(enc == wm ? ~ck : 0u));
+      L = (int)__builtin_ctzll(__builtin_amdgcn_ballot_w64(enc == wm && ck == km));
+    }
+    const uint32_t wkey = (uint32_t)__builtin_amdgcn_readlane((int)ck, L);
+    acc += (int)wkey;
+    const float lx = b1 ? hx[1] : hx[0], ly = b1 ? hy[1] : hy[0], lz = b1 ? hz[1] : hz[0];
+    const int lk = b1 ? hk[1] : hk[0];
+    if (!(VAR & 1))
+      if (lane == L) scl[jj & 255] = make_float4(lx, ly, lz, __int_as_float(lk));
+    const float cx = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, lx), L));
+    const float cy = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, ly), L));
+    const float cz = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, lz), L));
+    const f2 c2x = {cx, cx}, c2y = {cy, cy}, c2z = {cz, cz};
+    const f2 dx = hx - c2x, dy = hy - c2y, dz = hz - c2z;
+    const f2 d = (dx * dx + dy * dy) + dz * dz;
+    hv[0] = min(hv[0], __float_as_int(d.x));
+    hv[1] = min(hv[1], __float_as_int(d.y));
+  }
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(c1)::"memory");
+  __syncthreads();
+  out[lane] = acc + hv[0] + hv[1] + __float_as_int(scl[lane].x);
+  if (lane == 0) cyc[0] = c1 - c0;
+}
 }  // namespace
 }  // namespace pn2
 
 extern "C" {
+
+// Hot-loop micro-benchmark: cycles for `iters` picks of variant `var` (hot_loop_bench).
+int pn2_hot_loop_bench(const float* xyz, int iters, int var, int32_t* out,
+                       unsigned long long* cyc_dev) {
+  hipStream_t s = 0;
+#define PN2_HB(V) \
+  if (var == V) hipLaunchKernelGGL(pn2::hot_loop_bench<V>, dim3(1), dim3(64), 0, s, xyz, iters, out, cyc_dev); else
+  PN2_HB(0) PN2_HB(1) PN2_HB(2) PN2_HB(3) PN2_HB(4) PN2_HB(7) { return PN2_EINVAL; }
+#undef PN2_HB
+  return (int)hipDeviceSynchronize();
+}
+
+// Diagnostic entry: stamped hot-set sampler (fps_hot.h) over B clouds; out (16 clouds x 16
+// waves x 8): per wave the cycles of phases 0 cold pass, 1 lane top-3, 2 row extraction,
+// 3 extraction barrier, 4 hot phase (wave 0) / wait (others), 5 loop-top barrier; [6] refresh
+// rounds, [7] hot picks (wave 0).
+int pn2_fps_hot_stamp(const float* xyz, int B, int N, int npoint, int32_t* idx,
+                      unsigned long long* out_host) {
+  hipStream_t s = 0;
+  if (N > 8192 || N <= 4096) return PN2_EINVAL;
+  hipLaunchKernelGGL((pn2::fps_hot_kernel<256, 32, 2, 8, 256, true>), dim3(B), dim3(256), 0, s,
+                     xyz, N, npoint, idx, nullptr);
+  hipError_t e = hipDeviceSynchronize();
+  if (e != hipSuccess) return (int)e;
+  e = hipMemcpyFromSymbol(out_host, HIP_SYMBOL(pn2::g_stamp),
+                          sizeof(unsigned long long) * 16 * 16 * 8);
+  return (int)e;
+}
+
+// Diagnostic entry: stamped asynchronous hot-set sampler (fps_hota_kernel<8, 16, 4>); out as
+// pn2_fps_hot_stamp with 9 waves: phases 0 B1 wait, 1 write-out, 2 cold catch-up, 3 top-3 +
+// extraction, 4 B2 wait, 5 hot setup, 6 hot loop / cold async loop; row 12: [0] kernel
+// cycles, [1] real time (10 ns), [2] rounds, [3] hot picks, [4] tie paths, [5] centres applied
+// asynchronously (wave 1), [6] idle spins (wave 1).
+int pn2_fps_hota_stamp(const float* xyz, int B, int N, int npoint, int32_t* idx,
+                       unsigned long long* out_host) {
+  hipStream_t s = 0;
+  if (N > 8192) return PN2_EINVAL;
+  hipLaunchKernelGGL((pn2::fps_hota_kernel<7, 20, 4, 8192, 256, true>), dim3(B), dim3(512), 0, s,
+                     xyz, N, npoint, idx, nullptr);
+  hipError_t e = hipDeviceSynchronize();
+  if (e != hipSuccess) return (int)e;
+  e = hipMemcpyFromSymbol(out_host, HIP_SYMBOL(pn2::g_stamp),
+                          sizeof(unsigned long long) * 16 * 16 * 8);
+  return (int)e;
+}
 
 // Diagnostic entry: stamped v2 run; out[w*8+ph] = cycles of phase ph summed over the
 // iterations, for wave w of cloud 0 (ph: 0 scan, 1 wave reduce, 2 write+barrier,
