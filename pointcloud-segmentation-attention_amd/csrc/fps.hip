@@ -12,6 +12,7 @@
 // workspace (fps_ws_kernel). Measured variants live in tools/fps_lab.
 #include "fps_kernels.h"
 #include "fps_hot.h"
+#include "fps_cull.h"
 
 // Code placement of the SA1 (256 x 32) sampler's iteration loop. The loop runs ~6 % slower
 // when it starts at an address = 0 mod 8 than at 4 mod 8 (tools/pad_fps.py,
@@ -183,7 +184,8 @@ int fps_impl(const float* xyz, int B, int N, int M, int32_t* idx, float* nx, voi
   else if (N <= 2048) launch_v9<256, 8, 2, true>(xyz, B, N, M, idx, nx, s);
   else if (N <= 4096) launch_v9<256, 16, 4, true>(xyz, B, N, M, idx, nx, s);
   else if (N <= 8192) {
-    if (g_fps_algo >= 2) launch_hot<256, 32>(xyz, B, N, M, idx, nx, s, g_fps_algo == 3 || g_fps_algo == 5,
+    if (g_fps_algo == 6) launch_cull<16, 9>(xyz, B, N, M, idx, nx, s);
+    else if (g_fps_algo >= 2) launch_hot<256, 32>(xyz, B, N, M, idx, nx, s, g_fps_algo == 3 || g_fps_algo == 5,
                                              g_fps_algo >= 4);
     else launch_v9<256, 32, 4, true, false, PN2_SA1_PAD>(xyz, B, N, M, idx, nx, s);
   }
@@ -204,7 +206,7 @@ int pn2_fps_max_points(void) { return pn2::kMaxRegPoints; }
 
 int pn2_fps_set_algo(int algo) {
   const int old = pn2::g_fps_algo;
-  if (algo >= 0 && algo <= 5) pn2::g_fps_algo = algo;
+  if (algo >= 0 && algo <= 6) pn2::g_fps_algo = algo;
   return old;
 }
 

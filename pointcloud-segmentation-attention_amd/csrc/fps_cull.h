@@ -1,0 +1,682 @@
+// Culled hot-set farthest-point sampler for large clouds (SA1: 8,192 -> 1,024) on gfx950.
+// Reference: farthestpointsamplingKernel, pointnet2_tensorflow/tf_ops/sampling/
+// tf_sampling_g.cu:105-170 -- running min distance (:139-145), argmax with the tie rule of the
+// 512-thread tree (:146-163), the new centre is the argmax (:164-167).
+//
+// Same output as fps_v9_kernel, bit for bit; a different schedule of the same arithmetic.
+//  * CELLS. The cloud is counting-sorted by a 16^3 Morton bucket, and every wave slot (64
+//    consecutive sorted points) is a cell with a bounding box and the exact maximum Tmax of
+//    its running mins. A centre c can lower a point of the cell only if its box lower bound
+//    lb(c) < Tmax. lb is computed in fp32 with the same rounding steps as the distance, and
+//    every step is monotone, so fl-dist(p, c) >= lb for every p in the box: a skipped
+//    (cell, centre) pair leaves every running min unchanged, exactly.
+//  * HOT SET. After each refresh the points above a threshold tau (the smallest of NT fractions
+//    of the global max whose count fits K = 128) form the hot set. Wave 0 picks from it alone:
+//    while its best value is > tau it beats every other point (they are all <= tau, and
+//    running mins only decrease), so it IS the reference's next centre; the wave updates the
+//    hot values and goes on -- no block-wide argmax per pick.
+//  * REFRESH. When the hot best drops to <= tau, every wave applies the batch of centres
+//    picked since the last refresh to its cells (culled; two centres per packed pass), the
+//    changed cells' Tmax are recomputed, and a new tau and hot set are chosen. If no fraction
+//    fits (more than K points tie near the max), one exact block argmax picks the centre.
+// Exactness does not depend on the sort: any cell layout gives the same picks; the sort only
+// decides how much the box test skips (tools/model_fps_cull.py models it on the SA1 crops:
+// ~34 refreshes for 1,023 picks, ~93 % of (cell, centre) pairs skipped).
+#pragma once
+#include "fps_kernels.h"
+
+namespace pn2 {
+namespace {
+
+__device__ unsigned long long g_cull_stats[16 * 8];  // STAMP builds: per-cloud counters
+
+// float max over the wave (every lane gets it); DPP rows, then the gfx950 permlane swaps
+PN2_DEV float wave_max_f32(float v) {
+#define PN2_FMAX_DPP(C) v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp( \
+                              __float_as_int(v), __float_as_int(v), C, 0xF, 0xF, false)))
+  PN2_FMAX_DPP(kDppXor1);
+  PN2_FMAX_DPP(kDppXor2);
+  PN2_FMAX_DPP(kDppHalfMirror);
+  PN2_FMAX_DPP(kDppMirror);
+#undef PN2_FMAX_DPP
+  {
+    auto x = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = fmaxf(__uint_as_float(x[0]), __uint_as_float(x[1]));
+  }
+  {
+    auto x = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = fmaxf(__uint_as_float(x[0]), __uint_as_float(x[1]));
+  }
+  return v;
+}
+
+// signed 32-bit max over the wave (every lane gets it): v_max_i32_dpp rows, permlane swaps
+PN2_DEV int wave_max_i32(int v) {
+#define PN2_IMAX_DPP(C) v = max(v, __builtin_amdgcn_update_dpp(v, v, C, 0xF, 0xF, false))
+  PN2_IMAX_DPP(kDppXor1);
+  PN2_IMAX_DPP(kDppXor2);
+  PN2_IMAX_DPP(kDppHalfMirror);
+  PN2_IMAX_DPP(kDppMirror);
+#undef PN2_IMAX_DPP
+  {
+    auto x = __builtin_amdgcn_permlane16_swap((uint32_t)v, (uint32_t)v, false, false);
+    v = max((int)x[0], (int)x[1]);
+  }
+  {
+    auto x = __builtin_amdgcn_permlane32_swap((uint32_t)v, (uint32_t)v, false, false);
+    v = max((int)x[0], (int)x[1]);
+  }
+  return v;
+}
+
+// tie key: smaller = earlier in the reference's order (k mod 512, k div 512); N < 2^25
+PN2_DEV uint32_t cull_key(int k) { return ((uint32_t)(k & 511) << 16) | ((uint32_t)k >> 9); }
+
+// exclusive prefix sum over the wave (Hillis-Steele on ds_swizzle-free shuffles)
+PN2_DEV uint32_t wave_excl_scan(uint32_t v, int lane) {
+  uint32_t s = v;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const uint32_t u = (uint32_t)__shfl_up((int)s, o, kWave);
+    s += lane >= o ? u : 0u;
+  }
+  return s - v;
+}
+
+// the box lower bound of a centre: every step rounds monotonically, so it never exceeds the
+// fp32 distance (((dx*dx)+(dy*dy))+(dz*dz)) of any point inside the box
+PN2_DEV float box_lb(float4 lo, float4 hi, float cx, float cy, float cz) {
+  const float gx = fmaxf(fmaxf(lo.x - cx, cx - hi.x), 0.0f);
+  const float gy = fmaxf(fmaxf(lo.y - cy, cy - hi.y), 0.0f);
+  const float gz = fmaxf(fmaxf(lo.z - cz, cz - hi.z), 0.0f);
+  return (gx * gx + gy * gy) + gz * gz;
+}
+
+// threshold fractions of the global max, ascending (chosen: the first whose count fits)
+__constant__ float kCullFrac[12] = {0.6f, 0.7f, 0.75f, 0.8f, 0.84f, 0.87f,
+                                    0.9f, 0.92f, 0.94f, 0.96f, 0.98f, 0.99f};
+
+
+// STAMP builds: s_memtime of an event of round r of cloud 0, wave WV (g_iter[r * 16 + F])
+#define PN2_TRACE(F, WV)                                                                   \
+  if constexpr (STAMP) {                                                                   \
+    if (b == 0 && lane == 0 && w == (WV) && round < 256)                                   \
+      g_iter[round * 16 + (F)] = __builtin_amdgcn_s_memtime();                             \
+  }
+
+// bits s, s + PPT, s + 2 PPT, ... (GRP of them): the lanes that test cell s in a group
+template <int PPT, int GRP>
+PN2_DEV constexpr uint64_t cell_lanes(int s) {
+  uint64_t m = 0;
+  for (int i = 0; i < GRP; ++i) m |= 1ull << (PPT * i + s);
+  return m;
+}
+
+// NPTS points at most; wave 0 is the hot wave, waves 1..NW-1 hold the cold cells (PPT cells of
+// 64 sorted points per wave).
+template <int NW, int PPT, int NPTS, bool STAMP = false, int PRIO = 0>
+__global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __restrict__ xyz, int N,
+                                                           int M, int32_t* __restrict__ idx,
+                                                           float* __restrict__ new_xyz) {
+  constexpr int BLOCK = 64 * NW;
+  constexpr int NCW = NW - 1;           // cold waves
+  constexpr int NCELL = NCW * PPT;
+  constexpr int GRP = kWave / PPT;      // centres per group test (lane = centre * PPT + cell)
+  constexpr int K = 128;                // hot-set capacity: two entries per lane of wave 0
+  constexpr int NT = 12;                // thresholds
+  constexpr int NWIN = 4;               // thresholds counted per refresh
+  constexpr int NBK = 4096;             // sort buckets (16^3 Morton)
+  constexpr int SPT = NPTS / BLOCK;     // setup: points per thread
+  static_assert(NCELL * kWave >= NPTS, "cold capacity");
+  static_assert(NPTS % BLOCK == 0 && NBK % BLOCK == 0, "setup strides");
+  static_assert(PPT <= 32 && GRP >= 1, "slot masks");
+  static_assert(NW * NWIN == kWave && NWIN == 4, "choice: one lane per (threshold, wave)");
+  using f2 = float __attribute__((ext_vector_type(2)));
+
+  __shared__ float sxyz[3 * NPTS];
+  __shared__ int sperm[NPTS];         // sorted position -> point index
+  __shared__ uint32_t shist[NBK];     // bucket counts, then offsets
+  __shared__ float4 scell[2 * NCELL]; // cell boxes (lo, hi)
+  __shared__ float4 scl[K + 1];       // centres of the current batch (x, y, z, idx)
+  __shared__ uint2 sh[K];             // hot entries (running min bits, point index)
+  __shared__ uint64_t swk[NW];        // per-wave (value + 1, ~key) of the exact argmax
+  __shared__ float sbox[NW][8];
+  __shared__ int swmax[NW];
+  __shared__ int sj[2], sstop[2];     // published centres of a batch; end of the batch (by round parity)
+  __shared__ uint32_t swcnt[NW][4];   // per-wave counts above the round's thresholds
+
+  const int b = blockIdx.x;
+  const int t = threadIdx.x, lane = t & (kWave - 1);
+  const int w = __builtin_amdgcn_readfirstlane(t / kWave);
+  const int cw = w - 1;  // cold wave index (-1: the hot wave)
+  const float* __restrict__ P = xyz + (size_t)b * N * 3;
+  int32_t* __restrict__ I = idx + (size_t)b * M;
+  float* __restrict__ NX = new_xyz ? new_xyz + (size_t)b * M * 3 : nullptr;
+  unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, st_prev = 0;
+  unsigned long long n_refresh = 0, n_stall = 0, n_pairs = 0, n_hot = 0, clk0 = 0;
+  unsigned long long n_tail_cyc = 0, n_tail_grp = 0, t_stop = 0;
+  if constexpr (STAMP) {
+    clk0 = __builtin_amdgcn_s_memtime();
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_prev)::"memory");
+  }
+
+  // ---- setup: LDS copy, bounding box, counting sort by Morton bucket, cells -------------
+  for (int e = t; e < 3 * N; e += BLOCK) sxyz[e] = P[e];
+  for (int e = t; e < NBK; e += BLOCK) shist[e] = 0u;
+  if (t < NW * 4) swcnt[t / 4][t % 4] = 0u;
+  __syncthreads();
+  {
+    float mx[3] = {-INFINITY, -INFINITY, -INFINITY}, mn[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int k = t; k < N; k += BLOCK) {
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+        mx[a] = fmaxf(mx[a], sxyz[3 * k + a]);
+        mn[a] = fmaxf(mn[a], -sxyz[3 * k + a]);
+      }
+    }
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      mx[a] = wave_max_f32(mx[a]);
+      mn[a] = wave_max_f32(mn[a]);
+    }
+    if (lane == 0) {
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+        sbox[w][a] = mx[a];
+        sbox[w][4 + a] = mn[a];
+      }
+    }
+  }
+  __syncthreads();
+  float blo[3], bsc[3];
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    float hi = -INFINITY, nlo = -INFINITY;
+    for (int v = 0; v < NW; ++v) {
+      hi = fmaxf(hi, sbox[v][a]);
+      nlo = fmaxf(nlo, sbox[v][4 + a]);
+    }
+    blo[a] = -nlo;
+    const float ext = hi - blo[a];
+    bsc[a] = ext > 0.0f ? 16.0f / ext : 0.0f;
+  }
+  int code[SPT], rank[SPT];
+#pragma unroll
+  for (int i = 0; i < SPT; ++i) {
+    const int k = t + i * BLOCK;
+    if (k < N) {
+      uint32_t c = 0;
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+        const int q = min(max((int)((sxyz[3 * k + a] - blo[a]) * bsc[a]), 0), 15);
+#pragma unroll
+        for (int bit = 0; bit < 4; ++bit) c |= (uint32_t)((q >> bit) & 1) << (3 * bit + a);
+      }
+      code[i] = (int)c;
+      rank[i] = (int)atomicAdd(&shist[c], 1u);
+    } else {
+      code[i] = 0;
+      rank[i] = 0;
+    }
+  }
+  __syncthreads();
+  {
+    constexpr int PB = NBK / BLOCK;
+    uint32_t c[PB], s = 0;
+#pragma unroll
+    for (int i = 0; i < PB; ++i) {
+      c[i] = shist[PB * t + i];
+      s += c[i];
+    }
+    const uint32_t ex = wave_excl_scan(s, lane);
+    if (lane == kWave - 1) swmax[w] = (int)(ex + s);
+    __syncthreads();
+    uint32_t base = 0;
+    for (int v = 0; v < w; ++v) base += (uint32_t)swmax[v];
+    uint32_t run = base + ex;
+#pragma unroll
+    for (int i = 0; i < PB; ++i) {
+      shist[PB * t + i] = run;
+      run += c[i];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < SPT; ++i) {
+    const int k = t + i * BLOCK;
+    if (k < N) sperm[shist[code[i]] + rank[i]] = k;
+  }
+  __syncthreads();
+  // cell boxes: 8 lanes per cell, each folds 8 consecutive sorted points, then DPP within 8
+  for (int c = t >> 3; c < NCELL; c += BLOCK / 8) {
+    float lo3[3] = {INFINITY, INFINITY, INFINITY}, hi3[3] = {-INFINITY, -INFINITY, -INFINITY};
+    const int base = c * kWave + (t & 7) * 8;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int pos = base + i;
+      if (pos < N) {
+        const int k = sperm[pos];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+          lo3[a] = fminf(lo3[a], sxyz[3 * k + a]);
+          hi3[a] = fmaxf(hi3[a], sxyz[3 * k + a]);
+        }
+      }
+    }
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+#define PN2_BOX_DPP(C)                                                                       \
+  lo3[a] = fminf(lo3[a], __int_as_float(__builtin_amdgcn_update_dpp(                         \
+                             __float_as_int(lo3[a]), __float_as_int(lo3[a]), C, 0xF, 0xF,    \
+                             false)));                                                       \
+  hi3[a] = fmaxf(hi3[a], __int_as_float(__builtin_amdgcn_update_dpp(                         \
+                             __float_as_int(hi3[a]), __float_as_int(hi3[a]), C, 0xF, 0xF,    \
+                             false)))
+      PN2_BOX_DPP(kDppXor1);
+      PN2_BOX_DPP(kDppXor2);
+      PN2_BOX_DPP(kDppHalfMirror);
+#undef PN2_BOX_DPP
+    }
+    if ((t & 7) == 0) {
+      scell[2 * c] = make_float4(lo3[0], lo3[1], lo3[2], 0.0f);
+      scell[2 * c + 1] = make_float4(hi3[0], hi3[1], hi3[2], 0.0f);
+    }
+  }
+  if (t == 0) {  // the first batch: centre 0 (tf_sampling_g.cu:121-125), already complete
+    scl[0] = make_float4(sxyz[0], sxyz[1], sxyz[2], __int_as_float(0));
+    sj[0] = 1;
+    sstop[0] = 1;
+    sj[1] = 0;
+    sstop[1] = 0;
+    swmax[0] = -1;  // the hot wave holds no cell
+  }
+  __syncthreads();
+
+  // cold registers: slot s of cold lane (cw, lane) = sorted position (cw * PPT + s) * 64 + lane
+  float px[PPT], py[PPT], pz[PPT];
+  int tb[PPT];
+  int Tm[PPT];  // exact max running min of each cell (wave-uniform), -1 = empty cell
+  // group test: lane l tests cell (cw, l % PPT) against centre l / PPT of the group
+  float4 glo = make_float4(INFINITY, INFINITY, INFINITY, 0.0f), ghi = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.0f);
+  int tmv = -1;
+  if (cw >= 0) {
+#pragma unroll
+    for (int s = 0; s < PPT; ++s) {
+      const int pos = (cw * PPT + s) * kWave + lane;
+      const bool in = pos < N;
+      const int k = in ? sperm[pos] : 0;
+      px[s] = sxyz[3 * k];
+      py[s] = sxyz[3 * k + 1];
+      pz[s] = sxyz[3 * k + 2];
+      tb[s] = in ? __float_as_int(kInitTemp) : -1;
+      Tm[s] = __builtin_amdgcn_ballot_w64(in) != 0 ? __float_as_int(kInitTemp) : -1;
+    }
+    if (lane < GRP * PPT) {
+      glo = scell[2 * (cw * PPT + lane % PPT)];
+      ghi = scell[2 * (cw * PPT + lane % PPT) + 1];
+    }
+#pragma unroll
+    for (int s = 0; s < PPT; ++s) tmv = lane % PPT == s ? Tm[s] : tmv;
+  }
+  PN2_STAMP(7)
+
+  int j = 0;                // picks written to the outputs
+  int rp = 0;               // round parity: sj[rp], sstop[rp] describe this round's batch
+  int tlo = 2;              // first threshold of the counted window
+  float topf = kInitTemp;   // scale of this round's thresholds (the last known maximum)
+  int T = 0, nh = 0;        // the hot phase's threshold and hot-set size
+  bool hot_turn = false;
+  for (int round = 0; round <= M; ++round) {
+    // this round's thresholds (every wave computes the same bits)
+    int tau[NWIN];
+#pragma unroll
+    for (int i = 0; i < NWIN; ++i)
+      tau[i] = (int)uniform_u32((uint32_t)__float_as_int(topf * kCullFrac[tlo + i]));
+    if (w == 0) {
+      if (hot_turn) {
+        // ---- hot phase: certified picks while the best hot value is above T, each one
+        // published to the cold waves at once (scl[jj], then the count sj; DS operations of
+        // one wave execute in order, so a cold wave that reads the count reads the centre)
+        int hv[2], hk[2];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const int e = lane + q * kWave;
+          const uint2 en = e < nh ? sh[e] : make_uint2(0xFFFFFFFFu, 0u);
+          hv[q] = (int)en.x;
+          hk[q] = (int)en.y;
+        }
+        // entry 0 of a lane is the earlier one in tie order: a strict '>' picks between them
+        if (hv[1] >= 0 && (hv[0] < 0 || cull_key(hk[1]) < cull_key(hk[0]))) {
+          const int v = hv[0], k = hk[0];
+          hv[0] = hv[1]; hk[0] = hk[1];
+          hv[1] = v; hk[1] = k;
+        }
+        const uint32_t key0 = cull_key(hk[0]), key1 = cull_key(hk[1]);
+        f2 hx, hy, hz;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          hx[q] = sxyz[3 * hk[q]];
+          hy[q] = sxyz[3 * hk[q] + 1];
+          hz[q] = sxyz[3 * hk[q] + 2];
+        }
+        const int lim = min(K, M - j);
+        int jj = 0;
+        unsigned long long th0 = 0;
+        if constexpr (STAMP) th0 = __builtin_amdgcn_s_memtime();
+        if constexpr (PRIO > 0) __builtin_amdgcn_s_setprio(PRIO);
+        for (; jj < lim; ++jj) {
+          const bool b1 = hv[1] > hv[0];
+          const int cv = b1 ? hv[1] : hv[0];
+          const int wm = __builtin_amdgcn_readfirstlane(wave_max_i32(cv));
+          if (!(wm > T)) break;
+          const uint64_t hold = __builtin_amdgcn_ballot_w64(cv == wm);
+          int L;
+          if (__builtin_popcountll(hold) == 1) {
+            L = (int)__builtin_ctzll(hold);
+          } else {  // equal values: the smallest tie key among the holders
+            const uint32_t ck = b1 ? key1 : key0;
+            const uint32_t km = ~uniform_u32(wave_max_u32(cv == wm ? ~ck : 0u));
+            L = (int)__builtin_ctzll(__builtin_amdgcn_ballot_w64(cv == wm && ck == km));
+          }
+          const float lx = b1 ? hx[1] : hx[0], ly = b1 ? hy[1] : hy[0], lz = b1 ? hz[1] : hz[0];
+          const int lk = b1 ? hk[1] : hk[0];
+          const float cx = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__float_as_int(lx), L));
+          const float cy = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__float_as_int(ly), L));
+          const float cz = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__float_as_int(lz), L));
+          const int ck = __builtin_amdgcn_readlane(lk, L);
+          if (lane == 0) {
+            scl[jj] = make_float4(cx, cy, cz, __int_as_float(ck));
+            asm volatile("" ::: "memory");
+            *(volatile int*)&sj[rp] = jj + 1;
+          }
+          const f2 c2x = {cx, cx}, c2y = {cy, cy}, c2z = {cz, cz};
+          const f2 dx = hx - c2x, dy = hy - c2y, dz = hz - c2z;
+          const f2 d = (dx * dx + dy * dy) + dz * dz;
+          hv[0] = min(hv[0], __float_as_int(d.x));
+          hv[1] = min(hv[1], __float_as_int(d.y));
+        }
+        if constexpr (PRIO > 0) __builtin_amdgcn_s_setprio(0);
+        if (lane == 0) {
+          asm volatile("" ::: "memory");
+          *(volatile int*)&sstop[rp] = 1;
+        }
+        if constexpr (STAMP) {
+          n_hot += jj;
+          if (b == 0 && lane == 0 && round < 256) {
+            g_iter[round * 16 + 0] = th0;
+            g_iter[round * 16 + 1] = __builtin_amdgcn_s_memtime();
+            g_iter[round * 16 + 2] = jj;
+          }
+        }
+      }
+      PN2_STAMP(7)
+    } else {
+      // ---- cold waves: count this round's thresholds per cell (8 bits each, packed), then
+      // apply the batch's centres as the hot wave publishes them, GRP at a time (the last,
+      // short group after the end flag), culled by the box test; a touched cell's Tmax and
+      // counts are refreshed right after its group
+      auto count_cell = [&](int s) -> uint32_t {
+        uint32_t c = 0;
+        if (Tm[s] > tau[0]) {
+#pragma unroll
+          for (int i = 0; i < NWIN; ++i)
+            if (Tm[s] > tau[i])
+              c |= (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(tb[s] > tau[i]))
+                   << (8 * i);
+        }
+        return c;
+      };
+      uint32_t csv = 0;  // lane s: cell s's packed counts
+#pragma unroll
+      for (int s = 0; s < PPT; ++s) {
+        const uint32_t c = count_cell(s);
+        csv = lane == s ? c : csv;
+      }
+      PN2_TRACE(11, 1)
+      int applied = 0;
+      bool stop = false;
+      unsigned long long tc0 = 0, tgrp = 0, tcnt0 = 0;
+      int lag_at_stop = 0;
+      if constexpr (STAMP) tc0 = __builtin_amdgcn_s_memtime();
+      for (int it = 0; it < (1 << 22); ++it) {
+        const int av = __builtin_amdgcn_readfirstlane(
+            __hip_atomic_load(&sj[rp], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+        if (av - applied >= GRP || (stop && av > applied)) {
+          const int a1 = min(av, applied + GRP);
+          if constexpr (STAMP) tcnt0 = __builtin_amdgcn_s_memtime();
+          const int ci = applied + lane / PPT;
+          const bool valid = lane < GRP * PPT && ci < a1;
+          const float4 cv = scl[valid ? ci : 0];
+          const float lb = box_lb(glo, ghi, cv.x, cv.y, cv.z);
+          const uint64_t m = __builtin_amdgcn_ballot_w64(valid && __float_as_int(lb) < tmv);
+          if constexpr (STAMP) n_pairs += __builtin_popcountll(m);
+          if (m) {
+#pragma unroll
+            for (int s = 0; s < PPT; ++s) {
+              uint64_t ms = m & cell_lanes<PPT, GRP>(s);
+              if (!ms) continue;
+              while (ms) {  // two centres per packed pass (a lone last one is applied twice)
+                const int la = (int)__builtin_ctzll(ms);
+                ms &= ms - 1;
+                const int lb2 = ms ? (int)__builtin_ctzll(ms) : la;
+                ms &= ms ? ms - 1 : 0;
+                const float ax = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__float_as_int(cv.x), la));
+                const float ay = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__float_as_int(cv.y), la));
+                const float az = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__float_as_int(cv.z), la));
+                const float bx = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__float_as_int(cv.x), lb2));
+                const float by = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__float_as_int(cv.y), lb2));
+                const float bz = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__float_as_int(cv.z), lb2));
+                const f2 qx = {px[s], px[s]}, qy = {py[s], py[s]}, qz = {pz[s], pz[s]};
+                const f2 cx = {ax, bx}, cy = {ay, by}, cz = {az, bz};
+                const f2 dx = qx - cx, dy = qy - cy, dz = qz - cz;
+                const f2 d = (dx * dx + dy * dy) + dz * dz;
+                tb[s] = min(min(tb[s], __float_as_int(d.x)), __float_as_int(d.y));
+              }
+              Tm[s] = __builtin_amdgcn_readfirstlane(wave_max_i32(tb[s]));
+              tmv = lane % PPT == s ? Tm[s] : tmv;
+              const uint32_t c = count_cell(s);
+              csv = lane == s ? c : csv;
+            }
+          }
+          applied = a1;
+          if constexpr (STAMP) {
+            n_tail_grp += stop ? 1 : 0;
+            tgrp += __builtin_amdgcn_s_memtime() - tcnt0;
+          }
+          continue;
+        }
+        if (stop) break;  // the end flag was seen before av was read: av is final
+        stop = __hip_atomic_load(&sstop[rp], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != 0;
+        if constexpr (STAMP) if (stop) {
+          t_stop = __builtin_amdgcn_s_memtime();
+          lag_at_stop = __hip_atomic_load(&sj[rp], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) - applied;
+        }
+        if (!stop) __builtin_amdgcn_s_sleep(1);
+      }
+      if constexpr (STAMP) {
+        const unsigned long long tend = __builtin_amdgcn_s_memtime();
+        n_tail_cyc += tend - t_stop;
+        if (b == 0 && lane == 0 && round < 128) g_iter[2048 + round * 16 + w] = tend;
+        if (b == 0 && lane == 0 && round < 256 && w == 1) {
+          g_iter[round * 16 + 3] = t_stop;
+          g_iter[round * 16 + 4] = tend;
+          g_iter[round * 16 + 5] = (unsigned long long)lag_at_stop | (tgrp << 16);
+          g_iter[round * 16 + 10] = tc0;
+        }
+      }
+      PN2_STAMP(0)
+      int wmax = -1;
+#pragma unroll
+      for (int s = 0; s < PPT; ++s) wmax = max(wmax, Tm[s]);
+      if (lane == 0) swmax[w] = wmax;
+      // totals over the cells (lanes 0..PPT-1 of row 0): 16-bit fields, row sums
+      static_assert(PPT <= 16, "cells in DPP row 0");
+      uint32_t lo = (csv & 0xFFu) | ((csv & 0xFF00u) << 8);
+      uint32_t hi = ((csv >> 16) & 0xFFu) | ((csv >> 8) & 0xFF0000u);
+#define PN2_ADD_DPP(V, C) V += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)V, C, 0xF, 0xF, false)
+      PN2_ADD_DPP(lo, kDppXor1); PN2_ADD_DPP(hi, kDppXor1);
+      PN2_ADD_DPP(lo, kDppXor2); PN2_ADD_DPP(hi, kDppXor2);
+      PN2_ADD_DPP(lo, kDppHalfMirror); PN2_ADD_DPP(hi, kDppHalfMirror);
+      PN2_ADD_DPP(lo, kDppMirror); PN2_ADD_DPP(hi, kDppMirror);
+#undef PN2_ADD_DPP
+      if (lane < NWIN) {
+        const uint32_t v = lane < 2 ? lo : hi;
+        swcnt[w][lane] = (lane & 1) ? v >> 16 : v & 0xFFFFu;
+      }
+      PN2_STAMP(1)
+    }
+    __syncthreads();  // B1: the batch is complete and applied; Tmax and counts are current
+    PN2_STAMP(2)
+    PN2_TRACE(6, 0)
+    const int nb = sj[rp];
+    for (int e = t; e < nb; e += BLOCK) {
+      const float4 c = scl[e];
+      I[j + e] = __float_as_int(c.w);
+      if (NX) {
+        NX[3 * (j + e)] = c.x;
+        NX[3 * (j + e) + 1] = c.y;
+        NX[3 * (j + e) + 2] = c.z;
+      }
+    }
+    j += nb;
+    if (j >= M) break;
+    if constexpr (STAMP) ++n_refresh;
+    int top;
+    {
+      const int v = lane < NW ? swmax[lane] : -1;
+      top = __builtin_amdgcn_readfirstlane(wave_max_i32(v));
+    }
+    // ---- choice: the lowest window threshold whose total count is in [1, K]. Lane
+    // 16 i + v holds wave v's count above tau[i]; 16-lane row sums give the totals.
+    const int cvw = lane & (NW - 1), ciw = lane / NW;
+    const uint32_t cnt = swcnt[cvw][ciw];
+    uint32_t tot = cnt;
+#define PN2_ADD_DPP(C) tot += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)tot, C, 0xF, 0xF, false)
+    PN2_ADD_DPP(kDppXor1);
+    PN2_ADD_DPP(kDppXor2);
+    PN2_ADD_DPP(kDppHalfMirror);
+    PN2_ADD_DPP(kDppMirror);
+#undef PN2_ADD_DPP
+    const uint64_t fit = __builtin_amdgcn_ballot_w64(cvw == 0 && tot >= 1u && tot <= (uint32_t)K);
+    const int ti = fit ? (int)__builtin_ctzll(fit) / NW : -1;
+    const bool stall = ti < 0;
+    T = 0;
+#pragma unroll
+    for (int i = 0; i < NWIN; ++i) T = ti == i ? tau[i] : T;
+    nh = stall ? 0 : __builtin_amdgcn_readlane((int)tot, ti * NW);
+    int wbase = 0;  // this wave's first hot entry: the counts of the waves before it
+    {
+      uint32_t pre = ciw == ti && cvw < w ? cnt : 0u;
+#define PN2_ADD_DPP(C) pre += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)pre, C, 0xF, 0xF, false)
+      PN2_ADD_DPP(kDppXor1);
+      PN2_ADD_DPP(kDppXor2);
+      PN2_ADD_DPP(kDppHalfMirror);
+      PN2_ADD_DPP(kDppMirror);
+#undef PN2_ADD_DPP
+      if (!stall) wbase = __builtin_amdgcn_readlane((int)pre, ti * NW);
+    }
+    // next window: two below this choice (lower thresholds = bigger hot sets), or up; the next
+    // thresholds scale with this round's maximum
+    tlo = !stall ? min(max(tlo + ti - 2, 0), NT - NWIN) : min(tlo + NWIN, NT - NWIN);
+    topf = __int_as_float(max(top, 0));
+    if (t == 0) {  // the next round's batch starts empty (its flags were last read in round - 1)
+      sj[rp ^ 1] = 0;
+      sstop[rp ^ 1] = 0;
+    }
+    PN2_STAMP(3)
+    PN2_TRACE(7, 0)
+    if (!stall) {
+      if (cw >= 0) {
+        // ---- hot set: every point above T, at this wave's offset
+        int base = wbase;
+#pragma unroll
+        for (int s = 0; s < PPT; ++s) {
+          if (Tm[s] > T) {
+            const uint64_t m = __builtin_amdgcn_ballot_w64(tb[s] > T);
+            const uint32_t below = __builtin_amdgcn_mbcnt_hi(
+                (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            if (tb[s] > T)
+              sh[base + (int)below] =
+                  make_uint2((uint32_t)tb[s], (uint32_t)sperm[(cw * PPT + s) * kWave + lane]);
+            base += __builtin_popcountll(m);
+          }
+        }
+      }
+    } else {
+      // ---- exact block argmax: (value desc, key asc) as one 64-bit max
+      uint64_t best = 0;
+      if (cw >= 0) {
+#pragma unroll
+        for (int s = 0; s < PPT; ++s) {
+          const uint64_t v = tb[s] < 0 ? 0ull
+                                       : pack64(~cull_key(sperm[(cw * PPT + s) * kWave + lane]),
+                                                (uint32_t)tb[s] + 1u);
+          best = v > best ? v : best;
+        }
+        best = wave_max_u64(best);
+      }
+      if (lane == 0) swk[w] = best;
+      if constexpr (STAMP) ++n_stall;
+    }
+    PN2_STAMP(4)
+    PN2_TRACE(9, 1)
+    __syncthreads();  // B2: hot set (or the per-wave argmax) complete
+    PN2_STAMP(5)
+    PN2_TRACE(8, 0)
+    if (stall) {
+      uint64_t best = lane < NW ? swk[lane] : 0ull;
+      best = uniform_u64(wave_max_u64(best));
+      const uint32_t key = ~(uint32_t)best;
+      const int k = (int)((key >> 16) + ((key & 0xFFFFu) << 9));
+      if (top <= 0) {
+        // every running min is 0 and stays 0: each remaining pick is the same point
+        for (int e = j + t; e < M; e += BLOCK) {
+          I[e] = k;
+          if (NX) {
+            NX[3 * e] = sxyz[3 * k];
+            NX[3 * e + 1] = sxyz[3 * k + 1];
+            NX[3 * e + 2] = sxyz[3 * k + 2];
+          }
+        }
+        break;
+      }
+      if (t == 0) {
+        scl[0] = make_float4(sxyz[3 * k], sxyz[3 * k + 1], sxyz[3 * k + 2], __int_as_float(k));
+        asm volatile("" ::: "memory");
+        *(volatile int*)&sj[rp ^ 1] = 1;
+        asm volatile("" ::: "memory");
+        *(volatile int*)&sstop[rp ^ 1] = 1;
+      }
+    }
+    hot_turn = !stall;
+    rp ^= 1;
+    PN2_STAMP(6)
+  }
+  if constexpr (STAMP) {
+    if (lane == 0 && b < 16) {
+#pragma unroll
+      for (int ph = 0; ph < 8; ++ph) g_stamp[(b * 16 + w) * 8 + ph] = st_acc[ph];
+      if (w == 0) {
+        g_cull_stats[b * 8 + 0] = __builtin_amdgcn_s_memtime() - clk0;
+        g_cull_stats[b * 8 + 1] = n_refresh;
+        g_cull_stats[b * 8 + 2] = n_stall;
+        g_cull_stats[b * 8 + 4] = n_hot;
+      }
+      if (w == 1) {
+        g_cull_stats[b * 8 + 3] = n_pairs;
+        g_cull_stats[b * 8 + 6] = n_tail_cyc;
+        g_cull_stats[b * 8 + 7] = n_tail_grp;
+      }
+      if (w == 2) g_cull_stats[b * 8 + 5] = n_pairs;
+    }
+  }
+}
+
+template <int NW, int PPT>
+void launch_cull(const float* xyz, int B, int N, int M, int32_t* idx, float* nx, hipStream_t s) {
+  hipLaunchKernelGGL((fps_hotcull_kernel<NW, PPT, 8192>), dim3(B), dim3(64 * NW), 0, s, xyz, N, M,
+                     idx, nx);
+}
+
+}  // namespace
+}  // namespace pn2

@@ -4,6 +4,7 @@
 // by tools/fps_lab/Makefile. DESIGN.md records what each variant taught.
 #include "../../pointcloud-segmentation-attention_amd/csrc/fps_kernels.h"
 #include "../../pointcloud-segmentation-attention_amd/csrc/fps_hot.h"
+#include "../../pointcloud-segmentation-attention_amd/csrc/fps_cull.h"
 
 namespace pn2 {
 namespace {
@@ -2018,6 +2019,32 @@ int pn2_fps_tune(const float* xyz, int B, int N, int npoint, int32_t* idx, float
                  int variant, int block, int ppt, pn2_stream_t stream) {
   return pn2::fps_tune_impl(xyz, B, N, npoint, idx, new_xyz, variant, block, ppt,
                             (hipStream_t)stream);
+}
+
+// Diagnostic entry: stamped culled hot-set sampler (fps_cull.h); out (16 clouds x 16 waves x
+// 8): per wave the cycles of phases 0 cold async apply (incl. waiting), 1 Tmax, 2 B_A,
+// 3 outputs + counts, 4 B_B, 5 choice + append, 6 B_C, 7 hot phase (wave 0) + setup;
+// stats (16 clouds x 8): [0] kernel cycles, [1] refreshes, [2] stalls, [3] applied (cell,
+// centre) pairs of wave 1, [4] hot picks, [5] pairs of wave 2.
+int pn2_fps_cull_stamp(const float* xyz, int B, int N, int npoint, int32_t* idx,
+                       unsigned long long* out_host, unsigned long long* stats_host) {
+  hipStream_t s = 0;
+  if (N > 8192) return PN2_EINVAL;
+  hipLaunchKernelGGL((pn2::fps_hotcull_kernel<16, 9, 8192, true>), dim3(B), dim3(1024), 0, s, xyz, N,
+                     npoint, idx, nullptr);
+  hipError_t e = hipDeviceSynchronize();
+  if (e != hipSuccess) return (int)e;
+  e = hipMemcpyFromSymbol(out_host, HIP_SYMBOL(pn2::g_stamp),
+                          sizeof(unsigned long long) * 16 * 16 * 8);
+  if (e != hipSuccess) return (int)e;
+  e = hipMemcpyFromSymbol(stats_host, HIP_SYMBOL(pn2::g_cull_stats),
+                          sizeof(unsigned long long) * 16 * 8);
+  return (int)e;
+}
+
+// Diagnostic: the per-round trace the stamped hot-cull sampler leaves in g_iter (cloud 0).
+int pn2_fps_cull_trace(unsigned long long* out_host) {
+  return (int)hipMemcpyFromSymbol(out_host, HIP_SYMBOL(pn2::g_iter), sizeof(unsigned long long) * 4096);
 }
 
 }  // extern "C"
