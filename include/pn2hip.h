@@ -103,10 +103,10 @@ int pn2_fps(const float* xyz, int B, int N, int npoint, int32_t* idx, pn2_stream
 int pn2_fps_gather(const float* xyz, int B, int N, int npoint, int32_t* idx, float* new_xyz,
                    pn2_stream_t stream);
 int pn2_fps_max_points(void);
-/* Sampler schedule for large clouds (process-wide; tests and A/B timing): 0 = the measured
- * default, 1 = the block-scan sampler (one block argmax per pick), 2 = the hot-set sampler
- * (certified picks from a 128-point hot set, batched refreshes). Identical outputs. Returns the
- * previous setting; out-of-range values only query. */
+/* Sampler schedule for 4096 < N <= 8192 (process-wide; tests and A/B timing): 0 = the default
+ * (culled hot-set sampler), 1 = the v9 block-scan sampler (one block argmax per pick), 6 = the
+ * culled hot-set sampler without the hot wave's issue-priority boost. Identical outputs.
+ * Returns the previous setting; other values only query. */
 int pn2_fps_set_algo(int algo);
 size_t pn2_fps_workspace_size(int B, int N);
 int pn2_fps_ws(const float* xyz, int B, int N, int npoint, int32_t* idx, float* new_xyz,

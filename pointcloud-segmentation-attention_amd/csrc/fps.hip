@@ -11,7 +11,6 @@
 // pointnet_util.py:34). Clouds beyond kMaxRegPoints keep the running min in a caller-provided
 // workspace (fps_ws_kernel). Measured variants live in tools/fps_lab.
 #include "fps_kernels.h"
-#include "fps_hot.h"
 #include "fps_cull.h"
 
 // Code placement of the SA1 (256 x 32) sampler's iteration loop. The loop runs ~6 % slower
@@ -110,7 +109,8 @@ __global__ void gather_point_grad_kernel(const float* __restrict__ out_g,
 
 constexpr int kMaxRegPoints = 1024 * 16;
 
-// Sampler selection for large clouds: 0 = measured default, 1 = v9 block scan, 2 = hot set.
+// Sampler selection for 4096 < N <= 8192: 0 = default (culled hot set, hot-wave priority 3),
+// 1 = v9 block scan, 6 = culled hot set without the priority boost.
 int g_fps_algo = 0;
 
 // ---- sampler chain: SA1..SAk's samplers of one cloud, stage 2.. in ONE workgroup -----------
@@ -184,10 +184,11 @@ int fps_impl(const float* xyz, int B, int N, int M, int32_t* idx, float* nx, voi
   else if (N <= 2048) launch_v9<256, 8, 2, true>(xyz, B, N, M, idx, nx, s);
   else if (N <= 4096) launch_v9<256, 16, 4, true>(xyz, B, N, M, idx, nx, s);
   else if (N <= 8192) {
-    if (g_fps_algo == 6) launch_cull<16, 9>(xyz, B, N, M, idx, nx, s);
-    else if (g_fps_algo >= 2) launch_hot<256, 32>(xyz, B, N, M, idx, nx, s, g_fps_algo == 3 || g_fps_algo == 5,
-                                             g_fps_algo >= 4);
-    else launch_v9<256, 32, 4, true, false, PN2_SA1_PAD>(xyz, B, N, M, idx, nx, s);
+    // culled hot-set sampler (fps_cull.h; 0.50 vs 0.71 ms at B = 16); the v9
+    // block-scan sampler stays selectable for A/B timing and parity cross-checks
+    if (g_fps_algo == 1) launch_v9<256, 32, 4, true, false, PN2_SA1_PAD>(xyz, B, N, M, idx, nx, s);
+    else if (g_fps_algo == 6) launch_hotcull<16, 9, 0>(xyz, B, N, M, idx, nx, s);
+    else launch_hotcull<16, 9, 3>(xyz, B, N, M, idx, nx, s);
   }
   else if (N <= kMaxRegPoints) launch_v9<512, 32, 4>(xyz, B, N, M, idx, nx, s);
   else {
@@ -206,7 +207,7 @@ int pn2_fps_max_points(void) { return pn2::kMaxRegPoints; }
 
 int pn2_fps_set_algo(int algo) {
   const int old = pn2::g_fps_algo;
-  if (algo >= 0 && algo <= 6) pn2::g_fps_algo = algo;
+  if (algo == 0 || algo == 1 || algo == 6) pn2::g_fps_algo = algo;
   return old;
 }
 

@@ -29,6 +29,8 @@ namespace pn2 {
 namespace {
 
 __device__ unsigned long long g_cull_stats[16 * 8];  // STAMP builds: per-cloud counters
+__device__ unsigned long long g_cull_wave[16 * 16 * 4];
+__device__ unsigned long long g_cull_round[16 * 64];  // STAMP: cloud 0, round 23: per wave event times  // STAMP: per wave groups, group cycles, pairs, polls
 
 // float max over the wave (every lane gets it); DPP rows, then the gfx950 permlane swaps
 PN2_DEV float wave_max_f32(float v) {
@@ -126,6 +128,7 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
   constexpr int NT = 12;                // thresholds
   constexpr int NWIN = 4;               // thresholds counted per refresh
   constexpr int NBK = 4096;             // sort buckets (16^3 Morton)
+  constexpr int kEnd = 1 << 16;         // sj flag: the batch is complete
   constexpr int SPT = NPTS / BLOCK;     // setup: points per thread
   static_assert(NCELL * kWave >= NPTS, "cold capacity");
   static_assert(NPTS % BLOCK == 0 && NBK % BLOCK == 0, "setup strides");
@@ -142,7 +145,7 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
   __shared__ uint64_t swk[NW];        // per-wave (value + 1, ~key) of the exact argmax
   __shared__ float sbox[NW][8];
   __shared__ int swmax[NW];
-  __shared__ int sj[2], sstop[2];     // published centres of a batch; end of the batch (by round parity)
+  __shared__ int sj[2];               // published centres of a batch | kEnd once complete (by round parity)
   __shared__ uint32_t swcnt[NW][4];   // per-wave counts above the round's thresholds
 
   const int b = blockIdx.x;
@@ -155,6 +158,7 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
   unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, st_prev = 0;
   unsigned long long n_refresh = 0, n_stall = 0, n_pairs = 0, n_hot = 0, clk0 = 0;
   unsigned long long n_tail_cyc = 0, n_tail_grp = 0, t_stop = 0;
+  unsigned long long n_grp = 0, n_grp_cyc = 0, n_poll = 0;
   if constexpr (STAMP) {
     clk0 = __builtin_amdgcn_s_memtime();
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_prev)::"memory");
@@ -284,10 +288,8 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
   }
   if (t == 0) {  // the first batch: centre 0 (tf_sampling_g.cu:121-125), already complete
     scl[0] = make_float4(sxyz[0], sxyz[1], sxyz[2], __int_as_float(0));
-    sj[0] = 1;
-    sstop[0] = 1;
+    sj[0] = 1 | kEnd;
     sj[1] = 0;
-    sstop[1] = 0;
     swmax[0] = -1;  // the hot wave holds no cell
   }
   __syncthreads();
@@ -321,17 +323,11 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
   PN2_STAMP(7)
 
   int j = 0;                // picks written to the outputs
-  int rp = 0;               // round parity: sj[rp], sstop[rp] describe this round's batch
+  int rp = 0;               // round parity: sj[rp] describes this round's batch
   int tlo = 2;              // first threshold of the counted window
-  float topf = kInitTemp;   // scale of this round's thresholds (the last known maximum)
   int T = 0, nh = 0;        // the hot phase's threshold and hot-set size
   bool hot_turn = false;
   for (int round = 0; round <= M; ++round) {
-    // this round's thresholds (every wave computes the same bits)
-    int tau[NWIN];
-#pragma unroll
-    for (int i = 0; i < NWIN; ++i)
-      tau[i] = (int)uniform_u32((uint32_t)__float_as_int(topf * kCullFrac[tlo + i]));
     if (w == 0) {
       if (hot_turn) {
         // ---- hot phase: certified picks while the best hot value is above T, each one
@@ -398,9 +394,14 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
         if constexpr (PRIO > 0) __builtin_amdgcn_s_setprio(0);
         if (lane == 0) {
           asm volatile("" ::: "memory");
-          *(volatile int*)&sstop[rp] = 1;
+          *(volatile int*)&sj[rp] = jj | kEnd;
         }
         if constexpr (STAMP) {
+          if (b == 0 && lane == 0 && round == 23) {
+            g_cull_round[0] = th0;
+            g_cull_round[1] = __builtin_amdgcn_s_memtime();
+            g_cull_round[2] = jj;
+          }
           n_hot += jj;
           if (b == 0 && lane == 0 && round < 256) {
             g_iter[round * 16 + 0] = th0;
@@ -411,39 +412,32 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
       }
       PN2_STAMP(7)
     } else {
-      // ---- cold waves: count this round's thresholds per cell (8 bits each, packed), then
-      // apply the batch's centres as the hot wave publishes them, GRP at a time (the last,
-      // short group after the end flag), culled by the box test; a touched cell's Tmax and
-      // counts are refreshed right after its group
-      auto count_cell = [&](int s) -> uint32_t {
-        uint32_t c = 0;
-        if (Tm[s] > tau[0]) {
-#pragma unroll
-          for (int i = 0; i < NWIN; ++i)
-            if (Tm[s] > tau[i])
-              c |= (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(tb[s] > tau[i]))
-                   << (8 * i);
-        }
-        return c;
-      };
-      uint32_t csv = 0;  // lane s: cell s's packed counts
-#pragma unroll
-      for (int s = 0; s < PPT; ++s) {
-        const uint32_t c = count_cell(s);
-        csv = lane == s ? c : csv;
-      }
+      // ---- cold waves: apply the batch's centres as the hot wave publishes them, GRP at a
+      // time (the last, short group after the end flag), culled by the box test against the
+      // cells' Tmax (stale within the round = larger = still a valid bound). A touched cell is
+      // marked dirty; its exact Tmax is recomputed when the wave would otherwise wait, and the
+      // rest at the end of the batch.
+      uint32_t dirty = 0;
       PN2_TRACE(11, 1)
       int applied = 0;
       bool stop = false;
       unsigned long long tc0 = 0, tgrp = 0, tcnt0 = 0;
       int lag_at_stop = 0;
+      t_stop = 0;
+      int n_ev = 0;
       if constexpr (STAMP) tc0 = __builtin_amdgcn_s_memtime();
       for (int it = 0; it < (1 << 22); ++it) {
-        const int av = __builtin_amdgcn_readfirstlane(
+        const int sv = __builtin_amdgcn_readfirstlane(
             __hip_atomic_load(&sj[rp], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+        const int av = sv & (kEnd - 1);
+        stop = (sv & kEnd) != 0;  // set in the same word as the final count
         if (av - applied >= GRP || (stop && av > applied)) {
           const int a1 = min(av, applied + GRP);
-          if constexpr (STAMP) tcnt0 = __builtin_amdgcn_s_memtime();
+          if constexpr (PRIO > 0) __builtin_amdgcn_s_setprio(PRIO - 1);
+          if constexpr (STAMP) {
+            tcnt0 = __builtin_amdgcn_s_memtime();
+            if (b == 0 && round == 23 && lane == 0 && n_ev < 60) g_cull_round[w * 64 + 2 + n_ev++] = tcnt0 | ((unsigned long long)applied << 48) | ((unsigned long long)(av & 0xFF) << 56);
+          }
           const int ci = applied + lane / PPT;
           const bool valid = lane < GRP * PPT && ci < a1;
           const float4 cv = scl[valid ? ci : 0];
@@ -472,31 +466,44 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
                 const f2 d = (dx * dx + dy * dy) + dz * dz;
                 tb[s] = min(min(tb[s], __float_as_int(d.x)), __float_as_int(d.y));
               }
-              Tm[s] = __builtin_amdgcn_readfirstlane(wave_max_i32(tb[s]));
-              tmv = lane % PPT == s ? Tm[s] : tmv;
-              const uint32_t c = count_cell(s);
-              csv = lane == s ? c : csv;
+              dirty |= 1u << s;
             }
           }
           applied = a1;
+          if constexpr (PRIO > 0) __builtin_amdgcn_s_setprio(0);
           if constexpr (STAMP) {
             n_tail_grp += stop ? 1 : 0;
-            tgrp += __builtin_amdgcn_s_memtime() - tcnt0;
+            const unsigned long long dt = __builtin_amdgcn_s_memtime() - tcnt0;
+            tgrp += dt;
+            n_grp += 1;
+            n_grp_cyc += dt;
           }
           continue;
         }
-        if (stop) break;  // the end flag was seen before av was read: av is final
-        stop = __hip_atomic_load(&sstop[rp], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != 0;
-        if constexpr (STAMP) if (stop) {
-          t_stop = __builtin_amdgcn_s_memtime();
-          lag_at_stop = __hip_atomic_load(&sj[rp], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) - applied;
+        if (stop) break;  // av is final
+        if (dirty) {  // idle: refresh one dirty cell instead of waiting
+          const int s0 = __builtin_ctz(dirty);
+#pragma unroll
+          for (int s = 0; s < PPT; ++s) {
+            if (s == s0) {
+              Tm[s] = __builtin_amdgcn_readfirstlane(wave_max_i32(tb[s]));
+              tmv = lane % PPT == s ? Tm[s] : tmv;
+            }
+          }
+          dirty &= dirty - 1;
+          continue;
         }
-        if (!stop) __builtin_amdgcn_s_sleep(1);
+        if constexpr (STAMP) if (t_stop == 0) t_stop = __builtin_amdgcn_s_memtime();
+        if constexpr (STAMP) ++n_poll;
       }
       if constexpr (STAMP) {
         const unsigned long long tend = __builtin_amdgcn_s_memtime();
         n_tail_cyc += tend - t_stop;
         if (b == 0 && lane == 0 && round < 128) g_iter[2048 + round * 16 + w] = tend;
+        if (b == 0 && lane == 0 && round == 23) {
+          g_cull_round[w * 64 + 0] = t_stop;
+          g_cull_round[w * 64 + 1] = tend;
+        }
         if (b == 0 && lane == 0 && round < 256 && w == 1) {
           g_iter[round * 16 + 3] = t_stop;
           g_iter[round * 16 + 4] = tend;
@@ -505,30 +512,24 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
         }
       }
       PN2_STAMP(0)
+#pragma unroll
+      for (int s = 0; s < PPT; ++s) {
+        if (dirty & (1u << s)) {
+          Tm[s] = __builtin_amdgcn_readfirstlane(wave_max_i32(tb[s]));
+          tmv = lane % PPT == s ? Tm[s] : tmv;
+        }
+      }
+      dirty = 0;
       int wmax = -1;
 #pragma unroll
       for (int s = 0; s < PPT; ++s) wmax = max(wmax, Tm[s]);
       if (lane == 0) swmax[w] = wmax;
-      // totals over the cells (lanes 0..PPT-1 of row 0): 16-bit fields, row sums
-      static_assert(PPT <= 16, "cells in DPP row 0");
-      uint32_t lo = (csv & 0xFFu) | ((csv & 0xFF00u) << 8);
-      uint32_t hi = ((csv >> 16) & 0xFFu) | ((csv >> 8) & 0xFF0000u);
-#define PN2_ADD_DPP(V, C) V += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)V, C, 0xF, 0xF, false)
-      PN2_ADD_DPP(lo, kDppXor1); PN2_ADD_DPP(hi, kDppXor1);
-      PN2_ADD_DPP(lo, kDppXor2); PN2_ADD_DPP(hi, kDppXor2);
-      PN2_ADD_DPP(lo, kDppHalfMirror); PN2_ADD_DPP(hi, kDppHalfMirror);
-      PN2_ADD_DPP(lo, kDppMirror); PN2_ADD_DPP(hi, kDppMirror);
-#undef PN2_ADD_DPP
-      if (lane < NWIN) {
-        const uint32_t v = lane < 2 ? lo : hi;
-        swcnt[w][lane] = (lane & 1) ? v >> 16 : v & 0xFFFFu;
-      }
       PN2_STAMP(1)
     }
     __syncthreads();  // B1: the batch is complete and applied; Tmax and counts are current
     PN2_STAMP(2)
     PN2_TRACE(6, 0)
-    const int nb = sj[rp];
+    const int nb = sj[rp] & (kEnd - 1);
     for (int e = t; e < nb; e += BLOCK) {
       const float4 c = scl[e];
       I[j + e] = __float_as_int(c.w);
@@ -546,6 +547,30 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
       const int v = lane < NW ? swmax[lane] : -1;
       top = __builtin_amdgcn_readfirstlane(wave_max_i32(v));
     }
+    // ---- this round's thresholds (fractions of the exact maximum; every wave computes the
+    // same bits) and each wave's counts above them (cells at or below a threshold count 0)
+    int tau[NWIN];
+    {
+      const float tf = __int_as_float(max(top, 0));
+#pragma unroll
+      for (int i = 0; i < NWIN; ++i)
+        tau[i] = (int)uniform_u32((uint32_t)__float_as_int(tf * kCullFrac[tlo + i]));
+    }
+    if (cw >= 0) {
+      uint32_t mine = 0;
+#pragma unroll
+      for (int i = 0; i < NWIN; ++i) {
+        uint32_t c = 0;
+#pragma unroll
+        for (int s = 0; s < PPT; ++s)
+          if (Tm[s] > tau[i]) c += __builtin_popcountll(__builtin_amdgcn_ballot_w64(tb[s] > tau[i]));
+        mine = lane == i ? c : mine;
+      }
+      if (lane < NWIN) swcnt[w][lane] = mine;
+    }
+    PN2_STAMP(3)
+    __syncthreads();  // B2: counts complete
+    PN2_STAMP(4)
     // ---- choice: the lowest window threshold whose total count is in [1, K]. Lane
     // 16 i + v holds wave v's count above tau[i]; 16-lane row sums give the totals.
     const int cvw = lane & (NW - 1), ciw = lane / NW;
@@ -578,12 +603,7 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
     // next window: two below this choice (lower thresholds = bigger hot sets), or up; the next
     // thresholds scale with this round's maximum
     tlo = !stall ? min(max(tlo + ti - 2, 0), NT - NWIN) : min(tlo + NWIN, NT - NWIN);
-    topf = __int_as_float(max(top, 0));
-    if (t == 0) {  // the next round's batch starts empty (its flags were last read in round - 1)
-      sj[rp ^ 1] = 0;
-      sstop[rp ^ 1] = 0;
-    }
-    PN2_STAMP(3)
+    if (t == 0) sj[rp ^ 1] = 0;  // the next round's batch starts empty (last read in round - 1)
     PN2_TRACE(7, 0)
     if (!stall) {
       if (cw >= 0) {
@@ -618,10 +638,10 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
       if (lane == 0) swk[w] = best;
       if constexpr (STAMP) ++n_stall;
     }
-    PN2_STAMP(4)
-    PN2_TRACE(9, 1)
-    __syncthreads();  // B2: hot set (or the per-wave argmax) complete
     PN2_STAMP(5)
+    PN2_TRACE(9, 1)
+    __syncthreads();  // B3: hot set (or the per-wave argmax) complete
+    PN2_STAMP(6)
     PN2_TRACE(8, 0)
     if (stall) {
       uint64_t best = lane < NW ? swk[lane] : 0ull;
@@ -643,9 +663,7 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
       if (t == 0) {
         scl[0] = make_float4(sxyz[3 * k], sxyz[3 * k + 1], sxyz[3 * k + 2], __int_as_float(k));
         asm volatile("" ::: "memory");
-        *(volatile int*)&sj[rp ^ 1] = 1;
-        asm volatile("" ::: "memory");
-        *(volatile int*)&sstop[rp ^ 1] = 1;
+        *(volatile int*)&sj[rp ^ 1] = 1 | kEnd;
       }
     }
     hot_turn = !stall;
@@ -656,6 +674,10 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
     if (lane == 0 && b < 16) {
 #pragma unroll
       for (int ph = 0; ph < 8; ++ph) g_stamp[(b * 16 + w) * 8 + ph] = st_acc[ph];
+      g_cull_wave[(b * 16 + w) * 4 + 0] = n_grp;
+      g_cull_wave[(b * 16 + w) * 4 + 1] = n_grp_cyc;
+      g_cull_wave[(b * 16 + w) * 4 + 2] = n_pairs;
+      g_cull_wave[(b * 16 + w) * 4 + 3] = n_poll;
       if (w == 0) {
         g_cull_stats[b * 8 + 0] = __builtin_amdgcn_s_memtime() - clk0;
         g_cull_stats[b * 8 + 1] = n_refresh;
@@ -672,10 +694,10 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
   }
 }
 
-template <int NW, int PPT>
-void launch_cull(const float* xyz, int B, int N, int M, int32_t* idx, float* nx, hipStream_t s) {
-  hipLaunchKernelGGL((fps_hotcull_kernel<NW, PPT, 8192>), dim3(B), dim3(64 * NW), 0, s, xyz, N, M,
-                     idx, nx);
+template <int NW, int PPT, int PRIO = 0>
+void launch_hotcull(const float* xyz, int B, int N, int M, int32_t* idx, float* nx, hipStream_t s) {
+  hipLaunchKernelGGL((fps_hotcull_kernel<NW, PPT, 8192, false, PRIO>), dim3(B), dim3(64 * NW), 0, s,
+                     xyz, N, M, idx, nx);
 }
 
 }  // namespace

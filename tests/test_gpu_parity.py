@@ -49,6 +49,10 @@ def _cloud(pkg, kind, B, N, seed=0):
         g = np.stack(np.meshgrid(*[np.arange(16)] * 3, indexing="ij"), -1).reshape(-1, 3)
         rng = np.random.default_rng(seed)
         return np.stack([g[rng.integers(0, len(g), N)] for _ in range(B)]).astype(np.float32)
+    if kind == "fewuniq":  # 300 distinct points drawn with replacement: npoint > #unique
+        rng = np.random.default_rng(seed)
+        u = rng.random((300, 3)).astype(np.float32)
+        return np.stack([u[rng.integers(0, 300, N)] for _ in range(B)])
     raise ValueError(kind)
 
 
@@ -81,6 +85,37 @@ def test_fps_vs_oracle(env, kind, B, N, M):
     assert np.array_equal(_bits(new_xyz.cpu().numpy()), _bits(O.gather_point(x, ref)))
     only = pkg.tf_sampling.farthest_point_sample(M, torch.from_numpy(x).to(dev))
     assert np.array_equal(only.cpu().numpy(), ref)
+
+
+# SA1-size clouds (4096 < N <= 8192) run the culled hot-set sampler by default; every schedule
+# selectable through pn2_fps_set_algo (0 default, 1 v9 block scan, 6 no priority boost) must
+# give the oracle's indices: ScanNet crops with duplicates, uniform, the integer lattice (exact
+# ties everywhere), npoint beyond the distinct points, npoint > N, tiny npoint, odd N.
+SAMPLER_CASES = [
+    ("scannet", 16, 8192, 1024), ("uniform", 4, 8192, 1024), ("grid", 4, 8192, 1024),
+    ("grid", 2, 8192, 4000), ("dup", 2, 5000, 40), ("fewuniq", 2, 8192, 600),
+    ("scannet", 2, 4097, 4097), ("uniform", 2, 6000, 7000), ("scannet", 3, 8192, 2),
+    ("scannet", 3, 8192, 1), ("scannet", 2, 7777, 1500),
+]
+
+
+@pytest.mark.parametrize("algo", [0, 1, 6])
+@pytest.mark.parametrize("kind,B,N,M", SAMPLER_CASES)
+def test_fps_sampler_schedules(env, algo, kind, B, N, M):
+    pkg, O, torch, dev = env
+    lib = pkg._lib.lib()
+    x = _cloud(pkg, kind, B, N, seed=3)
+    old = lib.pn2_fps_set_algo(algo)
+    try:
+        idx, new_xyz = pkg.tf_sampling.farthest_point_sample_and_gather(
+            M, torch.from_numpy(x).to(dev))
+        torch.cuda.synchronize()
+    finally:
+        lib.pn2_fps_set_algo(old)
+    ref = O.fps(x, M)
+    got = idx.cpu().numpy()
+    assert np.array_equal(got, ref), f"algo {algo}: {(got != ref).sum()} FPS indices differ"
+    assert np.array_equal(_bits(new_xyz.cpu().numpy()), _bits(O.gather_point(x, ref)))
 
 
 @pytest.mark.parametrize("kind,B,N,M", [c for c in FPS_CASES if c[2] <= 16384])

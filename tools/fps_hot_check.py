@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""GPU A/B of the SA1 samplers (pn2_fps_set_algo: 1 = v9 block scan, 2 = hot set):
+"""GPU A/B of the SA1 samplers (pn2_fps_set_algo: 0 = culled hot set, 1 = v9 block scan,
+6 = culled hot set without the priority boost):
 index-exact against the oracle and against each other on tie-heavy and ScanNet-like clouds,
 then HIP-event kernel times at the cfg2 SA1 shape (B = 16, 8192 -> 1024).
 
@@ -40,8 +41,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--quick", action="store_true")
-    ap.add_argument("--algo", type=int, default=2)
-    ap.add_argument("--algos", default="1,2")
+    ap.add_argument("--algo", type=int, default=0)
+    ap.add_argument("--algos", default="1,0")
     ap.add_argument("--no-check", action="store_true")
     args = ap.parse_args()
     import torch
@@ -107,7 +108,7 @@ def main():
             assert rc == 0
             if r >= 2:
                 times[algo].append(e0.elapsed_time(e1))
-    out = {"sa1_B16_ms": {{1: "v9", 2: "hot", 3: "hot_sb", 4: "hot_async"}.get(a, str(a)): {"median": statistics.median(v),
+    out = {"sa1_B16_ms": {{0: "cull", 1: "v9", 6: "cull_noprio"}.get(a, str(a)): {"median": statistics.median(v),
                                                           "min": min(v)} for a, v in times.items()},
            "all_exact": ok}
     print(json.dumps(out), flush=True)

@@ -29,7 +29,7 @@
 // A numpy model of this schedule on the SA1 crops (ScanNet-like, duplicates) refreshes ~48
 // times for 1,023 picks with PH = 2, E = 8.
 #pragma once
-#include "fps_kernels.h"
+#include "../../pointcloud-segmentation-attention_amd/csrc/fps_kernels.h"
 
 namespace pn2 {
 namespace {

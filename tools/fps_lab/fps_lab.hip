@@ -3,7 +3,7 @@
 // and tools/stamp_fps.py. NOT part of libpn2hip.so: built into tools/fps_lab/libpn2fpslab.so
 // by tools/fps_lab/Makefile. DESIGN.md records what each variant taught.
 #include "../../pointcloud-segmentation-attention_amd/csrc/fps_kernels.h"
-#include "../../pointcloud-segmentation-attention_amd/csrc/fps_hot.h"
+#include "fps_hot.h"
 #include "../../pointcloud-segmentation-attention_amd/csrc/fps_cull.h"
 
 namespace pn2 {
@@ -2030,7 +2030,7 @@ int pn2_fps_cull_stamp(const float* xyz, int B, int N, int npoint, int32_t* idx,
                        unsigned long long* out_host, unsigned long long* stats_host) {
   hipStream_t s = 0;
   if (N > 8192) return PN2_EINVAL;
-  hipLaunchKernelGGL((pn2::fps_hotcull_kernel<16, 9, 8192, true>), dim3(B), dim3(1024), 0, s, xyz, N,
+  hipLaunchKernelGGL((pn2::fps_hotcull_kernel<16, 9, 8192, true, 3>), dim3(B), dim3(1024), 0, s, xyz, N,
                      npoint, idx, nullptr);
   hipError_t e = hipDeviceSynchronize();
   if (e != hipSuccess) return (int)e;
@@ -2043,6 +2043,12 @@ int pn2_fps_cull_stamp(const float* xyz, int B, int N, int npoint, int32_t* idx,
 }
 
 // Diagnostic: the per-round trace the stamped hot-cull sampler leaves in g_iter (cloud 0).
+int pn2_fps_cull_waves(unsigned long long* out_host) {
+  return (int)hipMemcpyFromSymbol(out_host, HIP_SYMBOL(pn2::g_cull_wave), sizeof(unsigned long long) * 16 * 16 * 4);
+}
+int pn2_fps_cull_round(unsigned long long* out_host) {
+  return (int)hipMemcpyFromSymbol(out_host, HIP_SYMBOL(pn2::g_cull_round), sizeof(unsigned long long) * 16 * 64);
+}
 int pn2_fps_cull_trace(unsigned long long* out_host) {
   return (int)hipMemcpyFromSymbol(out_host, HIP_SYMBOL(pn2::g_iter), sizeof(unsigned long long) * 4096);
 }

@@ -28,6 +28,14 @@ for kind in ("scannet", "uniform"):
     old = lib.pn2_fps_set_algo(1)
     ref = pkg.tf_sampling.farthest_point_sample(M, x)
     lib.pn2_fps_set_algo(old)
+    wv = np.zeros(16 * 16 * 4, np.uint64)
+    L.pn2_fps_cull_waves.argtypes = [ctypes.c_void_p]
+    assert L.pn2_fps_cull_waves(wv.ctypes.data) == 0
+    wv = wv.reshape(16, 16, 4).astype(np.float64)
+    print(json.dumps({"kind": kind, "per_wave_groups": [round(v) for v in wv[:, :, 0].mean(0)],
+                      "per_wave_cyc_per_group": [round(v) for v in (wv[:, :, 1] / np.maximum(wv[:, :, 0], 1)).mean(0)],
+                      "per_wave_pairs": [round(v) for v in wv[:, :, 2].mean(0)],
+                      "per_wave_polls": [round(v) for v in wv[:, :, 3].mean(0)]}), flush=True)
     a = buf.reshape(16, 16, 8).astype(np.float64)
     st = stats.reshape(16, 8).astype(np.float64)
     print(json.dumps({
