@@ -327,6 +327,7 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
   int tlo = 2;              // first threshold of the counted window
   int T = 0, nh = 0;        // the hot phase's threshold and hot-set size
   bool hot_turn = false;
+  uint32_t dirty = 0;  // cold waves: cells whose Tmax is stale (an upper bound)
   for (int round = 0; round <= M; ++round) {
     if (w == 0) {
       if (hot_turn) {
@@ -417,7 +418,6 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
       // cells' Tmax (stale within the round = larger = still a valid bound). A touched cell is
       // marked dirty; its exact Tmax is recomputed when the wave would otherwise wait, and the
       // rest at the end of the batch.
-      uint32_t dirty = 0;
       PN2_TRACE(11, 1)
       int applied = 0;
       bool stop = false;
@@ -441,6 +441,14 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
           const int ci = applied + lane / PPT;
           const bool valid = lane < GRP * PPT && ci < a1;
           const float4 cv = scl[valid ? ci : 0];
+          if (cw == 0 && valid && lane % PPT == 0) {  // wave 1 stores the batch's outputs
+            I[j + ci] = __float_as_int(cv.w);
+            if (NX) {
+              NX[3 * (j + ci)] = cv.x;
+              NX[3 * (j + ci) + 1] = cv.y;
+              NX[3 * (j + ci) + 2] = cv.z;
+            }
+          }
           const float lb = box_lb(glo, ghi, cv.x, cv.y, cv.z);
           const uint64_t m = __builtin_amdgcn_ballot_w64(valid && __float_as_int(lb) < tmv);
           if constexpr (STAMP) n_pairs += __builtin_popcountll(m);
@@ -512,34 +520,31 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
         }
       }
       PN2_STAMP(0)
-#pragma unroll
-      for (int s = 0; s < PPT; ++s) {
-        if (dirty & (1u << s)) {
-          Tm[s] = __builtin_amdgcn_readfirstlane(wave_max_i32(tb[s]));
-          tmv = lane % PPT == s ? Tm[s] : tmv;
-        }
-      }
-      dirty = 0;
+      // end of the batch: this wave's exact maximum. A dirty cell is refreshed only if its
+      // stale Tmax (an upper bound) exceeds the maximum of the exact ones; the others stay
+      // dirty (refreshed while waiting next round) without affecting the maximum.
       int wmax = -1;
 #pragma unroll
-      for (int s = 0; s < PPT; ++s) wmax = max(wmax, Tm[s]);
+      for (int s = 0; s < PPT; ++s)
+        if (!(dirty & (1u << s))) wmax = max(wmax, Tm[s]);
+#pragma unroll
+      for (int s = 0; s < PPT; ++s) {
+        if ((dirty & (1u << s)) && Tm[s] > wmax) {
+          Tm[s] = __builtin_amdgcn_readfirstlane(wave_max_i32(tb[s]));
+          tmv = lane % PPT == s ? Tm[s] : tmv;
+          dirty &= ~(1u << s);
+          wmax = max(wmax, Tm[s]);
+        }
+      }
       if (lane == 0) swmax[w] = wmax;
       PN2_STAMP(1)
     }
     __syncthreads();  // B1: the batch is complete and applied; Tmax and counts are current
     PN2_STAMP(2)
     PN2_TRACE(6, 0)
-    const int nb = sj[rp] & (kEnd - 1);
-    for (int e = t; e < nb; e += BLOCK) {
-      const float4 c = scl[e];
-      I[j + e] = __float_as_int(c.w);
-      if (NX) {
-        NX[3 * (j + e)] = c.x;
-        NX[3 * (j + e) + 1] = c.y;
-        NX[3 * (j + e) + 2] = c.z;
-      }
-    }
-    j += nb;
+    // (cold wave 1 stored the batch's outputs group by group, so the barriers' s_waitcnt finds
+    // at most the last group's stores outstanding)
+    j += sj[rp] & (kEnd - 1);
     if (j >= M) break;
     if constexpr (STAMP) ++n_refresh;
     int top;
@@ -557,16 +562,18 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
         tau[i] = (int)uniform_u32((uint32_t)__float_as_int(tf * kCullFrac[tlo + i]));
     }
     if (cw >= 0) {
-      uint32_t mine = 0;
+      uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+      static_assert(NWIN == 4, "four counters");
 #pragma unroll
-      for (int i = 0; i < NWIN; ++i) {
-        uint32_t c = 0;
-#pragma unroll
-        for (int s = 0; s < PPT; ++s)
-          if (Tm[s] > tau[i]) c += __builtin_popcountll(__builtin_amdgcn_ballot_w64(tb[s] > tau[i]));
-        mine = lane == i ? c : mine;
+      for (int s = 0; s < PPT; ++s) {
+        if (Tm[s] > tau[0]) {
+          c0 += __builtin_popcountll(__builtin_amdgcn_ballot_w64(tb[s] > tau[0]));
+          c1 += __builtin_popcountll(__builtin_amdgcn_ballot_w64(tb[s] > tau[1]));
+          c2 += __builtin_popcountll(__builtin_amdgcn_ballot_w64(tb[s] > tau[2]));
+          c3 += __builtin_popcountll(__builtin_amdgcn_ballot_w64(tb[s] > tau[3]));
+        }
       }
-      if (lane < NWIN) swcnt[w][lane] = mine;
+      if (lane < NWIN) swcnt[w][lane] = lane == 0 ? c0 : lane == 1 ? c1 : lane == 2 ? c2 : c3;
     }
     PN2_STAMP(3)
     __syncthreads();  // B2: counts complete

@@ -69,3 +69,12 @@ if hasattr(L, "pn2_fps_cull_trace"):
         ends = [int(v - base) for v in r[128 + i // 16][(i % 16):(i % 16) + 1]] if False else None
         ends = [int(tr[2048 + i * 16 + v]) - int(r[i, 1]) if r[i, 1] else None for v in range(1, 16)]
         print(json.dumps({"round": i, "picks": int(r[i, 2]), "cold_end_minus_hot_end": ends}), flush=True)
+    gaps = [int(r[i, 6] - r[i, 1]) for i in range(1, 60) if r[i, 2] > 0 and r[i, 6] > r[i, 1]]
+    nxt = [int(r[i + 1, 0] - r[i, 6]) for i in range(1, 60) if r[i + 1, 2] > 0 and r[i + 1, 0] > r[i, 6]]
+    picks = [int(r[i, 2]) for i in range(1, 60) if r[i, 2] > 0]
+    print(json.dumps({"hot_end_to_B1": gaps, "B1_to_next_hot": nxt, "picks": picks}), flush=True)
+    for i in range(20, 31):
+        ends = [int(tr[2048 + i * 16 + v]) for v in range(1, 16)]
+        he = int(r[i, 1])
+        print(json.dumps({"round": i, "picks": int(r[i, 2]), "cold_end_minus_hot_end": [e - he for e in ends],
+                          "B1_minus_hot_end": int(r[i, 6]) - he}), flush=True)
