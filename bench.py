@@ -122,7 +122,7 @@ def pmc_traffic(config, B):
         return None, None
     with open(files[-1]) as f:
         d = json.load(f)
-    ks = [k for k in d["kernels"] if k.startswith("fps_v")]
+    ks = [k for k in d["kernels"] if k.startswith(("fps_hotcull", "fps_v"))]
     if not ks:
         return None, None
     k = max(ks, key=lambda k: d["kernels"][k]["fetch_bytes"] or 0)  # SA1 = largest sampler
@@ -136,26 +136,22 @@ def pmc_traffic(config, B):
 MAX_CLOCK_GHZ = 2.4  # MI355X_MICROARCH.md, chip-level parameters
 
 
-def sa1_valu_bound(config, ns_per_iteration):
-    """Per-CU VALU bound of the SA1 sampler (one workgroup = one CU per cloud): the loop's
-    VALU instructions per iteration (static count of the built kernel,
-    profiles/<round>/sa1_loop_isa.json from tools/sa1_loop_isa.py) x 4 cycles (wave64, one wave
-    per SIMD) against the measured iteration at the max clock (a lower clock under load only
-    raises the fraction). Only for the 8192-point sampler that file describes."""
+def sa1_latency(config, fps_ms, M1):
+    """The SA1 sampler's own bound: its picks are a serial chain. For the culled hot-set
+    sampler (N <= 8192: cfg2, cfg3) the committed stamp summary
+    (profiles/<round>/sa1_cull_stamps.json, tools/stamp_fps_cull.py) splits a launch into the
+    hot wave's pick loop (cycles per pick) and the per-round refresh (rounds x cycles)."""
     import glob
-    if config not in ("cfg2", "cfg3"):
-        return None
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "sa1_loop_isa.json")))
-    if not files:
-        return None
-    with open(files[-1]) as f:
-        d = json.load(f)
-    cycles = ns_per_iteration * MAX_CLOCK_GHZ
-    return {"valu_instr_per_iteration": d["mix"]["valu"],
-            "floor_cycles_per_iteration": d["valu_issue_floor_cycles"],
-            "cycles_per_iteration_at_max_clock": cycles,
-            "frac": d["valu_issue_floor_cycles"] / cycles,
-            "source": os.path.relpath(files[-1], ROOT)}
+    out = {"ns_per_pick": fps_ms * 1e6 / max(1, M1 - 1)}
+    if config in ("cfg2", "cfg3"):
+        files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "sa1_cull_stamps.json")))
+        if files:
+            with open(files[-1]) as f:
+                d = json.load(f)
+            out.update({k: d[k] for k in ("hot_cycles_per_pick", "rounds", "round_cycles",
+                                          "setup_cycles") if k in d})
+            out["source"] = os.path.relpath(files[-1], ROOT)
+    return out
 
 
 def _e2e_child(args, e2e):
@@ -442,11 +438,10 @@ def main():
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS,
                          "traffic": traffic, "traffic_source": traffic_src,
                          "avg_launch_ms": fps_ms, "algorithmic_bytes_per_launch": fps_bytes,
-                         "ns_per_iteration": fps_ms * 1e6 / max(1, M1 - 1),
-                         "valu": sa1_valu_bound(args.config, fps_ms * 1e6 / max(1, M1 - 1)),
-                         "note": "latency-bound serial argmax (M-1 dependent block-wide "
-                                 "reductions); the HBM fraction is structurally low, the "
-                                 "per-CU VALU-issue fraction ('valu') is the bound that applies"},
+                         "latency": sa1_latency(args.config, fps_ms, M1),
+                         "note": "latency-bound serial argmax (M-1 dependent picks, one CU per "
+                                 "cloud); the HBM fraction is structurally low, the pick "
+                                 "chain ('latency') is the bound that applies"},
             "step_hbm": {"algorithmic_bytes": step_bytes,
                          "achieved_GBps": step_bytes * world / (elapsed / args.steps) / 1e9,
                          "frac": step_bytes * world / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBPS},

@@ -104,8 +104,8 @@ int pn2_fps_gather(const float* xyz, int B, int N, int npoint, int32_t* idx, flo
                    pn2_stream_t stream);
 int pn2_fps_max_points(void);
 /* Sampler schedule for 4096 < N <= 8192 (process-wide; tests and A/B timing): 0 = the default
- * (culled hot-set sampler), 1 = the v9 block-scan sampler (one block argmax per pick), 6 = the
- * culled hot-set sampler without the hot wave's issue-priority boost. Identical outputs.
+ * (culled hot-set sampler, 256 hot entries), 1 = the v9 block-scan sampler (one block argmax per
+ * pick), 6 = the culled hot-set sampler with 128 hot entries. Identical outputs.
  * Returns the previous setting; other values only query. */
 int pn2_fps_set_algo(int algo);
 size_t pn2_fps_workspace_size(int B, int N);

@@ -109,8 +109,8 @@ __global__ void gather_point_grad_kernel(const float* __restrict__ out_g,
 
 constexpr int kMaxRegPoints = 1024 * 16;
 
-// Sampler selection for 4096 < N <= 8192: 0 = default (culled hot set, hot-wave priority 3),
-// 1 = v9 block scan, 6 = culled hot set without the priority boost.
+// Sampler selection for 4096 < N <= 8192: 0 = default (culled hot set, 256 hot entries),
+// 1 = v9 block scan, 6 = culled hot set with 128 hot entries.
 int g_fps_algo = 0;
 
 // ---- sampler chain: SA1..SAk's samplers of one cloud, stage 2.. in ONE workgroup -----------
@@ -184,11 +184,11 @@ int fps_impl(const float* xyz, int B, int N, int M, int32_t* idx, float* nx, voi
   else if (N <= 2048) launch_v9<256, 8, 2, true>(xyz, B, N, M, idx, nx, s);
   else if (N <= 4096) launch_v9<256, 16, 4, true>(xyz, B, N, M, idx, nx, s);
   else if (N <= 8192) {
-    // culled hot-set sampler (fps_cull.h; 0.50 vs 0.71 ms at B = 16); the v9
+    // culled hot-set sampler (fps_cull.h; 0.47 vs 0.71 ms at B = 16); the v9
     // block-scan sampler stays selectable for A/B timing and parity cross-checks
     if (g_fps_algo == 1) launch_v9<256, 32, 4, true, false, PN2_SA1_PAD>(xyz, B, N, M, idx, nx, s);
-    else if (g_fps_algo == 6) launch_hotcull<16, 9, 0>(xyz, B, N, M, idx, nx, s);
-    else launch_hotcull<16, 9, 3>(xyz, B, N, M, idx, nx, s);
+    else if (g_fps_algo == 6) launch_hotcull<16, 9, 3, 2>(xyz, B, N, M, idx, nx, s);
+    else launch_hotcull<16, 9, 3, 4>(xyz, B, N, M, idx, nx, s);
   }
   else if (N <= kMaxRegPoints) launch_v9<512, 32, 4>(xyz, B, N, M, idx, nx, s);
   else {

@@ -29,8 +29,8 @@ namespace pn2 {
 namespace {
 
 __device__ unsigned long long g_cull_stats[16 * 8];  // STAMP builds: per-cloud counters
-__device__ unsigned long long g_cull_wave[16 * 16 * 4];
-__device__ unsigned long long g_cull_round[16 * 64];  // STAMP: cloud 0, round 23: per wave event times  // STAMP: per wave groups, group cycles, pairs, polls
+__device__ unsigned long long g_cull_wave[16 * 16 * 4];  // STAMP: per wave groups, group cycles, pairs, polls
+__device__ unsigned long long g_cull_ev[64 * 16 * 8];   // STAMP: cloud 0, rounds < 64: per wave events
 
 // float max over the wave (every lane gets it); DPP rows, then the gfx950 permlane swaps
 PN2_DEV float wave_max_f32(float v) {
@@ -99,12 +99,10 @@ __constant__ float kCullFrac[12] = {0.6f, 0.7f, 0.75f, 0.8f, 0.84f, 0.87f,
                                     0.9f, 0.92f, 0.94f, 0.96f, 0.98f, 0.99f};
 
 
-// STAMP builds: s_memtime of an event of round r of cloud 0, wave WV (g_iter[r * 16 + F])
-#define PN2_TRACE(F, WV)                                                                   \
-  if constexpr (STAMP) {                                                                   \
-    if (b == 0 && lane == 0 && w == (WV) && round < 256)                                   \
-      g_iter[round * 16 + (F)] = __builtin_amdgcn_s_memtime();                             \
-  }
+// STAMP builds: s_memtime of event K of this round, kept in SGPRs and stored for cloud 0 after
+// the round's last barrier (a store before a barrier would make its s_waitcnt wait for it)
+#define PN2_EV(K)                                                                          \
+  if constexpr (STAMP) ev[K] = __builtin_amdgcn_s_memtime();
 
 // bits s, s + PPT, s + 2 PPT, ... (GRP of them): the lanes that test cell s in a group
 template <int PPT, int GRP>
@@ -116,24 +114,23 @@ PN2_DEV constexpr uint64_t cell_lanes(int s) {
 
 // NPTS points at most; wave 0 is the hot wave, waves 1..NW-1 hold the cold cells (PPT cells of
 // 64 sorted points per wave).
-template <int NW, int PPT, int NPTS, bool STAMP = false, int PRIO = 0>
+template <int NW, int PPT, int NPTS, bool STAMP = false, int PRIO = 0, int HQ = 2>
 __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __restrict__ xyz, int N,
                                                            int M, int32_t* __restrict__ idx,
                                                            float* __restrict__ new_xyz) {
   constexpr int BLOCK = 64 * NW;
-  constexpr int NCW = NW - 1;           // cold waves
+  constexpr int NCW = NW - 1;  // cold waves
   constexpr int NCELL = NCW * PPT;
   constexpr int GRP = kWave / PPT;      // centres per group test (lane = centre * PPT + cell)
-  constexpr int K = 128;                // hot-set capacity: two entries per lane of wave 0
+  constexpr int K = 64 * HQ;            // hot-set capacity: HQ entries per lane of wave 0
   constexpr int NT = 12;                // thresholds
   constexpr int NWIN = 4;               // thresholds counted per refresh
   constexpr int NBK = 4096;             // sort buckets (16^3 Morton)
   constexpr int kEnd = 1 << 16;         // sj flag: the batch is complete
-  constexpr int SPT = NPTS / BLOCK;     // setup: points per thread
+  constexpr int SPT = (NPTS + BLOCK - 1) / BLOCK;  // setup: points per thread
   static_assert(NCELL * kWave >= NPTS, "cold capacity");
-  static_assert(NPTS % BLOCK == 0 && NBK % BLOCK == 0, "setup strides");
   static_assert(PPT <= 32 && GRP >= 1, "slot masks");
-  static_assert(NW * NWIN == kWave && NWIN == 4, "choice: one lane per (threshold, wave)");
+  static_assert(NW <= 16 && NWIN == 4, "choice: lane 16 i + v = (threshold i, wave v)");
   using f2 = float __attribute__((ext_vector_type(2)));
 
   __shared__ float sxyz[3 * NPTS];
@@ -157,7 +154,8 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
   float* __restrict__ NX = new_xyz ? new_xyz + (size_t)b * M * 3 : nullptr;
   unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, st_prev = 0;
   unsigned long long n_refresh = 0, n_stall = 0, n_pairs = 0, n_hot = 0, clk0 = 0;
-  unsigned long long n_tail_cyc = 0, n_tail_grp = 0, t_stop = 0;
+  unsigned long long n_tail_grp = 0;
+  unsigned long long ev[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // STAMP: this round's events
   unsigned long long n_grp = 0, n_grp_cyc = 0, n_poll = 0;
   if constexpr (STAMP) {
     clk0 = __builtin_amdgcn_s_memtime();
@@ -225,11 +223,11 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
   }
   __syncthreads();
   {
-    constexpr int PB = NBK / BLOCK;
+    constexpr int PB = (NBK + BLOCK - 1) / BLOCK;
     uint32_t c[PB], s = 0;
 #pragma unroll
     for (int i = 0; i < PB; ++i) {
-      c[i] = shist[PB * t + i];
+      c[i] = PB * t + i < NBK ? shist[PB * t + i] : 0u;
       s += c[i];
     }
     const uint32_t ex = wave_excl_scan(s, lane);
@@ -240,7 +238,7 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
     uint32_t run = base + ex;
 #pragma unroll
     for (int i = 0; i < PB; ++i) {
-      shist[PB * t + i] = run;
+      if (PB * t + i < NBK) shist[PB * t + i] = run;
       run += c[i];
     }
   }
@@ -290,7 +288,7 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
     scl[0] = make_float4(sxyz[0], sxyz[1], sxyz[2], __int_as_float(0));
     sj[0] = 1 | kEnd;
     sj[1] = 0;
-    swmax[0] = -1;  // the hot wave holds no cell
+    for (int v = 0; v < NW; ++v) swmax[v] = -1;  // waves without cells keep -1
   }
   __syncthreads();
 
@@ -334,36 +332,65 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
         // ---- hot phase: certified picks while the best hot value is above T, each one
         // published to the cold waves at once (scl[jj], then the count sj; DS operations of
         // one wave execute in order, so a cold wave that reads the count reads the centre)
-        int hv[2], hk[2];
+        static_assert(HQ == 2 || HQ == 4, "hot entries per lane");
+        int hv[HQ], hk[HQ];
+        uint32_t hkey[HQ];
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
+        for (int q = 0; q < HQ; ++q) {
           const int e = lane + q * kWave;
           const uint2 en = e < nh ? sh[e] : make_uint2(0xFFFFFFFFu, 0u);
           hv[q] = (int)en.x;
           hk[q] = (int)en.y;
+          hkey[q] = hv[q] >= 0 ? cull_key(hk[q]) : 0xFFFFFFFFu;
         }
-        // entry 0 of a lane is the earlier one in tie order: a strict '>' picks between them
-        if (hv[1] >= 0 && (hv[0] < 0 || cull_key(hk[1]) < cull_key(hk[0]))) {
-          const int v = hv[0], k = hk[0];
-          hv[0] = hv[1]; hk[0] = hk[1];
-          hv[1] = v; hk[1] = k;
-        }
-        const uint32_t key0 = cull_key(hk[0]), key1 = cull_key(hk[1]);
-        f2 hx, hy, hz;
+        // a lane's entries in tie order (odd-even transposition sort by key): then a tournament
+        // of strict '>' comparisons, lower entry first, picks the reference's winner in a lane
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
-          hx[q] = sxyz[3 * hk[q]];
-          hy[q] = sxyz[3 * hk[q] + 1];
-          hz[q] = sxyz[3 * hk[q] + 2];
+        for (int pass = 0; pass < HQ; ++pass) {
+#pragma unroll
+          for (int q = pass & 1; q + 1 < HQ; q += 2) {
+            if (hkey[q + 1] < hkey[q]) {
+              const int v = hv[q], k = hk[q];
+              const uint32_t y = hkey[q];
+              hv[q] = hv[q + 1]; hk[q] = hk[q + 1]; hkey[q] = hkey[q + 1];
+              hv[q + 1] = v; hk[q + 1] = k; hkey[q + 1] = y;
+            }
+          }
+        }
+        constexpr int HP = HQ / 2;  // coordinate pairs
+        f2 hx[HP], hy[HP], hz[HP];
+#pragma unroll
+        for (int q = 0; q < HQ; ++q) {
+          hx[q / 2][q % 2] = sxyz[3 * hk[q]];
+          hy[q / 2][q % 2] = sxyz[3 * hk[q] + 1];
+          hz[q / 2][q % 2] = sxyz[3 * hk[q] + 2];
         }
         const int lim = min(K, M - j);
         int jj = 0;
-        unsigned long long th0 = 0;
-        if constexpr (STAMP) th0 = __builtin_amdgcn_s_memtime();
         if constexpr (PRIO > 0) __builtin_amdgcn_s_setprio(PRIO);
+        // every hot-set load is complete before the loop: the wait-count pass then has no
+        // pending LDS load to wait for inside it, and the picks' publishing stores stay off
+        // the dependency chain (an in-loop lgkmcnt(0) would wait for the previous pick's)
+        __builtin_amdgcn_s_waitcnt(0xC07F);
         for (; jj < lim; ++jj) {
-          const bool b1 = hv[1] > hv[0];
-          const int cv = b1 ? hv[1] : hv[0];
+          // the lane's best entry (value desc, then entry order = tie order)
+          const bool b01 = hv[1] > hv[0];
+          int cv = b01 ? hv[1] : hv[0];
+          float lx = b01 ? hx[0][1] : hx[0][0], ly = b01 ? hy[0][1] : hy[0][0],
+                lz = b01 ? hz[0][1] : hz[0][0];
+          int lk = b01 ? hk[1] : hk[0];
+          uint32_t ck = b01 ? hkey[1] : hkey[0];
+          if constexpr (HQ == 4) {
+            const bool b23 = hv[3] > hv[2];
+            const int v23 = b23 ? hv[3] : hv[2];
+            const bool bh = v23 > cv;
+            cv = bh ? v23 : cv;
+            lx = bh ? (b23 ? hx[1][1] : hx[1][0]) : lx;
+            ly = bh ? (b23 ? hy[1][1] : hy[1][0]) : ly;
+            lz = bh ? (b23 ? hz[1][1] : hz[1][0]) : lz;
+            lk = bh ? (b23 ? hk[3] : hk[2]) : lk;
+            ck = bh ? (b23 ? hkey[3] : hkey[2]) : ck;
+          }
           const int wm = __builtin_amdgcn_readfirstlane(wave_max_i32(cv));
           if (!(wm > T)) break;
           const uint64_t hold = __builtin_amdgcn_ballot_w64(cv == wm);
@@ -371,61 +398,47 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
           if (__builtin_popcountll(hold) == 1) {
             L = (int)__builtin_ctzll(hold);
           } else {  // equal values: the smallest tie key among the holders
-            const uint32_t ck = b1 ? key1 : key0;
             const uint32_t km = ~uniform_u32(wave_max_u32(cv == wm ? ~ck : 0u));
             L = (int)__builtin_ctzll(__builtin_amdgcn_ballot_w64(cv == wm && ck == km));
           }
-          const float lx = b1 ? hx[1] : hx[0], ly = b1 ? hy[1] : hy[0], lz = b1 ? hz[1] : hz[0];
-          const int lk = b1 ? hk[1] : hk[0];
           const float cx = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__float_as_int(lx), L));
           const float cy = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__float_as_int(ly), L));
           const float cz = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__float_as_int(lz), L));
-          const int ck = __builtin_amdgcn_readlane(lk, L);
+          const int cidx = __builtin_amdgcn_readlane(lk, L);
           if (lane == 0) {
-            scl[jj] = make_float4(cx, cy, cz, __int_as_float(ck));
+            scl[jj] = make_float4(cx, cy, cz, __int_as_float(cidx));
             asm volatile("" ::: "memory");
-            *(volatile int*)&sj[rp] = jj + 1;
+            __hip_atomic_store(&sj[rp], jj + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           }
           const f2 c2x = {cx, cx}, c2y = {cy, cy}, c2z = {cz, cz};
-          const f2 dx = hx - c2x, dy = hy - c2y, dz = hz - c2z;
-          const f2 d = (dx * dx + dy * dy) + dz * dz;
-          hv[0] = min(hv[0], __float_as_int(d.x));
-          hv[1] = min(hv[1], __float_as_int(d.y));
+#pragma unroll
+          for (int h = 0; h < HP; ++h) {
+            const f2 dx = hx[h] - c2x, dy = hy[h] - c2y, dz = hz[h] - c2z;
+            const f2 d = (dx * dx + dy * dy) + dz * dz;
+            hv[2 * h] = min(hv[2 * h], __float_as_int(d.x));
+            hv[2 * h + 1] = min(hv[2 * h + 1], __float_as_int(d.y));
+          }
         }
         if constexpr (PRIO > 0) __builtin_amdgcn_s_setprio(0);
         if (lane == 0) {
           asm volatile("" ::: "memory");
-          *(volatile int*)&sj[rp] = jj | kEnd;
+          __hip_atomic_store(&sj[rp], jj | kEnd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
         if constexpr (STAMP) {
-          if (b == 0 && lane == 0 && round == 23) {
-            g_cull_round[0] = th0;
-            g_cull_round[1] = __builtin_amdgcn_s_memtime();
-            g_cull_round[2] = jj;
-          }
           n_hot += jj;
-          if (b == 0 && lane == 0 && round < 256) {
-            g_iter[round * 16 + 0] = th0;
-            g_iter[round * 16 + 1] = __builtin_amdgcn_s_memtime();
-            g_iter[round * 16 + 2] = jj;
-          }
         }
       }
+      PN2_EV(0)
       PN2_STAMP(7)
-    } else {
+    } else if (cw >= 0) {
       // ---- cold waves: apply the batch's centres as the hot wave publishes them, GRP at a
       // time (the last, short group after the end flag), culled by the box test against the
       // cells' Tmax (stale within the round = larger = still a valid bound). A touched cell is
       // marked dirty; its exact Tmax is recomputed when the wave would otherwise wait, and the
       // rest at the end of the batch.
-      PN2_TRACE(11, 1)
       int applied = 0;
       bool stop = false;
-      unsigned long long tc0 = 0, tgrp = 0, tcnt0 = 0;
-      int lag_at_stop = 0;
-      t_stop = 0;
-      int n_ev = 0;
-      if constexpr (STAMP) tc0 = __builtin_amdgcn_s_memtime();
+      unsigned long long tcnt0 = 0;
       for (int it = 0; it < (1 << 22); ++it) {
         const int sv = __builtin_amdgcn_readfirstlane(
             __hip_atomic_load(&sj[rp], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
@@ -434,10 +447,7 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
         if (av - applied >= GRP || (stop && av > applied)) {
           const int a1 = min(av, applied + GRP);
           if constexpr (PRIO > 0) __builtin_amdgcn_s_setprio(PRIO - 1);
-          if constexpr (STAMP) {
-            tcnt0 = __builtin_amdgcn_s_memtime();
-            if (b == 0 && round == 23 && lane == 0 && n_ev < 60) g_cull_round[w * 64 + 2 + n_ev++] = tcnt0 | ((unsigned long long)applied << 48) | ((unsigned long long)(av & 0xFF) << 56);
-          }
+          if constexpr (STAMP) tcnt0 = __builtin_amdgcn_s_memtime();
           const int ci = applied + lane / PPT;
           const bool valid = lane < GRP * PPT && ci < a1;
           const float4 cv = scl[valid ? ci : 0];
@@ -482,7 +492,6 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
           if constexpr (STAMP) {
             n_tail_grp += stop ? 1 : 0;
             const unsigned long long dt = __builtin_amdgcn_s_memtime() - tcnt0;
-            tgrp += dt;
             n_grp += 1;
             n_grp_cyc += dt;
           }
@@ -501,24 +510,9 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
           dirty &= dirty - 1;
           continue;
         }
-        if constexpr (STAMP) if (t_stop == 0) t_stop = __builtin_amdgcn_s_memtime();
         if constexpr (STAMP) ++n_poll;
       }
-      if constexpr (STAMP) {
-        const unsigned long long tend = __builtin_amdgcn_s_memtime();
-        n_tail_cyc += tend - t_stop;
-        if (b == 0 && lane == 0 && round < 128) g_iter[2048 + round * 16 + w] = tend;
-        if (b == 0 && lane == 0 && round == 23) {
-          g_cull_round[w * 64 + 0] = t_stop;
-          g_cull_round[w * 64 + 1] = tend;
-        }
-        if (b == 0 && lane == 0 && round < 256 && w == 1) {
-          g_iter[round * 16 + 3] = t_stop;
-          g_iter[round * 16 + 4] = tend;
-          g_iter[round * 16 + 5] = (unsigned long long)lag_at_stop | (tgrp << 16);
-          g_iter[round * 16 + 10] = tc0;
-        }
-      }
+      PN2_EV(0)
       PN2_STAMP(0)
       // end of the batch: this wave's exact maximum. A dirty cell is refreshed only if its
       // stale Tmax (an upper bound) exceeds the maximum of the exact ones; the others stay
@@ -537,11 +531,12 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
         }
       }
       if (lane == 0) swmax[w] = wmax;
+      PN2_EV(1)
       PN2_STAMP(1)
     }
     __syncthreads();  // B1: the batch is complete and applied; Tmax and counts are current
+    PN2_EV(2)
     PN2_STAMP(2)
-    PN2_TRACE(6, 0)
     // (cold wave 1 stored the batch's outputs group by group, so the barriers' s_waitcnt finds
     // at most the last group's stores outstanding)
     j += sj[rp] & (kEnd - 1);
@@ -575,13 +570,15 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
       }
       if (lane < NWIN) swcnt[w][lane] = lane == 0 ? c0 : lane == 1 ? c1 : lane == 2 ? c2 : c3;
     }
+    PN2_EV(3)
     PN2_STAMP(3)
     __syncthreads();  // B2: counts complete
+    PN2_EV(4)
     PN2_STAMP(4)
     // ---- choice: the lowest window threshold whose total count is in [1, K]. Lane
     // 16 i + v holds wave v's count above tau[i]; 16-lane row sums give the totals.
-    const int cvw = lane & (NW - 1), ciw = lane / NW;
-    const uint32_t cnt = swcnt[cvw][ciw];
+    const int cvw = lane & 15, ciw = lane >> 4;
+    const uint32_t cnt = cvw < NW ? swcnt[cvw][ciw] : 0u;
     uint32_t tot = cnt;
 #define PN2_ADD_DPP(C) tot += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)tot, C, 0xF, 0xF, false)
     PN2_ADD_DPP(kDppXor1);
@@ -590,12 +587,12 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
     PN2_ADD_DPP(kDppMirror);
 #undef PN2_ADD_DPP
     const uint64_t fit = __builtin_amdgcn_ballot_w64(cvw == 0 && tot >= 1u && tot <= (uint32_t)K);
-    const int ti = fit ? (int)__builtin_ctzll(fit) / NW : -1;
+    const int ti = fit ? (int)__builtin_ctzll(fit) >> 4 : -1;
     const bool stall = ti < 0;
     T = 0;
 #pragma unroll
     for (int i = 0; i < NWIN; ++i) T = ti == i ? tau[i] : T;
-    nh = stall ? 0 : __builtin_amdgcn_readlane((int)tot, ti * NW);
+    nh = stall ? 0 : __builtin_amdgcn_readlane((int)tot, ti * 16);
     int wbase = 0;  // this wave's first hot entry: the counts of the waves before it
     {
       uint32_t pre = ciw == ti && cvw < w ? cnt : 0u;
@@ -605,13 +602,12 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
       PN2_ADD_DPP(kDppHalfMirror);
       PN2_ADD_DPP(kDppMirror);
 #undef PN2_ADD_DPP
-      if (!stall) wbase = __builtin_amdgcn_readlane((int)pre, ti * NW);
+      if (!stall) wbase = __builtin_amdgcn_readlane((int)pre, ti * 16);
     }
     // next window: two below this choice (lower thresholds = bigger hot sets), or up; the next
     // thresholds scale with this round's maximum
     tlo = !stall ? min(max(tlo + ti - 2, 0), NT - NWIN) : min(tlo + NWIN, NT - NWIN);
     if (t == 0) sj[rp ^ 1] = 0;  // the next round's batch starts empty (last read in round - 1)
-    PN2_TRACE(7, 0)
     if (!stall) {
       if (cw >= 0) {
         // ---- hot set: every point above T, at this wave's offset
@@ -645,11 +641,17 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
       if (lane == 0) swk[w] = best;
       if constexpr (STAMP) ++n_stall;
     }
+    PN2_EV(5)
     PN2_STAMP(5)
-    PN2_TRACE(9, 1)
     __syncthreads();  // B3: hot set (or the per-wave argmax) complete
+    PN2_EV(6)
     PN2_STAMP(6)
-    PN2_TRACE(8, 0)
+    if constexpr (STAMP) {
+      if (b == 0 && lane == 0 && round < 64) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) g_cull_ev[(round * 16 + w) * 8 + k] = ev[k];
+      }
+    }
     if (stall) {
       uint64_t best = lane < NW ? swk[lane] : 0ull;
       best = uniform_u64(wave_max_u64(best));
@@ -670,7 +672,7 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
       if (t == 0) {
         scl[0] = make_float4(sxyz[3 * k], sxyz[3 * k + 1], sxyz[3 * k + 2], __int_as_float(k));
         asm volatile("" ::: "memory");
-        *(volatile int*)&sj[rp ^ 1] = 1 | kEnd;
+        __hip_atomic_store(&sj[rp ^ 1], 1 | kEnd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
     }
     hot_turn = !stall;
@@ -693,7 +695,6 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
       }
       if (w == 1) {
         g_cull_stats[b * 8 + 3] = n_pairs;
-        g_cull_stats[b * 8 + 6] = n_tail_cyc;
         g_cull_stats[b * 8 + 7] = n_tail_grp;
       }
       if (w == 2) g_cull_stats[b * 8 + 5] = n_pairs;
@@ -701,10 +702,10 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
   }
 }
 
-template <int NW, int PPT, int PRIO = 0>
+template <int NW, int PPT, int PRIO = 0, int HQ = 2>
 void launch_hotcull(const float* xyz, int B, int N, int M, int32_t* idx, float* nx, hipStream_t s) {
-  hipLaunchKernelGGL((fps_hotcull_kernel<NW, PPT, 8192, false, PRIO>), dim3(B), dim3(64 * NW), 0, s,
-                     xyz, N, M, idx, nx);
+  hipLaunchKernelGGL((fps_hotcull_kernel<NW, PPT, 8192, false, PRIO, HQ>), dim3(B),
+                     dim3(64 * NW), 0, s, xyz, N, M, idx, nx);
 }
 
 }  // namespace

@@ -1,5 +1,6 @@
 """bench.py's inputs that do not need a GPU: the committed PMC summary behind roofline.traffic,
-the static SA1 loop count behind roofline.valu, and the CPU baseline leg (a short sample)."""
+the committed stamp summary behind roofline.latency, and the CPU baseline leg (a short
+sample)."""
 import importlib.util
 import os
 
@@ -23,11 +24,12 @@ def test_pmc_traffic_of_the_sa1_sampler(bench):
     assert 1.0 <= traffic / algorithmic <= 1.2, (traffic, algorithmic)
 
 
-def test_valu_bound_of_the_sa1_sampler(bench):
-    v = bench.sa1_valu_bound("cfg2", 702.0)
-    assert v["floor_cycles_per_iteration"] == 4 * v["valu_instr_per_iteration"]
-    assert 0.3 < v["frac"] < 1.0
-    assert bench.sa1_valu_bound("cfg5", 1300.0) is None  # a different sampler instantiation
+def test_latency_of_the_sa1_sampler(bench):
+    v = bench.sa1_latency("cfg2", 0.47, 1024)
+    assert abs(v["ns_per_pick"] - 0.47e6 / 1023) < 1e-6
+    # the culled sampler's stamp summary: hot pick loop + per-round refreshes + setup
+    assert v["rounds"] > 0 and v["hot_cycles_per_pick"] > 0 and v["source"].endswith(".json")
+    assert "rounds" not in bench.sa1_latency("cfg5", 1.3, 512)  # a different sampler
 
 
 def test_cpu_baseline_leg(bench):

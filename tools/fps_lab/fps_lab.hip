@@ -2030,7 +2030,7 @@ int pn2_fps_cull_stamp(const float* xyz, int B, int N, int npoint, int32_t* idx,
                        unsigned long long* out_host, unsigned long long* stats_host) {
   hipStream_t s = 0;
   if (N > 8192) return PN2_EINVAL;
-  hipLaunchKernelGGL((pn2::fps_hotcull_kernel<16, 9, 8192, true, 3>), dim3(B), dim3(1024), 0, s, xyz, N,
+  hipLaunchKernelGGL((pn2::fps_hotcull_kernel<16, 9, 8192, true, 3, 4>), dim3(B), dim3(1024), 0, s, xyz, N,
                      npoint, idx, nullptr);
   hipError_t e = hipDeviceSynchronize();
   if (e != hipSuccess) return (int)e;
@@ -2046,11 +2046,8 @@ int pn2_fps_cull_stamp(const float* xyz, int B, int N, int npoint, int32_t* idx,
 int pn2_fps_cull_waves(unsigned long long* out_host) {
   return (int)hipMemcpyFromSymbol(out_host, HIP_SYMBOL(pn2::g_cull_wave), sizeof(unsigned long long) * 16 * 16 * 4);
 }
-int pn2_fps_cull_round(unsigned long long* out_host) {
-  return (int)hipMemcpyFromSymbol(out_host, HIP_SYMBOL(pn2::g_cull_round), sizeof(unsigned long long) * 16 * 64);
-}
-int pn2_fps_cull_trace(unsigned long long* out_host) {
-  return (int)hipMemcpyFromSymbol(out_host, HIP_SYMBOL(pn2::g_iter), sizeof(unsigned long long) * 4096);
+int pn2_fps_cull_events(unsigned long long* out_host) {
+  return (int)hipMemcpyFromSymbol(out_host, HIP_SYMBOL(pn2::g_cull_ev), sizeof(unsigned long long) * 64 * 16 * 8);
 }
 
 }  // extern "C"

@@ -1,7 +1,12 @@
 #!/usr/bin/env python3
-"""Diagnostic: phase cycles of the culled hot-set sampler (fps_cull_kernel, stamped lab build),
-B = 16 SA1 clouds, index-exact against the production v9 sampler: refreshes, stalls, applied
-(cell, centre) pairs, cycles per phase (wave 0 and the mean of the other waves)."""
+"""Diagnostic: phase cycles of the culled hot-set sampler (fps_hotcull_kernel, stamped lab
+build), B = 16 SA1 clouds, index-exact against the v9 sampler: refreshes, stalls, applied
+(cell, centre) pairs, cycles per phase (wave 0 and the mean of the other waves), per-wave
+group costs and the per-round event breakdown.
+
+    python tools/stamp_fps_cull.py [--json profiles/r2/sa1_cull_stamps.json]
+
+--json writes the ScanNet summary bench.py reports as roofline.latency."""
 import ctypes, importlib, json, os, sys
 import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -12,6 +17,11 @@ pkg = importlib.import_module(PKG_NAME)
 L = ctypes.CDLL(os.path.join(ROOT, "tools", "fps_lab", "libpn2fpslab.so"))
 L.pn2_fps_cull_stamp.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                  ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+import argparse
+ap = argparse.ArgumentParser()
+ap.add_argument("--json")
+ARGS = ap.parse_args()
+SUMMARY = {}
 NAMES = ["cold_async", "tmax", "B_A", "out_count", "B_B", "append", "B_C", "hot_setup"]
 dev = torch.device("cuda:0")
 lib = pkg._lib.lib()
@@ -45,36 +55,42 @@ for kind in ("scannet", "uniform"):
         "wave0": {n: round(v) for n, v in zip(NAMES, a[:, 0, :].mean(0))},
         "others": {n: round(v) for n, v in zip(NAMES, a[:, 1:, :].mean((0, 1)))},
     }), flush=True)
-# per-round timeline of cloud 0 (STAMP build, g_iter, cycles from the round's B2 of round 0):
-# hot phase start/end/picks, wave 1 round start / counts done / stop seen / loop end, wave 0
-# after B1 / after the choice / after B2, wave 1 before B2; wave 1 lag at stop, group cycles
-if hasattr(L, "pn2_fps_cull_trace"):
-    tr = np.zeros(4096, np.uint64)
-    L.pn2_fps_cull_trace.argtypes = [ctypes.c_void_p]
-    assert L.pn2_fps_cull_trace(tr.ctypes.data) == 0
-    r = tr.reshape(256, 16).astype(np.int64)
-    for i in list(range(0, 12)) + list(range(20, 26)):
-        base = r[i, 6]
-        rel = lambda v: int(v - base) if v else None
-        x = int(r[i, 5])
-        print(json.dumps({"round": i, "picks": int(r[i, 2]), "w0_B1": 0, "w0_choice": rel(r[i, 7]),
-                          "w1_pre_B2": rel(r[i, 9]), "w0_B2": rel(r[i, 8]),
-                          "next_w1_start": rel(r[i + 1, 10]), "next_w1_counts": rel(r[i + 1, 11]),
-                          "next_hot": [rel(r[i + 1, 0]), rel(r[i + 1, 1])], "next_picks": int(r[i + 1, 2]),
-                          "next_w1_stop_end": [rel(r[i + 1, 3]), rel(r[i + 1, 4])],
-                          "next_B1": rel(r[i + 1, 6]),
-                          "next_w1_lag": int(r[i + 1, 5]) & 0xFFFF, "next_w1_grp": (int(r[i + 1, 5]) >> 16) & 0xFFFF}), flush=True)
-    for i in (20, 21, 22, 23, 24, 25, 40):
-        base = r[i, 1]
-        ends = [int(v - base) for v in r[128 + i // 16][(i % 16):(i % 16) + 1]] if False else None
-        ends = [int(tr[2048 + i * 16 + v]) - int(r[i, 1]) if r[i, 1] else None for v in range(1, 16)]
-        print(json.dumps({"round": i, "picks": int(r[i, 2]), "cold_end_minus_hot_end": ends}), flush=True)
-    gaps = [int(r[i, 6] - r[i, 1]) for i in range(1, 60) if r[i, 2] > 0 and r[i, 6] > r[i, 1]]
-    nxt = [int(r[i + 1, 0] - r[i, 6]) for i in range(1, 60) if r[i + 1, 2] > 0 and r[i + 1, 0] > r[i, 6]]
-    picks = [int(r[i, 2]) for i in range(1, 60) if r[i, 2] > 0]
-    print(json.dumps({"hot_end_to_B1": gaps, "B1_to_next_hot": nxt, "picks": picks}), flush=True)
-    for i in range(20, 31):
-        ends = [int(tr[2048 + i * 16 + v]) for v in range(1, 16)]
-        he = int(r[i, 1])
-        print(json.dumps({"round": i, "picks": int(r[i, 2]), "cold_end_minus_hot_end": [e - he for e in ends],
-                          "B1_minus_hot_end": int(r[i, 6]) - he}), flush=True)
+# per-round events of cloud 0 (register-buffered, stored after each round's last barrier):
+# wave 0: [0] hot phase end; cold waves: [0] async loop end, [1] tail end; all: [2] after B1,
+# [3] before B2 (counts), [4] after B2, [5] before B3 (append), [6] after B3
+    L.pn2_fps_cull_events.argtypes = [ctypes.c_void_p]
+    evb = np.zeros(64 * 16 * 8, np.uint64)
+    assert L.pn2_fps_cull_events(evb.ctypes.data) == 0
+    E = evb.reshape(64, 16, 8).astype(np.int64)
+    rows = []
+    for r_ in range(2, 40):
+        h_end = E[r_, 0, 0]
+        if h_end == 0 or E[r_, 0, 2] == 0:
+            continue
+        cold_end = E[r_, 1:, 1].max()
+        rows.append({"hot_end_to_last_loop_end": int(E[r_, 1:, 0].max() - h_end),
+                     "tail_max": int((E[r_, 1:, 1] - E[r_, 1:, 0]).max()),
+                     "hot_end_to_last_cold": int(cold_end - h_end),
+                     "last_cold_to_B1": int(E[r_, 0, 2] - cold_end),
+                     "B1_to_B2": int(E[r_, 0, 4] - E[r_, 0, 2]),
+                     "count_max": int((E[r_, 1:, 3] - E[r_, 1:, 2]).max()),
+                     "B2_to_B3": int(E[r_, 0, 6] - E[r_, 0, 4]),
+                     "append_max": int((E[r_, 1:, 5] - E[r_, 1:, 4]).max()),
+                     "B3_to_next_hot_end": int(E[r_ + 1, 0, 0] - E[r_, 0, 6]) if E[r_ + 1, 0, 0] else None})
+    keys = rows[0].keys()
+    med = {k: float(np.median([r[k] for r in rows if r[k] is not None])) for k in keys}
+    print(json.dumps({"kind": kind, "median_per_round": med, "rounds": len(rows)}), flush=True)
+    if kind == "scannet":
+        setup = float(a[:, 1:, 7].mean())  # cold waves' phase 7 = setup only
+        hot_total = float(a[:, 0, 7].mean()) - setup
+        SUMMARY.update({
+            "workload": "B=16 ScanNet crops, 8192 -> 1024 (cfg2 SA1), stamped lab build",
+            "kernel_cycles": float(st[:, 0].mean()), "setup_cycles": setup,
+            "hot_cycles_per_pick": hot_total / float(st[:, 4].mean()),
+            "rounds": float(st[:, 1].mean()), "stalls": float(st[:, 2].mean()),
+            "round_cycles": (float(st[:, 0].mean()) - setup - hot_total) / float(st[:, 1].mean()),
+            "median_round_events": med})
+
+if ARGS.json:
+    with open(ARGS.json, "w") as f:
+        json.dump(SUMMARY, f, indent=1)
