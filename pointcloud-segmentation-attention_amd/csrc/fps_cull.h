@@ -133,7 +133,7 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
   static_assert(NW <= 16 && NWIN == 4, "choice: lane 16 i + v = (threshold i, wave v)");
   using f2 = float __attribute__((ext_vector_type(2)));
 
-  __shared__ float sxyz[3 * NPTS];
+  __shared__ __attribute__((aligned(16))) float sxyz[3 * NPTS];
   __shared__ int sperm[NPTS];         // sorted position -> point index
   __shared__ uint32_t shist[NBK];     // bucket counts, then offsets
   __shared__ float4 scell[2 * NCELL]; // cell boxes (lo, hi)
@@ -163,7 +163,14 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
   }
 
   // ---- setup: LDS copy, bounding box, counting sort by Morton bucket, cells -------------
-  for (int e = t; e < 3 * N; e += BLOCK) sxyz[e] = P[e];
+  if ((((uintptr_t)P) & 15) == 0) {  // 16 B per lane: one pass of wide coalesced loads
+    const int n4 = (3 * N) >> 2;
+    const float4* __restrict__ P4 = reinterpret_cast<const float4*>(P);
+    for (int e = t; e < n4; e += BLOCK) reinterpret_cast<float4*>(sxyz)[e] = P4[e];
+    for (int e = 4 * n4 + t; e < 3 * N; e += BLOCK) sxyz[e] = P[e];
+  } else {
+    for (int e = t; e < 3 * N; e += BLOCK) sxyz[e] = P[e];
+  }
   for (int e = t; e < NBK; e += BLOCK) shist[e] = 0u;
   if (t < NW * 4) swcnt[t / 4][t % 4] = 0u;
   __syncthreads();
