@@ -145,10 +145,15 @@ __global__ __launch_bounds__(kNNBlock) void three_nn_kernel(const float* __restr
 template <int BLOCK, bool LDS>
 __global__ __launch_bounds__(BLOCK) void three_nn_grid_kernel(
     const void* __restrict__ kgrid, int m, const void* __restrict__ ugrid,
-    const float* __restrict__ xyz1, int n, float* __restrict__ dist, int32_t* __restrict__ idx) {
+    const float* __restrict__ xyz1, int n, int B, float* __restrict__ dist,
+    int32_t* __restrict__ idx) {
   extern __shared__ float4 s_pts[];  // LDS: m sorted known points, then ncell+1 offsets
-  const int b = blockIdx.y;
-  const int i = blockIdx.x * BLOCK + threadIdx.x;
+  // logical block (cloud b, row block x), XCD-aware: the blocks of a cloud share one L2
+  const int R = (n + BLOCK - 1) / BLOCK;
+  const int Lg = xcd_block(blockIdx.x, R * B);
+  if (Lg >= R * B) return;
+  const int b = Lg / R;
+  const int i = (Lg - b * R) * BLOCK + threadIdx.x;
   const GridView g = grid_view(kgrid, b, m);
   const GridHdr& h = g.h;
   const float4* __restrict__ pts = g.pts;
@@ -296,14 +301,20 @@ __global__ __launch_bounds__(kNNBlock) void fp_fused_kernel(
     const float* __restrict__ pdist, const int32_t* __restrict__ pidx,
     const void* __restrict__ ugrid,
     const float* __restrict__ points1, int C1, const float* __restrict__ points2, int C2, int n,
-    int m, int cw, FastDiv div_cw, float* __restrict__ out) {
+    int m, int cw, FastDiv div_cw, int B, int Z, float* __restrict__ out) {
   using VecT = typename std::conditional<VEC == 4, float4, float>::type;
   __shared__ float4 sk[PRE ? 1 : kNNTile];
   __shared__ int4 s_idx[kNNRows];
   __shared__ float4 s_w[kNNRows];
   __shared__ int s_row[PRE ? kNNRows : 1];
-  const int b = blockIdx.y;
-  const int j0 = blockIdx.x * kNNRows;
+  // logical block (cloud b, channel slice z, row block x), XCD-aware: the blocks of a cloud
+  // share one L2, which then holds that cloud's points2 rows once
+  const int R = (n + kNNRows - 1) / kNNRows;
+  const int Lg = xcd_block(blockIdx.x, R * B * Z);
+  if (Lg >= R * B * Z) return;
+  const int b = Lg / (R * Z);
+  const int zb = (Lg - b * R * Z) / R;
+  const int j0 = (Lg - b * R * Z - zb * R) * kNNRows;
   if constexpr (PRE) {
     int jj = j0 + (int)threadIdx.x;
     if (threadIdx.x < kNNRows && jj < n) {
@@ -334,7 +345,7 @@ __global__ __launch_bounds__(kNNBlock) void fp_fused_kernel(
   __syncthreads();
   const int Cout = C2 + C1;             // floats
   const int c2v = C2 / VEC, coutv = Cout / VEC;
-  const int cb = blockIdx.z * cw;       // first vector column of this workgroup
+  const int cb = zb * cw;               // first vector column of this workgroup
   const int ce = min(coutv, cb + cw);
   if (ce <= cb) return;
   // element e -> (row e / cw, column cb + e % cw); the last channel slice can be narrower
@@ -401,11 +412,12 @@ int fp_launch(const float* xyz1, const float* xyz2, const float* pdist, const in
     zsplit *= 2;
   const int cw = (coutv + zsplit - 1) / zsplit;
   if ((long long)kNNRows * cw * cw >= (1LL << 32)) return PN2_EINVAL;
-  const dim3 grid(row_blocks, B, zsplit);
+  if ((long long)row_blocks * B * zsplit >= (1LL << 31) - 8) return PN2_EINVAL;
+  const dim3 grid(xcd_grid((long long)row_blocks * B * zsplit));
   const FastDiv div = make_fastdiv((uint32_t)cw);
 #define PN2_FP(V, P)                                                                           \
   hipLaunchKernelGGL((fp_fused_kernel<V, P>), grid, dim3(kNNBlock), 0, stream, xyz1, xyz2,    \
-                     pdist, pidx, ugrid, points1, C1, points2, C2, n, m, cw, div, out)
+                     pdist, pidx, ugrid, points1, C1, points2, C2, n, m, cw, div, B, zsplit, out)
   if (vec4) { if (pre) PN2_FP(4, true); else PN2_FP(4, false); }
   else { if (pre) PN2_FP(1, true); else PN2_FP(1, false); }
 #undef PN2_FP
@@ -520,16 +532,17 @@ int pn2_three_nn_grid(const void* known_grid, const void* unknown_grid, const fl
   if ((long long)B * n == 0) return PN2_OK;
   if (!known_grid || !dist || !idx || (!unknown_grid && !xyz1)) return PN2_EINVAL;
   constexpr int BLOCK = 256;
-  const dim3 grid((n + BLOCK - 1) / BLOCK, B);
+  if ((long long)((n + BLOCK - 1) / BLOCK) * B >= (1LL << 31) - 8) return PN2_EINVAL;
+  const dim3 grid(pn2::xcd_grid((long long)((n + BLOCK - 1) / BLOCK) * B));
   // an automatic-edge known grid has at most max(m, kAutoMinCells) cells (grid.h); an
   // explicit-edge one may have up to kGridCap and is read from global memory
   const size_t lds = (size_t)m * 16 + (size_t)(std::max(m, pn2::kAutoMinCells) + 1) * 4;
   if (lds <= 64 * 1024)
     hipLaunchKernelGGL((pn2::three_nn_grid_kernel<BLOCK, true>), grid, dim3(BLOCK), lds,
-                       (hipStream_t)stream, known_grid, m, unknown_grid, xyz1, n, dist, idx);
+                       (hipStream_t)stream, known_grid, m, unknown_grid, xyz1, n, B, dist, idx);
   else
     hipLaunchKernelGGL((pn2::three_nn_grid_kernel<BLOCK, false>), grid, dim3(BLOCK), 0,
-                       (hipStream_t)stream, known_grid, m, unknown_grid, xyz1, n, dist, idx);
+                       (hipStream_t)stream, known_grid, m, unknown_grid, xyz1, n, B, dist, idx);
   PN2_RETURN_LAUNCH();
 }
 
