@@ -133,7 +133,10 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
   static_assert(NW <= 16 && NWIN == 4, "choice: lane 16 i + v = (threshold i, wave v)");
   using f2 = float __attribute__((ext_vector_type(2)));
 
-  __shared__ __attribute__((aligned(16))) float sxyz[3 * NPTS];
+  // the cloud's coordinates: an LDS copy when it fits beside the rest (NPTS <= 8192),
+  // otherwise read from global memory (L2) -- only at setup and once per round
+  constexpr bool XYZ_LDS = NPTS <= 8192;
+  __shared__ __attribute__((aligned(16))) float sxyz[XYZ_LDS ? 3 * NPTS : 4];
   __shared__ int sperm[NPTS];         // sorted position -> point index
   __shared__ uint32_t shist[NBK];     // bucket counts, then offsets
   __shared__ float4 scell[2 * NCELL]; // cell boxes (lo, hi)
@@ -163,14 +166,17 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
   }
 
   // ---- setup: LDS copy, bounding box, counting sort by Morton bucket, cells -------------
-  if ((((uintptr_t)P) & 15) == 0) {  // 16 B per lane: one pass of wide coalesced loads
-    const int n4 = (3 * N) >> 2;
-    const float4* __restrict__ P4 = reinterpret_cast<const float4*>(P);
-    for (int e = t; e < n4; e += BLOCK) reinterpret_cast<float4*>(sxyz)[e] = P4[e];
-    for (int e = 4 * n4 + t; e < 3 * N; e += BLOCK) sxyz[e] = P[e];
-  } else {
-    for (int e = t; e < 3 * N; e += BLOCK) sxyz[e] = P[e];
+  if constexpr (XYZ_LDS) {
+    if ((((uintptr_t)P) & 15) == 0) {  // 16 B per lane: one pass of wide coalesced loads
+      const int n4 = (3 * N) >> 2;
+      const float4* __restrict__ P4 = reinterpret_cast<const float4*>(P);
+      for (int e = t; e < n4; e += BLOCK) reinterpret_cast<float4*>(sxyz)[e] = P4[e];
+      for (int e = 4 * n4 + t; e < 3 * N; e += BLOCK) sxyz[e] = P[e];
+    } else {
+      for (int e = t; e < 3 * N; e += BLOCK) sxyz[e] = P[e];
+    }
   }
+  const float* __restrict__ X = XYZ_LDS ? (const float*)sxyz : P;  // coordinates
   for (int e = t; e < NBK; e += BLOCK) shist[e] = 0u;
   if (t < NW * 4) swcnt[t / 4][t % 4] = 0u;
   __syncthreads();
@@ -179,8 +185,8 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
     for (int k = t; k < N; k += BLOCK) {
 #pragma unroll
       for (int a = 0; a < 3; ++a) {
-        mx[a] = fmaxf(mx[a], sxyz[3 * k + a]);
-        mn[a] = fmaxf(mn[a], -sxyz[3 * k + a]);
+        mx[a] = fmaxf(mx[a], X[3 * k + a]);
+        mn[a] = fmaxf(mn[a], -X[3 * k + a]);
       }
     }
 #pragma unroll
@@ -217,7 +223,7 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
       uint32_t c = 0;
 #pragma unroll
       for (int a = 0; a < 3; ++a) {
-        const int q = min(max((int)((sxyz[3 * k + a] - blo[a]) * bsc[a]), 0), 15);
+        const int q = min(max((int)((X[3 * k + a] - blo[a]) * bsc[a]), 0), 15);
 #pragma unroll
         for (int bit = 0; bit < 4; ++bit) c |= (uint32_t)((q >> bit) & 1) << (3 * bit + a);
       }
@@ -267,8 +273,8 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
         const int k = sperm[pos];
 #pragma unroll
         for (int a = 0; a < 3; ++a) {
-          lo3[a] = fminf(lo3[a], sxyz[3 * k + a]);
-          hi3[a] = fmaxf(hi3[a], sxyz[3 * k + a]);
+          lo3[a] = fminf(lo3[a], X[3 * k + a]);
+          hi3[a] = fmaxf(hi3[a], X[3 * k + a]);
         }
       }
     }
@@ -292,7 +298,7 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
     }
   }
   if (t == 0) {  // the first batch: centre 0 (tf_sampling_g.cu:121-125), already complete
-    scl[0] = make_float4(sxyz[0], sxyz[1], sxyz[2], __int_as_float(0));
+    scl[0] = make_float4(X[0], X[1], X[2], __int_as_float(0));
     sj[0] = 1 | kEnd;
     sj[1] = 0;
     for (int v = 0; v < NW; ++v) swmax[v] = -1;  // waves without cells keep -1
@@ -312,9 +318,9 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
       const int pos = (cw * PPT + s) * kWave + lane;
       const bool in = pos < N;
       const int k = in ? sperm[pos] : 0;
-      px[s] = sxyz[3 * k];
-      py[s] = sxyz[3 * k + 1];
-      pz[s] = sxyz[3 * k + 2];
+      px[s] = X[3 * k];
+      py[s] = X[3 * k + 1];
+      pz[s] = X[3 * k + 2];
       tb[s] = in ? __float_as_int(kInitTemp) : -1;
       Tm[s] = __builtin_amdgcn_ballot_w64(in) != 0 ? __float_as_int(kInitTemp) : -1;
     }
@@ -368,9 +374,9 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
         f2 hx[HP], hy[HP], hz[HP];
 #pragma unroll
         for (int q = 0; q < HQ; ++q) {
-          hx[q / 2][q % 2] = sxyz[3 * hk[q]];
-          hy[q / 2][q % 2] = sxyz[3 * hk[q] + 1];
-          hz[q / 2][q % 2] = sxyz[3 * hk[q] + 2];
+          hx[q / 2][q % 2] = X[3 * hk[q]];
+          hy[q / 2][q % 2] = X[3 * hk[q] + 1];
+          hz[q / 2][q % 2] = X[3 * hk[q] + 2];
         }
         const int lim = min(K, M - j);
         int jj = 0;
@@ -669,15 +675,15 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
         for (int e = j + t; e < M; e += BLOCK) {
           I[e] = k;
           if (NX) {
-            NX[3 * e] = sxyz[3 * k];
-            NX[3 * e + 1] = sxyz[3 * k + 1];
-            NX[3 * e + 2] = sxyz[3 * k + 2];
+            NX[3 * e] = X[3 * k];
+            NX[3 * e + 1] = X[3 * k + 1];
+            NX[3 * e + 2] = X[3 * k + 2];
           }
         }
         break;
       }
       if (t == 0) {
-        scl[0] = make_float4(sxyz[3 * k], sxyz[3 * k + 1], sxyz[3 * k + 2], __int_as_float(k));
+        scl[0] = make_float4(X[3 * k], X[3 * k + 1], X[3 * k + 2], __int_as_float(k));
         asm volatile("" ::: "memory");
         __hip_atomic_store(&sj[rp ^ 1], 1 | kEnd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
@@ -709,9 +715,9 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
   }
 }
 
-template <int NW, int PPT, int PRIO = 0, int HQ = 2>
+template <int NW, int PPT, int PRIO = 0, int HQ = 2, int NPTS = 8192>
 void launch_hotcull(const float* xyz, int B, int N, int M, int32_t* idx, float* nx, hipStream_t s) {
-  hipLaunchKernelGGL((fps_hotcull_kernel<NW, PPT, 8192, false, PRIO, HQ>), dim3(B),
+  hipLaunchKernelGGL((fps_hotcull_kernel<NW, PPT, NPTS, false, PRIO, HQ>), dim3(B),
                      dim3(64 * NW), 0, s, xyz, N, M, idx, nx);
 }
 
