@@ -114,7 +114,7 @@ PN2_DEV constexpr uint64_t cell_lanes(int s) {
 
 // NPTS points at most; wave 0 is the hot wave, waves 1..NW-1 hold the cold cells (PPT cells of
 // 64 sorted points per wave).
-template <int NW, int PPT, int NPTS, bool STAMP = false, int PRIO = 0, int HQ = 2>
+template <int NW, int PPT, int NPTS, bool STAMP = false, int PRIO = 0, int HQ = 2, int PPC = 1>
 __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __restrict__ xyz, int N,
                                                            int M, int32_t* __restrict__ idx,
                                                            float* __restrict__ new_xyz) {
@@ -128,7 +128,9 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
   constexpr int NBK = 4096;             // sort buckets (16^3 Morton)
   constexpr int kEnd = 1 << 16;         // sj flag: the batch is complete
   constexpr int SPT = (NPTS + BLOCK - 1) / BLOCK;  // setup: points per thread
-  static_assert(NCELL * kWave >= NPTS, "cold capacity");
+  static_assert(PPC == 1 || PPC == 2, "points per lane per cell");
+  constexpr int CP = kWave * PPC;        // points per cell
+  static_assert(NCELL * CP >= NPTS, "cold capacity");
   static_assert(PPT <= 32 && GRP >= 1, "slot masks");
   static_assert(NW <= 16 && NWIN == 4, "choice: lane 16 i + v = (threshold i, wave v)");
   using f2 = float __attribute__((ext_vector_type(2)));
@@ -265,9 +267,9 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
   // cell boxes: 8 lanes per cell, each folds 8 consecutive sorted points, then DPP within 8
   for (int c = t >> 3; c < NCELL; c += BLOCK / 8) {
     float lo3[3] = {INFINITY, INFINITY, INFINITY}, hi3[3] = {-INFINITY, -INFINITY, -INFINITY};
-    const int base = c * kWave + (t & 7) * 8;
+    const int base = c * CP + (t & 7) * (8 * PPC);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < 8 * PPC; ++i) {
       const int pos = base + i;
       if (pos < N) {
         const int k = sperm[pos];
@@ -305,9 +307,13 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
   }
   __syncthreads();
 
-  // cold registers: slot s of cold lane (cw, lane) = sorted position (cw * PPT + s) * 64 + lane
-  float px[PPT], py[PPT], pz[PPT];
-  int tb[PPT];
+  // cold registers: point h of cell s of cold lane (cw, lane) = sorted position
+  // (cw * PPT + s) * CP + h * 64 + lane, held at index s * PPC + h
+  float px[PPT * PPC], py[PPT * PPC], pz[PPT * PPC];
+  int tb[PPT * PPC];
+  auto spos = [&](int s, int h) { return (cw * PPT + s) * CP + h * kWave + lane; };
+  // a cell's maximum running min (every lane gets it)
+#define PN2_CELLMAX(s) wave_max_i32(PPC == 1 ? tb[(s) * PPC] : max(tb[(s) * PPC], tb[(s) * PPC + PPC - 1]))
   int Tm[PPT];  // exact max running min of each cell (wave-uniform), -1 = empty cell
   // group test: lane l tests cell (cw, l % PPT) against centre l / PPT of the group
   float4 glo = make_float4(INFINITY, INFINITY, INFINITY, 0.0f), ghi = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.0f);
@@ -315,14 +321,19 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
   if (cw >= 0) {
 #pragma unroll
     for (int s = 0; s < PPT; ++s) {
-      const int pos = (cw * PPT + s) * kWave + lane;
-      const bool in = pos < N;
-      const int k = in ? sperm[pos] : 0;
-      px[s] = X[3 * k];
-      py[s] = X[3 * k + 1];
-      pz[s] = X[3 * k + 2];
-      tb[s] = in ? __float_as_int(kInitTemp) : -1;
-      Tm[s] = __builtin_amdgcn_ballot_w64(in) != 0 ? __float_as_int(kInitTemp) : -1;
+      bool any = false;
+#pragma unroll
+      for (int h = 0; h < PPC; ++h) {
+        const int pos = spos(s, h);
+        const bool in = pos < N;
+        const int k = in ? sperm[pos] : 0;
+        px[s * PPC + h] = X[3 * k];
+        py[s * PPC + h] = X[3 * k + 1];
+        pz[s * PPC + h] = X[3 * k + 2];
+        tb[s * PPC + h] = in ? __float_as_int(kInitTemp) : -1;
+        any = any || __builtin_amdgcn_ballot_w64(in) != 0;
+      }
+      Tm[s] = any ? __float_as_int(kInitTemp) : -1;
     }
     if (lane < GRP * PPT) {
       glo = scell[2 * (cw * PPT + lane % PPT)];
@@ -339,8 +350,166 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
   int T = 0, nh = 0;        // the hot phase's threshold and hot-set size
   bool hot_turn = false;
   uint32_t dirty = 0;  // cold waves: cells whose Tmax is stale (an upper bound)
-  for (int round = 0; round <= M; ++round) {
-    if (w == 0) {
+  // One round's end, after the hot phase (wave 0) or the cold application (waves 1..): three
+  // barriers with the choice between them. Instantiated separately for the hot wave and the
+  // cold waves, so the hot wave's loop carries none of the cold waves' point registers.
+  auto round_end = [&](auto cold_tag, int round) -> bool {
+    constexpr bool COLD = decltype(cold_tag)::value;
+    __syncthreads();  // B1: the batch is complete and applied; Tmax and counts are current
+    PN2_EV(2)
+    PN2_STAMP(2)
+    // (cold wave 1 stored the batch's outputs group by group, so the barriers' s_waitcnt finds
+    // at most the last group's stores outstanding)
+    j += sj[rp] & (kEnd - 1);
+    if (j >= M) return true;
+    if constexpr (STAMP) ++n_refresh;
+    int top;
+    {
+      const int v = lane < NW ? swmax[lane] : -1;
+      top = __builtin_amdgcn_readfirstlane(wave_max_i32(v));
+    }
+    // ---- this round's thresholds (fractions of the exact maximum; every wave computes the
+    // same bits) and each wave's counts above them (cells at or below a threshold count 0)
+    int tau[NWIN];
+    {
+      const float tf = __int_as_float(max(top, 0));
+#pragma unroll
+      for (int i = 0; i < NWIN; ++i)
+        tau[i] = (int)uniform_u32((uint32_t)__float_as_int(tf * kCullFrac[tlo + i]));
+    }
+    if constexpr (COLD) {
+      uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+      static_assert(NWIN == 4, "four counters");
+#pragma unroll
+      for (int s = 0; s < PPT; ++s) {
+        if (Tm[s] > tau[0]) {
+#pragma unroll
+          for (int h = 0; h < PPC; ++h) {
+            const int e = s * PPC + h;
+            c0 += __builtin_popcountll(__builtin_amdgcn_ballot_w64(tb[e] > tau[0]));
+            c1 += __builtin_popcountll(__builtin_amdgcn_ballot_w64(tb[e] > tau[1]));
+            c2 += __builtin_popcountll(__builtin_amdgcn_ballot_w64(tb[e] > tau[2]));
+            c3 += __builtin_popcountll(__builtin_amdgcn_ballot_w64(tb[e] > tau[3]));
+          }
+        }
+      }
+      if (lane < NWIN) swcnt[w][lane] = lane == 0 ? c0 : lane == 1 ? c1 : lane == 2 ? c2 : c3;
+    }
+    PN2_EV(3)
+    PN2_STAMP(3)
+    __syncthreads();  // B2: counts complete
+    PN2_EV(4)
+    PN2_STAMP(4)
+    // ---- choice: the lowest window threshold whose total count is in [1, K]. Lane
+    // 16 i + v holds wave v's count above tau[i]; 16-lane row sums give the totals.
+    const int cvw = lane & 15, ciw = lane >> 4;
+    const uint32_t cnt = cvw < NW ? swcnt[cvw][ciw] : 0u;
+    uint32_t tot = cnt;
+#define PN2_ADD_DPP(C) tot += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)tot, C, 0xF, 0xF, false)
+    PN2_ADD_DPP(kDppXor1);
+    PN2_ADD_DPP(kDppXor2);
+    PN2_ADD_DPP(kDppHalfMirror);
+    PN2_ADD_DPP(kDppMirror);
+#undef PN2_ADD_DPP
+    const uint64_t fit = __builtin_amdgcn_ballot_w64(cvw == 0 && tot >= 1u && tot <= (uint32_t)K);
+    const int ti = fit ? (int)__builtin_ctzll(fit) >> 4 : -1;
+    const bool stall = ti < 0;
+    T = 0;
+#pragma unroll
+    for (int i = 0; i < NWIN; ++i) T = ti == i ? tau[i] : T;
+    nh = stall ? 0 : __builtin_amdgcn_readlane((int)tot, ti * 16);
+    int wbase = 0;  // this wave's first hot entry: the counts of the waves before it
+    {
+      uint32_t pre = ciw == ti && cvw < w ? cnt : 0u;
+#define PN2_ADD_DPP(C) pre += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)pre, C, 0xF, 0xF, false)
+      PN2_ADD_DPP(kDppXor1);
+      PN2_ADD_DPP(kDppXor2);
+      PN2_ADD_DPP(kDppHalfMirror);
+      PN2_ADD_DPP(kDppMirror);
+#undef PN2_ADD_DPP
+      if (!stall) wbase = __builtin_amdgcn_readlane((int)pre, ti * 16);
+    }
+    // next window: two below this choice (lower thresholds = bigger hot sets), or up; the next
+    // thresholds scale with this round's maximum
+    tlo = !stall ? min(max(tlo + ti - 2, 0), NT - NWIN) : min(tlo + NWIN, NT - NWIN);
+    if (t == 0) sj[rp ^ 1] = 0;  // the next round's batch starts empty (last read in round - 1)
+    if (!stall) {
+      if constexpr (COLD) {
+        // ---- hot set: every point above T, at this wave's offset
+        int base = wbase;
+#pragma unroll
+        for (int s = 0; s < PPT; ++s) {
+          if (Tm[s] > T) {
+#pragma unroll
+            for (int h = 0; h < PPC; ++h) {
+              const int e = s * PPC + h;
+              const uint64_t m = __builtin_amdgcn_ballot_w64(tb[e] > T);
+              const uint32_t below = __builtin_amdgcn_mbcnt_hi(
+                  (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+              if (tb[e] > T)
+                sh[base + (int)below] = make_uint2((uint32_t)tb[e], (uint32_t)sperm[spos(s, h)]);
+              base += __builtin_popcountll(m);
+            }
+          }
+        }
+      }
+    } else {
+      // ---- exact block argmax: (value desc, key asc) as one 64-bit max
+      uint64_t best = 0;
+      if constexpr (COLD) {
+#pragma unroll
+        for (int e = 0; e < PPT * PPC; ++e) {
+          const uint64_t v = tb[e] < 0 ? 0ull
+                                       : pack64(~cull_key(sperm[spos(e / PPC, e % PPC)]),
+                                                (uint32_t)tb[e] + 1u);
+          best = v > best ? v : best;
+        }
+        best = wave_max_u64(best);
+      }
+      if (lane == 0) swk[w] = best;
+      if constexpr (STAMP) ++n_stall;
+    }
+    PN2_EV(5)
+    PN2_STAMP(5)
+    __syncthreads();  // B3: hot set (or the per-wave argmax) complete
+    PN2_EV(6)
+    PN2_STAMP(6)
+    if constexpr (STAMP) {
+      if (b == 0 && lane == 0 && round < 64) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) g_cull_ev[(round * 16 + w) * 8 + k] = ev[k];
+      }
+    }
+    if (stall) {
+      uint64_t best = lane < NW ? swk[lane] : 0ull;
+      best = uniform_u64(wave_max_u64(best));
+      const uint32_t key = ~(uint32_t)best;
+      const int k = (int)((key >> 16) + ((key & 0xFFFFu) << 9));
+      if (top <= 0) {
+        // every running min is 0 and stays 0: each remaining pick is the same point
+        for (int e = j + t; e < M; e += BLOCK) {
+          I[e] = k;
+          if (NX) {
+            NX[3 * e] = X[3 * k];
+            NX[3 * e + 1] = X[3 * k + 1];
+            NX[3 * e + 2] = X[3 * k + 2];
+          }
+        }
+        return true;
+      }
+      if (t == 0) {
+        scl[0] = make_float4(X[3 * k], X[3 * k + 1], X[3 * k + 2], __int_as_float(k));
+        asm volatile("" ::: "memory");
+        __hip_atomic_store(&sj[rp ^ 1], 1 | kEnd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    }
+    hot_turn = !stall;
+    rp ^= 1;
+    PN2_STAMP(6)
+    return false;
+  };
+  if (w == 0) {
+    for (int round = 0; round <= M; ++round) {
       if (hot_turn) {
         // ---- hot phase: certified picks while the best hot value is above T, each one
         // published to the cold waves at once (scl[jj], then the count sj; DS operations of
@@ -443,7 +612,10 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
       }
       PN2_EV(0)
       PN2_STAMP(7)
-    } else if (cw >= 0) {
+      if (round_end(std::false_type{}, round)) break;
+    }
+  } else {
+    for (int round = 0; round <= M; ++round) {
       // ---- cold waves: apply the batch's centres as the hot wave publishes them, GRP at a
       // time (the last, short group after the end flag), culled by the box test against the
       // cells' Tmax (stale within the round = larger = still a valid bound). A touched cell is
@@ -491,11 +663,15 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
                 const float bx = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__float_as_int(cv.x), lb2));
                 const float by = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__float_as_int(cv.y), lb2));
                 const float bz = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__float_as_int(cv.z), lb2));
-                const f2 qx = {px[s], px[s]}, qy = {py[s], py[s]}, qz = {pz[s], pz[s]};
                 const f2 cx = {ax, bx}, cy = {ay, by}, cz = {az, bz};
-                const f2 dx = qx - cx, dy = qy - cy, dz = qz - cz;
-                const f2 d = (dx * dx + dy * dy) + dz * dz;
-                tb[s] = min(min(tb[s], __float_as_int(d.x)), __float_as_int(d.y));
+#pragma unroll
+                for (int h = 0; h < PPC; ++h) {
+                  const int e = s * PPC + h;
+                  const f2 qx = {px[e], px[e]}, qy = {py[e], py[e]}, qz = {pz[e], pz[e]};
+                  const f2 dx = qx - cx, dy = qy - cy, dz = qz - cz;
+                  const f2 d = (dx * dx + dy * dy) + dz * dz;
+                  tb[e] = min(min(tb[e], __float_as_int(d.x)), __float_as_int(d.y));
+                }
               }
               dirty |= 1u << s;
             }
@@ -516,7 +692,7 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
 #pragma unroll
           for (int s = 0; s < PPT; ++s) {
             if (s == s0) {
-              Tm[s] = __builtin_amdgcn_readfirstlane(wave_max_i32(tb[s]));
+              Tm[s] = __builtin_amdgcn_readfirstlane(PN2_CELLMAX(s));
               tmv = lane % PPT == s ? Tm[s] : tmv;
             }
           }
@@ -537,7 +713,7 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
 #pragma unroll
       for (int s = 0; s < PPT; ++s) {
         if ((dirty & (1u << s)) && Tm[s] > wmax) {
-          Tm[s] = __builtin_amdgcn_readfirstlane(wave_max_i32(tb[s]));
+          Tm[s] = __builtin_amdgcn_readfirstlane(PN2_CELLMAX(s));
           tmv = lane % PPT == s ? Tm[s] : tmv;
           dirty &= ~(1u << s);
           wmax = max(wmax, Tm[s]);
@@ -546,151 +722,8 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
       if (lane == 0) swmax[w] = wmax;
       PN2_EV(1)
       PN2_STAMP(1)
+      if (round_end(std::true_type{}, round)) break;
     }
-    __syncthreads();  // B1: the batch is complete and applied; Tmax and counts are current
-    PN2_EV(2)
-    PN2_STAMP(2)
-    // (cold wave 1 stored the batch's outputs group by group, so the barriers' s_waitcnt finds
-    // at most the last group's stores outstanding)
-    j += sj[rp] & (kEnd - 1);
-    if (j >= M) break;
-    if constexpr (STAMP) ++n_refresh;
-    int top;
-    {
-      const int v = lane < NW ? swmax[lane] : -1;
-      top = __builtin_amdgcn_readfirstlane(wave_max_i32(v));
-    }
-    // ---- this round's thresholds (fractions of the exact maximum; every wave computes the
-    // same bits) and each wave's counts above them (cells at or below a threshold count 0)
-    int tau[NWIN];
-    {
-      const float tf = __int_as_float(max(top, 0));
-#pragma unroll
-      for (int i = 0; i < NWIN; ++i)
-        tau[i] = (int)uniform_u32((uint32_t)__float_as_int(tf * kCullFrac[tlo + i]));
-    }
-    if (cw >= 0) {
-      uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
-      static_assert(NWIN == 4, "four counters");
-#pragma unroll
-      for (int s = 0; s < PPT; ++s) {
-        if (Tm[s] > tau[0]) {
-          c0 += __builtin_popcountll(__builtin_amdgcn_ballot_w64(tb[s] > tau[0]));
-          c1 += __builtin_popcountll(__builtin_amdgcn_ballot_w64(tb[s] > tau[1]));
-          c2 += __builtin_popcountll(__builtin_amdgcn_ballot_w64(tb[s] > tau[2]));
-          c3 += __builtin_popcountll(__builtin_amdgcn_ballot_w64(tb[s] > tau[3]));
-        }
-      }
-      if (lane < NWIN) swcnt[w][lane] = lane == 0 ? c0 : lane == 1 ? c1 : lane == 2 ? c2 : c3;
-    }
-    PN2_EV(3)
-    PN2_STAMP(3)
-    __syncthreads();  // B2: counts complete
-    PN2_EV(4)
-    PN2_STAMP(4)
-    // ---- choice: the lowest window threshold whose total count is in [1, K]. Lane
-    // 16 i + v holds wave v's count above tau[i]; 16-lane row sums give the totals.
-    const int cvw = lane & 15, ciw = lane >> 4;
-    const uint32_t cnt = cvw < NW ? swcnt[cvw][ciw] : 0u;
-    uint32_t tot = cnt;
-#define PN2_ADD_DPP(C) tot += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)tot, C, 0xF, 0xF, false)
-    PN2_ADD_DPP(kDppXor1);
-    PN2_ADD_DPP(kDppXor2);
-    PN2_ADD_DPP(kDppHalfMirror);
-    PN2_ADD_DPP(kDppMirror);
-#undef PN2_ADD_DPP
-    const uint64_t fit = __builtin_amdgcn_ballot_w64(cvw == 0 && tot >= 1u && tot <= (uint32_t)K);
-    const int ti = fit ? (int)__builtin_ctzll(fit) >> 4 : -1;
-    const bool stall = ti < 0;
-    T = 0;
-#pragma unroll
-    for (int i = 0; i < NWIN; ++i) T = ti == i ? tau[i] : T;
-    nh = stall ? 0 : __builtin_amdgcn_readlane((int)tot, ti * 16);
-    int wbase = 0;  // this wave's first hot entry: the counts of the waves before it
-    {
-      uint32_t pre = ciw == ti && cvw < w ? cnt : 0u;
-#define PN2_ADD_DPP(C) pre += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)pre, C, 0xF, 0xF, false)
-      PN2_ADD_DPP(kDppXor1);
-      PN2_ADD_DPP(kDppXor2);
-      PN2_ADD_DPP(kDppHalfMirror);
-      PN2_ADD_DPP(kDppMirror);
-#undef PN2_ADD_DPP
-      if (!stall) wbase = __builtin_amdgcn_readlane((int)pre, ti * 16);
-    }
-    // next window: two below this choice (lower thresholds = bigger hot sets), or up; the next
-    // thresholds scale with this round's maximum
-    tlo = !stall ? min(max(tlo + ti - 2, 0), NT - NWIN) : min(tlo + NWIN, NT - NWIN);
-    if (t == 0) sj[rp ^ 1] = 0;  // the next round's batch starts empty (last read in round - 1)
-    if (!stall) {
-      if (cw >= 0) {
-        // ---- hot set: every point above T, at this wave's offset
-        int base = wbase;
-#pragma unroll
-        for (int s = 0; s < PPT; ++s) {
-          if (Tm[s] > T) {
-            const uint64_t m = __builtin_amdgcn_ballot_w64(tb[s] > T);
-            const uint32_t below = __builtin_amdgcn_mbcnt_hi(
-                (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-            if (tb[s] > T)
-              sh[base + (int)below] =
-                  make_uint2((uint32_t)tb[s], (uint32_t)sperm[(cw * PPT + s) * kWave + lane]);
-            base += __builtin_popcountll(m);
-          }
-        }
-      }
-    } else {
-      // ---- exact block argmax: (value desc, key asc) as one 64-bit max
-      uint64_t best = 0;
-      if (cw >= 0) {
-#pragma unroll
-        for (int s = 0; s < PPT; ++s) {
-          const uint64_t v = tb[s] < 0 ? 0ull
-                                       : pack64(~cull_key(sperm[(cw * PPT + s) * kWave + lane]),
-                                                (uint32_t)tb[s] + 1u);
-          best = v > best ? v : best;
-        }
-        best = wave_max_u64(best);
-      }
-      if (lane == 0) swk[w] = best;
-      if constexpr (STAMP) ++n_stall;
-    }
-    PN2_EV(5)
-    PN2_STAMP(5)
-    __syncthreads();  // B3: hot set (or the per-wave argmax) complete
-    PN2_EV(6)
-    PN2_STAMP(6)
-    if constexpr (STAMP) {
-      if (b == 0 && lane == 0 && round < 64) {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) g_cull_ev[(round * 16 + w) * 8 + k] = ev[k];
-      }
-    }
-    if (stall) {
-      uint64_t best = lane < NW ? swk[lane] : 0ull;
-      best = uniform_u64(wave_max_u64(best));
-      const uint32_t key = ~(uint32_t)best;
-      const int k = (int)((key >> 16) + ((key & 0xFFFFu) << 9));
-      if (top <= 0) {
-        // every running min is 0 and stays 0: each remaining pick is the same point
-        for (int e = j + t; e < M; e += BLOCK) {
-          I[e] = k;
-          if (NX) {
-            NX[3 * e] = X[3 * k];
-            NX[3 * e + 1] = X[3 * k + 1];
-            NX[3 * e + 2] = X[3 * k + 2];
-          }
-        }
-        break;
-      }
-      if (t == 0) {
-        scl[0] = make_float4(X[3 * k], X[3 * k + 1], X[3 * k + 2], __int_as_float(k));
-        asm volatile("" ::: "memory");
-        __hip_atomic_store(&sj[rp ^ 1], 1 | kEnd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      }
-    }
-    hot_turn = !stall;
-    rp ^= 1;
-    PN2_STAMP(6)
   }
   if constexpr (STAMP) {
     if (lane == 0 && b < 16) {
@@ -715,9 +748,9 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
   }
 }
 
-template <int NW, int PPT, int PRIO = 0, int HQ = 2, int NPTS = 8192>
+template <int NW, int PPT, int PRIO = 0, int HQ = 2, int NPTS = 8192, int PPC = 1>
 void launch_hotcull(const float* xyz, int B, int N, int M, int32_t* idx, float* nx, hipStream_t s) {
-  hipLaunchKernelGGL((fps_hotcull_kernel<NW, PPT, NPTS, false, PRIO, HQ>), dim3(B),
+  hipLaunchKernelGGL((fps_hotcull_kernel<NW, PPT, NPTS, false, PRIO, HQ, PPC>), dim3(B),
                      dim3(64 * NW), 0, s, xyz, N, M, idx, nx);
 }
 
