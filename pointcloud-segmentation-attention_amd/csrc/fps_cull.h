@@ -54,7 +54,9 @@ PN2_DEV float wave_max_f32(float v) {
 
 // signed 32-bit max over the wave (every lane gets it): v_max_i32_dpp rows, permlane swaps
 PN2_DEV int wave_max_i32(int v) {
-#define PN2_IMAX_DPP(C) v = max(v, __builtin_amdgcn_update_dpp(v, v, C, 0xF, 0xF, false))
+// (old = 0: every lane has a valid source in these patterns, so the old value is never used,
+// and the move folds into v_max_i32_dpp)
+#define PN2_IMAX_DPP(C) v = max(v, __builtin_amdgcn_update_dpp(0, v, C, 0xF, 0xF, false))
   PN2_IMAX_DPP(kDppXor1);
   PN2_IMAX_DPP(kDppXor2);
   PN2_IMAX_DPP(kDppHalfMirror);
@@ -573,6 +575,8 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
             lk = bh ? (b23 ? hk[3] : hk[2]) : lk;
             ck = bh ? (b23 ? hkey[3] : hkey[2]) : ck;
           }
+          // the winner's coordinates are selected here, beside the reduction, not after it
+          asm volatile("" ::"v"(lx), "v"(ly), "v"(lz), "v"(lk));
           const int wm = __builtin_amdgcn_readfirstlane(wave_max_i32(cv));
           if (!(wm > T)) break;
           const uint64_t hold = __builtin_amdgcn_ballot_w64(cv == wm);
@@ -586,12 +590,7 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
           const float cx = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__float_as_int(lx), L));
           const float cy = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__float_as_int(ly), L));
           const float cz = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__float_as_int(lz), L));
-          const int cidx = __builtin_amdgcn_readlane(lk, L);
-          if (lane == 0) {
-            scl[jj] = make_float4(cx, cy, cz, __int_as_float(cidx));
-            asm volatile("" ::: "memory");
-            __hip_atomic_store(&sj[rp], jj + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          }
+          // the hot update first (the next pick depends on it), then the publishing stores
           const f2 c2x = {cx, cx}, c2y = {cy, cy}, c2z = {cz, cz};
 #pragma unroll
           for (int h = 0; h < HP; ++h) {
@@ -599,6 +598,13 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
             const f2 d = (dx * dx + dy * dy) + dz * dz;
             hv[2 * h] = min(hv[2 * h], __float_as_int(d.x));
             hv[2 * h + 1] = min(hv[2 * h + 1], __float_as_int(d.y));
+          }
+          const int cidx = __builtin_amdgcn_readlane(lk, L);
+          __builtin_amdgcn_sched_barrier(0);
+          if (lane == 0) {
+            scl[jj] = make_float4(cx, cy, cz, __int_as_float(cidx));
+            asm volatile("" ::: "memory");
+            __hip_atomic_store(&sj[rp], jj + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           }
         }
         if constexpr (PRIO > 0) __builtin_amdgcn_s_setprio(0);
