@@ -73,6 +73,28 @@ PN2_DEV int wave_max_i32(int v) {
   return v;
 }
 
+// signed 32-bit max over the wave, valid in lane 63 only: the DPP row reduction, then the
+// row broadcasts (row_bcast:15 into rows 1 and 3, row_bcast:31 into rows 2 and 3)
+PN2_DEV int wave_max_i32_l63(int v) {
+#define PN2_IMAX_DPP(C, R) v = max(v, __builtin_amdgcn_update_dpp(0, v, C, R, 0xF, false))
+  PN2_IMAX_DPP(kDppXor1, 0xF);
+  PN2_IMAX_DPP(kDppXor2, 0xF);
+  PN2_IMAX_DPP(kDppHalfMirror, 0xF);
+  PN2_IMAX_DPP(kDppMirror, 0xF);
+#undef PN2_IMAX_DPP
+  // the broadcasts leave the rows outside row_mask unwritten (dst == src), which the
+  // update_dpp builtin cannot express without an extra move: written directly, with the
+  // DPP read-after-VALU-write wait states spelled out
+  asm volatile(
+      "s_nop 1\n\t"
+      "v_max_i32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
+      "s_nop 1\n\t"
+      "v_max_i32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf\n\t"
+      "s_nop 1"
+      : "+v"(v));
+  return v;
+}
+
 // tie key: smaller = earlier in the reference's order (k mod 512, k div 512); N < 2^25
 PN2_DEV uint32_t cull_key(int k) { return ((uint32_t)(k & 511) << 16) | ((uint32_t)k >> 9); }
 
@@ -577,7 +599,7 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
           }
           // the winner's coordinates are selected here, beside the reduction, not after it
           asm volatile("" ::"v"(lx), "v"(ly), "v"(lz), "v"(lk));
-          const int wm = __builtin_amdgcn_readfirstlane(wave_max_i32(cv));
+          const int wm = __builtin_amdgcn_readlane(wave_max_i32_l63(cv), 63);
           if (!(wm > T)) break;
           const uint64_t hold = __builtin_amdgcn_ballot_w64(cv == wm);
           int L;
