@@ -291,18 +291,17 @@ __global__ __launch_bounds__(kBlock) void three_interp_grad_kernel(
 }
 
 // pointnet_fp_module geometry. Workgroup (x, b, z): unknown points [64x, 64x+64) of cloud b,
-// output channels [z*cw, (z+1)*cw) of the Cout = C2 + C1 concat row (in units of VEC floats).
+// columns [z*cw, (z+1)*cw) of the Cout = C2 + C1 concat row (V2- / V1-float columns).
 // PRE: the three neighbours come from a previous three_nn (pdist, pidx) instead of the scan;
 // with `ugrid` (a grid over the unknown points) the workgroup's 64 rows are 64 consecutive
 // points in cell order, so their neighbours' feature rows are shared through the caches.
-template <int VEC, bool PRE>
+template <int V2, int V1, bool PRE, int UN>
 __global__ __launch_bounds__(kNNBlock) void fp_fused_kernel(
     const float* __restrict__ xyz1, const float* __restrict__ xyz2,
     const float* __restrict__ pdist, const int32_t* __restrict__ pidx,
     const void* __restrict__ ugrid,
     const float* __restrict__ points1, int C1, const float* __restrict__ points2, int C2, int n,
     int m, int cw, FastDiv div_cw, int B, int Z, float* __restrict__ out) {
-  using VecT = typename std::conditional<VEC == 4, float4, float>::type;
   __shared__ float4 sk[PRE ? 1 : kNNTile];
   __shared__ int4 s_idx[kNNRows];
   __shared__ float4 s_w[kNNRows];
@@ -344,42 +343,110 @@ __global__ __launch_bounds__(kNNBlock) void fp_fused_kernel(
   }
   __syncthreads();
   const int Cout = C2 + C1;             // floats
-  const int c2v = C2 / VEC, coutv = Cout / VEC;
-  const int cb = zb * cw;               // first vector column of this workgroup
+  // columns: c2v interpolated ones of V2 floats, then c1v concat ones of V1 floats
+  const int c2v = C2 / V2, coutv = c2v + C1 / V1;
+  const int cb = zb * cw;               // first column of this workgroup
   const int ce = min(coutv, cb + cw);
   if (ce <= cb) return;
   // element e -> (row e / cw, column cb + e % cw); the last channel slice can be narrower
   // than cw (coutv % zsplit != 0), its surplus columns are skipped
   const int nrows = min(kNNRows, n - j0);
   const int elems = nrows * cw;
-  const VecT* P2 = reinterpret_cast<const VecT*>(points2 + (size_t)b * m * C2);
-  const VecT* P1 = reinterpret_cast<const VecT*>(points1 + (size_t)b * n * C1);
-  VecT* O = reinterpret_cast<VecT*>(out + (size_t)b * n * Cout);
-  for (int e = threadIdx.x; e < elems; e += kNNBlock) {
-    const int rl = (int)fdiv((uint32_t)e, div_cw);
-    const int c = cb + (e - rl * cw);
-    if (c >= ce) continue;
-    int r;
-    if constexpr (PRE) r = s_row[rl];
-    else r = j0 + rl;
-    VecT v;
-    if (c < c2v) {  // three_interpolate (tf_interpolate.cpp:119): ((p1*w1)+(p2*w2))+(p3*w3)
-      const int4 I = s_idx[rl];
-      const float4 W = s_w[rl];
-      const VecT a = P2[(size_t)I.x * c2v + c], bb = P2[(size_t)I.y * c2v + c],
-                 cc = P2[(size_t)I.z * c2v + c];
-      if constexpr (VEC == 4) {
-        v.x = (a.x * W.x + bb.x * W.y) + cc.x * W.z;
-        v.y = (a.y * W.x + bb.y * W.y) + cc.y * W.z;
-        v.z = (a.z * W.x + bb.z * W.y) + cc.z * W.z;
-        v.w = (a.w * W.x + bb.w * W.y) + cc.w * W.z;
-      } else {
-        v = (a * W.x + bb * W.y) + cc * W.z;
+  using V2T = typename std::conditional<V2 == 4, float4, float>::type;
+  using V1T = typename std::conditional<V1 == 4, float4, float>::type;
+  const V2T* P2 = reinterpret_cast<const V2T*>(points2 + (size_t)b * m * C2);
+  const float* P1 = points1 + (size_t)b * n * C1;
+  float* O = out + (size_t)b * n * Cout;
+  // U elements per thread in flight: every element's loads are issued before any element is
+  // combined, so a thread waits for one memory round trip per U elements (one per element
+  // made this loop latency-bound: 34 dependent trips per thread at Cout = 137).
+  constexpr int U = UN;
+  for (int e0 = threadIdx.x; e0 < elems; e0 += kNNBlock * U) {
+    V2T a[U], bb[U], cc[U];
+    V1T q[U];  // (both branches set every array: arrays set on one branch went to scratch)
+    float4 W[U];
+    bool cat[U], ok[U];
+    size_t o[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = e0 + u * kNNBlock;
+      const int rl = (int)fdiv((uint32_t)(e < elems ? e : e0), div_cw);
+      int c = cb + ((e < elems ? e : e0) - rl * cw);
+      ok[u] = e < elems && c < ce;
+      c = min(c, ce - 1);  // (a skipped element still loads from inside the rows)
+      int r;
+      if constexpr (PRE) r = s_row[rl];
+      else r = j0 + rl;
+      cat[u] = c >= c2v;
+      W[u] = s_w[rl];
+      if constexpr (V1 == V2) {
+        // one width: no branch; a concat element loads its points1 value three times (same
+        // address) and is selected as is
+        const int4 I = s_idx[rl];
+        const V2T* P1v = reinterpret_cast<const V2T*>(P1);
+        const V2T* pa = cat[u] ? P1v + (size_t)r * (C1 / V1) + (c - c2v) : P2 + (size_t)I.x * c2v + c;
+        const V2T* pb = cat[u] ? pa : P2 + (size_t)I.y * c2v + c;
+        const V2T* pc = cat[u] ? pa : P2 + (size_t)I.z * c2v + c;
+        a[u] = *pa;
+        bb[u] = *pb;
+        cc[u] = *pc;
+        q[u] = V1T{};
+        o[u] = (size_t)r * Cout + (size_t)c * V2;  // (C2 + (c - c2v) V1 = c V2 here)
+      } else if (!cat[u]) {
+        q[u] = V1T{};
+        const int4 I = s_idx[rl];
+        a[u] = P2[(size_t)I.x * c2v + c];
+        bb[u] = P2[(size_t)I.y * c2v + c];
+        cc[u] = P2[(size_t)I.z * c2v + c];
+        o[u] = (size_t)r * Cout + (size_t)c * V2;
+      } else {  // concat [interpolated, points1] (pointnet_util.py:226)
+        q[u] = *reinterpret_cast<const V1T*>(P1 + (size_t)r * C1 + (size_t)(c - c2v) * V1);
+        a[u] = bb[u] = cc[u] = V2T{};
+        o[u] = (size_t)r * Cout + C2 + (size_t)(c - c2v) * V1;
       }
-    } else {        // concat [interpolated, points1] (pointnet_util.py:226)
-      v = P1[(size_t)r * (C1 / VEC) + (c - c2v)];
     }
-    O[(size_t)r * coutv + c] = v;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (!ok[u]) continue;
+      if constexpr (V1 == V2) {
+        // three_interpolate (tf_interpolate.cpp:119): ((p1*w1)+(p2*w2))+(p3*w3), or the copy
+        // (selected per component: a select of whole float4 values went through scratch)
+        const bool k = cat[u];
+        if constexpr (V2 == 4) {
+          float4 v;
+          v.x = k ? a[u].x : (a[u].x * W[u].x + bb[u].x * W[u].y) + cc[u].x * W[u].z;
+          v.y = k ? a[u].y : (a[u].y * W[u].x + bb[u].y * W[u].y) + cc[u].y * W[u].z;
+          v.z = k ? a[u].z : (a[u].z * W[u].x + bb[u].z * W[u].y) + cc[u].z * W[u].z;
+          v.w = k ? a[u].w : (a[u].w * W[u].x + bb[u].w * W[u].y) + cc[u].w * W[u].z;
+          *reinterpret_cast<float4*>(O + o[u]) = v;
+        } else {
+          O[o[u]] = k ? a[u] : (a[u] * W[u].x + bb[u] * W[u].y) + cc[u] * W[u].z;
+        }
+        continue;
+      }
+      if (cat[u]) {
+        *reinterpret_cast<V1T*>(O + o[u]) = q[u];
+        continue;
+      }
+      // three_interpolate (tf_interpolate.cpp:119): ((p1*w1)+(p2*w2))+(p3*w3)
+      if constexpr (V2 == 4) {
+        float4 v;
+        v.x = (a[u].x * W[u].x + bb[u].x * W[u].y) + cc[u].x * W[u].z;
+        v.y = (a[u].y * W[u].x + bb[u].y * W[u].y) + cc[u].y * W[u].z;
+        v.z = (a[u].z * W[u].x + bb[u].z * W[u].y) + cc[u].z * W[u].z;
+        v.w = (a[u].w * W[u].x + bb[u].w * W[u].y) + cc[u].w * W[u].z;
+        if (V1 == 4 || (o[u] & 3) == 0) {  // 16 B aligned (always when C1 % 4 == 0)
+          *reinterpret_cast<float4*>(O + o[u]) = v;
+        } else {  // a row of odd width C2 + C1 starts off 16 B: four dword stores
+          O[o[u]] = v.x;
+          O[o[u] + 1] = v.y;
+          O[o[u] + 2] = v.z;
+          O[o[u] + 3] = v.w;
+        }
+      } else {
+        O[o[u]] = (a[u] * W[u].x + bb[u] * W[u].y) + cc[u] * W[u].z;
+      }
+    }
   }
 }
 
@@ -398,11 +465,11 @@ int fp_launch(const float* xyz1, const float* xyz2, const float* pdist, const in
               const void* ugrid, const float* points1, int C1, const float* points2, int C2,
               int B, int n, int m, float* out, hipStream_t stream) {
   const bool pre = pdist != nullptr;
-  const int Cout = C1 + C2;
-  const bool vec4 = (C1 % 4 == 0) && (C2 % 4 == 0) &&
-                    ((((uintptr_t)points1 | (uintptr_t)points2 | (uintptr_t)out) & 15) == 0);
-  const int VEC = vec4 ? 4 : 1;
-  const int coutv = Cout / VEC;
+  // interpolated columns of 4 floats when C2 % 4 == 0 (16 B aligned loads and, on rows that
+  // start 16 B aligned, stores); concat columns of 4 when C1 % 4 == 0 as well
+  const bool v2 = C2 % 4 == 0 && ((((uintptr_t)points2 | (uintptr_t)out) & 15) == 0);
+  const bool v1 = v2 && C1 % 4 == 0 && (((uintptr_t)points1 & 15) == 0);
+  const int coutv = C2 / (v2 ? 4 : 1) + C1 / (v1 ? 4 : 1);
   const int row_blocks = (n + kNNRows - 1) / kNNRows;
   // split the channels over grid.z until ~2 workgroups per CU, keeping >= 16 vector columns
   // per workgroup and (search variant) not re-running a long known-point scan too often
@@ -415,12 +482,23 @@ int fp_launch(const float* xyz1, const float* xyz2, const float* pdist, const in
   if ((long long)row_blocks * B * zsplit >= (1LL << 31) - 8) return PN2_EINVAL;
   const dim3 grid(xcd_grid((long long)row_blocks * B * zsplit));
   const FastDiv div = make_fastdiv((uint32_t)cw);
-#define PN2_FP(V, P)                                                                           \
-  hipLaunchKernelGGL((fp_fused_kernel<V, P>), grid, dim3(kNNBlock), 0, stream, xyz1, xyz2,    \
-                     pdist, pidx, ugrid, points1, C1, points2, C2, n, m, cw, div, B, zsplit, out)
-  if (vec4) { if (pre) PN2_FP(4, true); else PN2_FP(4, false); }
-  else { if (pre) PN2_FP(1, true); else PN2_FP(1, false); }
+  static const int unroll = [] {  // (PN2_FP_UNROLL: A/B knob of tools/bench_fp.py)
+    const char* e = getenv("PN2_FP_UNROLL");
+    return e ? atoi(e) : 0;
+  }();
+#define PN2_FP(V2, V1, P)                                                                      \
+  if (unroll == 1) PN2_FPU(V2, V1, P, 1);                                                      \
+  else if (unroll == 4) PN2_FPU(V2, V1, P, 4);                                                \
+  else PN2_FPU(V2, V1, P, 2)
+#define PN2_FPU(V2, V1, P, U)                                                                  \
+  hipLaunchKernelGGL((fp_fused_kernel<V2, V1, P, U>), grid, dim3(kNNBlock), 0, stream, xyz1,  \
+                     xyz2, pdist, pidx, ugrid, points1, C1, points2, C2, n, m, cw, div, B,     \
+                     zsplit, out)
+  if (v1) { if (pre) PN2_FP(4, 4, true); else PN2_FP(4, 4, false); }
+  else if (v2) { if (pre) PN2_FP(4, 1, true); else PN2_FP(4, 1, false); }
+  else { if (pre) PN2_FP(1, 1, true); else PN2_FP(1, 1, false); }
 #undef PN2_FP
+#undef PN2_FPU
   PN2_RETURN_LAUNCH();
 }
 

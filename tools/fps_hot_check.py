@@ -108,7 +108,7 @@ def main():
             assert rc == 0
             if r >= 2:
                 times[algo].append(e0.elapsed_time(e1))
-    out = {"sa1_B16_ms": {{0: "cull", 1: "v9", 6: "cull_k128"}.get(a, str(a)): {"median": statistics.median(v),
+    out = {"sa1_B16_ms": {{0: "cull", 1: "v9", 6: "cull_k128", 7: "cull_solo"}.get(a, str(a)): {"median": statistics.median(v),
                                                           "min": min(v)} for a, v in times.items()},
            "all_exact": ok}
     print(json.dumps(out), flush=True)

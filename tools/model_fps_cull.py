@@ -60,7 +60,9 @@ def box_lb(lo, hi, c):
         np.float32)
 
 
-def simulate(x, M, K, C, fracs):
+def simulate(x, M, K, C, fracs, ref_prev=False):
+    """ref_prev: thresholds are fractions of the previous round's threshold (or of the stall's
+    value) instead of the exact maximum, so each cold wave can count before the round's barrier"""
     n = len(x)
     order = np.argsort(morton(x), kind="stable")
     ncell = (n + C - 1) // C
@@ -74,6 +76,7 @@ def simulate(x, M, K, C, fracs):
     tmax = np.full(ncell, INIT, np.float32)
     picks, pending = [0], [0]
     st = dict(refresh=0, stall=0, pairs=0, pairs_full=0, hot_picks=0)
+    ref = np.float32(3e38)
     while len(picks) < M:
         st["refresh"] += 1
         for c in pending:  # cold pass with the box test against the stale cell maxima
@@ -86,9 +89,10 @@ def simulate(x, M, K, C, fracs):
         pending = []
         tmax = np.array([t[m].max() for m in members], np.float32)
         top = t.max()
+        base = ref if ref_prev else top
         tau = None
         for f in fracs:  # smallest threshold whose hot set fits
-            cand = np.float32(top * np.float32(f))
+            cand = np.float32(base * np.float32(f))
             if cand < top and np.count_nonzero(t > cand) <= K:
                 tau = cand
                 break
@@ -98,7 +102,9 @@ def simulate(x, M, K, C, fracs):
             p = int(cand[np.argmin(keys[cand])])
             picks.append(p)
             pending.append(p)
+            ref = top
             continue
+        ref = tau
         H = np.flatnonzero(t > tau)
         hv = t[H].copy()
         while len(picks) < M:
@@ -123,6 +129,7 @@ def main():
     ap.add_argument("--K", default="128")
     ap.add_argument("--cells", default="64,256,512")
     ap.add_argument("--kind", default="scannet")
+    ap.add_argument("--ref-prev", action="store_true")
     ap.add_argument("--fracs", default="0.5,0.7,0.8,0.85,0.9,0.93,0.95,0.97,0.98,0.99,0.995")
     a = ap.parse_args()
     pkg = importlib.import_module("pointcloud-segmentation-attention_amd")
@@ -132,7 +139,7 @@ def main():
         ref = fps_exact(x, a.M)
         for K in [int(v) for v in a.K.split(",")]:
             for C in [int(v) for v in a.cells.split(",")]:
-                p, st = simulate(x, a.M, K, C, fr)
+                p, st = simulate(x, a.M, K, C, fr, a.ref_prev)
                 st.update(cloud=cid, K=K, C=C, exact=bool(np.array_equal(p, ref)))
                 print(json.dumps(st), flush=True)
 
