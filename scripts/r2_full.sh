@@ -13,5 +13,5 @@ step pytest && timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeou
 && step pmc_fetch && timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $OUT/pmc_FETCH_SIZE_$TAG -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --e2e-steps 0 > $OUT/pmc_FETCH_SIZE_$TAG.log 2>&1 \
 && step pmc_write && timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $OUT/pmc_WRITE_SIZE_$TAG -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --e2e-steps 0 > $OUT/pmc_WRITE_SIZE_$TAG.log 2>&1 \
 && python3 tools/pmc_summary.py $OUT/pmc_FETCH_SIZE_$TAG $OUT/pmc_WRITE_SIZE_$TAG > $OUT/pmc_traffic_cfg2_B16.json \
-&& step stamps && timeout -k 10 120 python -u tools/stamp_fps_cull.py --json $OUT/sa1_cull_stamps.json > $OUT/stamp_cull_$TAG.log 2>&1 \
+&& step stamps && timeout -k 10 300 make -s -C tools/fps_lab > $OUT/lab_build.log 2>&1 && timeout -k 10 120 python -u tools/stamp_fps_cull.py --json $OUT/sa1_cull_stamps.json > $OUT/stamp_cull_$TAG.log 2>&1 \
 && echo "== done"
