@@ -621,12 +621,28 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
             hv[2 * h] = min(hv[2 * h], __float_as_int(d.x));
             hv[2 * h + 1] = min(hv[2 * h + 1], __float_as_int(d.y));
           }
-          const int cidx = __builtin_amdgcn_readlane(lk, L);
           __builtin_amdgcn_sched_barrier(0);
-          if (lane == 0) {
-            scl[jj] = make_float4(cx, cy, cz, __int_as_float(cidx));
-            asm volatile("" ::: "memory");
-            __hip_atomic_store(&sj[rp], jj + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          // publish from the winning lane itself (exec = lane L only): its lx, ly, lz, lk are
+          // the centre, so neither a readlane of the index nor moves of the SGPR copies into
+          // lane 0 are needed; the count follows the centre (DS operations of one wave
+          // execute in order)
+          {
+            const uint32_t a_c = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float4*)&scl[jj];
+            const uint32_t a_n = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) int*)&sj[rp];
+            uint64_t sv;
+            asm volatile(
+                "s_mov_b64 %[sv], exec\n\t"
+                "s_lshl_b64 exec, 1, %[L]\n\t"
+                "ds_write_b32 %[a], %[x]\n\t"
+                "ds_write_b32 %[a], %[y] offset:4\n\t"
+                "ds_write_b32 %[a], %[z] offset:8\n\t"
+                "ds_write_b32 %[a], %[k] offset:12\n\t"
+                "ds_write_b32 %[c], %[n]\n\t"
+                "s_mov_b64 exec, %[sv]"
+                : [sv] "=&s"(sv)
+                : [L] "s"(L), [a] "v"(a_c), [c] "v"(a_n), [x] "v"(lx), [y] "v"(ly), [z] "v"(lz),
+                  [k] "v"(lk), [n] "v"(jj + 1)
+                : "memory");
           }
         }
         if constexpr (PRIO > 0) __builtin_amdgcn_s_setprio(0);
