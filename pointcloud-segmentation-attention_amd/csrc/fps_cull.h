@@ -612,16 +612,6 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
           const float cx = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__float_as_int(lx), L));
           const float cy = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__float_as_int(ly), L));
           const float cz = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__float_as_int(lz), L));
-          // the hot update first (the next pick depends on it), then the publishing stores
-          const f2 c2x = {cx, cx}, c2y = {cy, cy}, c2z = {cz, cz};
-#pragma unroll
-          for (int h = 0; h < HP; ++h) {
-            const f2 dx = hx[h] - c2x, dy = hy[h] - c2y, dz = hz[h] - c2z;
-            const f2 d = (dx * dx + dy * dy) + dz * dz;
-            hv[2 * h] = min(hv[2 * h], __float_as_int(d.x));
-            hv[2 * h + 1] = min(hv[2 * h + 1], __float_as_int(d.y));
-          }
-          __builtin_amdgcn_sched_barrier(0);
           // publish from the winning lane itself (exec = lane L only): its lx, ly, lz, lk are
           // the centre, so neither a readlane of the index nor moves of the SGPR copies into
           // lane 0 are needed; the count follows the centre (DS operations of one wave
@@ -643,6 +633,16 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
                 : [L] "s"(L), [a] "v"(a_c), [c] "v"(a_n), [x] "v"(lx), [y] "v"(ly), [z] "v"(lz),
                   [k] "v"(lk), [n] "v"(jj + 1)
                 : "memory");
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          // the hot update (the next pick depends on it)
+          const f2 c2x = {cx, cx}, c2y = {cy, cy}, c2z = {cz, cz};
+#pragma unroll
+          for (int h = 0; h < HP; ++h) {
+            const f2 dx = hx[h] - c2x, dy = hy[h] - c2y, dz = hz[h] - c2z;
+            const f2 d = (dx * dx + dy * dy) + dz * dz;
+            hv[2 * h] = min(hv[2 * h], __float_as_int(d.x));
+            hv[2 * h + 1] = min(hv[2 * h + 1], __float_as_int(d.y));
           }
         }
         if constexpr (PRIO > 0) __builtin_amdgcn_s_setprio(0);
