@@ -332,10 +332,13 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
   __syncthreads();
 
   // cold registers: point h of cell s of cold lane (cw, lane) = sorted position
-  // (cw * PPT + s) * CP + h * 64 + lane, held at index s * PPC + h
+  // (s * NCW + cw) * CP + h * 64 + lane, held at index s * PPC + h: slot s of the cold waves
+  // is cells s * NCW ... s * NCW + NCW - 1 of the Morton order, so every wave's cells spread
+  // over the whole cloud and the waves get similar numbers of (cell, centre) pairs (with
+  // contiguous cells the wave holding the region being sampled lagged the others)
   float px[PPT * PPC], py[PPT * PPC], pz[PPT * PPC];
   int tb[PPT * PPC];
-  auto spos = [&](int s, int h) { return (cw * PPT + s) * CP + h * kWave + lane; };
+  auto spos = [&](int s, int h) { return (s * NCW + cw) * CP + h * kWave + lane; };
   // a cell's maximum running min (every lane gets it)
 #define PN2_CELLMAX(s) wave_max_i32(PPC == 1 ? tb[(s) * PPC] : max(tb[(s) * PPC], tb[(s) * PPC + PPC - 1]))
   int Tm[PPT];  // exact max running min of each cell (wave-uniform), -1 = empty cell
@@ -360,8 +363,8 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
       Tm[s] = any ? __float_as_int(kInitTemp) : -1;
     }
     if (lane < GRP * PPT) {
-      glo = scell[2 * (cw * PPT + lane % PPT)];
-      ghi = scell[2 * (cw * PPT + lane % PPT) + 1];
+      glo = scell[2 * ((lane % PPT) * NCW + cw)];
+      ghi = scell[2 * ((lane % PPT) * NCW + cw) + 1];
     }
 #pragma unroll
     for (int s = 0; s < PPT; ++s) tmv = lane % PPT == s ? Tm[s] : tmv;
