@@ -33,29 +33,54 @@ __global__ __launch_bounds__(kBlock) void group_concat_kernel(
     const float* __restrict__ new_xyz, const int32_t* __restrict__ idx, int N, int C, int M,
     int ns, int Cout, int layout, int rows, FastDiv div_cout, FastDiv div_ns, FastDiv div_m,
     uint32_t total_rows, float* __restrict__ grouped_xyz, float* __restrict__ out) {
+  // the tile's neighbour indices are staged in LDS first (one coalesced load per row), and a
+  // thread then issues the gathers of kU elements before it stores any: one element at a time
+  // made each element two dependent memory trips (idx, then the gather), latency-bound
+  constexpr int kU = 4;
+  __shared__ int s_idx[kTileElems];
   const uint32_t r0 = blockIdx.x * (uint32_t)rows;
   const int nrows = (int)min((uint32_t)rows, total_rows - r0);
   const int elems = nrows * Cout;
-  for (int e = threadIdx.x; e < elems; e += kBlock) {
-    const uint32_t rl = fdiv((uint32_t)e, div_cout);
-    const int c = e - (int)rl * Cout;
-    const uint32_t r = r0 + rl;         // row = (b*M + j)*ns + k
-    const uint32_t g = fdiv(r, div_ns);  // group = b*M + j
-    const uint32_t b = fdiv(g, div_m);
-    const int i = idx[r];
-    float v;
-    int cx = -1;  // xyz channel, or -1 for a feature channel
-    int cp = c;   // feature channel
-    if (layout == kXyzOnly) cx = c;
-    else if (layout == kXyzFirst) { if (c < 3) cx = c; else cp = c - 3; }
-    else if (layout == kXyzLast) { if (c >= C) cx = c - C; }
-    if (cx >= 0) {
-      v = xyz[((size_t)b * N + i) * 3 + cx] - new_xyz[(size_t)g * 3 + cx];  // pointnet_util.py:40
-      if (grouped_xyz) grouped_xyz[(size_t)r * 3 + cx] = v;
-    } else {
-      v = points[((size_t)b * N + i) * C + cp];
+  for (int rl = threadIdx.x; rl < nrows; rl += kBlock) s_idx[rl] = idx[r0 + rl];
+  __syncthreads();
+  for (int e0 = threadIdx.x; e0 < elems; e0 += kBlock * kU) {
+    float a[kU], d[kU];
+    int cxs[kU];
+    uint32_t rs[kU];
+    int cs[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int e = e0 + u * kBlock < elems ? e0 + u * kBlock : e0;  // (skipped below)
+      const uint32_t rl = fdiv((uint32_t)e, div_cout);
+      const int c = e - (int)rl * Cout;
+      const uint32_t r = r0 + rl;          // row = (b*M + j)*ns + k
+      const uint32_t g = fdiv(r, div_ns);  // group = b*M + j
+      const uint32_t b = fdiv(g, div_m);
+      const int i = s_idx[rl];
+      int cx = -1;  // xyz channel, or -1 for a feature channel
+      int cp = c;   // feature channel
+      if (layout == kXyzOnly) cx = c;
+      else if (layout == kXyzFirst) { if (c < 3) cx = c; else cp = c - 3; }
+      else if (layout == kXyzLast) { if (c >= C) cx = c - C; }
+      const float* pa = cx >= 0 ? xyz + ((size_t)b * N + i) * 3 + cx
+                                : points + ((size_t)b * N + i) * C + cp;
+      a[u] = *pa;
+      d[u] = 0.0f;
+      if (cx >= 0) d[u] = new_xyz[(size_t)g * 3 + cx];  // (feature lanes issue no load)
+      cxs[u] = cx;
+      rs[u] = r;
+      cs[u] = c;
     }
-    out[(size_t)r * Cout + c] = v;
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      if (e0 + u * kBlock >= elems) break;
+      float v = a[u];
+      if (cxs[u] >= 0) {
+        v = a[u] - d[u];  // pointnet_util.py:40
+        if (grouped_xyz) grouped_xyz[(size_t)rs[u] * 3 + cxs[u]] = v;
+      }
+      out[(size_t)rs[u] * Cout + cs[u]] = v;
+    }
   }
 }
 
