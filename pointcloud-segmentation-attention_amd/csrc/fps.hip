@@ -184,7 +184,7 @@ int fps_impl(const float* xyz, int B, int N, int M, int32_t* idx, float* nx, voi
   else if (N <= 2048) launch_v9<256, 8, 2, true>(xyz, B, N, M, idx, nx, s);
   else if (N <= 4096) launch_v9<256, 16, 4, true>(xyz, B, N, M, idx, nx, s);
   else if (N <= 8192) {
-    // culled hot-set sampler (fps_cull.h; 0.47 vs 0.71 ms at B = 16); the v9
+    // culled hot-set sampler (fps_cull.h; 0.40 vs 0.71 ms at B = 16); the v9
     // block-scan sampler stays selectable for A/B timing and parity cross-checks
     if (g_fps_algo == 1) launch_v9<256, 32, 4, true, false, PN2_SA1_PAD>(xyz, B, N, M, idx, nx, s);
     else if (g_fps_algo == 6) launch_hotcull<16, 9, 3, 2>(xyz, B, N, M, idx, nx, s);

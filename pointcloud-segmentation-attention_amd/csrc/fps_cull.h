@@ -11,7 +11,7 @@
 //    every step is monotone, so fl-dist(p, c) >= lb for every p in the box: a skipped
 //    (cell, centre) pair leaves every running min unchanged, exactly.
 //  * HOT SET. After each refresh the points above a threshold tau (the smallest of NT fractions
-//    of the global max whose count fits K = 128) form the hot set. Wave 0 picks from it alone:
+//    of the global max whose count fits K = 64 * HQ, 256 by default) form the hot set. Wave 0 picks from it alone:
 //    while its best value is > tau it beats every other point (they are all <= tau, and
 //    running mins only decrease), so it IS the reference's next centre; the wave updates the
 //    hot values and goes on -- no block-wide argmax per pick.
@@ -21,7 +21,7 @@
 //    fits (more than K points tie near the max), one exact block argmax picks the centre.
 // Exactness does not depend on the sort: any cell layout gives the same picks; the sort only
 // decides how much the box test skips (tools/model_fps_cull.py models it on the SA1 crops:
-// ~34 refreshes for 1,023 picks, ~93 % of (cell, centre) pairs skipped).
+// ~34 refreshes for 1,023 picks at K = 128; 25 measured at K = 256, ~93 % of (cell, centre) pairs skipped).
 #pragma once
 #include "fps_kernels.h"
 
