@@ -99,8 +99,19 @@ SAMPLER_CASES = [
 ]
 
 
-@pytest.mark.parametrize("algo", [0, 1, 6])
-@pytest.mark.parametrize("kind,B,N,M", SAMPLER_CASES)
+# MSG SA1-size clouds (8192 < N <= 16384, cfg5) run the culled sampler with its coordinates in
+# L2 (algo 0) or the v9 512 x 32 block scan (algo 1)
+MSG_SAMPLER_CASES = [
+    ("scannet", 8, 16384, 512), ("uniform", 2, 16384, 512), ("grid", 2, 16384, 1024),
+    ("grid", 1, 16384, 4000), ("dup", 1, 12000, 40), ("fewuniq", 2, 16384, 600),
+    ("scannet", 1, 8193, 8193), ("uniform", 1, 12000, 13000), ("scannet", 2, 16384, 1),
+    ("scannet", 2, 11111, 2000),
+]
+
+
+@pytest.mark.parametrize("algo,kind,B,N,M",
+                         [(a,) + c for a in (0, 1, 6) for c in SAMPLER_CASES]
+                         + [(a,) + c for a in (0, 1) for c in MSG_SAMPLER_CASES])
 def test_fps_sampler_schedules(env, algo, kind, B, N, M):
     pkg, O, torch, dev = env
     lib = pkg._lib.lib()

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """GPU A/B of the SA1 samplers (pn2_fps_set_algo: 0 = culled hot set, 1 = v9 block scan,
-6 = culled hot set without the priority boost):
+6 = culled hot set with 128 hot entries; --msg: the MSG SA1 size, 8192 < N <= 16384, where 0 is
+the culled sampler reading coordinates from L2 and 1 the v9 512 x 32 block scan):
 index-exact against the oracle and against each other on tie-heavy and ScanNet-like clouds,
 then HIP-event kernel times at the cfg2 SA1 shape (B = 16, 8192 -> 1024).
 
@@ -44,6 +45,9 @@ def main():
     ap.add_argument("--algo", type=int, default=0)
     ap.add_argument("--algos", default="1,0")
     ap.add_argument("--no-check", action="store_true")
+    ap.add_argument("--shape", default="16,8192,1024", help="B,N,M of the timed launch")
+    ap.add_argument("--msg", action="store_true",
+                    help="check the MSG SA1 size (8192 < N <= 16384) instead of the SA1 cases")
     args = ap.parse_args()
     import torch
     from conftest import PKG_NAME
@@ -67,6 +71,11 @@ def main():
              ("grid", 2, 8192, 4000), ("dup", 2, 5000, 40), ("fewuniq", 2, 8192, 600),
              ("scannet", 2, 4097, 4097), ("uniform", 2, 6000, 7000), ("scannet", 3, 8192, 2),
              ("scannet", 3, 8192, 1), ("scannet", 2, 7777, 1500)]
+    if args.msg:
+        cases = [("scannet", 8, 16384, 512), ("uniform", 2, 16384, 512), ("grid", 2, 16384, 1024),
+                 ("grid", 1, 16384, 4000), ("dup", 1, 12000, 40), ("fewuniq", 2, 16384, 600),
+                 ("scannet", 1, 8193, 8193), ("uniform", 1, 12000, 13000), ("scannet", 2, 16384, 1),
+                 ("scannet", 2, 11111, 2000)]
     if args.quick:
         cases = cases[:3]
     if args.no_check:
@@ -86,11 +95,12 @@ def main():
         first = int(np.argmax((i2 != ref).any(0))) if e2 else -1
         print(json.dumps({"case": [kind, B, N, M], "hot_idx_diff": e2, "v9_idx_diff": e1,
                           "hot_new_xyz_diff": nxe, "first_bad_j": first, "ok": good}), flush=True)
-    # timing at the cfg2 SA1 shape
-    x = cloud(pkg, "scannet", 16, 8192)
+    # timing at the given shape (default: the cfg2 SA1 shape)
+    TB, TN, TM = (int(v) for v in args.shape.split(","))
+    x = cloud(pkg, "scannet", TB, TN)
     xt = torch.from_numpy(x).to(dev)
-    idx = torch.empty((16, 1024), dtype=torch.int32, device=dev)
-    nx = torch.empty((16, 1024, 3), dtype=torch.float32, device=dev)
+    idx = torch.empty((TB, TM), dtype=torch.int32, device=dev)
+    nx = torch.empty((TB, TM, 3), dtype=torch.float32, device=dev)
     s = torch.cuda.current_stream()
     algos = [int(a) for a in args.algos.split(",")]
     times = {a: [] for a in algos}
@@ -99,7 +109,7 @@ def main():
             old = lib.pn2_fps_set_algo(algo)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(s)
-            rc = lib.pn2_fps_gather(ctypes.c_void_p(xt.data_ptr()), 16, 8192, 1024,
+            rc = lib.pn2_fps_gather(ctypes.c_void_p(xt.data_ptr()), TB, TN, TM,
                                     ctypes.c_void_p(idx.data_ptr()), ctypes.c_void_p(nx.data_ptr()),
                                     ctypes.c_void_p(s.cuda_stream))
             e1.record(s)
@@ -108,7 +118,8 @@ def main():
             assert rc == 0
             if r >= 2:
                 times[algo].append(e0.elapsed_time(e1))
-    out = {"sa1_B16_ms": {{0: "cull", 1: "v9", 6: "cull_k128", 7: "cull_solo"}.get(a, str(a)): {"median": statistics.median(v),
+    out = {"shape": [TB, TN, TM],
+           "ms": {{0: "default", 1: "v9", 6: "cull_k128", }.get(a, str(a)): {"median": statistics.median(v),
                                                           "min": min(v)} for a, v in times.items()},
            "all_exact": ok}
     print(json.dumps(out), flush=True)
