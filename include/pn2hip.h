@@ -103,9 +103,10 @@ int pn2_fps(const float* xyz, int B, int N, int npoint, int32_t* idx, pn2_stream
 int pn2_fps_gather(const float* xyz, int B, int N, int npoint, int32_t* idx, float* new_xyz,
                    pn2_stream_t stream);
 int pn2_fps_max_points(void);
-/* Sampler schedule for 4096 < N <= 8192 (process-wide; tests and A/B timing): 0 = the default
- * (culled hot-set sampler, 256 hot entries), 1 = the v9 block-scan sampler (one block argmax per
- * pick), 6 = the culled hot-set sampler with 128 hot entries. Identical outputs.
+/* Sampler schedule for 4096 < N <= 16384 (process-wide; tests and A/B timing): 0 = the default
+ * (culled hot-set sampler, 256 hot entries; coordinates in LDS up to 8192 points, in L2 above),
+ * 1 = the v9 block-scan sampler (one block argmax per pick), 6 = the culled hot-set sampler with
+ * 128 hot entries (N <= 8192 only). Identical outputs.
  * Returns the previous setting; other values only query. */
 int pn2_fps_set_algo(int algo);
 size_t pn2_fps_workspace_size(int B, int N);
