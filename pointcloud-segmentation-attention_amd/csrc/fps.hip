@@ -192,9 +192,9 @@ int fps_impl(const float* xyz, int B, int N, int M, int32_t* idx, float* nx, voi
   }
   else if (N <= kMaxRegPoints) {
     // MSG SA1 size (cfg5, 16384 -> 512): the culled sampler with coordinates read from L2 and
-    // two points per lane per cell (135 cells of 128 points): 0.42 vs 0.59 ms for v9 512 x 32
-    // at B = 8 (tools/fps_hot_check.py --msg, profiles/r2/fps_msg_ab.log), index-exact; it
-    // spills (128 VGPRs at 16 waves), and 12 waves (0.49 ms) or 8 waves (0.66 ms) spill more
+    // two points per lane per cell (135 cells of 128 points), the cold points' z in LDS: 0.33
+    // vs 0.59 ms for v9 512 x 32 at B = 8 (tools/fps_hot_check.py --msg,
+    // profiles/r2/fps_msg_ab.log), index-exact; 12 or 8 waves spill more (0.49, 0.66 ms)
     if (g_fps_algo == 1) launch_v9<512, 32, 4>(xyz, B, N, M, idx, nx, s);
     else launch_hotcull<16, 9, 3, 4, 16384, 2>(xyz, B, N, M, idx, nx, s);
   }

@@ -173,6 +173,11 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
   __shared__ int swmax[NW];
   __shared__ int sj[2];               // published centres of a batch | kEnd once complete (by round parity)
   __shared__ uint32_t swcnt[NW][4];   // per-wave counts above the round's thresholds
+  // without the LDS copy (NPTS > 8192) the cold points' z coordinates live in the freed LDS
+  // instead of VGPRs (at 16 waves the kernel is held to 128 VGPRs): lane-consecutive, so a
+  // cold wave's read of one slot is conflict-free
+  constexpr bool ZLDS = !XYZ_LDS;
+  __shared__ float scz[ZLDS ? NCW * PPT * PPC * kWave : 1];
 
   const int b = blockIdx.x;
   const int t = threadIdx.x, lane = t & (kWave - 1);
@@ -356,7 +361,8 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
         const int k = in ? sperm[pos] : 0;
         px[s * PPC + h] = X[3 * k];
         py[s * PPC + h] = X[3 * k + 1];
-        pz[s * PPC + h] = X[3 * k + 2];
+        if constexpr (ZLDS) scz[(cw * PPT * PPC + s * PPC + h) * kWave + lane] = X[3 * k + 2];
+        else pz[s * PPC + h] = X[3 * k + 2];
         tb[s * PPC + h] = in ? __float_as_int(kInitTemp) : -1;
         any = any || __builtin_amdgcn_ballot_w64(in) != 0;
       }
@@ -714,7 +720,8 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
 #pragma unroll
                 for (int h = 0; h < PPC; ++h) {
                   const int e = s * PPC + h;
-                  const f2 qx = {px[e], px[e]}, qy = {py[e], py[e]}, qz = {pz[e], pz[e]};
+                  const float zz = ZLDS ? scz[(cw * PPT * PPC + e) * kWave + lane] : pz[e];
+                  const f2 qx = {px[e], px[e]}, qy = {py[e], py[e]}, qz = {zz, zz};
                   const f2 dx = qx - cx, dy = qy - cy, dz = qz - cz;
                   const f2 d = (dx * dx + dy * dy) + dz * dz;
                   tb[e] = min(min(tb[e], __float_as_int(d.x)), __float_as_int(d.y));
