@@ -46,9 +46,12 @@
  *  - every buffer is a caller-owned DEVICE pointer, row-major, channel-last, contiguous;
  *    float = IEEE fp32, indices int32 — the reference's tensor dtypes;
  *  - every launch goes on `stream` (a hipStream_t; NULL = legacy default stream); nothing
- *    synchronises, nothing allocates, so every call can be captured into a hipGraph;
+ *    synchronises, nothing allocates on the device (the first sampler call pins one 4-byte
+ *    host word for device fault codes), so every call can be captured into a hipGraph;
  *  - return 0 on success, PN2_EINVAL (-22) for a shape/attribute error (where the reference
- *    raises InvalidArgument through OP_REQUIRES), or a positive hipError_t from the launch.
+ *    raises InvalidArgument through OP_REQUIRES), PN2_EFAULT (-14) when an earlier sampler
+ *    launch reported a device fault (pn2_fault_status), or a positive hipError_t from the
+ *    launch.
  */
 #ifndef PN2HIP_H
 #define PN2HIP_H
@@ -64,6 +67,17 @@ typedef void* pn2_stream_t; /* hipStream_t */
 
 #define PN2_OK 0
 #define PN2_EINVAL (-22)
+#define PN2_EFAULT (-14) /* an earlier launch stored a device fault code (pn2_fault_status)   */
+
+/* device fault codes (pn2_fault_status) */
+#define PN2_FAULT_FPS_POLL 1 /* culled sampler: a cold wave waited past its poll bound for
+                                 centres the hot wave never published; that launch's indices
+                                 are not trustworthy                                      */
+
+/* pn2_fps_gather_sched schedules (all give identical outputs) */
+#define PN2_FPS_AUTO 0           /* the library's choice by N (what pn2_fps* run)            */
+#define PN2_FPS_BLOCKSCAN 1      /* one block-wide argmax per pick (the v9 register sampler) */
+#define PN2_FPS_HOTCULL_K128 6   /* culled hot-set sampler with 128 hot entries, N <= 8192  */
 
 /* flags of pn2_group_concat / pn2_sample_and_group */
 #define PN2_USE_XYZ 1  /* concat the centred xyz with the grouped features (use_xyz=True)      */
@@ -103,12 +117,16 @@ int pn2_fps(const float* xyz, int B, int N, int npoint, int32_t* idx, pn2_stream
 int pn2_fps_gather(const float* xyz, int B, int N, int npoint, int32_t* idx, float* new_xyz,
                    pn2_stream_t stream);
 int pn2_fps_max_points(void);
-/* Sampler schedule for 4096 < N <= 16384 (process-wide; tests and A/B timing): 0 = the default
- * (culled hot-set sampler, 256 hot entries; coordinates in LDS up to 8192 points, in L2 above),
- * 1 = the v9 block-scan sampler (one block argmax per pick), 6 = the culled hot-set sampler with
- * 128 hot entries (N <= 8192 only). Identical outputs.
- * Returns the previous setting; other values only query. */
-int pn2_fps_set_algo(int algo);
+/* pn2_fps_gather with an explicit sampler schedule, per call (no process-wide state; used by
+ * the parity tests and A/B timing). PN2_FPS_AUTO = pn2_fps_gather; the other schedules exist
+ * only where the culled hot-set sampler is the default (4096 < N <= 16384;
+ * PN2_FPS_HOTCULL_K128 only up to N = 8192) and return PN2_EINVAL elsewhere. */
+int pn2_fps_gather_sched(const float* xyz, int B, int N, int npoint, int32_t* idx,
+                         float* new_xyz, int schedule, pn2_stream_t stream);
+/* The device fault word: 0, or the PN2_FAULT_* code a sampler launch stored (valid once that
+ * launch's stream has synchronised). clear != 0 resets it. The next pn2_fps* call also
+ * reports a stored fault, as PN2_EFAULT, and resets it. */
+int pn2_fault_status(int clear);
 size_t pn2_fps_workspace_size(int B, int N);
 int pn2_fps_ws(const float* xyz, int B, int N, int npoint, int32_t* idx, float* new_xyz,
                void* workspace, size_t workspace_bytes, pn2_stream_t stream);

@@ -40,7 +40,15 @@ LIB_PATH = _impl.LIB_PATH
 InvalidArgumentError = _impl.InvalidArgumentError
 Pn2RuntimeError = _impl.Pn2RuntimeError
 
-from . import ops  # noqa: E402
+
+
+def __getattr__(name):
+    """`pn2hip.ops` loads lazily: importing pn2hip must not require libpn2torch.so (the C ABI
+    and ctypes users do not need it); the first use of `ops` raises if it is missing."""
+    if name == "ops":
+        return importlib.import_module(f"{__name__}.ops")
+    raise AttributeError(f"module {__name__!r} has no attribute {name!r}")
+
 
 REFERENCE_NAMES = ("tf_sampling", "tf_grouping", "tf_interpolate", "pointnet_util", "tf_util",
                    "attention_layer")

@@ -16,6 +16,9 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PN2HIP_LIB") or os.path.join(_HERE, "libpn2hip.so")
 
 PN2_EINVAL = -22
+PN2_EFAULT = -14
+PN2_FAULT_FPS_POLL = 1
+PN2_FPS_AUTO, PN2_FPS_BLOCKSCAN, PN2_FPS_HOTCULL_K128 = 0, 1, 6
 PN2_USE_XYZ = 1
 PN2_XYZ_LAST = 2
 POOL_MODES = {"max": 0, "avg": 1, "weighted_avg": 2, "max_and_avg": 3}
@@ -48,7 +51,8 @@ SIGNATURES = {
     "pn2_fps": (_I, [_P, _I, _I, _I, _P, _P]),
     "pn2_fps_gather": (_I, [_P, _I, _I, _I, _P, _P, _P]),
     "pn2_fps_max_points": (_I, []),
-    "pn2_fps_set_algo": (_I, [_I]),
+    "pn2_fps_gather_sched": (_I, [_P, _I, _I, _I, _P, _P, _I, _P]),
+    "pn2_fault_status": (_I, [_I]),
     "pn2_prob_sample_workspace_size": (_S, [_I, _I]),
     "pn2_prob_sample": (_I, [_P, _P, _I, _I, _I, _P, _S, _P, _P]),
     "pn2_fps_workspace_size": (_S, [_I, _I]),
@@ -122,8 +126,21 @@ def check(rc, op):
         return
     if rc == PN2_EINVAL:
         raise InvalidArgumentError(f"{op}: invalid argument")
+    if rc == PN2_EFAULT:
+        raise Pn2RuntimeError(f"{op}: an earlier sampler launch reported a device fault "
+                              "(its indices are not trustworthy; see pn2_fault_status)")
     msg = lib().pn2_strerror(rc)
     raise Pn2RuntimeError(f"{op}: HIP error {rc}: {msg.decode() if msg else '?'}")
+
+
+def check_device_faults(device=None):
+    """Synchronise `device` and raise if a sampler launch stored a device fault code
+    (include/pn2hip.h pn2_fault_status); clears the code."""
+    torch.cuda.synchronize(device)
+    code = lib().pn2_fault_status(1)
+    if code:
+        raise Pn2RuntimeError(f"device fault {code} reported by a sampler launch "
+                              "(PN2_FAULT_FPS_POLL = 1: a cold wave's wait timed out)")
 
 
 def stream_of(t):

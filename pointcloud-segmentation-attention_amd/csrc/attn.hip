@@ -316,6 +316,8 @@ const char* pn2_version(void) { return "pn2hip 0.1 (gfx950)"; }
 const char* pn2_strerror(int status) {
   if (status == PN2_OK) return "ok";
   if (status == PN2_EINVAL) return "invalid argument (shape, attribute or null pointer)";
+  if (status == PN2_EFAULT)
+    return "device fault reported by an earlier sampler launch (see pn2_fault_status)";
   return hipGetErrorString((hipError_t)status);
 }
 

@@ -10,6 +10,8 @@
 // fps_v9_kernel in fps_kernels.h. gather_point is fused (thread 0 writes new_xyz,
 // pointnet_util.py:34). Clouds beyond kMaxRegPoints keep the running min in a caller-provided
 // workspace (fps_ws_kernel). Measured variants live in tools/fps_lab.
+#include <mutex>
+
 #include "fps_kernels.h"
 #include "fps_cull.h"
 
@@ -109,9 +111,38 @@ __global__ void gather_point_grad_kernel(const float* __restrict__ out_g,
 
 constexpr int kMaxRegPoints = 1024 * 16;
 
-// Sampler selection for 4096 < N <= 8192: 0 = default (culled hot set, 256 hot entries),
-// 1 = v9 block scan, 6 = culled hot set with 128 hot entries.
-int g_fps_algo = 0;
+// ---- device fault word ------------------------------------------------------------------
+// A kernel that finds a broken invariant (the culled sampler's cold waves waiting past their
+// poll bound, fps_cull.h) stores a PN2_FAULT_* code into one host-pinned, device-mapped word.
+// The host reads it without synchronising: the next pn2_fps* call reports it as PN2_EFAULT
+// (and clears it), and pn2_fault_status() returns it. Allocated at the first sampler launch
+// (never on a machine without a GPU); nullptr if that fails (then nothing is reported).
+std::once_flag g_fault_once;
+int* g_fault_host = nullptr;
+int* g_fault_dev = nullptr;
+
+int* fault_word_dev() {
+  std::call_once(g_fault_once, [] {
+    void* h = nullptr;
+    if (hipHostMalloc(&h, sizeof(int), hipHostMallocMapped | hipHostMallocPortable) != hipSuccess)
+      return;
+    *(volatile int*)h = 0;
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess) {
+      (void)hipHostFree(h);
+      return;
+    }
+    g_fault_host = (int*)h;
+    g_fault_dev = (int*)d;
+  });
+  return g_fault_dev;
+}
+
+// a fault stored by an earlier launch (visible once that launch's stream has synchronised)
+int take_fault() {
+  if (!g_fault_host) return 0;
+  return __atomic_exchange_n(g_fault_host, 0, __ATOMIC_ACQ_REL);
+}
 
 // ---- sampler chain: SA1..SAk's samplers of one cloud, stage 2.. in ONE workgroup -----------
 // The SSG stack samples 8192 -> 1024 -> 256 -> 64 -> 16, each stage from the previous stage's
@@ -165,8 +196,15 @@ __global__ __launch_bounds__(kChainBlock) void fps_chain_kernel(const float* __r
 }
 
 int fps_impl(const float* xyz, int B, int N, int M, int32_t* idx, float* nx, void* ws,
-             size_t ws_bytes, hipStream_t s) {
+             size_t ws_bytes, hipStream_t s, int sched = PN2_FPS_AUTO) {
   if (B < 0 || N < 0 || M <= 0 || (B > 0 && (!xyz || !idx))) return PN2_EINVAL;
+  // schedules other than AUTO exist only where the culled sampler runs (4096 < N <= 16384;
+  // the 128-entry variant up to 8192 points)
+  if (sched != PN2_FPS_AUTO && sched != PN2_FPS_BLOCKSCAN && sched != PN2_FPS_HOTCULL_K128)
+    return PN2_EINVAL;
+  if (sched != PN2_FPS_AUTO && (N <= 4096 || N > kMaxRegPoints)) return PN2_EINVAL;
+  if (sched == PN2_FPS_HOTCULL_K128 && N > 8192) return PN2_EINVAL;
+  if (take_fault()) return PN2_EFAULT;
   if (B == 0) return PN2_OK;
   if (N == 0) {
     const int total = B * M;
@@ -186,17 +224,20 @@ int fps_impl(const float* xyz, int B, int N, int M, int32_t* idx, float* nx, voi
   else if (N <= 8192) {
     // culled hot-set sampler (fps_cull.h; 0.40 vs 0.71 ms at B = 16); the v9
     // block-scan sampler stays selectable for A/B timing and parity cross-checks
-    if (g_fps_algo == 1) launch_v9<256, 32, 4, true, false, PN2_SA1_PAD>(xyz, B, N, M, idx, nx, s);
-    else if (g_fps_algo == 6) launch_hotcull<16, 9, 3, 2>(xyz, B, N, M, idx, nx, s);
-    else launch_hotcull<16, 9, 3, 4>(xyz, B, N, M, idx, nx, s);
+    if (sched == PN2_FPS_BLOCKSCAN)
+      launch_v9<256, 32, 4, true, false, PN2_SA1_PAD>(xyz, B, N, M, idx, nx, s);
+    else if (sched == PN2_FPS_HOTCULL_K128)
+      launch_hotcull<16, 9, 3, 2>(xyz, B, N, M, idx, nx, fault_word_dev(), s);
+    else
+      launch_hotcull<16, 9, 3, 4>(xyz, B, N, M, idx, nx, fault_word_dev(), s);
   }
   else if (N <= kMaxRegPoints) {
     // MSG SA1 size (cfg5, 16384 -> 512): the culled sampler with coordinates read from L2 and
     // two points per lane per cell (135 cells of 128 points), the cold points' z in LDS: 0.33
     // vs 0.59 ms for v9 512 x 32 at B = 8 (tools/fps_hot_check.py --msg,
     // profiles/r2/fps_msg_ab.log), index-exact; 12 or 8 waves spill more (0.49, 0.66 ms)
-    if (g_fps_algo == 1) launch_v9<512, 32, 4>(xyz, B, N, M, idx, nx, s);
-    else launch_hotcull<16, 9, 3, 4, 16384, 2>(xyz, B, N, M, idx, nx, s);
+    if (sched == PN2_FPS_BLOCKSCAN) launch_v9<512, 32, 4>(xyz, B, N, M, idx, nx, s);
+    else launch_hotcull<16, 9, 3, 4, 16384, 2>(xyz, B, N, M, idx, nx, fault_word_dev(), s);
   }
   else {
     if (!ws || ws_bytes < (size_t)B * N * sizeof(float)) return PN2_EINVAL;
@@ -212,10 +253,16 @@ extern "C" {
 
 int pn2_fps_max_points(void) { return pn2::kMaxRegPoints; }
 
-int pn2_fps_set_algo(int algo) {
-  const int old = pn2::g_fps_algo;
-  if (algo == 0 || algo == 1 || algo == 6) pn2::g_fps_algo = algo;
-  return old;
+int pn2_fault_status(int clear) {
+  if (!pn2::g_fault_host) return 0;
+  return clear ? __atomic_exchange_n(pn2::g_fault_host, 0, __ATOMIC_ACQ_REL)
+               : __atomic_load_n(pn2::g_fault_host, __ATOMIC_ACQUIRE);
+}
+
+int pn2_fps_gather_sched(const float* xyz, int B, int N, int npoint, int32_t* idx,
+                         float* new_xyz, int schedule, pn2_stream_t stream) {
+  return pn2::fps_impl(xyz, B, N, npoint, idx, new_xyz, nullptr, 0, (hipStream_t)stream,
+                       schedule);
 }
 
 int pn2_fps_chain(const float* xyz, int B, int N, int nstages, const int* npoint,

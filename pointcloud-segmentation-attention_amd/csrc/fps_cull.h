@@ -138,10 +138,19 @@ PN2_DEV constexpr uint64_t cell_lanes(int s) {
 
 // NPTS points at most; wave 0 is the hot wave, waves 1..NW-1 hold the cold cells (PPT cells of
 // 64 sorted points per wave).
+// The cold waves' wait for published centres is bounded (the hot wave always ends its batch,
+// so the bound is never reached in a correct run: ~0.1 s of polling against ~25 us per batch).
+// Reaching it stores PN2_FAULT_FPS_POLL into *fault (the host reports PN2_EFAULT); a build
+// with a tiny bound (csrc/Makefile target polltest) exercises that path.
+#ifndef PN2_FPS_POLL_LIMIT
+#define PN2_FPS_POLL_LIMIT (1 << 22)
+#endif
+
 template <int NW, int PPT, int NPTS, bool STAMP = false, int PRIO = 0, int HQ = 2, int PPC = 1>
 __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __restrict__ xyz, int N,
                                                            int M, int32_t* __restrict__ idx,
-                                                           float* __restrict__ new_xyz) {
+                                                           float* __restrict__ new_xyz,
+                                                           int* __restrict__ fault) {
   constexpr int BLOCK = 64 * NW;
   constexpr int NCW = NW - 1;  // cold waves
   constexpr int NCELL = NCW * PPT;
@@ -641,7 +650,7 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
                 : [sv] "=&s"(sv)
                 : [L] "s"(L), [a] "v"(a_c), [c] "v"(a_n), [x] "v"(lx), [y] "v"(ly), [z] "v"(lz),
                   [k] "v"(lk), [n] "v"(jj + 1)
-                : "memory");
+                : "memory", "scc");
           }
           __builtin_amdgcn_sched_barrier(0);
           // the hot update (the next pick depends on it)
@@ -677,7 +686,8 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
       int applied = 0;
       bool stop = false;
       unsigned long long tcnt0 = 0;
-      for (int it = 0; it < (1 << 22); ++it) {
+      int it = 0;
+      for (; it < PN2_FPS_POLL_LIMIT; ++it) {
         const int sv = __builtin_amdgcn_readfirstlane(
             __hip_atomic_load(&sj[rp], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
         const int av = sv & (kEnd - 1);
@@ -755,6 +765,8 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
         }
         if constexpr (STAMP) ++n_poll;
       }
+      if (it == PN2_FPS_POLL_LIMIT && fault && lane == 0)  // centres may be missing: report
+        __hip_atomic_store(fault, PN2_FAULT_FPS_POLL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       PN2_EV(0)
       PN2_STAMP(0)
       // end of the batch: this wave's exact maximum. A dirty cell is refreshed only if its
@@ -803,9 +815,10 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
 }
 
 template <int NW, int PPT, int PRIO = 0, int HQ = 2, int NPTS = 8192, int PPC = 1>
-void launch_hotcull(const float* xyz, int B, int N, int M, int32_t* idx, float* nx, hipStream_t s) {
+void launch_hotcull(const float* xyz, int B, int N, int M, int32_t* idx, float* nx, int* fault,
+                    hipStream_t s) {
   hipLaunchKernelGGL((fps_hotcull_kernel<NW, PPT, NPTS, false, PRIO, HQ, PPC>), dim3(B),
-                     dim3(64 * NW), 0, s, xyz, N, M, idx, nx);
+                     dim3(64 * NW), 0, s, xyz, N, M, idx, nx, fault);
 }
 
 }  // namespace

@@ -33,6 +33,8 @@ pn2_stream_t stream_of(const Tensor& t) {
 
 void check_rc(int rc, const char* op) {
   TORCH_CHECK_VALUE(rc != PN2_EINVAL, op, ": invalid argument");
+  TORCH_CHECK(rc != PN2_EFAULT, op, ": an earlier sampler launch reported a device fault ",
+              "(its indices are not trustworthy; see pn2_fault_status)");
   TORCH_CHECK(rc == 0, op, ": HIP error ", rc, ": ", pn2_strerror(rc));
 }
 
@@ -106,6 +108,30 @@ void chk_attn(const Tensor& Q, const Tensor& K, const Tensor& V) {
                         K.size(0) == Q.size(0) && K.size(1) == Q.size(1) && K.size(3) == Q.size(2),
                     "attn_reduce expects Q (B,M,C) and K, V (B,M,ns,C)");
   TORCH_CHECK_VALUE(Q.size(2) % 4 == 0, "attn_reduce expects C % 4 == 0 (key_dim 4)");
+}
+// fused group + centre + concat (pointnet_util.py:16-58 / :180-191): every tensor must agree
+// with xyz's batch and point count, or the kernel would index past idx, new_xyz or points
+void chk_group_concat(const Tensor& xyz, const std::optional<Tensor>& points,
+                      const Tensor& new_xyz, const Tensor& idx) {
+  TORCH_CHECK_VALUE(xyz.dim() == 3 && xyz.size(2) == 3 && new_xyz.dim() == 3 &&
+                        new_xyz.size(2) == 3 && idx.dim() == 3 && idx.size(1) == new_xyz.size(1),
+                    "group_concat expects xyz (B,N,3), new_xyz (B,M,3), idx (B,M,ns)");
+  TORCH_CHECK_VALUE(new_xyz.size(0) == xyz.size(0) && idx.size(0) == xyz.size(0),
+                    "group_concat expects xyz, new_xyz and idx with the same batch size");
+  if (points.has_value() && points->numel() > 0)
+    TORCH_CHECK_VALUE(points->dim() == 3 && points->size(0) == xyz.size(0) &&
+                          points->size(1) == xyz.size(1),
+                      "group_concat expects points (B,N,C) for xyz (B,N,3)");
+}
+// pooling over nsample (pointnet_util.py:130-145); weighted_avg needs grouped_xyz (B,M,ns,3)
+void chk_group_pool(const Tensor& x, const std::optional<Tensor>& gxyz, int64_t mode) {
+  TORCH_CHECK_VALUE(x.dim() == 4, "group_pool expects (B,M,ns,C) x");
+  TORCH_CHECK_VALUE(mode >= PN2_POOL_MAX && mode <= PN2_POOL_MAX_AND_AVG, "group_pool: unknown mode");
+  if (mode == PN2_POOL_WEIGHTED_AVG)
+    TORCH_CHECK_VALUE(gxyz.has_value() && gxyz->dim() == 4 && gxyz->size(0) == x.size(0) &&
+                          gxyz->size(1) == x.size(1) && gxyz->size(2) == x.size(2) &&
+                          gxyz->size(3) == 3,
+                      "group_pool weighted_avg needs grouped_xyz (B,M,ns,3)");
 }
 
 // Clouds / query batches at least this large take the spatial grid (identical results;
@@ -267,9 +293,7 @@ Tensor group_point_grad_hip(const Tensor& points, const Tensor& idx_, const Tens
 std::tuple<Tensor, Tensor> group_concat_hip(const Tensor& xyz_, const std::optional<Tensor>& points_,
                                             const Tensor& new_xyz_, const Tensor& idx_, bool use_xyz,
                                             bool xyz_last) {
-  TORCH_CHECK_VALUE(xyz_.dim() == 3 && xyz_.size(2) == 3 && new_xyz_.dim() == 3 &&
-                        new_xyz_.size(2) == 3 && idx_.dim() == 3 && idx_.size(1) == new_xyz_.size(1),
-                    "group_concat expects xyz (B,N,3), new_xyz (B,M,3), idx (B,M,ns)");
+  chk_group_concat(xyz_, points_, new_xyz_, idx_);
   Tensor xyz = dev(xyz_, "xyz", at::kFloat), new_xyz = dev(new_xyz_, "new_xyz", at::kFloat);
   Tensor idx = dev(idx_, "idx", at::kInt);
   Tensor points;
@@ -395,15 +419,10 @@ std::tuple<Tensor, Tensor, Tensor> attn_reduce_grad_hip(const Tensor& Q_, const 
 }
 
 Tensor group_pool_hip(const Tensor& x_, const std::optional<Tensor>& gxyz_, int64_t mode) {
-  TORCH_CHECK_VALUE(x_.dim() == 4, "group_pool expects (B,M,ns,C) x");
-  TORCH_CHECK_VALUE(mode >= PN2_POOL_MAX && mode <= PN2_POOL_MAX_AND_AVG, "group_pool: unknown mode");
+  chk_group_pool(x_, gxyz_, mode);
   Tensor x = dev(x_, "x", at::kFloat);
   Tensor gxyz;
-  if (mode == PN2_POOL_WEIGHTED_AVG) {
-    TORCH_CHECK_VALUE(gxyz_.has_value() && gxyz_->dim() == 4 && gxyz_->size(3) == 3,
-                      "group_pool weighted_avg needs grouped_xyz (B,M,ns,3)");
-    gxyz = dev(*gxyz_, "grouped_xyz", at::kFloat);
-  }
+  if (mode == PN2_POOL_WEIGHTED_AVG) gxyz = dev(*gxyz_, "grouped_xyz", at::kFloat);
   c10::hip::HIPGuard g(x.device().index());
   const int B = I(x.size(0)), M = I(x.size(1)), ns = I(x.size(2)), C = I(x.size(3));
   Tensor out = at::empty({B, M, mode == PN2_POOL_MAX_AND_AVG ? 2 * C : C}, f32(x));
@@ -461,8 +480,9 @@ Tensor group_point_grad_meta(const Tensor& points, const Tensor& idx, const Tens
   return at::empty(points.sizes(), mf(grad_out));
 }
 std::tuple<Tensor, Tensor> group_concat_meta(const Tensor& xyz, const std::optional<Tensor>& points,
-                                             const Tensor&, const Tensor& idx, bool use_xyz,
-                                             bool) {
+                                             const Tensor& new_xyz, const Tensor& idx,
+                                             bool use_xyz, bool) {
+  chk_group_concat(xyz, points, new_xyz, idx);
   const bool has = points.has_value() && points->numel() > 0;
   const int64_t C = has ? points->size(2) : 0;
   const int64_t cout = !has ? 3 : (use_xyz ? C + 3 : C);
@@ -502,8 +522,8 @@ std::tuple<Tensor, Tensor, Tensor> attn_reduce_grad_meta(const Tensor& Q, const 
   chk_attn(Q, K, V);
   return {at::empty(Q.sizes(), mf(Q)), at::empty(K.sizes(), mf(K)), at::empty(V.sizes(), mf(V))};
 }
-Tensor group_pool_meta(const Tensor& x, const std::optional<Tensor>&, int64_t mode) {
-  TORCH_CHECK_VALUE(x.dim() == 4, "group_pool expects (B,M,ns,C) x");
+Tensor group_pool_meta(const Tensor& x, const std::optional<Tensor>& gxyz, int64_t mode) {
+  chk_group_pool(x, gxyz, mode);
   return at::empty({x.size(0), x.size(1), mode == PN2_POOL_MAX_AND_AVG ? 2 * x.size(3) : x.size(3)},
                    mf(x));
 }

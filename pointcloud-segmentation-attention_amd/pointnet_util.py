@@ -145,11 +145,14 @@ def group_pool(new_points, pooling="max", grouped_xyz=None):
     return out
 
 
-def fp_interpolate(xyz1, xyz2, points1, points2, known_grid=None, unknown_grid=None):
+def fp_interpolate(xyz1, xyz2, points1, points2, known_grid=None, unknown_grid=None,
+                   return_nn=False):
     """Geometry of pointnet_fp_module (pointnet_util.py:218-228), before its MLP:
     three_nn, IDW weights, three_interpolate and concat [interpolated, points1].
     Returns (B, n, C2 + C1). known_grid / unknown_grid: optional grid.PointGrid over xyz2 /
-    xyz1 for the neighbour search (built here when the search is large)."""
+    xyz1 for the neighbour search (built here when the search is large).
+    return_nn: also return the three_nn (dist, idx) the layer used, or None when the search
+    ran fused inside the interpolation kernel (pn2_fp_fused keeps them in registers)."""
     xyz1 = device_tensor(xyz1, "xyz1", torch.float32)
     xyz2 = device_tensor(xyz2, "xyz2", torch.float32)
     points2 = device_tensor(points2, "points2", torch.float32)
@@ -157,7 +160,8 @@ def fp_interpolate(xyz1, xyz2, points1, points2, known_grid=None, unknown_grid=N
         dist, idx = tf_interpolate.three_nn(xyz1, xyz2, known_grid, unknown_grid)
         weight = tf_interpolate.idw_weights(dist)
         interp = tf_interpolate.three_interpolate(points2, idx, weight)
-        return interp if points1 is None else torch.cat([interp, points1], dim=2)
+        out = interp if points1 is None else torch.cat([interp, points1], dim=2)
+        return (out, (dist, idx)) if return_nn else out
     B, n, m = int(xyz1.shape[0]), int(xyz1.shape[1]), int(xyz2.shape[1])
     C2 = int(points2.shape[2])
     if points1 is not None:
@@ -166,16 +170,18 @@ def fp_interpolate(xyz1, xyz2, points1, points2, known_grid=None, unknown_grid=N
     else:
         C1 = 0
     out = torch.empty((B, n, C2 + C1), dtype=torch.float32, device=xyz1.device)
+    nn = None
     if known_grid is not None or tf_interpolate.use_grid(n, m):
         dist, idx = tf_interpolate.three_nn(xyz1, xyz2, known_grid, unknown_grid)
         check(lib().pn2_fp_apply(ptr(dist), ptr(idx),
                                  None if unknown_grid is None else ptr(unknown_grid.buf),
                                  ptr(points1), C1, ptr(points2), C2, B, n, m, ptr(out),
                                  stream_of(xyz1)), "fp_interpolate")
+        nn = (dist, idx)
     else:
         check(lib().pn2_fp_fused(ptr(xyz1), ptr(xyz2), ptr(points1), C1, ptr(points2), C2, B, n,
                                  m, ptr(out), stream_of(xyz1)), "fp_interpolate")
-    return out
+    return (out, nn) if return_nn else out
 
 
 # ---------------------------------------------------------------- whole SA / FP layers -----

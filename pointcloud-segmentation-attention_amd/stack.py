@@ -196,6 +196,7 @@ class Step:
         fp_feat = [inp["sa_out"][3]] + list(inp["fp_out"])
         v["xyz"] = [inp["xyz"], None, None, None, None]
         v["sa"], v["fp"] = [None] * 4, [None] * 4
+        v["bq"], v["nn"] = [None] * 4, [None] * 4  # kept for the parity tests (intermediates())
         tasks = []
         if big:  # the SA1 grid over the input cloud (also orders FP4's neighbour search)
             tasks.append(Task("grid1", 1, (), lambda: v.__setitem__(
@@ -213,6 +214,7 @@ class Step:
                 xyz, new_xyz = v["xyz"][i], v["xyz"][i + 1]
                 idx, _ = tf_grouping.query_ball_point(radius, nsample, xyz, new_xyz,
                                                       grid=v.get("grid1") if i == 0 else None)
+                v["bq"][i] = idx
                 new_points, _ = pointnet_util.group_concat(xyz, points[i], new_xyz, idx,
                                                            want_grouped_xyz=False)
                 out = [new_points]
@@ -224,9 +226,9 @@ class Step:
         def fp(i):
             def f():
                 k = 3 - i  # the FP layer whose coarse level (i+1) just became available
-                v["fp"][k] = pointnet_util.fp_interpolate(
+                v["fp"][k], v["nn"][k] = pointnet_util.fp_interpolate(
                     v["xyz"][i], v["xyz"][i + 1], points[i], fp_feat[k],
-                    unknown_grid=v.get("grid1") if i == 0 else None)
+                    unknown_grid=v.get("grid1") if i == 0 else None, return_nn=True)
             return f
 
         npoints = [sa_[0] for sa_ in SSG_SA]
@@ -337,7 +339,7 @@ class Step:
     def _tasks_msg(self):
         inp, v = self.inp, self.v
         v["xyz"] = [inp["xyz"], None, None]
-        v["gp"] = {}
+        v["gp"], v["bq"] = {}, {}
         tasks = []
 
         xyz0 = inp["xyz"]
@@ -361,6 +363,7 @@ class Step:
                 points = None if i == 0 else inp["sa_out"][0]
                 xyz, new_xyz = v["xyz"][i], v["xyz"][i + 1]
                 idx, _ = tf_grouping.query_ball_point(radius, nsample, xyz, new_xyz)
+                v["bq"][(i, r)] = idx
                 v["gp"][(i, r)] = pointnet_util.group_concat(xyz, points, new_xyz, idx,
                                                              xyz_last=True,
                                                              want_grouped_xyz=False)[0]
@@ -384,6 +387,27 @@ class Step:
         if self.kind == "ssg":
             return [t for o in v["sa"] for t in o] + list(v["fp"])
         return [v["gp"][k] for k in sorted(v["gp"])]
+
+    def intermediates(self):
+        """The index and copy results inside the step, by name (the parity tests compare them
+        bit for bit): 'fps<i>.idx' / 'fps<i>.new_xyz' (sampler i + fused gather),
+        'bq<i>.idx' (SSG) or 'bq<i>_<r>.idx' (MSG radius r) (ball query), and for FP layers
+        whose neighbour search ran as its own kernel 'nn<k>.idx' / 'nn<k>.dist' (k = the
+        FP layer, 1..4 = fa_layer1..4). Geometric step only."""
+        v, out = self.v, {}
+        samp = v.get("chain") or v.get("fps_out") or []
+        for i, (idx, nx) in enumerate(samp):
+            out[f"fps{i + 1}.idx"], out[f"fps{i + 1}.new_xyz"] = idx, nx
+        if self.kind == "ssg":
+            for i, idx in enumerate(v.get("bq", [])):
+                out[f"bq{i + 1}.idx"] = idx
+            for k, nn in enumerate(v.get("nn", [])):
+                if nn is not None:
+                    out[f"nn{k + 1}.dist"], out[f"nn{k + 1}.idx"] = nn
+        else:
+            for (i, r), idx in sorted(v.get("bq", {}).items()):
+                out[f"bq{i + 1}_{r}.idx"] = idx
+        return out
 
     # ------------------------------------------------------------------ execution
     def _stream(self, lane, main):
@@ -507,6 +531,9 @@ class GraphStep:
     def join(self):
         self.step.join()
         return self.outs
+
+    def intermediates(self):
+        return self.step.intermediates()
 
 
 class Pipeline:

@@ -87,46 +87,8 @@ def test_fps_vs_oracle(env, kind, B, N, M):
     assert np.array_equal(only.cpu().numpy(), ref)
 
 
-# SA1-size clouds (4096 < N <= 8192) run the culled hot-set sampler by default; every schedule
-# selectable through pn2_fps_set_algo (0 default, 1 v9 block scan, 6 no priority boost) must
-# give the oracle's indices: ScanNet crops with duplicates, uniform, the integer lattice (exact
-# ties everywhere), npoint beyond the distinct points, npoint > N, tiny npoint, odd N.
-SAMPLER_CASES = [
-    ("scannet", 16, 8192, 1024), ("uniform", 4, 8192, 1024), ("grid", 4, 8192, 1024),
-    ("grid", 2, 8192, 4000), ("dup", 2, 5000, 40), ("fewuniq", 2, 8192, 600),
-    ("scannet", 2, 4097, 4097), ("uniform", 2, 6000, 7000), ("scannet", 3, 8192, 2),
-    ("scannet", 3, 8192, 1), ("scannet", 2, 7777, 1500),
-]
-
-
-# MSG SA1-size clouds (8192 < N <= 16384, cfg5) run the culled sampler with its coordinates in
-# L2 (algo 0) or the v9 512 x 32 block scan (algo 1)
-MSG_SAMPLER_CASES = [
-    ("scannet", 8, 16384, 512), ("uniform", 2, 16384, 512), ("grid", 2, 16384, 1024),
-    ("grid", 1, 16384, 4000), ("dup", 1, 12000, 40), ("fewuniq", 2, 16384, 600),
-    ("scannet", 1, 8193, 8193), ("uniform", 1, 12000, 13000), ("scannet", 2, 16384, 1),
-    ("scannet", 2, 11111, 2000),
-]
-
-
-@pytest.mark.parametrize("algo,kind,B,N,M",
-                         [(a,) + c for a in (0, 1, 6) for c in SAMPLER_CASES]
-                         + [(a,) + c for a in (0, 1) for c in MSG_SAMPLER_CASES])
-def test_fps_sampler_schedules(env, algo, kind, B, N, M):
-    pkg, O, torch, dev = env
-    lib = pkg._lib.lib()
-    x = _cloud(pkg, kind, B, N, seed=3)
-    old = lib.pn2_fps_set_algo(algo)
-    try:
-        idx, new_xyz = pkg.tf_sampling.farthest_point_sample_and_gather(
-            M, torch.from_numpy(x).to(dev))
-        torch.cuda.synchronize()
-    finally:
-        lib.pn2_fps_set_algo(old)
-    ref = O.fps(x, M)
-    got = idx.cpu().numpy()
-    assert np.array_equal(got, ref), f"algo {algo}: {(got != ref).sum()} FPS indices differ"
-    assert np.array_equal(_bits(new_xyz.cpu().numpy()), _bits(O.gather_point(x, ref)))
+# (the per-schedule sampler cases, the full-size steps and the FPS golden vectors run first:
+# tests/test_gpu_a_fullsize.py)
 
 
 @pytest.mark.parametrize("kind,B,N,M", [c for c in FPS_CASES if c[2] <= 16384])
@@ -557,73 +519,6 @@ def test_gradients(env):
     for b in range(2):
         np.add.at(counts[b], gi[b].ravel(), 1.0)
     np.testing.assert_allclose(p.grad.cpu().numpy(), np.repeat(counts[..., None], 16, -1), **TOL)
-
-
-def _np_inputs(inp):
-    np_inp = {k: v for k, v in inp.items()}
-    for k in ("xyz", "feats"):
-        np_inp[k] = None if inp[k] is None else inp[k].cpu().numpy()
-    for k in ("sa_out", "fp_out"):
-        if k in inp:
-            np_inp[k] = [t.cpu().numpy() for t in inp[k]]
-    if "attn" in inp:
-        np_inp["attn"] = [tuple(t.cpu().numpy() for t in qkv) for qkv in inp["attn"]]
-    return np_inp
-
-
-def _check_outputs(outs, ref):
-    assert len(ref) == len(outs)
-    for k, (g, r) in enumerate(zip(outs, ref)):
-        g = g.cpu().numpy()
-        assert g.shape == r.shape, (k, g.shape, r.shape)
-        np.testing.assert_allclose(g, r, err_msg=f"output {k}", **TOL)
-
-
-@pytest.mark.timeout(300)
-@pytest.mark.parametrize("config,B", [("cfg2", 16), ("cfg3", 16), ("cfg5", 8)])
-def test_stack_full_size(env, config, B):
-    """The benchmark step at its BASELINE.json batch (cfg2/cfg3 B = 16, cfg5 B = 8: the launch
-    geometry of ball query and grouping depends on it), every output against the CPU
-    restatement."""
-    pkg, O, torch, dev = env
-    inp = pkg.stack.make_inputs(config, list(range(B)), dev)
-    outs = pkg.stack.run(inp)
-    torch.cuda.synchronize()
-    _check_outputs(outs, O.run_stack_cpu(_np_inputs(inp), config))
-
-
-@pytest.mark.timeout(300)
-@pytest.mark.parametrize("config,B", [("cfg2", 16), ("cfg3", 16), ("cfg5", 8)])
-def test_pipeline_full_size(env, config, B):
-    """What bench.py times: the software-pipelined hipGraph steps over 3 buffer sets, at the
-    BASELINE batch, after several rotations; the last step's outputs against the oracle."""
-    pkg, O, torch, dev = env
-    inp = pkg.stack.make_inputs(config, list(range(100, 100 + B)), dev)
-    pipe = pkg.stack.Pipeline(inp, graphs=True, nsets=3)
-    for _ in range(7):
-        pipe.run()
-    outs = pipe.join()
-    torch.cuda.synchronize()
-    _check_outputs(outs, O.run_stack_cpu(_np_inputs(inp), config))
-
-
-@pytest.mark.timeout(300)
-@pytest.mark.parametrize("rank", [1, 7])
-def test_cfg4_rank_shard(env, rank):
-    """cfg4 (B = 128 over 8 GPUs, 16 per rank): the shard a rank owns (global cloud ids from
-    shard.shard_ids, 16-31 for rank 1, 112-127 for rank 7) run on this GPU; outputs and the
-    per-cloud checksums that bench.py gathers equal the oracle's for the same global clouds."""
-    pkg, O, torch, dev = env
-    ids = pkg.shard.shard_ids(rank, 8, 16)
-    assert ids == list(range(16 * rank, 16 * rank + 16))
-    inp = pkg.stack.make_inputs("cfg2", ids, dev)
-    outs = pkg.stack.run(inp)
-    torch.cuda.synchronize()
-    ref = O.run_stack_cpu(_np_inputs(inp), "cfg2")
-    _check_outputs(outs, ref)
-    got = pkg.shard.cloud_checksums([o.cpu() for o in outs], 16)
-    want = pkg.shard.cloud_checksums([torch.from_numpy(r) for r in ref], 16)
-    np.testing.assert_allclose(got.numpy(), want.numpy(), rtol=1e-6, atol=1e-3)
 
 
 @pytest.mark.parametrize("config,B", [("cfg2", 4), ("cfg3", 2), ("cfg5", 2)])

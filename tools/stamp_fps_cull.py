@@ -35,9 +35,11 @@ for kind in ("scannet", "uniform"):
         rc = L.pn2_fps_cull_stamp(x.data_ptr(), B, N, M, idx.data_ptr(), buf.ctypes.data,
                                   stats.ctypes.data)
         assert rc == 0, rc
-    old = lib.pn2_fps_set_algo(1)
-    ref = pkg.tf_sampling.farthest_point_sample(M, x)
-    lib.pn2_fps_set_algo(old)
+    ref = torch.empty((B, M), dtype=torch.int32, device=dev)
+    rnx = torch.empty((B, M, 3), dtype=torch.float32, device=dev)
+    assert lib.pn2_fps_gather_sched(x.data_ptr(), B, N, M, ref.data_ptr(), rnx.data_ptr(),
+                                    pkg._lib.PN2_FPS_BLOCKSCAN,
+                                    torch.cuda.current_stream().cuda_stream) == 0
     wv = np.zeros(16 * 16 * 4, np.uint64)
     L.pn2_fps_cull_waves.argtypes = [ctypes.c_void_p]
     assert L.pn2_fps_cull_waves(wv.ctypes.data) == 0
