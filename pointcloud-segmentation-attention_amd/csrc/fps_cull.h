@@ -596,73 +596,145 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
         // pending LDS load to wait for inside it, and the picks' publishing stores stay off
         // the dependency chain (an in-loop lgkmcnt(0) would wait for the previous pick's)
         __builtin_amdgcn_s_waitcnt(0xC07F);
-        for (; jj < lim; ++jj) {
-          // the lane's best entry (value desc, then entry order = tie order)
-          const bool b01 = hv[1] > hv[0];
-          int cv = b01 ? hv[1] : hv[0];
-          float lx = b01 ? hx[0][1] : hx[0][0], ly = b01 ? hy[0][1] : hy[0][0],
-                lz = b01 ? hz[0][1] : hz[0][0];
-          int lk = b01 ? hk[1] : hk[0];
-          uint32_t ck = b01 ? hkey[1] : hkey[0];
-          if constexpr (HQ == 4) {
-            const bool b23 = hv[3] > hv[2];
-            const int v23 = b23 ? hv[3] : hv[2];
-            const bool bh = v23 > cv;
-            cv = bh ? v23 : cv;
-            lx = bh ? (b23 ? hx[1][1] : hx[1][0]) : lx;
-            ly = bh ? (b23 ? hy[1][1] : hy[1][0]) : ly;
-            lz = bh ? (b23 ? hz[1][1] : hz[1][0]) : lz;
-            lk = bh ? (b23 ? hk[3] : hk[2]) : lk;
-            ck = bh ? (b23 ? hkey[3] : hkey[2]) : ck;
-          }
-          // the winner's coordinates are selected here, beside the reduction, not after it
-          asm volatile("" ::"v"(lx), "v"(ly), "v"(lz), "v"(lk));
-          const int wm = __builtin_amdgcn_readlane(wave_max_i32_l63(cv), 63);
-          if (!(wm > T)) break;
-          const uint64_t hold = __builtin_amdgcn_ballot_w64(cv == wm);
-          int L;
-          if (__builtin_popcountll(hold) == 1) {
-            L = (int)__builtin_ctzll(hold);
-          } else {  // equal values: the smallest tie key among the holders
-            const uint32_t km = ~uniform_u32(wave_max_u32(cv == wm ? ~ck : 0u));
-            L = (int)__builtin_ctzll(__builtin_amdgcn_ballot_w64(cv == wm && ck == km));
-          }
-          const float cx = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__float_as_int(lx), L));
-          const float cy = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__float_as_int(ly), L));
-          const float cz = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__float_as_int(lz), L));
-          // publish from the winning lane itself (exec = lane L only): its lx, ly, lz, lk are
-          // the centre, so neither a readlane of the index nor moves of the SGPR copies into
-          // lane 0 are needed; the count follows the centre (DS operations of one wave
-          // execute in order)
-          {
-            const uint32_t a_c = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float4*)&scl[jj];
-            const uint32_t a_n = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) int*)&sj[rp];
-            uint64_t sv;
-            asm volatile(
-                "s_mov_b64 %[sv], exec\n\t"
-                "s_lshl_b64 exec, 1, %[L]\n\t"
-                "ds_write_b32 %[a], %[x]\n\t"
-                "ds_write_b32 %[a], %[y] offset:4\n\t"
-                "ds_write_b32 %[a], %[z] offset:8\n\t"
-                "ds_write_b32 %[a], %[k] offset:12\n\t"
-                "ds_write_b32 %[c], %[n]\n\t"
-                "s_mov_b64 exec, %[sv]"
-                : [sv] "=&s"(sv)
-                : [L] "s"(L), [a] "v"(a_c), [c] "v"(a_n), [x] "v"(lx), [y] "v"(ly), [z] "v"(lz),
-                  [k] "v"(lk), [n] "v"(jj + 1)
-                : "memory", "scc");
-          }
-          __builtin_amdgcn_sched_barrier(0);
-          // the hot update (the next pick depends on it)
-          const f2 c2x = {cx, cx}, c2y = {cy, cy}, c2z = {cz, cz};
+        // publishing addresses and the published count in VGPRs, advanced by one VALU add per
+        // pick (as SGPRs they cost an SALU add and a v_mov each for the DS stores)
+        int va_c, va_n, vcnt;
+        asm volatile("v_mov_b32 %0, %1" : "=v"(va_c)
+                     : "s"((uint32_t)(uintptr_t)(__attribute__((address_space(3))) float4*)&scl[0]));
+        asm volatile("v_mov_b32 %0, %1" : "=v"(va_n)
+                     : "s"((uint32_t)(uintptr_t)(__attribute__((address_space(3))) int*)&sj[rp]));
+        asm volatile("v_mov_b32 %0, 1" : "=v"(vcnt));
+        // the pick loop ends when the best hot value is no longer above T; it cannot run past
+        // the nh <= K hot entries (a picked entry drops to 0 <= T), so only the last batch of
+        // the cloud (fewer than K picks left) needs a count test per pick
+        auto pick_loop = [&](auto checked_tag) {
+          constexpr bool CHECKED = decltype(checked_tag)::value;
+          for (;;) {
+            int cv, lk, wm;
+            float lx, ly, lz;
+            uint64_t m01 = 0, m23 = 0, mh = 0;
+            if constexpr (HQ == 4) {
+              // the lane's best entry (value desc, then entry order = tie order: strict '>'
+              // keeps the lower entry) and its coordinates and index, interleaved with the
+              // wave max (DPP rows, then row_bcast:15 / :31 into lane 63): the selects fill
+              // the DPP read-after-write wait states (2 per step) that were s_nop before.
+              // Wait states inside the block: VALU-written SGPR mask -> v_cndmask 2, DPP
+              // source 2, readlane source 1.
+              int v23, r;
+              float tx, ty, tz;
+              int tk;
+              asm volatile(
+                  "v_cmp_gt_i32_e64 %[m01], %[h1], %[h0]\n\t"
+                  "v_cmp_gt_i32_e64 %[m23], %[h3], %[h2]\n\t"
+                  "v_max_i32_e32 %[cv], %[h0], %[h1]\n\t"
+                  "v_max_i32_e32 %[v23], %[h2], %[h3]\n\t"
+                  "v_cmp_gt_i32_e64 %[mh], %[v23], %[cv]\n\t"
+                  "v_max_i32_e32 %[cv], %[cv], %[v23]\n\t"
+                  "v_cndmask_b32_e64 %[lx], %[x0], %[x1], %[m01]\n\t"
+                  "v_cndmask_b32_e64 %[tx], %[x2], %[x3], %[m23]\n\t"
+                  "v_max_i32_dpp %[r], %[cv], %[cv] quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+                  "v_cndmask_b32_e64 %[ly], %[y0], %[y1], %[m01]\n\t"
+                  "v_cndmask_b32_e64 %[ty], %[y2], %[y3], %[m23]\n\t"
+                  "v_max_i32_dpp %[r], %[r], %[r] quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+                  "v_cndmask_b32_e64 %[lz], %[z0], %[z1], %[m01]\n\t"
+                  "v_cndmask_b32_e64 %[tz], %[z2], %[z3], %[m23]\n\t"
+                  "v_max_i32_dpp %[r], %[r], %[r] row_half_mirror row_mask:0xf bank_mask:0xf\n\t"
+                  "v_cndmask_b32_e64 %[lk], %[k0], %[k1], %[m01]\n\t"
+                  "v_cndmask_b32_e64 %[tk], %[k2], %[k3], %[m23]\n\t"
+                  "v_max_i32_dpp %[r], %[r], %[r] row_mirror row_mask:0xf bank_mask:0xf\n\t"
+                  "v_cndmask_b32_e64 %[lx], %[lx], %[tx], %[mh]\n\t"
+                  "v_cndmask_b32_e64 %[ly], %[ly], %[ty], %[mh]\n\t"
+                  "v_max_i32_dpp %[r], %[r], %[r] row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
+                  "v_cndmask_b32_e64 %[lz], %[lz], %[tz], %[mh]\n\t"
+                  "v_cndmask_b32_e64 %[lk], %[lk], %[tk], %[mh]\n\t"
+                  "v_max_i32_dpp %[r], %[r], %[r] row_bcast:31 row_mask:0xc bank_mask:0xf\n\t"
+                  "s_nop 0\n\t"
+                  "v_readlane_b32 %[wm], %[r], 63"
+                  : [m01] "=&s"(m01), [m23] "=&s"(m23), [mh] "=&s"(mh), [cv] "=&v"(cv),
+                    [v23] "=&v"(v23), [r] "=&v"(r), [lx] "=&v"(lx), [ly] "=&v"(ly),
+                    [lz] "=&v"(lz), [lk] "=&v"(lk), [tx] "=&v"(tx), [ty] "=&v"(ty),
+                    [tz] "=&v"(tz), [tk] "=&v"(tk), [wm] "=s"(wm)
+                  : [h0] "v"(hv[0]), [h1] "v"(hv[1]), [h2] "v"(hv[2]), [h3] "v"(hv[3]),
+                    [x0] "v"(hx[0][0]), [x1] "v"(hx[0][1]), [x2] "v"(hx[1][0]), [x3] "v"(hx[1][1]),
+                    [y0] "v"(hy[0][0]), [y1] "v"(hy[0][1]), [y2] "v"(hy[1][0]), [y3] "v"(hy[1][1]),
+                    [z0] "v"(hz[0][0]), [z1] "v"(hz[0][1]), [z2] "v"(hz[1][0]), [z3] "v"(hz[1][1]),
+                    [k0] "v"(hk[0]), [k1] "v"(hk[1]), [k2] "v"(hk[2]), [k3] "v"(hk[3]));
+            } else {
+              const bool b01 = hv[1] > hv[0];
+              cv = b01 ? hv[1] : hv[0];
+              lx = b01 ? hx[0][1] : hx[0][0];
+              ly = b01 ? hy[0][1] : hy[0][0];
+              lz = b01 ? hz[0][1] : hz[0][0];
+              lk = b01 ? hk[1] : hk[0];
+              // the winner's coordinates are selected here, beside the reduction, not after it
+              asm volatile("" ::"v"(lx), "v"(ly), "v"(lz), "v"(lk));
+              wm = __builtin_amdgcn_readlane(wave_max_i32_l63(cv), 63);
+            }
+            if (!(wm > T)) break;
+            const uint64_t hold = __builtin_amdgcn_ballot_w64(cv == wm);
+            int L;
+            if (__builtin_popcountll(hold) == 1) {
+              L = (int)__builtin_ctzll(hold);
+            } else {  // equal values: the smallest tie key among the holders
+              uint32_t ck;
+              if constexpr (HQ == 4) {  // the same selects as the lane's best entry
+                uint32_t k23;
+                asm volatile("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(ck)
+                             : "v"(hkey[0]), "v"(hkey[1]), "s"(m01));
+                asm volatile("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(k23)
+                             : "v"(hkey[2]), "v"(hkey[3]), "s"(m23));
+                asm volatile("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(ck) : "v"(k23), "s"(mh));
+              } else {
+                ck = hv[1] > hv[0] ? hkey[1] : hkey[0];
+              }
+              const uint32_t km = ~uniform_u32(wave_max_u32(cv == wm ? ~ck : 0u));
+              L = (int)__builtin_ctzll(__builtin_amdgcn_ballot_w64(cv == wm && ck == km));
+            }
+            // publish from the winning lane itself (exec = lane L only): its lx, ly, lz, lk are
+            // the centre, so neither a readlane of the index nor moves of the SGPR copies into
+            // lane 0 are needed; the count follows the centre (DS operations of one wave
+            // execute in order). The centre's coordinates are read back (v_readlane ignores
+            // exec) inside the same block, so no wait states follow the exec restore; L comes
+            // from SALU (no lane-select wait), and the first use of cx is 3 instructions on.
+            float cx, cy, cz;
+            {
+              uint64_t sv;
+              asm volatile(
+                  "s_mov_b64 %[sv], exec\n\t"
+                  "s_lshl_b64 exec, 1, %[L]\n\t"
+                  "ds_write_b32 %[a], %[x]\n\t"
+                  "ds_write_b32 %[a], %[y] offset:4\n\t"
+                  "ds_write_b32 %[a], %[z] offset:8\n\t"
+                  "ds_write_b32 %[a], %[k] offset:12\n\t"
+                  "ds_write_b32 %[c], %[n]\n\t"
+                  "v_readlane_b32 %[cx], %[x], %[L]\n\t"
+                  "v_readlane_b32 %[cy], %[y], %[L]\n\t"
+                  "v_readlane_b32 %[cz], %[z], %[L]\n\t"
+                  "s_mov_b64 exec, %[sv]"
+                  : [sv] "=&s"(sv), [cx] "=&s"(cx), [cy] "=&s"(cy), [cz] "=&s"(cz)
+                  : [L] "s"(L), [a] "v"(va_c), [c] "v"(va_n), [x] "v"(lx), [y] "v"(ly),
+                    [z] "v"(lz), [k] "v"(lk), [n] "v"(vcnt)
+                  : "memory", "scc");
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            // the hot update (the next pick depends on it)
+            const f2 c2x = {cx, cx}, c2y = {cy, cy}, c2z = {cz, cz};
 #pragma unroll
-          for (int h = 0; h < HP; ++h) {
-            const f2 dx = hx[h] - c2x, dy = hy[h] - c2y, dz = hz[h] - c2z;
-            const f2 d = (dx * dx + dy * dy) + dz * dz;
-            hv[2 * h] = min(hv[2 * h], __float_as_int(d.x));
-            hv[2 * h + 1] = min(hv[2 * h + 1], __float_as_int(d.y));
+            for (int h = 0; h < HP; ++h) {
+              const f2 dx = hx[h] - c2x, dy = hy[h] - c2y, dz = hz[h] - c2z;
+              const f2 d = (dx * dx + dy * dy) + dz * dz;
+              hv[2 * h] = min(hv[2 * h], __float_as_int(d.x));
+              hv[2 * h + 1] = min(hv[2 * h + 1], __float_as_int(d.y));
+            }
+            va_c += 16;
+            vcnt += 1;
+            if constexpr (CHECKED)
+              if (__builtin_amdgcn_readfirstlane(vcnt) > lim) break;
           }
-        }
+        };
+        if (lim >= K) pick_loop(std::false_type{});
+        else if (lim > 0) pick_loop(std::true_type{});
+        jj = __builtin_amdgcn_readfirstlane(vcnt) - 1;
         if constexpr (PRIO > 0) __builtin_amdgcn_s_setprio(0);
         if (lane == 0) {
           asm volatile("" ::: "memory");
