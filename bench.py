@@ -100,15 +100,19 @@ def cpu_baseline(config, B_per_step, seconds, threads):
     v1, c1, e1 = timed(1, seconds / 2)
     vt, ct, et = timed(threads, seconds / 2)
     est_all = v1 * nproc
+    eff = vt / (v1 * threads)  # measured 1 -> `threads` scaling efficiency
     return {"value": vt, "unit": "clouds/s", "cores": threads, "kind": "port",
             "value_1core": v1, "value_threads": vt, "threads": threads,
+            "scaling_efficiency_1_to_threads": eff,
             "cores_all": nproc, "value_all_cores_extrapolated": est_all,
+            "value_all_cores_at_measured_efficiency": est_all * eff,
             "cpu_model": _cpu_model(),
             "sample": f"{config} steps of the C restatement oracle/pn2_oracle.c: {c1} clouds "
                       f"(1 per call) in {e1:.1f} s on 1 thread; {ct} clouds ({threads} per call, "
                       f"OpenMP over clouds) in {et:.1f} s on {threads} threads (the box's CPU "
-                      f"share); all-cores figure = 1-core rate x {nproc} (nproc), extrapolated, "
-                      "not run (the box allows its CPU share only)"}
+                      f"share); all-cores figures = 1-core rate x {nproc} (nproc), linear (an upper "
+                      "bound) and at the measured 1->threads efficiency, extrapolated, not run "
+                      "(the box allows its CPU share only)"}
 
 
 def pmc_traffic(config, B):
@@ -136,21 +140,46 @@ def pmc_traffic(config, B):
 MAX_CLOCK_GHZ = 2.4  # MI355X_MICROARCH.md, chip-level parameters
 
 
-def sa1_latency(config, fps_ms, M1):
-    """The SA1 sampler's own bound: its picks are a serial chain. For the culled hot-set
-    sampler (N <= 8192: cfg2, cfg3) the committed stamp summary
-    (profiles/<round>/sa1_cull_stamps.json, tools/stamp_fps_cull.py) splits a launch into the
-    hot wave's pick loop (cycles per pick) and the per-round refresh (rounds x cycles)."""
+def _latest_profile(name):
     import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", name)))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        return json.load(f), os.path.relpath(files[-1], ROOT)
+
+
+def sa1_latency(config, fps_ms, M1, N):
+    """The SA1 sampler's own bound: its picks are a serial chain (tf_sampling_g.cu:124-168), one
+    CU per cloud. Measured: the committed stamp summary of the culled sampler
+    (profiles/<round>/sa1_cull_stamps.json, tools/stamp_fps_cull.py: cycles per pick of the hot
+    wave, rounds, cycles per round, setup). Floor: the same pieces run ALONE on one CU
+    (profiles/<round>/sampler_floor.json, tools/ubench/pick_floor.hip): the dependent chain of
+    one pick (lane best of 4, 64-lane DPP max, winner, coordinates, distance update) and the
+    synchronisation skeleton of a round end (3 barriers + 2 cross-wave reductions, 16 waves),
+    plus the cloud read at one CU's share of HBM. floor = setup + (M - 1) x pick + rounds x
+    round; frac = floor / measured launch (1 = the launch runs at the floor)."""
     out = {"ns_per_pick": fps_ms * 1e6 / max(1, M1 - 1)}
-    if config in ("cfg2", "cfg3"):
-        files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "sa1_cull_stamps.json")))
-        if files:
-            with open(files[-1]) as f:
-                d = json.load(f)
-            out.update({k: d[k] for k in ("hot_cycles_per_pick", "rounds", "round_cycles",
-                                          "setup_cycles") if k in d})
-            out["source"] = os.path.relpath(files[-1], ROOT)
+    st, st_src = _latest_profile("sa1_cull_stamps.json")
+    fl, fl_src = _latest_profile("sampler_floor.json")
+    if config in ("cfg2", "cfg3") and st:
+        out.update({k: st[k] for k in ("hot_cycles_per_pick", "rounds", "round_cycles",
+                                      "setup_cycles", "kernel_cycles") if k in st})
+        out["source"] = st_src
+    if fl:
+        out.update({"floor_cycles_per_pick": fl["pick_chain_cycles"],
+                    "floor_pick_step_cycles": fl["pick_step_cycles"],
+                    "floor_round_cycles": fl["round_sync_cycles"], "floor_source": fl_src})
+        # the cloud read once at one CU's share of the HBM peak (8 TB/s over 256 CUs)
+        out["floor_setup_cycles"] = N * 12 / (HBM_PEAK_GBPS / 256 / MAX_CLOCK_GHZ)
+        if "rounds" in out:
+            floor = (out["floor_setup_cycles"] + (M1 - 1) * out["floor_cycles_per_pick"]
+                     + out["rounds"] * out["floor_round_cycles"])
+            out["floor_launch_cycles"] = floor
+            out["floor_launch_ms"] = floor / (MAX_CLOCK_GHZ * 1e6)
+            if "hot_cycles_per_pick" in out:
+                out["frac_pick"] = out["floor_cycles_per_pick"] / out["hot_cycles_per_pick"]
+                out["frac_round"] = out["floor_round_cycles"] / out["round_cycles"]
     return out
 
 
@@ -414,6 +443,18 @@ def main():
         fps_bytes = B * (N * 12 + M1 * 16)
         achieved = fps_bytes / (fps_ms * 1e-3) / 1e9
         traffic, traffic_src = pmc_traffic(args.config, B)
+        lat = sa1_latency(args.config, fps_ms, M1, N)
+        hbm = {"achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+               "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
+               "traffic_source": traffic_src, "algorithmic_bytes_per_launch": fps_bytes}
+        if "floor_launch_ms" in lat:
+            # the bound that applies: the serial pick chain (HBM is 1.8 MB per launch); time-
+            # like, so achieved = the measured launch, peak = its floor, frac = peak / achieved
+            roof = {"bound": "latency", "achieved": fps_ms * 1e6, "peak": lat["floor_launch_ms"] * 1e6,
+                    "unit": "ns per launch", "frac": lat["floor_launch_ms"] / fps_ms}
+        else:
+            roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                    "frac": achieved / HBM_PEAK_GBPS}
         result = {
             "metric": METRIC, "value": value, "unit": "clouds/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
@@ -432,16 +473,14 @@ def main():
                        "lane0_priority": prio0,
                        "streams": ("SA1 sampler + 4 side streams" if overlap else "one stream")
                        + (f", steps software-pipelined over {args.sets} buffer sets" if pipelined else "")},
-            "roofline": {"kernel": f"SA1 sampler (FPS + gather fused): {B} clouds x {N} pts -> "
-                                   f"{M1}, one workgroup per cloud",
-                         "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS,
-                         "traffic": traffic, "traffic_source": traffic_src,
-                         "avg_launch_ms": fps_ms, "algorithmic_bytes_per_launch": fps_bytes,
-                         "latency": sa1_latency(args.config, fps_ms, M1),
-                         "note": "latency-bound serial argmax (M-1 dependent picks, one CU per "
-                                 "cloud); the HBM fraction is structurally low, the pick "
-                                 "chain ('latency') is the bound that applies"},
+            "roofline": dict(
+                {"kernel": f"SA1 sampler (FPS + gather fused): {B} clouds x {N} pts -> {M1}, "
+                           "one workgroup per cloud"},
+                **roof, traffic=traffic, traffic_source=traffic_src, avg_launch_ms=fps_ms,
+                algorithmic_bytes_per_launch=fps_bytes, latency=lat, hbm=hbm,
+                note="the SA1 sampler is a chain of M-1 dependent picks on one CU per cloud: "
+                     "its bound is latency (floor from tools/ubench/pick_floor.hip, "
+                     "roofline.latency); the HBM figures (roofline.hbm) are structurally low"),
             "step_hbm": {"algorithmic_bytes": step_bytes,
                          "achieved_GBps": step_bytes * world / (elapsed / args.steps) / 1e9,
                          "frac": step_bytes * world / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBPS},
@@ -459,7 +498,9 @@ def main():
                 cb["gpu_over_cpu"] = {"1core": value / cb["value_1core"],
                                       f"{cb['threads']}threads": value / cb["value_threads"],
                                       "all_cores_extrapolated":
-                                          value / cb["value_all_cores_extrapolated"]}
+                                          value / cb["value_all_cores_extrapolated"],
+                                      "all_cores_at_measured_efficiency":
+                                          value / cb["value_all_cores_at_measured_efficiency"]}
             except Exception as e:  # the baseline is reported, never the product
                 log(f"cpu baseline failed: {e!r}")
                 result["cpu_baseline"] = None

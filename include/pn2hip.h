@@ -16,9 +16,12 @@
  *   GroupPoint           tf_grouping.cpp:139-171, _g.cu:40-57    → pn2_group_point
  *   GroupPointGrad       tf_grouping.cpp:174-208, _g.cu:61-78    → pn2_group_point_grad
  *   ThreeNN              tf_interpolate.cpp:157-187, :60-103     → pn2_three_nn,
- *                                                                  pn2_three_nn_grid
- *   ThreeInterpolate     tf_interpolate.cpp:191-222, :107-127    → pn2_three_interpolate
- *   ThreeInterpolateGrad tf_interpolate.cpp:225-262, :131-153    → pn2_three_interpolate_grad
+ *                                                                  pn2_three_nn_grid,
+ *                                                                  pn2cpu_three_nn (host)
+ *   ThreeInterpolate     tf_interpolate.cpp:191-222, :107-127    → pn2_three_interpolate,
+ *                                                                  pn2cpu_three_interpolate
+ *   ThreeInterpolateGrad tf_interpolate.cpp:225-262, :131-153    → pn2_three_interpolate_grad,
+ *                                                                  pn2cpu_three_interpolate_grad
  *   IDW weights          pointnet_util.py:219-222                → pn2_idw_weights
  *   sample_and_group     pointnet_util.py:16-58 (SSG), :180-191  → pn2_sample_and_group,
  *                                                                  pn2_group_concat
@@ -238,6 +241,17 @@ int pn2_three_interpolate(const float* points, const int32_t* idx, const float* 
 int pn2_three_interpolate_grad(const float* grad_out, const int32_t* idx, const float* weight,
                                int B, int n, int C, int m, float* grad_points,
                                pn2_stream_t stream);
+/* Host twins of the three ops the reference registers ONLY on DEVICE_CPU
+ * (tf_interpolate.cpp:187,222,262): the same arguments minus the stream, HOST pointers,
+ * synchronous (std::thread over clouds), the reference's fp32 arithmetic and order, so the
+ * results equal threenn_cpu / threeinterpolate_cpu / threeinterpolate_grad_cpu bit for bit
+ * (the grad's sums keep the reference's order within a cloud). */
+int pn2cpu_three_nn(const float* xyz1, const float* xyz2, int B, int n, int m, float* dist,
+                    int32_t* idx);
+int pn2cpu_three_interpolate(const float* points, const int32_t* idx, const float* weight, int B,
+                             int m, int C, int n, float* out);
+int pn2cpu_three_interpolate_grad(const float* grad_out, const int32_t* idx, const float* weight,
+                                  int B, int n, int C, int m, float* grad_points);
 /* weight = (1/d)/sum(1/d), d = max(dist,1e-10)  (pointnet_util.py:219-222). */
 int pn2_idw_weights(const float* dist, int B, int n, float* weight, pn2_stream_t stream);
 /* pointnet_fp_module geometry (pointnet_util.py:218-226): three_nn + IDW weights +

@@ -79,6 +79,9 @@ SIGNATURES = {
     "pn2_three_interpolate": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P]),
     "pn2_three_interpolate_grad": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P]),
     "pn2_idw_weights": (_I, [_P, _I, _I, _P, _P]),
+    "pn2cpu_three_nn": (_I, [_P, _P, _I, _I, _I, _P, _P]),
+    "pn2cpu_three_interpolate": (_I, [_P, _P, _P, _I, _I, _I, _I, _P]),
+    "pn2cpu_three_interpolate_grad": (_I, [_P, _P, _P, _I, _I, _I, _I, _P]),
     "pn2_fp_fused": (_I, [_P, _P, _P, _I, _P, _I, _I, _I, _I, _P, _P]),
     "pn2_attn_reduce": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P]),
     "pn2_attn_reduce_grad": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P]),

@@ -138,6 +138,99 @@ PN2_DEV constexpr uint64_t cell_lanes(int s) {
 
 // NPTS points at most; wave 0 is the hot wave, waves 1..NW-1 hold the cold cells (PPT cells of
 // 64 sorted points per wave).
+// ---- the hot wave's pick step (also run alone by tools/ubench/pick_floor.hip) -------------
+using hf2 = float __attribute__((ext_vector_type(2)));
+
+// HQ = 4 entries per lane: the lane's best entry (value desc, then entry order = tie order:
+// strict '>' keeps the lower entry), its coordinates and index, interleaved with the wave max
+// (DPP rows, then row_bcast:15 / :31 into lane 63): the selects fill the DPP read-after-write
+// wait states (2 per step) that were s_nop before. Wait states inside the block: VALU-written
+// SGPR mask -> v_cndmask 2, DPP source 2, readlane source 1. m01 / m23 / mh are the lane's
+// select masks (the tie path repeats the selects on the tie keys with them).
+PN2_DEV void hot_best4(const int (&hv)[4], const hf2 (&hx)[2], const hf2 (&hy)[2],
+           const hf2 (&hz)[2], const int (&hk)[4], int& cv, float& lx, float& ly,
+           float& lz, int& lk, int& wm, uint64_t& m01, uint64_t& m23, uint64_t& mh) {
+  int v23, r, tk;
+  float tx, ty, tz;
+  asm volatile(
+      "v_cmp_gt_i32_e64 %[m01], %[h1], %[h0]\n\t"
+      "v_cmp_gt_i32_e64 %[m23], %[h3], %[h2]\n\t"
+      "v_max_i32_e32 %[cv], %[h0], %[h1]\n\t"
+      "v_max_i32_e32 %[v23], %[h2], %[h3]\n\t"
+      "v_cmp_gt_i32_e64 %[mh], %[v23], %[cv]\n\t"
+      "v_max_i32_e32 %[cv], %[cv], %[v23]\n\t"
+      "v_cndmask_b32_e64 %[lx], %[x0], %[x1], %[m01]\n\t"
+      "v_cndmask_b32_e64 %[tx], %[x2], %[x3], %[m23]\n\t"
+      "v_max_i32_dpp %[r], %[cv], %[cv] quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+      "v_cndmask_b32_e64 %[ly], %[y0], %[y1], %[m01]\n\t"
+      "v_cndmask_b32_e64 %[ty], %[y2], %[y3], %[m23]\n\t"
+      "v_max_i32_dpp %[r], %[r], %[r] quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
+      "v_cndmask_b32_e64 %[lz], %[z0], %[z1], %[m01]\n\t"
+      "v_cndmask_b32_e64 %[tz], %[z2], %[z3], %[m23]\n\t"
+      "v_max_i32_dpp %[r], %[r], %[r] row_half_mirror row_mask:0xf bank_mask:0xf\n\t"
+      "v_cndmask_b32_e64 %[lk], %[k0], %[k1], %[m01]\n\t"
+      "v_cndmask_b32_e64 %[tk], %[k2], %[k3], %[m23]\n\t"
+      "v_max_i32_dpp %[r], %[r], %[r] row_mirror row_mask:0xf bank_mask:0xf\n\t"
+      "v_cndmask_b32_e64 %[lx], %[lx], %[tx], %[mh]\n\t"
+      "v_cndmask_b32_e64 %[ly], %[ly], %[ty], %[mh]\n\t"
+      "v_max_i32_dpp %[r], %[r], %[r] row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
+      "v_cndmask_b32_e64 %[lz], %[lz], %[tz], %[mh]\n\t"
+      "v_cndmask_b32_e64 %[lk], %[lk], %[tk], %[mh]\n\t"
+      "v_max_i32_dpp %[r], %[r], %[r] row_bcast:31 row_mask:0xc bank_mask:0xf\n\t"
+      "s_nop 0\n\t"
+      "v_readlane_b32 %[wm], %[r], 63"
+      : [m01] "=&s"(m01), [m23] "=&s"(m23), [mh] "=&s"(mh), [cv] "=&v"(cv),
+        [v23] "=&v"(v23), [r] "=&v"(r), [lx] "=&v"(lx), [ly] "=&v"(ly),
+        [lz] "=&v"(lz), [lk] "=&v"(lk), [tx] "=&v"(tx), [ty] "=&v"(ty),
+        [tz] "=&v"(tz), [tk] "=&v"(tk), [wm] "=s"(wm)
+      : [h0] "v"(hv[0]), [h1] "v"(hv[1]), [h2] "v"(hv[2]), [h3] "v"(hv[3]),
+        [x0] "v"(hx[0][0]), [x1] "v"(hx[0][1]), [x2] "v"(hx[1][0]), [x3] "v"(hx[1][1]),
+        [y0] "v"(hy[0][0]), [y1] "v"(hy[0][1]), [y2] "v"(hy[1][0]), [y3] "v"(hy[1][1]),
+        [z0] "v"(hz[0][0]), [z1] "v"(hz[0][1]), [z2] "v"(hz[1][0]), [z3] "v"(hz[1][1]),
+        [k0] "v"(hk[0]), [k1] "v"(hk[1]), [k2] "v"(hk[2]), [k3] "v"(hk[3]));
+}
+
+// publish pick L from the winning lane itself (exec = lane L only): its lx, ly, lz, lk are the
+// centre, written to the batch slot at LDS address va_c, then the count vcnt to va_n (DS
+// operations of one wave execute in order, so a reader of the count reads the centre). The
+// centre's coordinates come back to SGPRs inside the same block (v_readlane ignores exec), so
+// no wait states follow the exec restore; L comes from SALU (no lane-select wait).
+PN2_DEV void hot_publish(int L, int va_c, int va_n, int vcnt, float lx, float ly, float lz,
+                         int lk, float& cx, float& cy, float& cz) {
+  uint64_t sv;
+  asm volatile(
+      "s_mov_b64 %[sv], exec\n\t"
+      "s_lshl_b64 exec, 1, %[L]\n\t"
+      "ds_write_b32 %[a], %[x]\n\t"
+      "ds_write_b32 %[a], %[y] offset:4\n\t"
+      "ds_write_b32 %[a], %[z] offset:8\n\t"
+      "ds_write_b32 %[a], %[k] offset:12\n\t"
+      "ds_write_b32 %[c], %[n]\n\t"
+      "v_readlane_b32 %[cx], %[x], %[L]\n\t"
+      "v_readlane_b32 %[cy], %[y], %[L]\n\t"
+      "v_readlane_b32 %[cz], %[z], %[L]\n\t"
+      "s_mov_b64 exec, %[sv]"
+      : [sv] "=&s"(sv), [cx] "=&s"(cx), [cy] "=&s"(cy), [cz] "=&s"(cz)
+      : [L] "s"(L), [a] "v"(va_c), [c] "v"(va_n), [x] "v"(lx), [y] "v"(ly), [z] "v"(lz),
+        [k] "v"(lk), [n] "v"(vcnt)
+      : "memory", "scc");
+}
+
+// the hot values after the pick (cx, cy, cz): running min with the fp32 distance
+// ((dx*dx + dy*dy) + dz*dz), two entries per packed instruction
+template <int HP>
+PN2_DEV void hot_update(int (&hv)[2 * HP], const hf2 (&hx)[HP], const hf2 (&hy)[HP],
+                        const hf2 (&hz)[HP], float cx, float cy, float cz) {
+  const hf2 c2x = {cx, cx}, c2y = {cy, cy}, c2z = {cz, cz};
+#pragma unroll
+  for (int h = 0; h < HP; ++h) {
+    const hf2 dx = hx[h] - c2x, dy = hy[h] - c2y, dz = hz[h] - c2z;
+    const hf2 d = (dx * dx + dy * dy) + dz * dz;
+    hv[2 * h] = min(hv[2 * h], __float_as_int(d.x));
+    hv[2 * h + 1] = min(hv[2 * h + 1], __float_as_int(d.y));
+  }
+}
+
 // The cold waves' wait for published centres is bounded (the hot wave always ends its batch,
 // so the bound is never reached in a correct run: ~0.1 s of polling against ~25 us per batch).
 // Reaching it stores PN2_FAULT_FPS_POLL into *fault (the host reports PN2_EFAULT); a build
@@ -614,51 +707,7 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
             float lx, ly, lz;
             uint64_t m01 = 0, m23 = 0, mh = 0;
             if constexpr (HQ == 4) {
-              // the lane's best entry (value desc, then entry order = tie order: strict '>'
-              // keeps the lower entry) and its coordinates and index, interleaved with the
-              // wave max (DPP rows, then row_bcast:15 / :31 into lane 63): the selects fill
-              // the DPP read-after-write wait states (2 per step) that were s_nop before.
-              // Wait states inside the block: VALU-written SGPR mask -> v_cndmask 2, DPP
-              // source 2, readlane source 1.
-              int v23, r;
-              float tx, ty, tz;
-              int tk;
-              asm volatile(
-                  "v_cmp_gt_i32_e64 %[m01], %[h1], %[h0]\n\t"
-                  "v_cmp_gt_i32_e64 %[m23], %[h3], %[h2]\n\t"
-                  "v_max_i32_e32 %[cv], %[h0], %[h1]\n\t"
-                  "v_max_i32_e32 %[v23], %[h2], %[h3]\n\t"
-                  "v_cmp_gt_i32_e64 %[mh], %[v23], %[cv]\n\t"
-                  "v_max_i32_e32 %[cv], %[cv], %[v23]\n\t"
-                  "v_cndmask_b32_e64 %[lx], %[x0], %[x1], %[m01]\n\t"
-                  "v_cndmask_b32_e64 %[tx], %[x2], %[x3], %[m23]\n\t"
-                  "v_max_i32_dpp %[r], %[cv], %[cv] quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
-                  "v_cndmask_b32_e64 %[ly], %[y0], %[y1], %[m01]\n\t"
-                  "v_cndmask_b32_e64 %[ty], %[y2], %[y3], %[m23]\n\t"
-                  "v_max_i32_dpp %[r], %[r], %[r] quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n\t"
-                  "v_cndmask_b32_e64 %[lz], %[z0], %[z1], %[m01]\n\t"
-                  "v_cndmask_b32_e64 %[tz], %[z2], %[z3], %[m23]\n\t"
-                  "v_max_i32_dpp %[r], %[r], %[r] row_half_mirror row_mask:0xf bank_mask:0xf\n\t"
-                  "v_cndmask_b32_e64 %[lk], %[k0], %[k1], %[m01]\n\t"
-                  "v_cndmask_b32_e64 %[tk], %[k2], %[k3], %[m23]\n\t"
-                  "v_max_i32_dpp %[r], %[r], %[r] row_mirror row_mask:0xf bank_mask:0xf\n\t"
-                  "v_cndmask_b32_e64 %[lx], %[lx], %[tx], %[mh]\n\t"
-                  "v_cndmask_b32_e64 %[ly], %[ly], %[ty], %[mh]\n\t"
-                  "v_max_i32_dpp %[r], %[r], %[r] row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
-                  "v_cndmask_b32_e64 %[lz], %[lz], %[tz], %[mh]\n\t"
-                  "v_cndmask_b32_e64 %[lk], %[lk], %[tk], %[mh]\n\t"
-                  "v_max_i32_dpp %[r], %[r], %[r] row_bcast:31 row_mask:0xc bank_mask:0xf\n\t"
-                  "s_nop 0\n\t"
-                  "v_readlane_b32 %[wm], %[r], 63"
-                  : [m01] "=&s"(m01), [m23] "=&s"(m23), [mh] "=&s"(mh), [cv] "=&v"(cv),
-                    [v23] "=&v"(v23), [r] "=&v"(r), [lx] "=&v"(lx), [ly] "=&v"(ly),
-                    [lz] "=&v"(lz), [lk] "=&v"(lk), [tx] "=&v"(tx), [ty] "=&v"(ty),
-                    [tz] "=&v"(tz), [tk] "=&v"(tk), [wm] "=s"(wm)
-                  : [h0] "v"(hv[0]), [h1] "v"(hv[1]), [h2] "v"(hv[2]), [h3] "v"(hv[3]),
-                    [x0] "v"(hx[0][0]), [x1] "v"(hx[0][1]), [x2] "v"(hx[1][0]), [x3] "v"(hx[1][1]),
-                    [y0] "v"(hy[0][0]), [y1] "v"(hy[0][1]), [y2] "v"(hy[1][0]), [y3] "v"(hy[1][1]),
-                    [z0] "v"(hz[0][0]), [z1] "v"(hz[0][1]), [z2] "v"(hz[1][0]), [z3] "v"(hz[1][1]),
-                    [k0] "v"(hk[0]), [k1] "v"(hk[1]), [k2] "v"(hk[2]), [k3] "v"(hk[3]));
+              hot_best4(hv, hx, hy, hz, hk, cv, lx, ly, lz, lk, wm, m01, m23, mh);
             } else {
               const bool b01 = hv[1] > hv[0];
               cv = b01 ? hv[1] : hv[0];
@@ -690,42 +739,10 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
               const uint32_t km = ~uniform_u32(wave_max_u32(cv == wm ? ~ck : 0u));
               L = (int)__builtin_ctzll(__builtin_amdgcn_ballot_w64(cv == wm && ck == km));
             }
-            // publish from the winning lane itself (exec = lane L only): its lx, ly, lz, lk are
-            // the centre, so neither a readlane of the index nor moves of the SGPR copies into
-            // lane 0 are needed; the count follows the centre (DS operations of one wave
-            // execute in order). The centre's coordinates are read back (v_readlane ignores
-            // exec) inside the same block, so no wait states follow the exec restore; L comes
-            // from SALU (no lane-select wait), and the first use of cx is 3 instructions on.
             float cx, cy, cz;
-            {
-              uint64_t sv;
-              asm volatile(
-                  "s_mov_b64 %[sv], exec\n\t"
-                  "s_lshl_b64 exec, 1, %[L]\n\t"
-                  "ds_write_b32 %[a], %[x]\n\t"
-                  "ds_write_b32 %[a], %[y] offset:4\n\t"
-                  "ds_write_b32 %[a], %[z] offset:8\n\t"
-                  "ds_write_b32 %[a], %[k] offset:12\n\t"
-                  "ds_write_b32 %[c], %[n]\n\t"
-                  "v_readlane_b32 %[cx], %[x], %[L]\n\t"
-                  "v_readlane_b32 %[cy], %[y], %[L]\n\t"
-                  "v_readlane_b32 %[cz], %[z], %[L]\n\t"
-                  "s_mov_b64 exec, %[sv]"
-                  : [sv] "=&s"(sv), [cx] "=&s"(cx), [cy] "=&s"(cy), [cz] "=&s"(cz)
-                  : [L] "s"(L), [a] "v"(va_c), [c] "v"(va_n), [x] "v"(lx), [y] "v"(ly),
-                    [z] "v"(lz), [k] "v"(lk), [n] "v"(vcnt)
-                  : "memory", "scc");
-            }
+            hot_publish(L, va_c, va_n, vcnt, lx, ly, lz, lk, cx, cy, cz);
             __builtin_amdgcn_sched_barrier(0);
-            // the hot update (the next pick depends on it)
-            const f2 c2x = {cx, cx}, c2y = {cy, cy}, c2z = {cz, cz};
-#pragma unroll
-            for (int h = 0; h < HP; ++h) {
-              const f2 dx = hx[h] - c2x, dy = hy[h] - c2y, dz = hz[h] - c2z;
-              const f2 d = (dx * dx + dy * dy) + dz * dz;
-              hv[2 * h] = min(hv[2 * h], __float_as_int(d.x));
-              hv[2 * h + 1] = min(hv[2 * h + 1], __float_as_int(d.y));
-            }
+            hot_update<HP>(hv, hx, hy, hz, cx, cy, cz);  // the next pick depends on it
             va_c += 16;
             vcnt += 1;
             if constexpr (CHECKED)

@@ -11,7 +11,10 @@
 // and torch.compile). Autograd for gather_point / group_point / three_interpolate (w.r.t.
 // the points only, tf_sampling.py:44-48, tf_grouping.py:42-46, tf_interpolate.py:29-34) and
 // attn_reduce is registered from Python (torch.library.register_autograd, _torch_ops.py).
-// No CPU kernel is registered: a CPU tensor fails in the dispatcher (no CPU fallback).
+// CPU kernels exist only for the three ops the reference itself runs on the CPU (ThreeNN,
+// ThreeInterpolate, ThreeInterpolateGrad: registered for DEVICE_CPU only,
+// tf_interpolate.cpp:187,222,262), through the host twins pn2cpu_* (csrc/cpu_interp.cpp);
+// every other op has no CPU kernel, so a CPU tensor fails in the dispatcher (no CPU fallback).
 #include <ATen/ATen.h>
 #include <c10/hip/HIPGuard.h>
 #include <c10/hip/HIPStream.h>
@@ -431,6 +434,48 @@ Tensor group_pool_hip(const Tensor& x_, const std::optional<Tensor>& gxyz_, int6
   return out;
 }
 
+// ------------------------------------------------------------------------- CPU kernels
+// (the reference's CPU-only ops; host twins in csrc/cpu_interp.cpp)
+Tensor host(const Tensor& t, const char* name, at::ScalarType dt) {
+  TORCH_CHECK(t.device().is_cpu(), name, " must be a CPU tensor here");
+  TORCH_CHECK_TYPE(t.scalar_type() == dt, name, " must be ", dt, ", got ", t.scalar_type());
+  return t.contiguous();
+}
+std::tuple<Tensor, Tensor> three_nn_cpu(const Tensor& xyz1_, const Tensor& xyz2_) {
+  chk_nn(xyz1_, xyz2_);
+  Tensor xyz1 = host(xyz1_, "xyz1", at::kFloat), xyz2 = host(xyz2_, "xyz2", at::kFloat);
+  const int B = I(xyz1.size(0)), n = I(xyz1.size(1)), m = I(xyz2.size(1));
+  Tensor dist = at::empty({B, n, 3}, f32(xyz1));
+  Tensor idx = at::empty({B, n, 3}, i32(xyz1));
+  check_rc(pn2cpu_three_nn(F(xyz1), F(xyz2), B, n, m, dist.data_ptr<float>(),
+                           idx.data_ptr<int32_t>()), "ThreeNN");
+  return {dist, idx};
+}
+Tensor three_interpolate_cpu(const Tensor& points_, const Tensor& idx_, const Tensor& weight_) {
+  chk_interp(points_, idx_, weight_, "ThreeInterpolate");
+  Tensor points = host(points_, "points", at::kFloat), idx = host(idx_, "idx", at::kInt);
+  Tensor weight = host(weight_, "weight", at::kFloat);
+  const int B = I(points.size(0)), m = I(points.size(1)), C = I(points.size(2)), n = I(idx.size(1));
+  Tensor out = at::empty({B, n, C}, f32(points));
+  check_rc(pn2cpu_three_interpolate(F(points), Ii(idx), F(weight), B, m, C, n,
+                                    out.data_ptr<float>()), "ThreeInterpolate");
+  return out;
+}
+Tensor three_interpolate_grad_cpu(const Tensor& points, const Tensor& idx_, const Tensor& weight_,
+                                  const Tensor& grad_out_) {
+  chk_interp(points, idx_, weight_, "ThreeInterpolateGrad");
+  const int B = I(points.size(0)), m = I(points.size(1)), C = I(points.size(2)), n = I(idx_.size(1));
+  TORCH_CHECK_VALUE(grad_out_.dim() == 3 && grad_out_.size(0) == B && grad_out_.size(1) == n &&
+                        grad_out_.size(2) == C,  // tf_interpolate.cpp:243
+                    "ThreeInterpolateGrad expects (b,n,c) grad_out shape");
+  Tensor idx = host(idx_, "idx", at::kInt), weight = host(weight_, "weight", at::kFloat);
+  Tensor grad_out = host(grad_out_, "grad_out", at::kFloat);
+  Tensor gp = at::empty({B, m, C}, f32(grad_out));
+  check_rc(pn2cpu_three_interpolate_grad(F(grad_out), Ii(idx), F(weight), B, n, C, m,
+                                         gp.data_ptr<float>()), "ThreeInterpolateGrad");
+  return gp;
+}
+
 // ------------------------------------------------------------------------- Meta kernels
 at::TensorOptions mf(const Tensor& t) { return t.options().dtype(at::kFloat); }
 at::TensorOptions mi(const Tensor& t) { return t.options().dtype(at::kInt); }
@@ -576,6 +621,12 @@ TORCH_LIBRARY_IMPL(pn2, CUDA, m) {
   m.impl("attn_reduce", &attn_reduce_hip);
   m.impl("attn_reduce_grad", &attn_reduce_grad_hip);
   m.impl("group_pool", &group_pool_hip);
+}
+
+TORCH_LIBRARY_IMPL(pn2, CPU, m) {
+  m.impl("three_nn", &three_nn_cpu);
+  m.impl("three_interpolate", &three_interpolate_cpu);
+  m.impl("three_interpolate_grad", &three_interpolate_grad_cpu);
 }
 
 TORCH_LIBRARY_IMPL(pn2, Meta, m) {

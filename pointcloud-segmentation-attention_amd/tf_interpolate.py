@@ -1,13 +1,25 @@
 """three_nn / three_interpolate — drop-in for
 pointnet2_tensorflow/tf_ops/interpolation_3d/tf_interpolate.py (same names, argument order,
 shapes, dtypes and error messages). The reference registers these ops for DEVICE_CPU only
-(tf_interpolate.cpp:187,222,262); here they are gfx950 kernels and the data never leaves HBM. Reference-signature calls go
+(tf_interpolate.cpp:187,222,262); here they are gfx950 kernels and the data never leaves HBM
+(CPU tensors run the host twins pn2cpu_*, as the reference does). Reference-signature calls go
 through the torch.ops.pn2 operators (csrc/torch_ops.cpp; autograd for three_interpolate in
 _torch_ops.py); three_nn with caller-built grids calls the C ABI directly.
 """
 import torch
 
 from ._lib import InvalidArgumentError, check, device_tensor, lib, ptr, stream_of
+
+
+def _tensor(t, name, dtype):
+    """An op input: on the GPU (the HIP kernels), or on the CPU -- these three ops are the
+    reference's CPU-only ones (tf_interpolate.cpp:187,222,262), so CPU tensors run the host
+    twins pn2cpu_* (csrc/cpu_interp.cpp) through the ops' CPU kernels."""
+    if isinstance(t, torch.Tensor) and t.device.type == "cpu":
+        if t.dtype != dtype:
+            raise TypeError(f"{name} must be {dtype}, got {t.dtype}")
+        return t.contiguous()
+    return device_tensor(t, name, dtype)
 from ._torch_ops import call
 from .grid import PointGrid
 
@@ -39,8 +51,14 @@ def three_nn(xyz1, xyz2, known_grid=None, unknown_grid=None):
         raise InvalidArgumentError("ThreeNN expects (b,n,3) xyz1 shape.")
     if xyz2.dim() != 3 or xyz2.shape[2] != 3:  # tf_interpolate.cpp:168
         raise InvalidArgumentError("ThreeNN expects (b,m,3) xyz2 shape.")
-    xyz1 = device_tensor(xyz1, "xyz1", torch.float32)
-    xyz2 = device_tensor(xyz2, "xyz2", torch.float32)
+    xyz1 = _tensor(xyz1, "xyz1", torch.float32)
+    xyz2 = _tensor(xyz2, "xyz2", torch.float32)
+    if xyz1.device != xyz2.device:
+        raise RuntimeError("ThreeNN: xyz1 and xyz2 must be on the same device")
+    if xyz1.device.type == "cpu":  # the reference's own placement (DEVICE_CPU only)
+        if known_grid is not None or unknown_grid is not None:
+            raise RuntimeError("ThreeNN grids are GPU structures")
+        return tuple(call("three_nn", xyz1, xyz2))
     if known_grid is None and unknown_grid is None:  # the op picks the grid search itself
         return tuple(call("three_nn", xyz1, xyz2))
     B, n, m = int(xyz1.shape[0]), int(xyz1.shape[1]), int(xyz2.shape[1])
@@ -77,9 +95,9 @@ def three_interpolate_grad(points, idx, weight, grad_out):
     B, m, C = (int(s) for s in points.shape)
     if tuple(grad_out.shape) != (B, idx.shape[1], C):  # :243
         raise InvalidArgumentError("ThreeInterpolateGrad expects (b,n,c) grad_out shape")
-    return call("three_interpolate_grad", points, device_tensor(idx, "idx", torch.int32),
-                                        device_tensor(weight, "weight", torch.float32),
-                                        device_tensor(grad_out, "grad_out", torch.float32))
+    return call("three_interpolate_grad", points, _tensor(idx, "idx", torch.int32),
+                                        _tensor(weight, "weight", torch.float32),
+                                        _tensor(grad_out, "grad_out", torch.float32))
 
 
 def three_interpolate(points, idx, weight):
@@ -93,9 +111,9 @@ def three_interpolate(points, idx, weight):
         out: (b,n,c) float32 array, interpolated point values — differentiable w.r.t. points
     """
     _check_interp(points, idx, weight)
-    return call("three_interpolate", device_tensor(points, "points", torch.float32),
-                                   device_tensor(idx, "idx", torch.int32),
-                                   device_tensor(weight, "weight", torch.float32))
+    return call("three_interpolate", _tensor(points, "points", torch.float32),
+                                   _tensor(idx, "idx", torch.int32),
+                                   _tensor(weight, "weight", torch.float32))
 
 
 def idw_weights(dist):

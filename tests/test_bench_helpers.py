@@ -27,14 +27,24 @@ def test_pmc_traffic_of_the_sa1_sampler(bench):
 
 
 def test_latency_of_the_sa1_sampler(bench):
-    v = bench.sa1_latency("cfg2", 0.47, 1024)
+    v = bench.sa1_latency("cfg2", 0.47, 1024, 8192)
     assert abs(v["ns_per_pick"] - 0.47e6 / 1023) < 1e-6
     # the culled sampler's stamp summary: hot pick loop + per-round refreshes + setup
     assert v["rounds"] > 0 and v["hot_cycles_per_pick"] > 0 and v["source"].endswith(".json")
-    assert "rounds" not in bench.sa1_latency("cfg5", 1.3, 512)  # a different sampler
+    # the latency floor (tools/ubench/pick_floor.hip): below the measured costs, and the
+    # launch floor composes setup + (M - 1) picks + rounds
+    assert 0 < v["floor_cycles_per_pick"] <= v["floor_pick_step_cycles"] <= v["hot_cycles_per_pick"]
+    assert 0 < v["floor_round_cycles"] <= v["round_cycles"]
+    want = v["floor_setup_cycles"] + 1023 * v["floor_cycles_per_pick"] + \
+        v["rounds"] * v["floor_round_cycles"]
+    assert abs(v["floor_launch_cycles"] - want) < 1e-6
+    assert 0 < v["frac_pick"] <= 1 and 0 < v["frac_round"] <= 1
+    assert "rounds" not in bench.sa1_latency("cfg5", 1.3, 512, 16384)  # a different sampler
 
 
 def test_cpu_baseline_leg(bench):
     r = bench.cpu_baseline("cfg2", 16, 0.2, 2)
     assert r["kind"] == "port" and r["cores"] == 2 and r["value"] > 0
     assert r["unit"] == "clouds/s"
+    assert r["value_all_cores_at_measured_efficiency"] == pytest.approx(
+        r["value_all_cores_extrapolated"] * r["scaling_efficiency_1_to_threads"])

@@ -16,7 +16,7 @@ HEADER = os.path.join(ROOT, "include", "pn2hip.h")
 def header_functions():
     text = open(HEADER).read()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return sorted(set(re.findall(r"\b(pn2_[a-z0-9_]+)\s*\(", text)))
+    return sorted(set(re.findall(r"\b(pn2(?:cpu)?_[a-z0-9_]+)\s*\(", text)))
 
 
 def test_header_declares_the_boundary():

@@ -31,11 +31,13 @@ def test_reference_error_messages(pn2):
 
 
 def test_no_cpu_fallback(pn2):
-    """Well-formed CPU tensors are refused: the product path is the HIP library only."""
+    """Well-formed CPU tensors are refused: the product path is the HIP library only (except
+    ThreeNN / ThreeInterpolate(+Grad), the reference's own CPU-only ops, which run the host
+    twins pn2cpu_*: tests/test_cpu_interp.py)."""
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         pn2.tf_sampling.farthest_point_sample(4, torch.zeros(1, 10, 3))
     with pytest.raises(RuntimeError, match="no CPU fallback"):
-        pn2.tf_interpolate.three_nn(torch.zeros(1, 10, 3), torch.zeros(1, 4, 3))
+        pn2.tf_grouping.query_ball_point(0.2, 8, torch.zeros(1, 10, 3), torch.zeros(1, 4, 3))
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         pn2.attention_layer.attention_reduce(torch.zeros(1, 2, 8), torch.zeros(1, 2, 4, 8),
                                              torch.zeros(1, 2, 4, 8))

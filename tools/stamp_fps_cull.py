@@ -14,7 +14,7 @@ sys.path.insert(0, ROOT); sys.path.insert(0, os.path.join(ROOT, "tests"))
 import torch  # noqa: E402
 from conftest import PKG_NAME  # noqa: E402
 pkg = importlib.import_module(PKG_NAME)
-L = ctypes.CDLL(os.path.join(ROOT, "tools", "fps_lab", "libpn2fpslab.so"))
+L = ctypes.CDLL(os.path.join(ROOT, "tools", "fps_stamp", "libpn2fpsstamp.so"))
 L.pn2_fps_cull_stamp.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                  ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
 import argparse
@@ -86,7 +86,7 @@ for kind in ("scannet", "uniform"):
         setup = float(a[:, 1:, 7].mean())  # cold waves' phase 7 = setup only
         hot_total = float(a[:, 0, 7].mean()) - setup
         SUMMARY.update({
-            "workload": "B=16 ScanNet crops, 8192 -> 1024 (cfg2 SA1), stamped lab build",
+            "workload": "B=16 ScanNet crops, 8192 -> 1024 (cfg2 SA1), stamped build (tools/fps_stamp)",
             "kernel_cycles": float(st[:, 0].mean()), "setup_cycles": setup,
             "hot_cycles_per_pick": hot_total / float(st[:, 4].mean()),
             "rounds": float(st[:, 1].mean()), "stalls": float(st[:, 2].mean()),
