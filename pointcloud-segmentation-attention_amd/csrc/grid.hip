@@ -171,11 +171,15 @@ __global__ __launch_bounds__(kBuildBlock) void grid_build_kernel(const float* __
 template <int BLOCK>
 __global__ __launch_bounds__(BLOCK) void ball_query_grid_kernel(
     const char* __restrict__ grid, const float* __restrict__ xyz2, int N, int M, float radius,
-    float thresh, int ns, int qpb, int words, int32_t* __restrict__ idx,
+    float thresh, int ns, int qpb, int words, int gx, int nblk, int32_t* __restrict__ idx,
     int32_t* __restrict__ pts_cnt) {
   constexpr int NW = BLOCK / kWave;
   extern __shared__ uint32_t bits[];  // NW x words
-  const int b = blockIdx.y;
+  // XCD-aware order (common.h): each XCD takes a contiguous range of (cloud, query chunk)
+  // blocks, so a cloud's grid is fetched into one L2, not into all eight
+  const int lb = xcd_block((int)blockIdx.x, nblk);
+  if (lb >= nblk) return;
+  const int b = lb / gx, bx = lb - b * gx;
   const int t = threadIdx.x, lane = t & (kWave - 1), w = t / kWave;
   const GridView g = grid_view(grid, b, N);
   const GridHdr& h = g.h;
@@ -184,8 +188,8 @@ __global__ __launch_bounds__(BLOCK) void ball_query_grid_kernel(
   uint32_t* mine = bits + (size_t)w * words;
   const int wpl = (words + kWave - 1) / kWave;  // bitmask words per lane, in lane order
 
-  const int q_end = min(M, (int)(blockIdx.x + 1) * qpb);
-  for (int q = blockIdx.x * qpb + w; q < q_end; q += NW) {
+  const int q_end = min(M, (bx + 1) * qpb);
+  for (int q = bx * qpb + w; q < q_end; q += NW) {
     for (int i = lane; i < words; i += kWave) mine[i] = 0u;
     const float* Q = xyz2 + ((size_t)b * M + q) * 3;
     const float qx = Q[0], qy = Q[1], qz = Q[2];
@@ -274,9 +278,12 @@ int pn2_ball_query_grid(const void* grid, const float* xyz2, int B, int N, int M
   qpb = ((qpb + NW - 1) / NW) * NW;
   const unsigned gx = (unsigned)((M + qpb - 1) / qpb);
   const size_t lds = (size_t)NW * (words > 0 ? words : 1) * 4;
-  hipLaunchKernelGGL((pn2::ball_query_grid_kernel<BLOCK>), dim3(gx, B), dim3(BLOCK), lds,
-                     (hipStream_t)stream, (const char*)grid, xyz2, N, M, radius,
-                     pn2_ball_threshold(radius), nsample, (int)qpb, words, idx, pts_cnt);
+  const long long nblk = (long long)gx * B;
+  if (nblk > INT32_MAX - pn2::kXcds) return PN2_EINVAL;
+  hipLaunchKernelGGL((pn2::ball_query_grid_kernel<BLOCK>), dim3(pn2::xcd_grid(nblk)), dim3(BLOCK),
+                     lds, (hipStream_t)stream, (const char*)grid, xyz2, N, M, radius,
+                     pn2_ball_threshold(radius), nsample, (int)qpb, words, (int)gx, (int)nblk,
+                     idx, pts_cnt);
   PN2_RETURN_LAUNCH();
 }
 

@@ -32,13 +32,17 @@ __global__ __launch_bounds__(kBlock) void group_concat_kernel(
     const float* __restrict__ xyz, const float* __restrict__ points,
     const float* __restrict__ new_xyz, const int32_t* __restrict__ idx, int N, int C, int M,
     int ns, int Cout, int layout, int rows, FastDiv div_cout, FastDiv div_ns, FastDiv div_m,
-    uint32_t total_rows, float* __restrict__ grouped_xyz, float* __restrict__ out) {
+    uint32_t total_rows, int tiles, float* __restrict__ grouped_xyz, float* __restrict__ out) {
   // the tile's neighbour indices are staged in LDS first (one coalesced load per row), and a
   // thread then issues the gathers of kU elements before it stores any: one element at a time
   // made each element two dependent memory trips (idx, then the gather), latency-bound
   constexpr int kU = 4;
   __shared__ int s_idx[kTileElems];
-  const uint32_t r0 = blockIdx.x * (uint32_t)rows;
+  // XCD-aware order (common.h): each XCD takes a contiguous range of tiles, so the rows of a
+  // cloud's xyz / points are fetched into one L2, not into all eight
+  const int tile = xcd_block((int)blockIdx.x, tiles);
+  if (tile >= tiles) return;  // padding blocks leave before the barrier
+  const uint32_t r0 = (uint32_t)tile * (uint32_t)rows;
   const int nrows = (int)min((uint32_t)rows, total_rows - r0);
   const int elems = nrows * Cout;
   for (int rl = threadIdx.x; rl < nrows; rl += kBlock) s_idx[rl] = idx[r0 + rl];
@@ -130,13 +134,13 @@ int launch_group(const float* xyz, const float* points, const float* new_xyz, co
     const int nb = B - b0 < chunk ? B - b0 : chunk;
     const long long total_rows = (long long)nb * M * ns;
     const long long tiles = (total_rows + rows - 1) / rows;
-    hipLaunchKernelGGL(group_concat_kernel, dim3((unsigned)tiles), dim3(kBlock), 0, s,
+    hipLaunchKernelGGL(group_concat_kernel, dim3(xcd_grid(tiles)), dim3(kBlock), 0, s,
                        xyz ? xyz + (size_t)b0 * N * 3 : nullptr,
                        points ? points + (size_t)b0 * N * C : nullptr,
                        new_xyz ? new_xyz + (size_t)b0 * M * 3 : nullptr,
                        idx + (size_t)b0 * M * ns, N, C, M, ns, Cout, layout, rows,
                        make_fastdiv((uint32_t)Cout), make_fastdiv((uint32_t)ns),
-                       make_fastdiv((uint32_t)M), (uint32_t)total_rows,
+                       make_fastdiv((uint32_t)M), (uint32_t)total_rows, (int)tiles,
                        grouped_xyz ? grouped_xyz + (size_t)b0 * M * ns * 3 : nullptr,
                        out + (size_t)b0 * M * ns * Cout);
     hipError_t e = hipGetLastError();
