@@ -354,13 +354,15 @@ def main():
     # clouds/s: with its side lanes fully concurrent the latency-bound sampler slows 0.715 ->
     # 0.80 ms), the whole model with high (its side lanes carry most of the work). "auto" =
     # default for the geometric step, high for the whole model.
-    hi_lane0 = torch.cuda.Stream(device=dev, priority=-1)
-
+    # Created only when used: a stream made before the step's side lanes takes a hardware
+    # queue, and one of the side lanes then shares one (stack.side_stream).
     def measure(model, steps, warmup):
         prio = args.lane0_priority
         if prio == "auto":
             prio = "high" if model else "default"
-        with torch.cuda.stream(hi_lane0 if prio == "high" else torch.cuda.current_stream(dev)):
+        lane0 = (torch.cuda.Stream(device=dev, priority=-1) if prio == "high"
+                 else torch.cuda.current_stream(dev))
+        with torch.cuda.stream(lane0):
             return _measure(model, steps, warmup) + (prio,)
 
     def _measure(model, steps, warmup):
@@ -471,7 +473,7 @@ def main():
                        "samplers: direct launches; side lanes: hipGraph replay",
                        "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "0")),
                        "lane0_priority": prio0,
-                       "streams": ("SA1 sampler + 4 side streams" if overlap else "one stream")
+                       "streams": ("SA1 sampler + 3 side streams" if overlap else "one stream")
                        + (f", steps software-pipelined over {args.sets} buffer sets" if pipelined else "")},
             "roofline": dict(
                 {"kernel": f"SA1 sampler (FPS + gather fused): {B} clouds x {N} pts -> {M1}, "

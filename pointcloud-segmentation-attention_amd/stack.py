@@ -35,7 +35,7 @@ SSG_SA_MLP = ((32, 32, 64), (64, 64, 128), (128, 128, 256), (256, 256, 512))
 SSG_FP_MLP = ((256, 256), (256, 256), (256, 128), (128, 128, 128))
 NUM_CLASSES = 21  # ScanNet (pointnet2_sem_seg_attention.py:17)
 
-NSIDE = 4  # side streams of the overlapped step (SSG)
+NSIDE = 4  # side streams of the whole-model step (the geometric steps use 3)
 
 CONFIGS = {
     # name: (points per cloud, kind, with_features, attention)
@@ -128,7 +128,8 @@ _SIDE = {}
 def side_stream(dev, lane):
     """The process-wide side stream of `lane` on `dev`: every Step shares them, so the
     sampler chain (the current stream) and the side lanes stay on distinct hardware queues
-    (HIP maps streams to GPU_MAX_HW_QUEUES queues round-robin at creation)."""
+    (HIP gives each new stream a new hardware queue up to GPU_MAX_HW_QUEUES, then shares the
+    least-used ones): the first Step creates lanes 1-3 before any other stream exists."""
     key = (str(dev), lane)
     if key not in _SIDE:
         _SIDE[key] = torch.cuda.Stream(device=dev)
@@ -151,11 +152,14 @@ class Step:
 
     The FPS samplers form a serial chain (each samples the previous layer's output) that
     keeps only B workgroups busy. The SA1 sampler (~85 % of the chain) runs on lane 0 with
-    nothing else in its way; SA2..SA4's samplers run fused on lane 4, so with pipelining the
+    nothing else in its way; SA2..SA4's samplers run fused on lane 3, so with pipelining the
     next step's SA1 sampler follows this one back to back. Everything that hangs off sampler
     i -- layer i's ball query / grouping / attention (lane 1) and the FP layer that
-    interpolates onto level i-1 (lanes 2-3; MSG: one lane per radius) -- waits for that
-    sampler only and runs concurrently with the samplers after it and with each other.
+    interpolates onto level i-1 (lane 2; MSG: radius 0 on lane 1, the others on lane 2) --
+    waits for that sampler only and runs concurrently with the samplers after it and with
+    each other. Three side lanes: with the current stream that is one stream per hardware
+    queue of the box (GPU_MAX_HW_QUEUES = 4); a fourth side lane shared a queue with lane 1
+    and serialised the FPS chain behind cfg3's attention.
     The SA1 ball-query grid needs only the input cloud and is built on lane 1 while SA1 is
     sampled. Lanes join lane 0 at the end of the step.
 
@@ -248,21 +252,21 @@ class Step:
             # Both are direct launches into fixed buffers.
             tasks.append(Task("fps1", 0, (), lambda: tf_sampling.farthest_point_sample_chain(
                 npoints[:1], xyz, out=v["chain"][:1]), direct=True))
-            tasks.append(Task("fps234", 4, ("fps1",), lambda: tf_sampling.farthest_point_sample_chain(
+            tasks.append(Task("fps234", 3, ("fps1",), lambda: tf_sampling.farthest_point_sample_chain(
                 npoints[1:], v["xyz"][1], out=v["chain"][1:]), direct=True))
             sampled = ("fps1", "fps234", "fps234", "fps234")
         else:
-            # lane 0: SA1's sampler alone; lane 4: SA2..SA4's samplers as one task
+            # lane 0: SA1's sampler alone; lane 3: SA2..SA4's samplers as one task
             tasks.append(Task("fps1", 0, (), fps(0)))
-            tasks.append(Task("fps234", 4, ("fps1",), lambda: [fps(i)() for i in (1, 2, 3)]))
+            tasks.append(Task("fps234", 3, ("fps1",), lambda: [fps(i)() for i in (1, 2, 3)]))
             sampled = ("fps1", "fps234", "fps234", "fps234")
         tasks.append(Task("sa1", 1, (sampled[0],), sa(0)))
         tasks.append(Task("fp4", 2, (sampled[0],) + grid_dep, fp(0)))
         for i in (1, 2, 3):
             tasks.append(Task(f"sa{i + 1}", 1, (sampled[i],), sa(i)))
         tasks.append(Task("fp3", 2, (sampled[1],), fp(1)))
-        tasks.append(Task("fp2", 3, (sampled[2],), fp(2)))
-        tasks.append(Task("fp1", 3, (sampled[3],), fp(3)))
+        tasks.append(Task("fp2", 2, (sampled[2],), fp(2)))
+        tasks.append(Task("fp1", 2, (sampled[3],), fp(3)))
         return tasks
 
     def _tasks_ssg_model(self):
@@ -369,15 +373,15 @@ class Step:
                                                              want_grouped_xyz=False)[0]
             return f
 
-        nr = max(len(sa_[1]) for sa_ in MSG_SA)
         for i in range(len(MSG_SA)):
-            # lane 0: SA1's sampler only; the later samplers run on lane nr + 1 after it
+            # lane 0: SA1's sampler only; the later samplers run on lane 3 after it; radius 0's
+            # grouping on lane 1, the other radii on lane 2
             if i == 0:
                 tasks.append(Task("fps1", 0, (), fps(0), direct=True))
             else:
-                tasks.append(Task(f"fps{i + 1}", nr + 1, (f"fps{i}",), fps(i), direct=True))
+                tasks.append(Task(f"fps{i + 1}", 3, (f"fps{i}",), fps(i), direct=True))
             for r in range(len(MSG_SA[i][1])):
-                tasks.append(Task(f"sa{i + 1}_{r}", 1 + r, (f"fps{i + 1}",), grp(i, r)))
+                tasks.append(Task(f"sa{i + 1}_{r}", 1 + min(r, 1), (f"fps{i + 1}",), grp(i, r)))
         return tasks
 
     def outputs(self):
