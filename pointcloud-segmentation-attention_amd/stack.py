@@ -187,6 +187,12 @@ class Step:
             dev = inp["xyz"].device
             self.streams = [None] + (list(streams[1:self.nlanes]) if streams else
                                      [side_stream(dev, lane) for lane in range(1, self.nlanes)])
+            # HIP binds a stream to a hardware queue when the stream is first used: use the
+            # lanes now, in order, so that they (not the warm-up or capture streams made later)
+            # get the queues the current stream does not hold
+            main = torch.cuda.current_stream(dev)
+            for st in self.streams[1:]:
+                st.wait_stream(main)
             self.done = {t.name: torch.cuda.Event() for t in self.tasks}
             self.lane_done = [torch.cuda.Event() for _ in range(self.nlanes)]
 

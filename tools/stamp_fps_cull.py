@@ -4,7 +4,9 @@ build), B = 16 SA1 clouds, index-exact against the v9 sampler: refreshes, stalls
 (cell, centre) pairs, cycles per phase (wave 0 and the mean of the other waves), per-wave
 group costs and the per-round event breakdown.
 
-    python tools/stamp_fps_cull.py [--json profiles/r2/sa1_cull_stamps.json]
+    python tools/stamp_fps_cull.py [--msg] [--json profiles/r2/sa1_cull_stamps.json]
+
+--msg: the MSG SA1 size (B = 8, 16384 -> 512, coordinates read from L2).
 
 --json writes the ScanNet summary bench.py reports as roofline.latency."""
 import ctypes, importlib, json, os, sys
@@ -15,25 +17,27 @@ import torch  # noqa: E402
 from conftest import PKG_NAME  # noqa: E402
 pkg = importlib.import_module(PKG_NAME)
 L = ctypes.CDLL(os.path.join(ROOT, "tools", "fps_stamp", "libpn2fpsstamp.so"))
-L.pn2_fps_cull_stamp.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
-                                 ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+for _f in (L.pn2_fps_cull_stamp, L.pn2_fps_cull_stamp_msg):
+    _f.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                   ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
 import argparse
 ap = argparse.ArgumentParser()
 ap.add_argument("--json")
+ap.add_argument("--msg", action="store_true")
 ARGS = ap.parse_args()
 SUMMARY = {}
 NAMES = ["cold_async", "tmax", "B_A", "out_count", "B_B", "append", "B_C", "hot_setup"]
 dev = torch.device("cuda:0")
 lib = pkg._lib.lib()
 for kind in ("scannet", "uniform"):
-    B, N, M = 16, 8192, 1024
+    B, N, M = (8, 16384, 512) if ARGS.msg else (16, 8192, 1024)
     x = torch.from_numpy(pkg.synth.batch(range(B), N, kind)[0]).to(dev)
     idx = torch.empty((B, M), dtype=torch.int32, device=dev)
     buf = np.zeros(16 * 16 * 8, np.uint64)
     stats = np.zeros(16 * 8, np.uint64)
     for _ in range(2):
-        rc = L.pn2_fps_cull_stamp(x.data_ptr(), B, N, M, idx.data_ptr(), buf.ctypes.data,
-                                  stats.ctypes.data)
+        rc = (L.pn2_fps_cull_stamp_msg if ARGS.msg else L.pn2_fps_cull_stamp)(
+            x.data_ptr(), B, N, M, idx.data_ptr(), buf.ctypes.data, stats.ctypes.data)
         assert rc == 0, rc
     ref = torch.empty((B, M), dtype=torch.int32, device=dev)
     rnx = torch.empty((B, M, 3), dtype=torch.float32, device=dev)
@@ -43,13 +47,13 @@ for kind in ("scannet", "uniform"):
     wv = np.zeros(16 * 16 * 4, np.uint64)
     L.pn2_fps_cull_waves.argtypes = [ctypes.c_void_p]
     assert L.pn2_fps_cull_waves(wv.ctypes.data) == 0
-    wv = wv.reshape(16, 16, 4).astype(np.float64)
+    wv = wv.reshape(16, 16, 4)[:B].astype(np.float64)
     print(json.dumps({"kind": kind, "per_wave_groups": [round(v) for v in wv[:, :, 0].mean(0)],
                       "per_wave_cyc_per_group": [round(v) for v in (wv[:, :, 1] / np.maximum(wv[:, :, 0], 1)).mean(0)],
                       "per_wave_pairs": [round(v) for v in wv[:, :, 2].mean(0)],
                       "per_wave_polls": [round(v) for v in wv[:, :, 3].mean(0)]}), flush=True)
-    a = buf.reshape(16, 16, 8).astype(np.float64)
-    st = stats.reshape(16, 8).astype(np.float64)
+    a = buf.reshape(16, 16, 8)[:B].astype(np.float64)
+    st = stats.reshape(16, 8)[:B].astype(np.float64)
     print(json.dumps({
         "kind": kind, "exact_vs_v9": bool(torch.equal(ref, idx)),
         "kernel_cycles": round(st[:, 0].mean()), "refresh": st[:, 1].mean(), "stall": st[:, 2].mean(),
@@ -86,7 +90,8 @@ for kind in ("scannet", "uniform"):
         setup = float(a[:, 1:, 7].mean())  # cold waves' phase 7 = setup only
         hot_total = float(a[:, 0, 7].mean()) - setup
         SUMMARY.update({
-            "workload": "B=16 ScanNet crops, 8192 -> 1024 (cfg2 SA1), stamped build (tools/fps_stamp)",
+            "workload": (f"B={B} ScanNet crops, {N} -> {M} ("
+                         + ("cfg5 MSG SA1" if ARGS.msg else "cfg2 SA1") + "), stamped build (tools/fps_stamp)"),
             "kernel_cycles": float(st[:, 0].mean()), "setup_cycles": setup,
             "hot_cycles_per_pick": hot_total / float(st[:, 4].mean()),
             "rounds": float(st[:, 1].mean()), "stalls": float(st[:, 2].mean()),
