@@ -289,6 +289,9 @@ def main():
                          "per bracketed step cost ~10 us of step time, DESIGN.md §5)")
     ap.add_argument("--sets", type=int, default=3,
                     help="buffer sets the pipelined steps rotate over (>= 2)")
+    ap.add_argument("--sampler-lanes", type=int, default=1,
+                    help="streams the pipelined steps' samplers alternate over (consecutive "
+                         "steps' samplers run at the same time on different CUs)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="join every step before the next (no overlap of step k's side work "
                          "with step k+1's samplers)")
@@ -374,6 +377,7 @@ def main():
         pipelined = overlap and not args.no_pipeline
         if pipelined:
             pipe = pkg.stack.Pipeline(inp, graphs=not args.eager, nsets=args.sets,
+                                      sampler_lanes=1 if model else args.sampler_lanes,
                                       private_streams=model)
         else:
             step = pkg.stack.Step(inp, overlap=overlap)
@@ -473,7 +477,10 @@ def main():
                        "samplers: direct launches; side lanes: hipGraph replay",
                        "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "0")),
                        "lane0_priority": prio0,
-                       "streams": ("SA1 sampler + 3 side streams" if overlap else "one stream")
+                       "streams": (("SA1 sampler + 3 side streams" if args.sampler_lanes <= 1 or args.model
+                                    else f"{args.sampler_lanes} sampler streams (consecutive steps' "
+                                    "samplers concurrent; SA2.. samplers behind SA1) + 2 side streams")
+                                   if overlap else "one stream")
                        + (f", steps software-pipelined over {args.sets} buffer sets" if pipelined else "")},
             "roofline": dict(
                 {"kernel": f"SA1 sampler (FPS + gather fused): {B} clouds x {N} pts -> {M1}, "

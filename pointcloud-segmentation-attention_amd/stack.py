@@ -171,7 +171,10 @@ class Step:
 
     SAMPLER = "fps1"
 
-    def __init__(self, inp, overlap=True, streams=None):
+    def __init__(self, inp, overlap=True, streams=None, chain_lane=3):
+        # chain_lane: the lane of the later samplers (SA2..SA4 / MSG SA2); 0 = behind the SA1
+        # sampler on its stream (Pipeline with several sampler lanes)
+        self.chain_lane = chain_lane if overlap else 0
         self.inp = inp
         self.kind = CONFIGS[inp["config"]][1]
         self.overlap = overlap and inp["xyz"].is_cuda
@@ -258,13 +261,13 @@ class Step:
             # Both are direct launches into fixed buffers.
             tasks.append(Task("fps1", 0, (), lambda: tf_sampling.farthest_point_sample_chain(
                 npoints[:1], xyz, out=v["chain"][:1]), direct=True))
-            tasks.append(Task("fps234", 3, ("fps1",), lambda: tf_sampling.farthest_point_sample_chain(
+            tasks.append(Task("fps234", self.chain_lane, ("fps1",), lambda: tf_sampling.farthest_point_sample_chain(
                 npoints[1:], v["xyz"][1], out=v["chain"][1:]), direct=True))
             sampled = ("fps1", "fps234", "fps234", "fps234")
         else:
             # lane 0: SA1's sampler alone; lane 3: SA2..SA4's samplers as one task
             tasks.append(Task("fps1", 0, (), fps(0)))
-            tasks.append(Task("fps234", 3, ("fps1",), lambda: [fps(i)() for i in (1, 2, 3)]))
+            tasks.append(Task("fps234", self.chain_lane, ("fps1",), lambda: [fps(i)() for i in (1, 2, 3)]))
             sampled = ("fps1", "fps234", "fps234", "fps234")
         tasks.append(Task("sa1", 1, (sampled[0],), sa(0)))
         tasks.append(Task("fp4", 2, (sampled[0],) + grid_dep, fp(0)))
@@ -385,7 +388,7 @@ class Step:
             if i == 0:
                 tasks.append(Task("fps1", 0, (), fps(0), direct=True))
             else:
-                tasks.append(Task(f"fps{i + 1}", 3, (f"fps{i}",), fps(i), direct=True))
+                tasks.append(Task(f"fps{i + 1}", self.chain_lane, (f"fps{i}",), fps(i), direct=True))
             for r in range(len(MSG_SA[i][1])):
                 tasks.append(Task(f"sa{i + 1}_{r}", 1 + min(r, 1), (f"fps{i + 1}",), grp(i, r)))
         return tasks
@@ -497,8 +500,8 @@ class GraphStep:
     on its lane's stream; replay() relaunches them with the same cross-stream events as the
     eager step. Inputs stay resident, outputs are overwritten in place at every replay."""
 
-    def __init__(self, inp, warmup=2, overlap=True, streams=None):
-        self.step = Step(inp, overlap=overlap, streams=streams)
+    def __init__(self, inp, warmup=2, overlap=True, streams=None, chain_lane=3):
+        self.step = Step(inp, overlap=overlap, streams=streams, chain_lane=chain_lane)
         dev = inp["xyz"].device
         warm = side_stream(dev, "warm")
         warm.wait_stream(torch.cuda.current_stream(dev))
@@ -553,9 +556,17 @@ class Pipeline:
     stream. Before a set is reused (step k + nsets) the HOST waits for that set's side lanes,
     so no buffer is overwritten while read and lane 0 carries no wait packet between
     samplers; with 3 sets the side work of a step has two sampler periods to finish. Every
-    step still does all of its work; run(k) returns after enqueueing, join() waits."""
+    step still does all of its work; run(k) returns after enqueueing, join() waits.
 
-    def __init__(self, inp, graphs=True, overlap=True, nsets=3, private_streams=False):
+    sampler_lanes > 1 (geometric steps): step k's samplers (SA1, then the later ones behind it
+    on the same stream) run on sampler stream k % sampler_lanes, so the samplers of
+    consecutive steps run at the same time on different CUs -- one sampler launch keeps B CUs
+    busy and the rest of the chip waits on its pick chain. The side lanes (1: ball query /
+    grouping / attention, 2: FP) are shared. Each stream is its own hardware queue:
+    1 + 2 + (sampler_lanes - 1) <= GPU_MAX_HW_QUEUES."""
+
+    def __init__(self, inp, graphs=True, overlap=True, nsets=3, private_streams=False,
+                 sampler_lanes=1):
         # private_streams: every buffer set gets its own side streams, so the side lanes of
         # consecutive steps overlap each other too (the whole-model step, whose lane-1 chain
         # of SA/FP layers is longer than a sampler period); otherwise the sets share them
@@ -566,12 +577,33 @@ class Pipeline:
                 return None
             return [None] + [side_stream(dev, (i, lane)) for lane in range(1, NSIDE + 1)]
 
-        mk = (lambda i: GraphStep(inp, overlap=overlap, streams=streams(i))) if graphs else \
-            (lambda i: Step(inp, overlap=overlap, streams=streams(i)))
+        multi = sampler_lanes > 1 and overlap and inp["xyz"].is_cuda and not private_streams
+        chain_lane = 0 if multi else 3
+        self.lane0 = [None]
+        if multi:
+            # queues go to streams in order of first use: the side lanes, then the extra
+            # sampler streams, all before the sets' warm-up and capture streams
+            cur = torch.cuda.current_stream(dev)
+            for lane in (1, 2):
+                side_stream(dev, lane).wait_stream(cur)
+            for i in range(1, sampler_lanes):
+                st = side_stream(dev, ("sampler", i))
+                st.wait_stream(cur)
+                self.lane0.append(st)
+        mk = (lambda i: GraphStep(inp, overlap=overlap, streams=streams(i), chain_lane=chain_lane)) \
+            if graphs else (lambda i: Step(inp, overlap=overlap, streams=streams(i),
+                                           chain_lane=chain_lane))
         self.sets = [mk(i) for i in range(max(2, nsets))]
         self.k = 0
 
     def run(self, sampler_events=None):
+        st = self.lane0[self.k % len(self.lane0)]
+        if st is not None:
+            with torch.cuda.stream(st):
+                return self._run(sampler_events)
+        return self._run(sampler_events)
+
+    def _run(self, sampler_events):
         s = self.sets[self.k % len(self.sets)]
         self.k += 1
         if isinstance(s, GraphStep):

@@ -115,19 +115,24 @@ def test_stack_full_size(env, config, B):
 
 
 @pytest.mark.timeout(300)
+@pytest.mark.parametrize("lanes", [1, 2])
 @pytest.mark.parametrize("config,B", CONFIGS)
-def test_pipeline_full_size(env, config, B):
+def test_pipeline_full_size(env, config, B, lanes):
     """What bench.py times: the software-pipelined hipGraph steps over 3 buffer sets, at the
-    BASELINE batch, after several rotations; the last step's outputs against the oracle."""
+    BASELINE batch, after several rotations, with one sampler stream or two (consecutive steps'
+    samplers concurrent); the last two steps' outputs (one per sampler stream) against the
+    oracle."""
     pkg, O, torch, dev = env
     inp = pkg.stack.make_inputs(config, list(range(100, 100 + B)), dev)
-    pipe = pkg.stack.Pipeline(inp, graphs=True, nsets=3)
+    pipe = pkg.stack.Pipeline(inp, graphs=True, nsets=3, sampler_lanes=lanes)
+    assert len(pipe.lane0) == lanes
     for _ in range(7):
         pipe.run()
     outs = pipe.join()
     torch.cuda.synchronize()
-    last = pipe.sets[(pipe.k - 1) % len(pipe.sets)]
-    check_step(O, config, inp, outs, last.intermediates())
+    for back in (1, 2):
+        s = pipe.sets[(pipe.k - back) % len(pipe.sets)]
+        check_step(O, config, inp, s.outs if back > 1 else outs, s.intermediates())
 
 
 @pytest.mark.timeout(300)
