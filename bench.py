@@ -292,6 +292,13 @@ def main():
     ap.add_argument("--sampler-lanes", type=int, default=1,
                     help="streams the pipelined steps' samplers alternate over (consecutive "
                          "steps' samplers run at the same time on different CUs)")
+    ap.add_argument("--private-side", action="store_true",
+                    help="every buffer set gets its own side streams (side work of consecutive "
+                         "steps runs concurrently; needs 1 + 2 x sets + sampler lanes - 1 "
+                         "hardware queues)")
+    ap.add_argument("--no-native-plan", action="store_true",
+                    help="enqueue each step with the Python task loop instead of one call into "
+                         "the native plan executor (include/pn2plan.h)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="join every step before the next (no overlap of step k's side work "
                          "with step k+1's samplers)")
@@ -378,7 +385,8 @@ def main():
         if pipelined:
             pipe = pkg.stack.Pipeline(inp, graphs=not args.eager, nsets=args.sets,
                                       sampler_lanes=1 if model else args.sampler_lanes,
-                                      private_streams=model)
+                                      private_streams=model or args.private_side,
+                                      native_plan=not args.no_native_plan)
         else:
             step = pkg.stack.Step(inp, overlap=overlap)
             graph = None if args.eager else pkg.stack.GraphStep(inp, overlap=overlap)
@@ -474,12 +482,15 @@ def main():
                        "clouds_per_gpu": B, "global_batch": world * B, "points": N,
                        "parallelism": f"dp{world} (batch split)",
                        "launch": "eager" if args.eager else
-                       "samplers: direct launches; side lanes: hipGraph replay",
+                       ("samplers: direct launches; side lanes: hipGraph replay"
+                        + ("; one native plan call per step (include/pn2plan.h)"
+                           if pipelined and not args.no_native_plan else "")),
                        "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "0")),
                        "lane0_priority": prio0,
                        "streams": (("SA1 sampler + 3 side streams" if args.sampler_lanes <= 1 or args.model
                                     else f"{args.sampler_lanes} sampler streams (consecutive steps' "
-                                    "samplers concurrent; SA2.. samplers behind SA1) + 2 side streams")
+                                    "samplers concurrent; SA2.. samplers behind SA1) + 2 side streams"
+                                    + (" per buffer set" if args.private_side else ""))
                                    if overlap else "one stream")
                        + (f", steps software-pipelined over {args.sets} buffer sets" if pipelined else "")},
             "roofline": dict(

@@ -16,9 +16,9 @@ Everything runs the gfx950 kernels of libpn2hip.so (C ABI: include/pn2hip.h).
 The directory name has hyphens, so import it with importlib:
     pn2 = importlib.import_module("pointcloud-segmentation-attention_amd")
 """
-from . import attention_layer, complete_scene_loader, data_transformation, grid, pointnet_util, \
+from . import attention_layer, complete_scene_loader, data_transformation, grid, plan, pointnet_util, \
     shard, stack, synth, tf_grouping, tf_interpolate, tf_sampling, tf_util
 from ._lib import LIB_PATH, InvalidArgumentError, Pn2RuntimeError, lib
 
 __all__ = ["tf_sampling", "tf_grouping", "tf_interpolate", "pointnet_util", "attention_layer", "grid", "tf_util", "data_transformation", "complete_scene_loader",
-           "synth", "stack", "shard", "lib", "LIB_PATH", "InvalidArgumentError", "Pn2RuntimeError"]
+           "synth", "stack", "shard", "plan", "lib", "LIB_PATH", "InvalidArgumentError", "Pn2RuntimeError"]

@@ -44,7 +44,7 @@ class MlpLayer(ctypes.Structure):
     _fields_ = [("packed", ctypes.c_void_p), ("cin", ctypes.c_int), ("cout", ctypes.c_int),
                 ("flags", ctypes.c_int)]
 
-# name -> (restype, argtypes); mirrors include/pn2hip.h (tests/test_capi.py checks the header)
+# name -> (restype, argtypes); mirrors include/pn2hip.h and include/pn2plan.h (tests/test_capi.py checks the header)
 SIGNATURES = {
     "pn2_version": (ctypes.c_char_p, []),
     "pn2_strerror": (ctypes.c_char_p, [_I]),
@@ -101,6 +101,17 @@ SIGNATURES = {
     "pn2_subvolume_slices": (_I, [_I]),
     "pn2_subvolume_select": (_I, [_P, _I, _P, _I, ctypes.c_double, _P, _P, _P, _P]),
     "pn2_gather_rows": (_I, [_P, _LL, _I, _P, _LL, _P, _P]),
+    # include/pn2plan.h: the native step executor
+    "pn2_plan_create": (_P, []),
+    "pn2_plan_destroy": (None, [_P]),
+    "pn2_plan_graph": (_I, [_P, _P, _P]),
+    "pn2_plan_record": (_I, [_P, _P, _P]),
+    "pn2_plan_wait": (_I, [_P, _P, _P]),
+    "pn2_plan_fps_chain": (_I, [_P, _P, _I, _I, _I, _P, _P, _P, _P]),
+    "pn2_plan_mark_timed": (_I, [_P]),
+    "pn2_plan_size": (_I, [_P]),
+    "pn2_plan_launch": (_I, [_P]),
+    "pn2_plan_launch_timed": (_I, [_P, _P, _P]),
 }
 
 _lib = None

@@ -157,6 +157,10 @@ inline FastDiv make_fastdiv(uint32_t d) {
 }
 PN2_DEV uint32_t fdiv(uint32_t n, FastDiv f) { return f.d == 1 ? n : __umulhi(n, f.magic); }
 
+// pn2_fps_chain's argument check (fps.hip), shared with the plan executor (plan.hip)
+int fps_chain_check(const float* xyz, int B, int N, int nstages, const int* npoint,
+                    int32_t* const* idx, float* const* new_xyz);
+
 }  // namespace pn2
 
 // launch-status helper for the C ABI

@@ -247,6 +247,21 @@ int fps_impl(const float* xyz, int B, int N, int M, int32_t* idx, float* nx, voi
 }
 
 }  // namespace
+
+// pn2_fps_chain's argument check, shared with the plan executor (plan.hip), which validates
+// a chain launch once when it is recorded
+int fps_chain_check(const float* xyz, int B, int N, int nstages, const int* npoint,
+                    int32_t* const* idx, float* const* new_xyz) {
+  if (B < 0 || N <= 0 || N > kMaxRegPoints || nstages < 1 || nstages > kChainMax || !npoint ||
+      !idx || !new_xyz)
+    return PN2_EINVAL;
+  for (int i = 0; i < nstages; ++i) {
+    if (npoint[i] <= 0 || !idx[i] || !new_xyz[i]) return PN2_EINVAL;
+    if (i + 1 < nstages && npoint[i] > kChainNext) return PN2_EINVAL;
+  }
+  if (B > 0 && (!xyz || B > 65535)) return PN2_EINVAL;
+  return PN2_OK;
+}
 }  // namespace pn2
 
 extern "C" {
@@ -267,15 +282,8 @@ int pn2_fps_gather_sched(const float* xyz, int B, int N, int npoint, int32_t* id
 
 int pn2_fps_chain(const float* xyz, int B, int N, int nstages, const int* npoint,
                   int32_t* const* idx, float* const* new_xyz, pn2_stream_t stream) {
-  if (B < 0 || N <= 0 || N > pn2::kMaxRegPoints || nstages < 1 || nstages > pn2::kChainMax ||
-      !npoint || !idx || !new_xyz)
-    return PN2_EINVAL;
-  for (int i = 0; i < nstages; ++i) {
-    if (npoint[i] <= 0 || !idx[i] || !new_xyz[i]) return PN2_EINVAL;
-    if (i + 1 < nstages && npoint[i] > pn2::kChainNext) return PN2_EINVAL;
-  }
-  if (B == 0) return PN2_OK;
-  if (!xyz || B > 65535) return PN2_EINVAL;
+  const int rc0 = pn2::fps_chain_check(xyz, B, N, nstages, npoint, idx, new_xyz);
+  if (rc0 != PN2_OK || B == 0) return rc0;
   hipStream_t s = (hipStream_t)stream;
   int first = 0;  // first stage of the fused tail
   if (N > pn2::kChainNext) {  // the big first stage as its own sampler launch

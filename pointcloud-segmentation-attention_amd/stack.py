@@ -140,11 +140,14 @@ class Task:
     """One piece of a step: `fn` runs on stream `lane` (0 = the sampler chain, 1.. = side
     streams) after the tasks named in `deps` (same-lane order is implicit)."""
 
-    def __init__(self, name, lane, deps, fn, direct=False):
+    def __init__(self, name, lane, deps, fn, direct=False, chain=None):
         self.name, self.lane, self.deps, self.fn = name, lane, tuple(deps), fn
         # direct: one C launch into fixed buffers; GraphStep launches it as is (a one-kernel
         # graph costs more queue time than the kernel launch itself)
         self.direct = direct
+        # chain: (npoints, xyz, outs) of a direct sampler launch (pn2_fps_chain into fixed
+        # buffers), so a native plan can record the same launch (Step.emit_plan)
+        self.chain = chain
 
 
 class Step:
@@ -208,8 +211,12 @@ class Step:
         # level lvl+1's features are the SA4 output (k=0) or the previous FP MLP's stand-in.
         fp_feat = [inp["sa_out"][3]] + list(inp["fp_out"])
         v["xyz"] = [inp["xyz"], None, None, None, None]
-        v["sa"], v["fp"] = [None] * 4, [None] * 4
+        v["sa"], v["fp"], v["att"] = [None] * 4, [None] * 4, [None] * 4
         v["bq"], v["nn"] = [None] * 4, [None] * 4  # kept for the parity tests (intermediates())
+        # with the later samplers behind SA1 on its stream (chain_lane 0: several sampler
+        # streams), lane 3 is free: the attention reductions (they read only their resident
+        # inputs) run there instead of inside lane 1's SA tasks
+        attn_lane = 3 if (self.chain_lane == 0 and self.overlap and "attn" in inp) else None
         tasks = []
         if big:  # the SA1 grid over the input cloud (also orders FP4's neighbour search)
             tasks.append(Task("grid1", 1, (), lambda: v.__setitem__(
@@ -230,10 +237,14 @@ class Step:
                 v["bq"][i] = idx
                 new_points, _ = pointnet_util.group_concat(xyz, points[i], new_xyz, idx,
                                                            want_grouped_xyz=False)
-                out = [new_points]
-                if "attn" in inp:  # attention instead of pooling (attention_layer.py:256-261)
-                    out.append(attention_layer.attention_reduce(*inp["attn"][i]))
-                v["sa"][i] = out
+                v["sa"][i] = new_points
+                if "attn" in inp and attn_lane is None:
+                    att(i)()
+            return f
+
+        def att(i):  # attention instead of pooling (attention_layer.py:256-261)
+            def f():
+                v["att"][i] = attention_layer.attention_reduce(*inp["attn"][i])
             return f
 
         def fp(i):
@@ -260,9 +271,11 @@ class Step:
             # fused in one launch, so the next step's SA1 sampler follows this one directly.
             # Both are direct launches into fixed buffers.
             tasks.append(Task("fps1", 0, (), lambda: tf_sampling.farthest_point_sample_chain(
-                npoints[:1], xyz, out=v["chain"][:1]), direct=True))
+                npoints[:1], xyz, out=v["chain"][:1]), direct=True,
+                chain=(npoints[:1], xyz, v["chain"][:1])))
             tasks.append(Task("fps234", self.chain_lane, ("fps1",), lambda: tf_sampling.farthest_point_sample_chain(
-                npoints[1:], v["xyz"][1], out=v["chain"][1:]), direct=True))
+                npoints[1:], v["xyz"][1], out=v["chain"][1:]), direct=True,
+                chain=(npoints[1:], v["xyz"][1], v["chain"][1:])))
             sampled = ("fps1", "fps234", "fps234", "fps234")
         else:
             # lane 0: SA1's sampler alone; lane 3: SA2..SA4's samplers as one task
@@ -276,6 +289,9 @@ class Step:
         tasks.append(Task("fp3", 2, (sampled[1],), fp(1)))
         tasks.append(Task("fp2", 2, (sampled[2],), fp(2)))
         tasks.append(Task("fp1", 2, (sampled[3],), fp(3)))
+        if attn_lane is not None:
+            for i in range(4):
+                tasks.append(Task(f"att{i + 1}", attn_lane, (), att(i)))
         return tasks
 
     def _tasks_ssg_model(self):
@@ -385,12 +401,17 @@ class Step:
         for i in range(len(MSG_SA)):
             # lane 0: SA1's sampler only; the later samplers run on lane 3 after it; radius 0's
             # grouping on lane 1, the other radii on lane 2
+            spec = ([MSG_SA[i][0]], v["xyz"][i], v["fps_out"][i:i + 1])
             if i == 0:
-                tasks.append(Task("fps1", 0, (), fps(0), direct=True))
+                tasks.append(Task("fps1", 0, (), fps(0), direct=True, chain=spec))
             else:
-                tasks.append(Task(f"fps{i + 1}", self.chain_lane, (f"fps{i}",), fps(i), direct=True))
+                tasks.append(Task(f"fps{i + 1}", self.chain_lane, (f"fps{i}",), fps(i), direct=True,
+                                  chain=spec))
             for r in range(len(MSG_SA[i][1])):
-                tasks.append(Task(f"sa{i + 1}_{r}", 1 + min(r, 1), (f"fps{i + 1}",), grp(i, r)))
+                # radius r on lane 1 + r when lane 3 is free (chain_lane 0), else radius 0 on
+                # lane 1 and the others on lane 2
+                lane = 1 + r if self.chain_lane == 0 and self.overlap else 1 + min(r, 1)
+                tasks.append(Task(f"sa{i + 1}_{r}", lane, (f"fps{i + 1}",), grp(i, r)))
         return tasks
 
     def outputs(self):
@@ -398,7 +419,8 @@ class Step:
         if "model" in self.inp:  # logits (B, N, 21), then the SA levels' features
             return [v["fp"][3]] + v["pts"][1:]
         if self.kind == "ssg":
-            return [t for o in v["sa"] for t in o] + list(v["fp"])
+            sa = [[p] + ([a] if "attn" in self.inp else []) for p, a in zip(v["sa"], v["att"])]
+            return [t for o in sa for t in o] + list(v["fp"])
         return [v["gp"][k] for k in sorted(v["gp"])]
 
     def intermediates(self):
@@ -472,6 +494,90 @@ class Step:
         self.lane_done[1].record(self.streams[1])
         return self.join() if join else None
 
+    def segments(self):
+        """The tasks grouped into launch segments for a native plan: consecutive tasks of one
+        lane (in list order) share a segment until a task whose result another lane waits for
+        (its release must not wait for the tasks after it); a direct task is a segment of its
+        own. A segment waits, up front, for every cross-lane dependency of its tasks -- never
+        earlier than a task would have, only later, so a consumer still cannot run before its
+        producer -- and releases its tasks' events at its end. Returned in an order in which
+        every segment comes after the segments it waits for and after the earlier segments of
+        its lane (the host enqueues waits after the records they refer to). On the SSG step
+        the side lanes become three segments: [grid1], [sa1..sa4], [fp4..fp1]."""
+        lane_of = {t.name: (t.lane if self.overlap else 0) for t in self.tasks}
+        xdeps = {t.name: any(t.name in u.deps and lane_of[u.name] != lane_of[t.name]
+                             for u in self.tasks) for t in self.tasks}
+        segs, open_seg = [], {}
+        for t in self.tasks:
+            lane = lane_of[t.name]
+            if t.direct:
+                open_seg.pop(lane, None)
+                segs.append([t])
+                continue
+            cur = open_seg.get(lane)
+            if cur is None:
+                cur = open_seg[lane] = []
+                segs.append(cur)
+            cur.append(t)
+            if xdeps[t.name]:
+                del open_seg[lane]
+        seg_of = {t.name: i for i, seg in enumerate(segs) for t in seg}
+        prev_same_lane = {}
+        preds = []
+        for i, seg in enumerate(segs):
+            lane = lane_of[seg[0].name]
+            p = {seg_of[d] for t in seg for d in t.deps if seg_of[d] != i}
+            if lane in prev_same_lane:
+                p.add(prev_same_lane[lane])
+            prev_same_lane[lane] = i
+            preds.append(p)
+        order, placed = [], set()
+        while len(order) < len(segs):  # topological, earliest segment first
+            i = next((i for i in range(len(segs)) if i not in placed and preds[i] <= placed), None)
+            if i is None:
+                raise RuntimeError("task dependencies form a cycle")
+            order.append(segs[i])
+            placed.add(i)
+        return order
+
+    @staticmethod
+    def segment_key(seg):
+        return "+".join(t.name for t in seg)
+
+    def emit_plan(self, plan, graphs, main):
+        """Record the step -- per launch segment (segments()): its cross-lane waits, its
+        hipGraph (graphs[segment_key]) or direct sampler launch (the task's `chain` spec), and
+        the release events other lanes wait for; lane 0 = `main`; then the lane join of run()
+        -- into a native plan (plan.Plan over include/pn2plan.h), so one host call enqueues
+        the whole step. The SA1 sampler is the plan's timed operation."""
+        assert self.overlap and self.synced_inputs
+        lane_of = {t.name: t.lane for t in self.tasks}
+        for seg in self.segments():
+            lane = seg[0].lane
+            st = self._stream(lane, main)
+            waits = []
+            for t in seg:
+                for d in t.deps:
+                    if lane_of[d] != lane and d not in waits:
+                        waits.append(d)
+            for d in waits:
+                plan.wait(st, self.done[d])
+            if seg[0].direct:
+                if seg[0].chain is None:
+                    raise RuntimeError(f"task {seg[0].name}: a direct task needs its chain spec")
+                plan.fps_chain(*seg[0].chain, st)
+            else:
+                plan.graph(graphs[self.segment_key(seg)], st)
+            if seg[0].name == self.SAMPLER:
+                plan.mark_timed()
+            for t in seg:
+                if any(t.name in u.deps and u.lane != lane for u in self.tasks):
+                    plan.record(self.done[t.name], st)
+        for lane in range(2, self.nlanes):
+            plan.record(self.lane_done[lane], self.streams[lane])
+            plan.wait(self.streams[1], self.lane_done[lane])
+        plan.record(self.lane_done[1], self.streams[1])
+
     def join(self):
         """Make the current stream wait for every lane; returns the outputs (None before the
         first run)."""
@@ -500,8 +606,11 @@ class GraphStep:
     on its lane's stream; replay() relaunches them with the same cross-stream events as the
     eager step. Inputs stay resident, outputs are overwritten in place at every replay."""
 
-    def __init__(self, inp, warmup=2, overlap=True, streams=None, chain_lane=3):
+    def __init__(self, inp, warmup=2, overlap=True, streams=None, chain_lane=3, segments=False):
+        # segments: capture one graph per launch segment (Step.segments(), for a native plan:
+        # replay_plan) instead of one per task (replay)
         self.step = Step(inp, overlap=overlap, streams=streams, chain_lane=chain_lane)
+        self.segmented = segments and self.step.overlap
         dev = inp["xyz"].device
         warm = side_stream(dev, "warm")
         warm.wait_stream(torch.cuda.current_stream(dev))
@@ -518,27 +627,54 @@ class GraphStep:
         self.graphs = {}
         cap = side_stream(dev, "capture")
 
-        def capture(t):
-            if t.direct:
-                return
+        def capture_tasks(ts, lane, key):
             g = torch.cuda.CUDAGraph()
             st = torch.cuda.current_stream(dev)
             cap.wait_stream(st)
-            lane = t.lane if self.step.overlap else 0
             if lane not in pools:
                 pools[lane] = torch.cuda.graph_pool_handle()
             with torch.cuda.graph(g, pool=pools[lane], stream=cap):
-                t.fn()
+                for t in ts:
+                    t.fn()
             st.wait_stream(cap)
-            self.graphs[t.name] = g
+            self.graphs[key] = g
 
-        self.step.run(launch=capture)
+        def capture(t):
+            if not t.direct:
+                capture_tasks([t], t.lane if self.step.overlap else 0, t.name)
+
+        if self.segmented:
+            # each segment's tasks as one graph, in segment order, on the segment's lane pool
+            # (the warm-up runs above made the direct samplers' outputs and synced the lanes)
+            for seg in self.step.segments():
+                if not seg[0].direct:
+                    capture_tasks(seg, seg[0].lane, Step.segment_key(seg))
+        else:
+            self.step.run(launch=capture)
         torch.cuda.synchronize(dev)
         self.outs = self.step.outputs()
 
     def replay(self, sampler_events=None, join=True):
+        if self.segmented:
+            raise RuntimeError("a segmented GraphStep replays through replay_plan()")
         self.step.run(sampler_events, join=join,
                       launch=lambda t: t.fn() if t.direct else self.graphs[t.name].replay())
+        return self.outs
+
+    def replay_plan(self, sampler_events=None):
+        """replay(join=False) through a native plan (one host call for the whole step): the
+        plan for the current stream as lane 0 is recorded at its first use."""
+        main = torch.cuda.current_stream(self.step.inp["xyz"].device)
+        if not hasattr(self, "plans"):
+            self.plans = {}
+        p = self.plans.get(main.cuda_stream)
+        if p is None:
+            from .plan import Plan
+            p = Plan()
+            self.step.emit_plan(p, self.graphs, main)
+            self.plans[main.cuda_stream] = p
+        p.launch(sampler_events)
+        self.step.ran = True
         return self.outs
 
     def join(self):
@@ -566,34 +702,49 @@ class Pipeline:
     1 + 2 + (sampler_lanes - 1) <= GPU_MAX_HW_QUEUES."""
 
     def __init__(self, inp, graphs=True, overlap=True, nsets=3, private_streams=False,
-                 sampler_lanes=1):
+                 sampler_lanes=1, native_plan=True):
         # private_streams: every buffer set gets its own side streams, so the side lanes of
         # consecutive steps overlap each other too (the whole-model step, whose lane-1 chain
-        # of SA/FP layers is longer than a sampler period); otherwise the sets share them
+        # of SA/FP layers is longer than a sampler period; the geometric step once its
+        # samplers run on several streams and the shared side lanes set the pace); otherwise
+        # the sets share them
         dev = inp["xyz"].device
+        nsets = max(2, nsets)
+        private = private_streams and overlap and inp["xyz"].is_cuda
 
         def streams(i):  # set 0 keeps the process-wide side streams
-            if i == 0 or not (private_streams and overlap and inp["xyz"].is_cuda):
+            if i == 0 or not private:
                 return None
             return [None] + [side_stream(dev, (i, lane)) for lane in range(1, NSIDE + 1)]
 
-        multi = sampler_lanes > 1 and overlap and inp["xyz"].is_cuda and not private_streams
+        multi = sampler_lanes > 1 and overlap and inp["xyz"].is_cuda
         chain_lane = 0 if multi else 3
         self.lane0 = [None]
         if multi:
-            # queues go to streams in order of first use: the side lanes, then the extra
-            # sampler streams, all before the sets' warm-up and capture streams
+            # queues go to streams in order of first use: set by set, its sampler stream (set 0:
+            # the current stream) then its side lanes 1-2 (shared: set 0's), all before the
+            # sets' warm-up and capture streams
             cur = torch.cuda.current_stream(dev)
-            for lane in (1, 2):
-                side_stream(dev, lane).wait_stream(cur)
-            for i in range(1, sampler_lanes):
-                st = side_stream(dev, ("sampler", i))
-                st.wait_stream(cur)
-                self.lane0.append(st)
-        mk = (lambda i: GraphStep(inp, overlap=overlap, streams=streams(i), chain_lane=chain_lane)) \
+            # lane 3 carries the attention reductions (cfg3) or MSG's third radius
+            uses3 = CONFIGS[inp["config"]][1] == "msg" or "attn" in inp
+            side_lanes = (1, 2, 3) if uses3 else (1, 2)
+            for i in range(max(sampler_lanes, nsets if private else 1)):
+                if 0 < i < sampler_lanes:
+                    st = side_stream(dev, ("sampler", i))
+                    st.wait_stream(cur)
+                    self.lane0.append(st)
+                if i == 0 or (private and i < nsets):
+                    for lane in side_lanes:
+                        side_stream(dev, lane if i == 0 else (i, lane)).wait_stream(cur)
+        # native_plan: a graph step is enqueued by ONE call into the C++ executor
+        # (include/pn2plan.h), its side lanes as a few segment graphs, instead of the per-task
+        # Python loop (DESIGN.md §3.6)
+        self.native_plan = native_plan and graphs and overlap and inp["xyz"].is_cuda
+        mk = (lambda i: GraphStep(inp, overlap=overlap, streams=streams(i), chain_lane=chain_lane,
+                                  segments=self.native_plan)) \
             if graphs else (lambda i: Step(inp, overlap=overlap, streams=streams(i),
                                            chain_lane=chain_lane))
-        self.sets = [mk(i) for i in range(max(2, nsets))]
+        self.sets = [mk(i) for i in range(nsets)]
         self.k = 0
 
     def run(self, sampler_events=None):
@@ -611,6 +762,8 @@ class Pipeline:
                 s.step.lane_done[1].synchronize()  # this set's previous side work
             else:
                 s.step.join()
+            if self.native_plan:
+                return s.replay_plan(sampler_events)
             return s.replay(sampler_events, join=False)
         s.join()
         return s.run(sampler_events, join=False)

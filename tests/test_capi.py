@@ -1,4 +1,5 @@
-"""CPU: the C-ABI library builds, loads and exports every entry point include/pn2hip.h declares.
+"""CPU: the C-ABI library builds, loads and exports every entry point include/*.h declares
+(pn2hip.h: the reference ops; pn2plan.h: the native step executor).
 No kernel is launched here (no GPU in the build container): only host functions and argument
 checks that return before any HIP call."""
 import ctypes
@@ -10,13 +11,19 @@ import numpy as np
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADER = os.path.join(ROOT, "include", "pn2hip.h")
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("pn2hip.h", "pn2plan.h")]
 
 
 def header_functions():
-    text = open(HEADER).read()
-    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return sorted(set(re.findall(r"\b(pn2(?:cpu)?_[a-z0-9_]+)\s*\(", text)))
+    names = set()
+    for h in HEADERS:
+        text = re.sub(r"/\*.*?\*/", "", open(h).read(), flags=re.S)
+        names |= set(re.findall(r"\b(pn2(?:cpu)?_[a-z0-9_]+)\s*\(", text))
+    return sorted(names)
+
+
+def test_headers_are_all_listed():
+    assert sorted(os.listdir(os.path.join(ROOT, "include"))) == sorted(os.path.basename(h) for h in HEADERS)
 
 
 def test_header_declares_the_boundary():
@@ -202,3 +209,39 @@ def test_scene_contract(pn2):
     assert lib.pn2_subvolume_slices(4096) == 1 and lib.pn2_subvolume_slices(4097) == 2
     assert lib.pn2_gather_rows(fake, 10, 6, fake, 4, fake, None) == E        # row bytes % 4
     assert lib.pn2_gather_rows(None, 10, 8, None, 0, None, None) == 0
+
+
+def test_plan_records_and_checks_without_launching(pn2):
+    """include/pn2plan.h: operations are validated when recorded; an empty plan launches as a
+    no-op (no HIP call)."""
+    lib = pn2.lib()
+    E = -22
+    p = lib.pn2_plan_create()
+    assert p
+    try:
+        assert lib.pn2_plan_size(p) == 0
+        assert lib.pn2_plan_mark_timed(p) == E            # nothing to mark
+        assert lib.pn2_plan_launch(p) == 0                 # empty: nothing enqueued
+        assert lib.pn2_plan_launch_timed(p, None, None) == 0
+        assert lib.pn2_plan_graph(p, None, None) == E      # null graph exec
+        assert lib.pn2_plan_record(p, None, None) == E     # null event
+        assert lib.pn2_plan_wait(p, None, None) == E
+        npoint = (ctypes.c_int * 2)(256, 64)
+        bufs = (ctypes.c_void_p * 2)(16, 32)
+        # the pn2_fps_chain checks: a fed stage above 1024 points, too many stages, null xyz
+        big = (ctypes.c_int * 2)(2048, 64)
+        assert lib.pn2_plan_fps_chain(p, 8, 2, 4096, 2, ctypes.addressof(big), ctypes.addressof(bufs),
+                                      ctypes.addressof(bufs), None) == E
+        assert lib.pn2_plan_fps_chain(p, 8, 2, 4096, 5, ctypes.addressof(npoint), ctypes.addressof(bufs),
+                                      ctypes.addressof(bufs), None) == E
+        assert lib.pn2_plan_fps_chain(p, None, 2, 4096, 2, ctypes.addressof(npoint),
+                                      ctypes.addressof(bufs), ctypes.addressof(bufs), None) == E
+        assert lib.pn2_plan_size(p) == 0                   # nothing appended on error
+        assert lib.pn2_plan_fps_chain(p, 8, 2, 4096, 2, ctypes.addressof(npoint),
+                                      ctypes.addressof(bufs), ctypes.addressof(bufs), None) == 0
+        assert lib.pn2_plan_size(p) == 1
+        assert lib.pn2_plan_mark_timed(p) == 0
+    finally:
+        lib.pn2_plan_destroy(p)
+    assert lib.pn2_plan_size(None) == E
+    assert lib.pn2_plan_launch(None) == E

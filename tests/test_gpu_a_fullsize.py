@@ -114,22 +114,43 @@ def test_stack_full_size(env, config, B):
     check_step(O, config, inp, outs, step.intermediates())
 
 
+def _poison_sampled(pipe, torch):
+    """Overwrite every set's sampled coordinates (the buffers the side lanes read) with 1e6:
+    a consumer that does not wait for its sampler then groups / interpolates against these
+    (in bounds: no neighbour within any radius, huge but finite distances) and the step's
+    outputs differ from the oracle's."""
+    for s in pipe.sets:
+        v = s.step.v
+        for _, nx in (v.get("chain") or v.get("fps_out")):
+            nx.fill_(1e6)
+    torch.cuda.synchronize()
+
+
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("lanes", [1, 2])
+@pytest.mark.parametrize("lanes,native", [(1, False), (1, True), (2, True)])
 @pytest.mark.parametrize("config,B", CONFIGS)
-def test_pipeline_full_size(env, config, B, lanes):
+def test_pipeline_full_size(env, config, B, lanes, native):
     """What bench.py times: the software-pipelined hipGraph steps over 3 buffer sets, at the
     BASELINE batch, after several rotations, with one sampler stream or two (consecutive steps'
-    samplers concurrent); the last two steps' outputs (one per sampler stream) against the
-    oracle."""
+    samplers concurrent), enqueued by the Python task loop or by the native plan
+    (include/pn2plan.h). The sampled coordinates of every set are poisoned before the last
+    three steps (a missing wait then shows), and the last two steps' outputs (one per sampler
+    stream) are compared with the oracle."""
     pkg, O, torch, dev = env
     inp = pkg.stack.make_inputs(config, list(range(100, 100 + B)), dev)
-    pipe = pkg.stack.Pipeline(inp, graphs=True, nsets=3, sampler_lanes=lanes)
+    pipe = pkg.stack.Pipeline(inp, graphs=True, nsets=3, sampler_lanes=lanes, native_plan=native)
     assert len(pipe.lane0) == lanes
+    assert pipe.native_plan == native
     for _ in range(7):
+        pipe.run()
+    pipe.join()
+    _poison_sampled(pipe, torch)
+    for _ in range(3):
         pipe.run()
     outs = pipe.join()
     torch.cuda.synchronize()
+    if native:
+        assert all(getattr(s, "plans", None) for s in pipe.sets), "a set ran without its plan"
     for back in (1, 2):
         s = pipe.sets[(pipe.k - back) % len(pipe.sets)]
         check_step(O, config, inp, s.outs if back > 1 else outs, s.intermediates())
