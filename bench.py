@@ -296,6 +296,9 @@ def main():
                     help="every buffer set gets its own side streams (side work of consecutive "
                          "steps runs concurrently; needs 1 + 2 x sets + sampler lanes - 1 "
                          "hardware queues)")
+    ap.add_argument("--diag-only", choices=["samplers", "side"], default=None,
+                    help="DIAGNOSTIC: time only the samplers or only the side-lane work of each "
+                         "step (the line is marked diagnostic; never a benchmark result)")
     ap.add_argument("--no-native-plan", action="store_true",
                     help="enqueue each step with the Python task loop instead of one call into "
                          "the native plan executor (include/pn2plan.h)")
@@ -386,7 +389,8 @@ def main():
             pipe = pkg.stack.Pipeline(inp, graphs=not args.eager, nsets=args.sets,
                                       sampler_lanes=1 if model else args.sampler_lanes,
                                       private_streams=model or args.private_side,
-                                      native_plan=not args.no_native_plan)
+                                      native_plan=not args.no_native_plan,
+                                      only=args.diag_only)
         else:
             step = pkg.stack.Step(inp, overlap=overlap)
             graph = None if args.eager else pkg.stack.GraphStep(inp, overlap=overlap)
@@ -409,14 +413,17 @@ def main():
         barrier()
         t0 = time.perf_counter()
         outs = None
+        timed_k = [] if args.diag_only == "side" else \
+            [k for k in range(steps) if k % args.time_every == 0]
         for k in range(steps):
-            outs = run_step(ev[k] if k % args.time_every == 0 else None)
+            outs = run_step(ev[k] if k in timed_k else None)
         outs = finish() or outs
         torch.cuda.synchronize()
         barrier()
         elapsed = pkg.shard.max_over_ranks(time.perf_counter() - t0, dev)
-        timed = [ev[k] for k in range(steps) if k % args.time_every == 0]
-        fps_ms = sum(a.elapsed_time(b) for a, b in timed) / len(timed)  # SA1 sampler, per launch
+        timed = [ev[k] for k in timed_k]
+        fps_ms = (sum(a.elapsed_time(b) for a, b in timed) / len(timed)  # SA1 sampler, per launch
+                  if timed else float("nan"))
         return elapsed, fps_ms, outs
 
     overlap = not args.no_overlap
@@ -508,6 +515,8 @@ def main():
         }
         if e2e is not None:
             result["e2e"] = e2e
+        if args.diag_only:
+            result["diagnostic"] = f"only the {args.diag_only} of each step ran: not a benchmark result"
         if world == 1 and not args.no_cpu_baseline and not args.model:
             try:
                 result["cpu_baseline"] = cpu_baseline(args.config, B, args.cpu_seconds,

@@ -142,18 +142,57 @@ __global__ __launch_bounds__(kNNBlock) void three_nn_kernel(const float* __restr
 // irrelevant. One lane per unknown point; when `ugrid` (a grid over the UNKNOWN points) is
 // given, lane i takes the i-th unknown in cell order, so the lanes of a wave share cells.
 // LDS: the known grid (sorted points + offsets) is staged once per workgroup when it fits.
-template <int BLOCK, bool LDS>
+//
+// QUAD: four lanes per unknown point (the scan path's quad). The single-lane walk is
+// latency-bound: at FP4 a launch is only 2048 waves (two per SIMD) and each lane's walk is a
+// chain of dependent LDS reads and inserts (69 candidates per unknown on average), so the
+// SIMDs mostly wait. With a quad, lane q of the quad takes every fourth point of each visited
+// range (its own top 3 over its share), a launch has four times the waves, and each lane's
+// chain is a quarter as long. At the end of every shell the quad merges its four lists (two
+// xor exchanges, the (d, k)-lexicographic insert) into a copy that every lane of the quad
+// holds, and tests the certificate on it -- the same test for all four lanes, so the quad
+// leaves the walk together; the merged copy is the result.
+#ifndef PN2_NN_QUAD
+#define PN2_NN_QUAD 1  // 0: one lane per unknown (A/B builds, tools/bench_nn.py)
+#endif
+
+// squared-gap certificate: every point outside the cell box [xl..xh] x [yl..yh] x [zl..zh]
+// (faces on the grid boundary excepted: nothing lies beyond them) is farther from p than
+// sqrt(d3), with slack for the rounding of the cell assignment and of the face coordinates
+PN2_DEV bool box_certifies(const GridHdr& h, float px, float py, float pz, int xl, int xh,
+                           int yl, int yh, int zl, int zh, float d3) {
+  if (!(d3 < __builtin_inff())) return false;
+  const float edge = 1.0f / h.inv;
+  float gap = __builtin_inff();
+  auto face = [&](float d, float pc, float o, int c) {
+    const float fc = o + (float)c * edge;
+    gap = fminf(gap, d - 1e-5f * (fabsf(pc) + fabsf(o) + fabsf(fc) + (float)c * edge) - 1e-30f);
+  };
+  if (xl > 0) face(px - (h.ox + (float)xl * edge), px, h.ox, xl);
+  if (xh < h.nx - 1) face((h.ox + (float)(xh + 1) * edge) - px, px, h.ox, xh + 1);
+  if (yl > 0) face(py - (h.oy + (float)yl * edge), py, h.oy, yl);
+  if (yh < h.ny - 1) face((h.oy + (float)(yh + 1) * edge) - py, py, h.oy, yh + 1);
+  if (zl > 0) face(pz - (h.oz + (float)zl * edge), pz, h.oz, zl);
+  if (zh < h.nz - 1) face((h.oz + (float)(zh + 1) * edge) - pz, pz, h.oz, zh + 1);
+  return gap > 0.0f && d3 < gap * gap * 0.9999f;
+}
+
+// G lanes per unknown point (1, or 4 = a quad); BLOCK / G unknowns per workgroup
+template <int BLOCK, bool LDS, int G>
 __global__ __launch_bounds__(BLOCK) void three_nn_grid_kernel(
     const void* __restrict__ kgrid, int m, const void* __restrict__ ugrid,
     const float* __restrict__ xyz1, int n, int B, float* __restrict__ dist,
     int32_t* __restrict__ idx) {
+  static_assert(G == 1 || G == 4, "one lane or a quad per unknown");
+  constexpr int QPB = BLOCK / G;  // unknowns per workgroup
   extern __shared__ float4 s_pts[];  // LDS: m sorted known points, then ncell+1 offsets
   // logical block (cloud b, row block x), XCD-aware: the blocks of a cloud share one L2
-  const int R = (n + BLOCK - 1) / BLOCK;
+  const int R = (n + QPB - 1) / QPB;
   const int Lg = xcd_block(blockIdx.x, R * B);
   if (Lg >= R * B) return;
   const int b = Lg / R;
-  const int i = (Lg - b * R) * BLOCK + threadIdx.x;
+  const int i = (Lg - b * R) * QPB + (int)threadIdx.x / G;
+  const int q = (int)threadIdx.x & (G - 1);
   const GridView g = grid_view(kgrid, b, m);
   const GridHdr& h = g.h;
   const float4* __restrict__ pts = g.pts;
@@ -168,7 +207,7 @@ __global__ __launch_bounds__(BLOCK) void three_nn_grid_kernel(
     pts = s_pts;
     off = s_off;
   }
-  if (i >= n) return;  // no barriers below
+  if (i >= n) return;  // no barriers below; a quad's lanes share i
   float px, py, pz;
   int u;
   if (ugrid) {
@@ -182,16 +221,24 @@ __global__ __launch_bounds__(BLOCK) void three_nn_grid_kernel(
   }
   Best3 best;
   best3_init(best);
-  auto visit = [&](int lo, int hi) {  // sorted points [lo, hi)
-    for (int e = lo; e < hi; ++e) {
-      const float4 q = pts[e];
-      best3_insert_lex(best, sqdist(q.x, q.y, q.z, px, py, pz), __float_as_int(q.w));
+  auto visit = [&](int lo, int hi) {  // sorted points [lo, hi), this lane's share
+    for (int e = lo + q; e < hi; e += G) {
+      const float4 p = pts[e];
+      best3_insert_lex(best, sqdist(p.x, p.y, p.z, px, py, pz), __float_as_int(p.w));
     }
+  };
+  auto merged = [&]() {  // the quad's top 3 (every lane of the quad gets the same)
+    Best3 mb = best;
+    if constexpr (G == 4) {
+      best3_merge_xor(mb, 1);
+      best3_merge_xor(mb, 2);
+    }
+    return mb;
   };
   const int cx = cell_coord(px, h.ox, h.inv, h.nx);
   const int cy = cell_coord(py, h.oy, h.inv, h.ny);
   const int cz = cell_coord(pz, h.oz, h.inv, h.nz);
-  const float edge = 1.0f / h.inv;
+  Best3 res;
   for (int s = 0;; ++s) {
     const int xl = cx - s, xh = cx + s, yl = cy - s, yh = cy + s, zl = cz - s, zh = cz + s;
     const int x0 = max(xl, 0), x1 = min(xh, h.nx - 1);
@@ -206,29 +253,16 @@ __global__ __launch_bounds__(BLOCK) void three_nn_grid_kernel(
         }
       }
     }
+    res = merged();
     if (xl <= 0 && yl <= 0 && zl <= 0 && xh >= h.nx - 1 && yh >= h.ny - 1 && zh >= h.nz - 1)
       break;  // every cell visited
-    if (best.d3 < __builtin_inff()) {
-      float gap = __builtin_inff();
-      // d = distance from p to the face at cell boundary c of an axis with origin o; the
-      // slack covers the rounding of the cell assignment and of the face coordinate
-      auto face = [&](float d, float pc, float o, int c) {
-        const float fc = o + (float)c * edge;
-        gap = fminf(gap, d - 1e-5f * (fabsf(pc) + fabsf(o) + fabsf(fc) + (float)c * edge) - 1e-30f);
-      };
-      if (xl > 0) face(px - (h.ox + (float)xl * edge), px, h.ox, xl);
-      if (xh < h.nx - 1) face((h.ox + (float)(xh + 1) * edge) - px, px, h.ox, xh + 1);
-      if (yl > 0) face(py - (h.oy + (float)yl * edge), py, h.oy, yl);
-      if (yh < h.ny - 1) face((h.oy + (float)(yh + 1) * edge) - py, py, h.oy, yh + 1);
-      if (zl > 0) face(pz - (h.oz + (float)zl * edge), pz, h.oz, zl);
-      if (zh < h.nz - 1) face((h.oz + (float)(zh + 1) * edge) - pz, pz, h.oz, zh + 1);
-      if (gap > 0.0f && best.d3 < gap * gap * 0.9999f) break;
-    }
+    if (box_certifies(h, px, py, pz, xl, xh, yl, yh, zl, zh, res.d3)) break;
   }
+  if (q != 0) return;
   float* D = dist + ((size_t)b * n + u) * 3;
   int32_t* I = idx + ((size_t)b * n + u) * 3;
-  D[0] = best.d1; D[1] = best.d2; D[2] = best.d3;
-  I[0] = best.i1; I[1] = best.i2; I[2] = best.i3;
+  D[0] = res.d1; D[1] = res.d2; D[2] = res.d3;
+  I[0] = res.i1; I[1] = res.i2; I[2] = res.i3;
 }
 
 __global__ void idw_kernel(const float* __restrict__ dist, int total, float* __restrict__ weight) {
@@ -610,16 +644,17 @@ int pn2_three_nn_grid(const void* known_grid, const void* unknown_grid, const fl
   if ((long long)B * n == 0) return PN2_OK;
   if (!known_grid || !dist || !idx || (!unknown_grid && !xyz1)) return PN2_EINVAL;
   constexpr int BLOCK = 256;
-  if ((long long)((n + BLOCK - 1) / BLOCK) * B >= (1LL << 31) - 8) return PN2_EINVAL;
-  const dim3 grid(pn2::xcd_grid((long long)((n + BLOCK - 1) / BLOCK) * B));
+  if ((long long)((n + BLOCK / 4 - 1) / (BLOCK / 4)) * B >= (1LL << 31) - 8) return PN2_EINVAL;
   // an automatic-edge known grid has at most max(m, kAutoMinCells) cells (grid.h); an
   // explicit-edge one may have up to kGridCap and is read from global memory
   const size_t lds = (size_t)m * 16 + (size_t)(std::max(m, pn2::kAutoMinCells) + 1) * 4;
+  constexpr int G = PN2_NN_QUAD ? 4 : 1;
+  const dim3 grid(pn2::xcd_grid((long long)((n + BLOCK / G - 1) / (BLOCK / G)) * B));
   if (lds <= 64 * 1024)
-    hipLaunchKernelGGL((pn2::three_nn_grid_kernel<BLOCK, true>), grid, dim3(BLOCK), lds,
+    hipLaunchKernelGGL((pn2::three_nn_grid_kernel<BLOCK, true, G>), grid, dim3(BLOCK), lds,
                        (hipStream_t)stream, known_grid, m, unknown_grid, xyz1, n, B, dist, idx);
   else
-    hipLaunchKernelGGL((pn2::three_nn_grid_kernel<BLOCK, false>), grid, dim3(BLOCK), 0,
+    hipLaunchKernelGGL((pn2::three_nn_grid_kernel<BLOCK, false, G>), grid, dim3(BLOCK), 0,
                        (hipStream_t)stream, known_grid, m, unknown_grid, xyz1, n, B, dist, idx);
   PN2_RETURN_LAUNCH();
 }

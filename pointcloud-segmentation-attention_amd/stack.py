@@ -36,6 +36,8 @@ SSG_FP_MLP = ((256, 256), (256, 256), (256, 128), (128, 128, 128))
 NUM_CLASSES = 21  # ScanNet (pointnet2_sem_seg_attention.py:17)
 
 NSIDE = 4  # side streams of the whole-model step (the geometric steps use 3)
+import os as _os
+SIDE_LAYOUT = _os.environ.get("PN2_SIDE_LAYOUT", "a")
 
 CONFIGS = {
     # name: (points per cloud, kind, with_features, attention)
@@ -216,7 +218,13 @@ class Step:
         # with the later samplers behind SA1 on its stream (chain_lane 0: several sampler
         # streams), lane 3 is free: the attention reductions (they read only their resident
         # inputs) run there instead of inside lane 1's SA tasks
-        attn_lane = 3 if (self.chain_lane == 0 and self.overlap and "attn" in inp) else None
+        multi = self.chain_lane == 0 and self.overlap
+        attn_lane = 3 if (multi and "attn" in inp) else None
+        # SIDE_LAYOUT "b" (experimental): FP1..FP3 on their own lane (cfg2: lane 3; cfg3: lane
+        # 4, the attention keeps lane 3), FP4 alone on lane 2
+        fp_small = 2
+        if multi and SIDE_LAYOUT == "b":
+            fp_small = 4 if attn_lane else 3
         tasks = []
         if big:  # the SA1 grid over the input cloud (also orders FP4's neighbour search)
             tasks.append(Task("grid1", 1, (), lambda: v.__setitem__(
@@ -286,9 +294,9 @@ class Step:
         tasks.append(Task("fp4", 2, (sampled[0],) + grid_dep, fp(0)))
         for i in (1, 2, 3):
             tasks.append(Task(f"sa{i + 1}", 1, (sampled[i],), sa(i)))
-        tasks.append(Task("fp3", 2, (sampled[1],), fp(1)))
-        tasks.append(Task("fp2", 2, (sampled[2],), fp(2)))
-        tasks.append(Task("fp1", 2, (sampled[3],), fp(3)))
+        tasks.append(Task("fp3", fp_small, (sampled[1],), fp(1)))
+        tasks.append(Task("fp2", fp_small, (sampled[2],), fp(2)))
+        tasks.append(Task("fp1", fp_small, (sampled[3],), fp(3)))
         if attn_lane is not None:
             for i in range(4):
                 tasks.append(Task(f"att{i + 1}", attn_lane, (), att(i)))
@@ -317,9 +325,11 @@ class Step:
             tasks.append(Task("grid1", 1, (), lambda: v.__setitem__(
                 "grid1", tf_grouping.BallGrid(xyz0, SSG_SA[0][1]))))
         tasks.append(Task("fps1", 0, (), lambda: tf_sampling.farthest_point_sample_chain(
-            npoints[:1], xyz0, out=v["chain"][:1]), direct=True))
+            npoints[:1], xyz0, out=v["chain"][:1]), direct=True,
+            chain=(npoints[:1], xyz0, v["chain"][:1])))
         tasks.append(Task("fps234", 4, ("fps1",), lambda: tf_sampling.farthest_point_sample_chain(
-            npoints[1:], v["xyz"][1], out=v["chain"][1:]), direct=True))
+            npoints[1:], v["xyz"][1], out=v["chain"][1:]), direct=True,
+            chain=(npoints[1:], v["xyz"][1], v["chain"][1:])))
         sampled = ("fps1", "fps234", "fps234", "fps234")
 
         def nn(k):  # FP layer k interpolates level 4-k onto level 3-k
@@ -494,11 +504,20 @@ class Step:
         self.lane_done[1].record(self.streams[1])
         return self.join() if join else None
 
+    def restrict(self, only):
+        """DIAGNOSTIC (bench.py --diag-only; never a measured step): keep only the samplers
+        ("samplers") or only the side-lane work ("side", on the sampled buffers the full
+        warm-up steps left), to see which part bounds a pipelined layout."""
+        keep = (lambda t: t.direct) if only == "samplers" else (lambda t: not t.direct)
+        names = {t.name for t in self.tasks if keep(t)}
+        self.tasks = [Task(t.name, t.lane, [d for d in t.deps if d in names], t.fn, t.direct,
+                           t.chain) for t in self.tasks if keep(t)]
+
     def segments(self):
         """The tasks grouped into launch segments for a native plan: consecutive tasks of one
         lane (in list order) share a segment until a task whose result another lane waits for
         (its release must not wait for the tasks after it); a direct task is a segment of its
-        own. A segment waits, up front, for every cross-lane dependency of its tasks -- never
+        own, and so is every task of the whole-model step. A segment waits, up front, for every cross-lane dependency of its tasks -- never
         earlier than a task would have, only later, so a consumer still cannot run before its
         producer -- and releases its tasks' events at its end. Returned in an order in which
         every segment comes after the segments it waits for and after the earlier segments of
@@ -508,9 +527,12 @@ class Step:
         xdeps = {t.name: any(t.name in u.deps and lane_of[u.name] != lane_of[t.name]
                              for u in self.tasks) for t in self.tasks}
         segs, open_seg = [], {}
+        # the whole-model step keeps one segment per task: its lane-1 chain of SA and FP
+        # layers waits for each neighbour search separately, not for all of them up front
+        merge = "model" not in self.inp
         for t in self.tasks:
             lane = lane_of[t.name]
-            if t.direct:
+            if t.direct or not merge:
                 open_seg.pop(lane, None)
                 segs.append([t])
                 continue
@@ -606,7 +628,8 @@ class GraphStep:
     on its lane's stream; replay() relaunches them with the same cross-stream events as the
     eager step. Inputs stay resident, outputs are overwritten in place at every replay."""
 
-    def __init__(self, inp, warmup=2, overlap=True, streams=None, chain_lane=3, segments=False):
+    def __init__(self, inp, warmup=2, overlap=True, streams=None, chain_lane=3, segments=False,
+                 only=None):
         # segments: capture one graph per launch segment (Step.segments(), for a native plan:
         # replay_plan) instead of one per task (replay)
         self.step = Step(inp, overlap=overlap, streams=streams, chain_lane=chain_lane)
@@ -619,6 +642,8 @@ class GraphStep:
                 self.step.run()
         torch.cuda.current_stream(dev).wait_stream(warm)
         torch.cuda.synchronize(dev)
+        if only:
+            self.step.restrict(only)
         # One memory pool PER LANE: graphs of one lane replay in capture order on one stream,
         # so a block one of them frees may be reused by a later one; graphs of different
         # lanes replay concurrently and must never share a block. (Tensors passed between
@@ -702,7 +727,7 @@ class Pipeline:
     1 + 2 + (sampler_lanes - 1) <= GPU_MAX_HW_QUEUES."""
 
     def __init__(self, inp, graphs=True, overlap=True, nsets=3, private_streams=False,
-                 sampler_lanes=1, native_plan=True):
+                 sampler_lanes=1, native_plan=True, only=None):
         # private_streams: every buffer set gets its own side streams, so the side lanes of
         # consecutive steps overlap each other too (the whole-model step, whose lane-1 chain
         # of SA/FP layers is longer than a sampler period; the geometric step once its
@@ -721,27 +746,21 @@ class Pipeline:
         chain_lane = 0 if multi else 3
         self.lane0 = [None]
         if multi:
-            # queues go to streams in order of first use: set by set, its sampler stream (set 0:
-            # the current stream) then its side lanes 1-2 (shared: set 0's), all before the
-            # sets' warm-up and capture streams
+            # queues go to streams in order of first use: the extra sampler streams now, then
+            # each set's side lanes when its Step is built (Step.__init__ touches them in
+            # order), all before the sets' warm-up and capture streams
             cur = torch.cuda.current_stream(dev)
-            # lane 3 carries the attention reductions (cfg3) or MSG's third radius
-            uses3 = CONFIGS[inp["config"]][1] == "msg" or "attn" in inp
-            side_lanes = (1, 2, 3) if uses3 else (1, 2)
-            for i in range(max(sampler_lanes, nsets if private else 1)):
-                if 0 < i < sampler_lanes:
-                    st = side_stream(dev, ("sampler", i))
-                    st.wait_stream(cur)
-                    self.lane0.append(st)
-                if i == 0 or (private and i < nsets):
-                    for lane in side_lanes:
-                        side_stream(dev, lane if i == 0 else (i, lane)).wait_stream(cur)
+            for i in range(1, sampler_lanes):
+                st = side_stream(dev, ("sampler", i))
+                st.wait_stream(cur)
+                self.lane0.append(st)
         # native_plan: a graph step is enqueued by ONE call into the C++ executor
         # (include/pn2plan.h), its side lanes as a few segment graphs, instead of the per-task
         # Python loop
         self.native_plan = native_plan and graphs and overlap and inp["xyz"].is_cuda
+        # only: DIAGNOSTIC restriction of every step to its samplers or its side work
         mk = (lambda i: GraphStep(inp, overlap=overlap, streams=streams(i), chain_lane=chain_lane,
-                                  segments=self.native_plan)) \
+                                  segments=self.native_plan, only=only)) \
             if graphs else (lambda i: Step(inp, overlap=overlap, streams=streams(i),
                                            chain_lane=chain_lane))
         self.sets = [mk(i) for i in range(nsets)]
