@@ -25,6 +25,13 @@ sys.path.insert(0, ROOT)
 # clouds/s, with 8 or 16 the side lanes run fully beside the SA1 sampler and slow it from
 # 0.72 to 0.81 ms (18.7k clouds/s) -- while the whole-model step gains (11.2k -> 14.5k).
 DEFAULT_HW_QUEUES = 4
+# The geometric step's pipeline layout per config, measured on MI355X (DESIGN.md §3.6,
+# profiles/r3/plan/): sampler streams (consecutive steps' samplers run concurrently, one
+# workgroup per cloud each), side-lane layout (stack.side_layout), hardware queues (one per
+# stream: samplers + side lanes) and buffer sets (how far the host may run ahead).
+LAYOUTS = {"cfg2": {"lanes": 3, "side": "b", "queues": 6, "sets": 9},
+           "cfg3": {"lanes": 2, "side": "a", "queues": 5, "sets": 6},
+           "cfg5": {"lanes": 5, "side": "a", "queues": 8, "sets": 10}}
 
 PKG = "pointcloud-segmentation-attention_amd"
 METRIC = "8192-pt clouds/sec through SA+FP layers, 1/2/4/8 MI355X; HBM GB/s vs peak"
@@ -192,8 +199,8 @@ def _e2e_child(args, e2e):
     import subprocess
     cmd = [sys.executable, os.path.abspath(__file__), "--model", "--config", args.config,
            "--steps", str(args.e2e_steps), "--warmup", str(min(args.warmup, 5)),
-           "--no-cpu-baseline", "--time-every", str(args.time_every), "--sets", str(args.sets),
-           "--lane0-priority", args.lane0_priority]
+           "--no-cpu-baseline", "--time-every", str(args.time_every), "--sets", "3",
+           "--lane0-priority", args.lane0_priority, "--hw-queues", str(DEFAULT_HW_QUEUES)]
     if args.batch:
         cmd += ["--batch", str(args.batch)]
     try:
@@ -270,8 +277,11 @@ def dry_run(args):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=500,
+                    help="timed steps (the pipelined steps' fill and drain are amortised over "
+                         "them: cfg2 63-64k clouds/s at 50 steps, 68-71k at 400, 72k at 1000, "
+                         "profiles/r3/steps)")
+    ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--config", default="cfg2", choices=sorted(WORKLOADS))
     ap.add_argument("--batch", type=int, default=None, help="clouds per GPU (default: config's)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -287,11 +297,16 @@ def main():
                     help="bracket every Nth timed step's SA1 sampler with HIP events (the "
                          "roofline's launch time is their mean; two event packets on lane 0 "
                          "per bracketed step cost ~10 us of step time, DESIGN.md §5)")
-    ap.add_argument("--sets", type=int, default=3,
-                    help="buffer sets the pipelined steps rotate over (>= 2)")
-    ap.add_argument("--sampler-lanes", type=int, default=1,
+    ap.add_argument("--sets", type=int, default=None,
+                    help="buffer sets the pipelined steps rotate over (>= 2; default: the "
+                         "config's LAYOUTS entry, 3 for --model)")
+    ap.add_argument("--sampler-lanes", type=int, default=None,
                     help="streams the pipelined steps' samplers alternate over (consecutive "
-                         "steps' samplers run at the same time on different CUs)")
+                         "steps' samplers run at the same time on different CUs; default: the "
+                         "config's LAYOUTS entry, 1 for --model)")
+    ap.add_argument("--side-layout", choices=["a", "b", "c", "d"], default=None,
+                    help="side-lane layout with several sampler streams (stack.side_layout; "
+                         "default: the config's LAYOUTS entry)")
     ap.add_argument("--private-side", action="store_true",
                     help="every buffer set gets its own side streams (side work of consecutive "
                          "steps runs concurrently; needs 1 + 2 x sets + sampler lanes - 1 "
@@ -333,6 +348,15 @@ def main():
         sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
     if args.dry_run:
         return dry_run(args)
+    lay = LAYOUTS[args.config]
+    if args.sampler_lanes is None:
+        args.sampler_lanes = 1 if args.model else lay["lanes"]
+    if args.sets is None:
+        args.sets = 3 if args.model else lay["sets"]
+    if args.side_layout is None:
+        args.side_layout = lay["side"]
+    if args.hw_queues is None and not args.model and args.sampler_lanes == lay["lanes"]:
+        args.hw_queues = lay["queues"]  # one queue per stream (the box's default is 4)
     if args.hw_queues is not None:
         os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, max(1, args.hw_queues)))
     else:
@@ -390,7 +414,7 @@ def main():
                                       sampler_lanes=1 if model else args.sampler_lanes,
                                       private_streams=model or args.private_side,
                                       native_plan=not args.no_native_plan,
-                                      only=args.diag_only)
+                                      only=args.diag_only, layout=args.side_layout)
         else:
             step = pkg.stack.Step(inp, overlap=overlap)
             graph = None if args.eager else pkg.stack.GraphStep(inp, overlap=overlap)
@@ -496,7 +520,8 @@ def main():
                        "lane0_priority": prio0,
                        "streams": (("SA1 sampler + 3 side streams" if args.sampler_lanes <= 1 or args.model
                                     else f"{args.sampler_lanes} sampler streams (consecutive steps' "
-                                    "samplers concurrent; SA2.. samplers behind SA1) + 2 side streams"
+                                    f"samplers concurrent; SA2.. samplers behind SA1) + side streams "
+                                    f"(layout {args.side_layout})"
                                     + (" per buffer set" if args.private_side else ""))
                                    if overlap else "one stream")
                        + (f", steps software-pipelined over {args.sets} buffer sets" if pipelined else "")},

@@ -36,8 +36,6 @@ SSG_FP_MLP = ((256, 256), (256, 256), (256, 128), (128, 128, 128))
 NUM_CLASSES = 21  # ScanNet (pointnet2_sem_seg_attention.py:17)
 
 NSIDE = 4  # side streams of the whole-model step (the geometric steps use 3)
-import os as _os
-SIDE_LAYOUT = _os.environ.get("PN2_SIDE_LAYOUT", "a")
 
 CONFIGS = {
     # name: (points per cloud, kind, with_features, attention)
@@ -138,6 +136,24 @@ def side_stream(dev, lane):
     return _SIDE[key]
 
 
+SIDE_LAYOUTS = ("a", "b", "c", "d")
+
+
+def side_layout(multi, attention, layout="a"):
+    """Side lanes of the SSG geometric step's later SA layers (sa234) and first three FP layers
+    (fp123); SA1 (with the grid) stays on lane 1, FP4 on lane 2, the attention reductions of
+    the multi-sampler layout on lane 3. Without several sampler streams: lanes 1 and 2.
+    With them: a = lanes 1 and 2; b = FP1-3 on a lane of their own; c = SA2-4 on a lane of
+    their own; d = both (measured: DESIGN.md §3.6)."""
+    if layout not in SIDE_LAYOUTS:
+        raise ValueError(f"side layout {layout!r}: one of {SIDE_LAYOUTS}")
+    if not multi:
+        return {"sa234": 1, "fp123": 2}
+    nxt = 4 if attention else 3
+    return {"a": {"sa234": 1, "fp123": 2}, "b": {"sa234": 1, "fp123": nxt},
+            "c": {"sa234": nxt, "fp123": 2}, "d": {"sa234": nxt, "fp123": nxt + 1}}[layout]
+
+
 class Task:
     """One piece of a step: `fn` runs on stream `lane` (0 = the sampler chain, 1.. = side
     streams) after the tasks named in `deps` (same-lane order is implicit)."""
@@ -176,10 +192,11 @@ class Step:
 
     SAMPLER = "fps1"
 
-    def __init__(self, inp, overlap=True, streams=None, chain_lane=3):
+    def __init__(self, inp, overlap=True, streams=None, chain_lane=3, layout="a"):
         # chain_lane: the lane of the later samplers (SA2..SA4 / MSG SA2); 0 = behind the SA1
-        # sampler on its stream (Pipeline with several sampler lanes)
+        # sampler on its stream (Pipeline with several sampler lanes); layout: side_layout()
         self.chain_lane = chain_lane if overlap else 0
+        self.layout = layout
         self.inp = inp
         self.kind = CONFIGS[inp["config"]][1]
         self.overlap = overlap and inp["xyz"].is_cuda
@@ -220,11 +237,7 @@ class Step:
         # inputs) run there instead of inside lane 1's SA tasks
         multi = self.chain_lane == 0 and self.overlap
         attn_lane = 3 if (multi and "attn" in inp) else None
-        # SIDE_LAYOUT "b" (experimental): FP1..FP3 on their own lane (cfg2: lane 3; cfg3: lane
-        # 4, the attention keeps lane 3), FP4 alone on lane 2
-        fp_small = 2
-        if multi and SIDE_LAYOUT == "b":
-            fp_small = 4 if attn_lane else 3
+        lane = side_layout(multi, attn_lane is not None, self.layout)
         tasks = []
         if big:  # the SA1 grid over the input cloud (also orders FP4's neighbour search)
             tasks.append(Task("grid1", 1, (), lambda: v.__setitem__(
@@ -293,10 +306,10 @@ class Step:
         tasks.append(Task("sa1", 1, (sampled[0],), sa(0)))
         tasks.append(Task("fp4", 2, (sampled[0],) + grid_dep, fp(0)))
         for i in (1, 2, 3):
-            tasks.append(Task(f"sa{i + 1}", 1, (sampled[i],), sa(i)))
-        tasks.append(Task("fp3", fp_small, (sampled[1],), fp(1)))
-        tasks.append(Task("fp2", fp_small, (sampled[2],), fp(2)))
-        tasks.append(Task("fp1", fp_small, (sampled[3],), fp(3)))
+            tasks.append(Task(f"sa{i + 1}", lane["sa234"], (sampled[i],), sa(i)))
+        tasks.append(Task("fp3", lane["fp123"], (sampled[1],), fp(1)))
+        tasks.append(Task("fp2", lane["fp123"], (sampled[2],), fp(2)))
+        tasks.append(Task("fp1", lane["fp123"], (sampled[3],), fp(3)))
         if attn_lane is not None:
             for i in range(4):
                 tasks.append(Task(f"att{i + 1}", attn_lane, (), att(i)))
@@ -629,10 +642,11 @@ class GraphStep:
     eager step. Inputs stay resident, outputs are overwritten in place at every replay."""
 
     def __init__(self, inp, warmup=2, overlap=True, streams=None, chain_lane=3, segments=False,
-                 only=None):
+                 only=None, layout="a"):
         # segments: capture one graph per launch segment (Step.segments(), for a native plan:
         # replay_plan) instead of one per task (replay)
-        self.step = Step(inp, overlap=overlap, streams=streams, chain_lane=chain_lane)
+        self.step = Step(inp, overlap=overlap, streams=streams, chain_lane=chain_lane,
+                         layout=layout)
         self.segmented = segments and self.step.overlap
         dev = inp["xyz"].device
         warm = side_stream(dev, "warm")
@@ -727,7 +741,7 @@ class Pipeline:
     1 + 2 + (sampler_lanes - 1) <= GPU_MAX_HW_QUEUES."""
 
     def __init__(self, inp, graphs=True, overlap=True, nsets=3, private_streams=False,
-                 sampler_lanes=1, native_plan=True, only=None):
+                 sampler_lanes=1, native_plan=True, only=None, layout="a"):
         # private_streams: every buffer set gets its own side streams, so the side lanes of
         # consecutive steps overlap each other too (the whole-model step, whose lane-1 chain
         # of SA/FP layers is longer than a sampler period; the geometric step once its
@@ -760,9 +774,9 @@ class Pipeline:
         self.native_plan = native_plan and graphs and overlap and inp["xyz"].is_cuda
         # only: DIAGNOSTIC restriction of every step to its samplers or its side work
         mk = (lambda i: GraphStep(inp, overlap=overlap, streams=streams(i), chain_lane=chain_lane,
-                                  segments=self.native_plan, only=only)) \
+                                  segments=self.native_plan, only=only, layout=layout)) \
             if graphs else (lambda i: Step(inp, overlap=overlap, streams=streams(i),
-                                           chain_lane=chain_lane))
+                                           chain_lane=chain_lane, layout=layout))
         self.sets = [mk(i) for i in range(nsets)]
         self.k = 0
 

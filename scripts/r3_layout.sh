@@ -5,9 +5,9 @@ OUT=gpurun_out/r3/layout
 mkdir -p $OUT
 for c in ${CONFIGS:-cfg2 cfg3}; do
   for lay in a b; do
-    for v in ${VARIANTS:-"3 6 9" "3 7 9" "4 8 8"}; do
-      set -- $v
-      for only in full side; do
+    for v in ${VARIANTS:-3:6:9 3:7:9 4:8:8}; do
+      set -- ${v//:/ }
+      for only in ${ONLY:-full side}; do
         D=""; [ "$only" != "full" ] && D="--diag-only $only"
         tag=${c}_${lay}_$1_$2_$3_$only
         PN2_SIDE_LAYOUT=$lay timeout -k 10 200 python3 bench.py --config $c --steps 400 --warmup 30 --no-cpu-baseline --e2e-steps 0 \

@@ -127,18 +127,20 @@ def _poison_sampled(pipe, torch):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("lanes,native", [(1, False), (1, True), (2, True)])
+@pytest.mark.parametrize("lanes,native,layout", [(1, False, "a"), (1, True, "a"), (2, True, "a"),
+                                                 (3, True, "b")])
 @pytest.mark.parametrize("config,B", CONFIGS)
-def test_pipeline_full_size(env, config, B, lanes, native):
+def test_pipeline_full_size(env, config, B, lanes, native, layout):
     """What bench.py times: the software-pipelined hipGraph steps over 3 buffer sets, at the
-    BASELINE batch, after several rotations, with one sampler stream or two (consecutive steps'
-    samplers concurrent), enqueued by the Python task loop or by the native plan
-    (include/pn2plan.h). The sampled coordinates of every set are poisoned before the last
-    three steps (a missing wait then shows), and the last two steps' outputs (one per sampler
-    stream) are compared with the oracle."""
+    BASELINE batch, after several rotations, with one, two or three sampler streams
+    (consecutive steps' samplers concurrent), enqueued by the Python task loop or by the native
+    plan (include/pn2plan.h), side layouts a and b (stack.side_layout). The sampled coordinates
+    of every set are poisoned before the last three steps (a missing wait then shows), and the
+    last two steps' outputs (one per sampler stream) are compared with the oracle."""
     pkg, O, torch, dev = env
     inp = pkg.stack.make_inputs(config, list(range(100, 100 + B)), dev)
-    pipe = pkg.stack.Pipeline(inp, graphs=True, nsets=3, sampler_lanes=lanes, native_plan=native)
+    pipe = pkg.stack.Pipeline(inp, graphs=True, nsets=3, sampler_lanes=lanes, native_plan=native,
+                              layout=layout)
     assert len(pipe.lane0) == lanes
     assert pipe.native_plan == native
     for _ in range(7):
