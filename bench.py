@@ -167,9 +167,11 @@ def sa1_latency(config, fps_ms, M1, N):
     plus the cloud read at one CU's share of HBM. floor = setup + (M - 1) x pick + rounds x
     round; frac = floor / measured launch (1 = the launch runs at the floor)."""
     out = {"ns_per_pick": fps_ms * 1e6 / max(1, M1 - 1)}
-    st, st_src = _latest_profile("sa1_cull_stamps.json")
+    # cfg2/cfg3 SA1 (8192 -> 1024) and cfg5's MSG SA1 (16384 -> 512) are stamped separately
+    st, st_src = _latest_profile("msg_cull_stamps.json" if config == "cfg5" else
+                                 "sa1_cull_stamps.json")
     fl, fl_src = _latest_profile("sampler_floor.json")
-    if config in ("cfg2", "cfg3") and st:
+    if config in ("cfg2", "cfg3", "cfg5") and st:
         out.update({k: st[k] for k in ("hot_cycles_per_pick", "rounds", "round_cycles",
                                       "setup_cycles", "kernel_cycles") if k in st})
         out["source"] = st_src

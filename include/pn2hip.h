@@ -227,6 +227,27 @@ int pn2_sample_and_group(const float* xyz, const float* points, int B, int N, in
                          float* new_xyz, int32_t* idx, int32_t* pts_cnt, float* grouped_xyz,
                          float* new_points, pn2_stream_t stream);
 
+/* Several set-abstraction layers' ball query + fused group/centre/concat in ONE launch
+ * (the SSG stack's SA2..SA4, or one MSG level's radii, which all wait for the same sampler).
+ * Per layer the outputs equal pn2_ball_query (idx, pts_cnt) followed by pn2_group_concat
+ * (new_points, grouped_xyz) with the same arguments, bit for bit. Limits: N <= 1024 points
+ * per cloud (the cloud is staged in LDS), nsample <= 128, at most PN2_SA_MAX_LAYERS layers;
+ * every layer has the same B. grouped_xyz may be NULL. */
+#define PN2_SA_MAX_LAYERS 4
+typedef struct pn2_sa_layer {
+  const float* xyz;     /* (B,N,3) */
+  const float* points;  /* (B,N,C) or NULL (then C is ignored and Cout = 3) */
+  const float* new_xyz; /* (B,M,3) query centres */
+  int N, C, M, nsample;
+  float radius;
+  int flags;            /* PN2_USE_XYZ | PN2_XYZ_LAST, as pn2_group_concat */
+  int32_t* idx;         /* (B,M,nsample) */
+  int32_t* pts_cnt;     /* (B,M) */
+  float* grouped_xyz;   /* (B,M,nsample,3) or NULL */
+  float* new_points;    /* (B,M,nsample,Cout) */
+} pn2_sa_layer;
+int pn2_ball_group_layers(const pn2_sa_layer* layers, int nlayers, int B, pn2_stream_t stream);
+
 /* ---------------------------------------------------------------- interpolation --------- */
 
 /* Three nearest known points (xyz2, (B,m,3)) of every unknown point (xyz1, (B,n,3)):
@@ -260,6 +281,20 @@ int pn2_idw_weights(const float* dist, int B, int n, float* weight, pn2_stream_t
 int pn2_fp_fused(const float* xyz1, const float* xyz2, const float* points1, int C1,
                  const float* points2, int C2, int B, int n, int m, float* out,
                  pn2_stream_t stream);
+
+/* Several pn2_fp_fused layers in ONE launch (the FP layers that wait for the same sampler):
+ * per layer exactly pn2_fp_fused's output, bit for bit. At most PN2_FP_MAX_LAYERS layers,
+ * every layer has the same B. */
+#define PN2_FP_MAX_LAYERS 4
+typedef struct pn2_fp_layer {
+  const float* xyz1;    /* (B,n,3) unknown points */
+  const float* xyz2;    /* (B,m,3) known points */
+  const float* points1; /* (B,n,C1) or NULL (C1 = 0) */
+  const float* points2; /* (B,m,C2) */
+  int C1, C2, n, m;
+  float* out;           /* (B,n,C2+C1) */
+} pn2_fp_layer;
+int pn2_fp_fused_layers(const pn2_fp_layer* layers, int nlayers, int B, pn2_stream_t stream);
 
 /* three_nn over pn2_grid_build(xyz2 = the m known points): the same dist/idx as
  * pn2_three_nn. `unknown_grid` (optional, a grid over the n unknown points xyz1) only orders

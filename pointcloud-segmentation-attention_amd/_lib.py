@@ -44,6 +44,28 @@ class MlpLayer(ctypes.Structure):
     _fields_ = [("packed", ctypes.c_void_p), ("cin", ctypes.c_int), ("cout", ctypes.c_int),
                 ("flags", ctypes.c_int)]
 
+class SaLayer(ctypes.Structure):
+    """struct pn2_sa_layer (include/pn2hip.h)."""
+    _fields_ = [("xyz", ctypes.c_void_p), ("points", ctypes.c_void_p),
+                ("new_xyz", ctypes.c_void_p), ("N", ctypes.c_int), ("C", ctypes.c_int),
+                ("M", ctypes.c_int), ("nsample", ctypes.c_int), ("radius", ctypes.c_float),
+                ("flags", ctypes.c_int), ("idx", ctypes.c_void_p), ("pts_cnt", ctypes.c_void_p),
+                ("grouped_xyz", ctypes.c_void_p), ("new_points", ctypes.c_void_p)]
+
+
+PN2_SA_MAX_LAYERS = 4
+
+
+class FpLayer(ctypes.Structure):
+    """struct pn2_fp_layer (include/pn2hip.h)."""
+    _fields_ = [("xyz1", ctypes.c_void_p), ("xyz2", ctypes.c_void_p),
+                ("points1", ctypes.c_void_p), ("points2", ctypes.c_void_p), ("C1", ctypes.c_int),
+                ("C2", ctypes.c_int), ("n", ctypes.c_int), ("m", ctypes.c_int),
+                ("out", ctypes.c_void_p)]
+
+
+PN2_FP_MAX_LAYERS = 4
+
 # name -> (restype, argtypes); mirrors include/pn2hip.h and include/pn2plan.h (tests/test_capi.py checks the header)
 SIGNATURES = {
     "pn2_version": (ctypes.c_char_p, []),
@@ -73,6 +95,7 @@ SIGNATURES = {
     "pn2_group_point": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _P]),
     "pn2_group_point_grad": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _P]),
     "pn2_group_concat": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P]),
+    "pn2_ball_group_layers": (_I, [_P, _I, _I, _P]),
     "pn2_sample_and_group": (_I, [_P, _P, _I, _I, _I, _I, _F, _I, _I, _P, _P, _P, _P, _P, _P,
                                   _P]),
     "pn2_three_nn": (_I, [_P, _P, _I, _I, _I, _P, _P, _P]),
@@ -82,6 +105,7 @@ SIGNATURES = {
     "pn2cpu_three_nn": (_I, [_P, _P, _I, _I, _I, _P, _P]),
     "pn2cpu_three_interpolate": (_I, [_P, _P, _P, _I, _I, _I, _I, _P]),
     "pn2cpu_three_interpolate_grad": (_I, [_P, _P, _P, _I, _I, _I, _I, _P]),
+    "pn2_fp_fused_layers": (_I, [_P, _I, _I, _P]),
     "pn2_fp_fused": (_I, [_P, _P, _P, _I, _P, _I, _I, _I, _I, _P, _P]),
     "pn2_attn_reduce": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P]),
     "pn2_attn_reduce_grad": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P]),

@@ -324,27 +324,37 @@ __global__ __launch_bounds__(kBlock) void three_interp_grad_kernel(
   }
 }
 
-// pointnet_fp_module geometry. Workgroup (x, b, z): unknown points [64x, 64x+64) of cloud b,
-// columns [z*cw, (z+1)*cw) of the Cout = C2 + C1 concat row (V2- / V1-float columns).
-// PRE: the three neighbours come from a previous three_nn (pdist, pidx) instead of the scan;
-// with `ugrid` (a grid over the unknown points) the workgroup's 64 rows are 64 consecutive
-// points in cell order, so their neighbours' feature rows are shared through the caches.
+// pointnet_fp_module geometry (fp_fused_kernel below). One FP layer's arguments (a launch may carry several, fp_fused_layers_kernel).
+struct FpLayer {
+  const float* xyz1;
+  const float* xyz2;
+  const float* pdist;
+  const int32_t* pidx;
+  const void* ugrid;
+  const float* points1;
+  const float* points2;
+  float* out;
+  int C1, C2, n, m, cw, B, Z;
+  FastDiv div_cw;
+};
+
 template <int V2, int V1, bool PRE, int UN>
-__global__ __launch_bounds__(kNNBlock) void fp_fused_kernel(
-    const float* __restrict__ xyz1, const float* __restrict__ xyz2,
-    const float* __restrict__ pdist, const int32_t* __restrict__ pidx,
-    const void* __restrict__ ugrid,
-    const float* __restrict__ points1, int C1, const float* __restrict__ points2, int C2, int n,
-    int m, int cw, FastDiv div_cw, int B, int Z, float* __restrict__ out) {
+PN2_DEV void fp_fused_body(const FpLayer& p, int Lg) {
   __shared__ float4 sk[PRE ? 1 : kNNTile];
   __shared__ int4 s_idx[kNNRows];
   __shared__ float4 s_w[kNNRows];
   __shared__ int s_row[PRE ? kNNRows : 1];
-  // logical block (cloud b, channel slice z, row block x), XCD-aware: the blocks of a cloud
-  // share one L2, which then holds that cloud's points2 rows once
+  const float* __restrict__ xyz1 = p.xyz1;
+  const float* __restrict__ xyz2 = p.xyz2;
+  const float* __restrict__ pdist = p.pdist;
+  const int32_t* __restrict__ pidx = p.pidx;
+  const void* __restrict__ ugrid = p.ugrid;
+  const float* __restrict__ points1 = p.points1;
+  const float* __restrict__ points2 = p.points2;
+  float* __restrict__ out = p.out;
+  const int C1 = p.C1, C2 = p.C2, n = p.n, m = p.m, cw = p.cw, Z = p.Z;
+  const FastDiv div_cw = p.div_cw;
   const int R = (n + kNNRows - 1) / kNNRows;
-  const int Lg = xcd_block(blockIdx.x, R * B * Z);
-  if (Lg >= R * B * Z) return;
   const int b = Lg / (R * Z);
   const int zb = (Lg - b * R * Z) / R;
   const int j0 = (Lg - b * R * Z - zb * R) * kNNRows;
@@ -484,6 +494,38 @@ __global__ __launch_bounds__(kNNBlock) void fp_fused_kernel(
   }
 }
 
+// Workgroup (x, b, z) of one layer: unknown points [64x, 64x+64) of cloud b, columns
+// [z*cw, (z+1)*cw) of the Cout = C2 + C1 concat row (V2- / V1-float columns). PRE: the three
+// neighbours come from a previous three_nn (pdist, pidx) instead of the scan; with `ugrid` (a
+// grid over the unknown points) the workgroup's 64 rows are 64 consecutive points in cell
+// order, so their neighbours' feature rows are shared through the caches. Logical blocks are
+// XCD-aware: the blocks of a cloud share one L2, which then holds its points2 rows once.
+template <int V2, int V1, bool PRE, int UN>
+__global__ __launch_bounds__(kNNBlock) void fp_fused_kernel(FpLayer p) {
+  const int total = (p.n + kNNRows - 1) / kNNRows * p.B * p.Z;
+  const int Lg = xcd_block(blockIdx.x, total);
+  if (Lg >= total) return;
+  fp_fused_body<V2, V1, PRE, UN>(p, Lg);
+}
+
+// Several FP layers in one launch (the FP layers that wait for the same sampler): logical
+// blocks [first[i], first[i+1]) are layer i's, in fp_fused_kernel's order.
+constexpr int kFpMaxLayers = PN2_FP_MAX_LAYERS;
+struct FpLayers {
+  FpLayer l[kFpMaxLayers];
+  int first[kFpMaxLayers + 1];
+  int nlayers;
+};
+template <int V2, int V1, bool PRE, int UN>
+__global__ __launch_bounds__(kNNBlock) void fp_fused_layers_kernel(FpLayers a) {
+  const int total = a.first[a.nlayers];
+  const int L = xcd_block(blockIdx.x, total);
+  if (L >= total) return;
+  int li = 0;
+  while (li + 1 < a.nlayers && L >= a.first[li + 1]) ++li;
+  fp_fused_body<V2, V1, PRE, UN>(a.l[li], L - a.first[li]);
+}
+
 // Largest batch chunk whose 32-bit row arithmetic stays exact (rows*n < 2^32, see FastDiv).
 int batch_chunk(int B, int n, int C, int rows) {
   if ((long long)rows * C * C >= (1LL << 32)) return 0;
@@ -494,10 +536,29 @@ int batch_chunk(int B, int n, int C, int rows) {
   return (int)(ch < B ? ch : B);
 }
 
-// Launch of fp_fused_kernel: the search (xyz1, xyz2) or precomputed neighbours (pdist, pidx).
-int fp_launch(const float* xyz1, const float* xyz2, const float* pdist, const int32_t* pidx,
-              const void* ugrid, const float* points1, int C1, const float* points2, int C2,
-              int B, int n, int m, float* out, hipStream_t stream) {
+// Channel split of an FP layer over grid.z (A/B knobs, tools/bench_layers.py): split until
+// PN2_FP_MIN_BLOCKS workgroups, keeping >= PN2_FP_MIN_COLS vector columns per workgroup and
+// (search variant, which scans the m known points again per slice) m * slices <= the budget
+#ifndef PN2_FP_MIN_BLOCKS
+#define PN2_FP_MIN_BLOCKS 512
+#endif
+#ifndef PN2_FP_MIN_COLS
+#define PN2_FP_MIN_COLS 16
+#endif
+#ifndef PN2_FP_SCAN_BUDGET
+#define PN2_FP_SCAN_BUDGET 4096
+#endif
+
+// One layer's launch configuration: the FpLayer and its kernel variant (vector widths, PRE).
+struct FpPlan {
+  FpLayer p;
+  int v2, v1, pre, blocks;
+};
+
+// The search (xyz1, xyz2) or precomputed neighbours (pdist, pidx).
+int fp_plan(const float* xyz1, const float* xyz2, const float* pdist, const int32_t* pidx,
+            const void* ugrid, const float* points1, int C1, const float* points2, int C2,
+            int B, int n, int m, float* out, FpPlan& f) {
   const bool pre = pdist != nullptr;
   // interpolated columns of 4 floats when C2 % 4 == 0 (16 B aligned loads and, on rows that
   // start 16 B aligned, stores); concat columns of 4 when C1 % 4 == 0 as well
@@ -508,31 +569,93 @@ int fp_launch(const float* xyz1, const float* xyz2, const float* pdist, const in
   // split the channels over grid.z until ~2 workgroups per CU, keeping >= 16 vector columns
   // per workgroup and (search variant) not re-running a long known-point scan too often
   int zsplit = 1;
-  while ((long long)row_blocks * B * zsplit < 512 && coutv / (zsplit * 2) >= 16 &&
-         (pre || (long long)m * zsplit * 2 <= 4096))
+  while ((long long)row_blocks * B * zsplit < PN2_FP_MIN_BLOCKS &&
+         coutv / (zsplit * 2) >= PN2_FP_MIN_COLS &&
+         (pre || (long long)m * zsplit * 2 <= PN2_FP_SCAN_BUDGET))
     zsplit *= 2;
   const int cw = (coutv + zsplit - 1) / zsplit;
   if ((long long)kNNRows * cw * cw >= (1LL << 32)) return PN2_EINVAL;
   if ((long long)row_blocks * B * zsplit >= (1LL << 31) - 8) return PN2_EINVAL;
-  const dim3 grid(xcd_grid((long long)row_blocks * B * zsplit));
-  const FastDiv div = make_fastdiv((uint32_t)cw);
+  f.p = FpLayer{xyz1, xyz2, pdist, pidx, ugrid, points1, points2, out,
+                C1, C2, n, m, cw, B, zsplit, make_fastdiv((uint32_t)cw)};
+  f.v2 = v2;
+  f.v1 = v1;
+  f.pre = pre;
+  f.blocks = row_blocks * B * zsplit;
+  return PN2_OK;
+}
+
+int fp_unroll() {
   static const int unroll = [] {  // (PN2_FP_UNROLL: A/B knob of tools/bench_fp.py)
     const char* e = getenv("PN2_FP_UNROLL");
     return e ? atoi(e) : 0;
   }();
-#define PN2_FP(V2, V1, P)                                                                      \
-  if (unroll == 1) PN2_FPU(V2, V1, P, 1);                                                      \
-  else if (unroll == 4) PN2_FPU(V2, V1, P, 4);                                                \
-  else PN2_FPU(V2, V1, P, 2)
-#define PN2_FPU(V2, V1, P, U)                                                                  \
-  hipLaunchKernelGGL((fp_fused_kernel<V2, V1, P, U>), grid, dim3(kNNBlock), 0, stream, xyz1,  \
-                     xyz2, pdist, pidx, ugrid, points1, C1, points2, C2, n, m, cw, div, B,     \
-                     zsplit, out)
-  if (v1) { if (pre) PN2_FP(4, 4, true); else PN2_FP(4, 4, false); }
-  else if (v2) { if (pre) PN2_FP(4, 1, true); else PN2_FP(4, 1, false); }
-  else { if (pre) PN2_FP(1, 1, true); else PN2_FP(1, 1, false); }
-#undef PN2_FP
-#undef PN2_FPU
+  return unroll;
+}
+
+// the kernel variant of `f` over `blocks` logical blocks: K = fp_fused_kernel (arg FpLayer) or
+// fp_fused_layers_kernel (arg FpLayers)
+#define PN2_FP_DISPATCH(KERNEL, f, arg, blocks, stream)                                        \
+  do {                                                                                         \
+    const dim3 grid__(xcd_grid(blocks));                                                       \
+    const int un__ = fp_unroll();                                                              \
+    if ((f).v1) { PN2_FP_PRE(KERNEL, 4, 4, f, arg, grid__, un__, stream); }                    \
+    else if ((f).v2) { PN2_FP_PRE(KERNEL, 4, 1, f, arg, grid__, un__, stream); }               \
+    else { PN2_FP_PRE(KERNEL, 1, 1, f, arg, grid__, un__, stream); }                           \
+  } while (0)
+#define PN2_FP_PRE(KERNEL, V2, V1, f, arg, grid, un, stream)                                   \
+  if ((f).pre) PN2_FP_UN(KERNEL, V2, V1, true, arg, grid, un, stream);                         \
+  else PN2_FP_UN(KERNEL, V2, V1, false, arg, grid, un, stream)
+#define PN2_FP_UN(KERNEL, V2, V1, P, arg, grid, un, stream)                                    \
+  if (un == 1) hipLaunchKernelGGL((KERNEL<V2, V1, P, 1>), grid, dim3(kNNBlock), 0, stream, arg); \
+  else if (un == 4) hipLaunchKernelGGL((KERNEL<V2, V1, P, 4>), grid, dim3(kNNBlock), 0, stream, arg); \
+  else hipLaunchKernelGGL((KERNEL<V2, V1, P, 2>), grid, dim3(kNNBlock), 0, stream, arg)
+
+int fp_launch(const float* xyz1, const float* xyz2, const float* pdist, const int32_t* pidx,
+              const void* ugrid, const float* points1, int C1, const float* points2, int C2,
+              int B, int n, int m, float* out, hipStream_t stream) {
+  FpPlan f;
+  const int rc = fp_plan(xyz1, xyz2, pdist, pidx, ugrid, points1, C1, points2, C2, B, n, m, out, f);
+  if (rc != PN2_OK) return rc;
+  PN2_FP_DISPATCH(fp_fused_kernel, f, f.p, f.blocks, stream);
+  PN2_RETURN_LAUNCH();
+}
+
+int fp_layers_launch(const pn2_fp_layer* layers, int nlayers, int B, hipStream_t stream) {
+  if (!layers || nlayers < 1 || nlayers > PN2_FP_MAX_LAYERS || B < 0 || B > 65535)
+    return PN2_EINVAL;
+  FpLayers a{};
+  FpPlan f0{};
+  long long blocks = 0;
+  int nl = 0;
+  for (int i = 0; i < nlayers; ++i) {
+    const pn2_fp_layer& s = layers[i];
+    if (s.n < 0 || s.m < 0 || s.C1 < 0 || s.C2 < 0) return PN2_EINVAL;
+    if (!s.points1 && s.C1 != 0) return PN2_EINVAL;
+    if ((long long)B * s.n == 0 || s.C1 + s.C2 == 0) continue;  // nothing to write
+    if (!s.xyz1 || !s.out || (s.m > 0 && !s.xyz2) || (s.C2 > 0 && !s.points2)) return PN2_EINVAL;
+    if (s.m == 0 && s.C2 > 0) return PN2_EINVAL;
+    FpPlan f;
+    const int rc = fp_plan(s.xyz1, s.xyz2, nullptr, nullptr, nullptr, s.points1, s.C1,
+                                s.points2, s.C2, B, s.n, s.m, s.out, f);
+    if (rc != PN2_OK) return rc;
+    if (nl == 0) f0 = f;
+    if (f.v2 != f0.v2 || f.v1 != f0.v1) {
+      // another kernel variant: this layer runs as its own launch
+      PN2_FP_DISPATCH(fp_fused_kernel, f, f.p, f.blocks, stream);
+      const hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return (int)e;
+      continue;
+    }
+    a.l[nl] = f.p;
+    a.first[nl] = (int)blocks;
+    blocks += f.blocks;
+    ++nl;
+  }
+  if (nl == 0) return PN2_OK;
+  a.first[nl] = (int)blocks;
+  a.nlayers = nl;
+  PN2_FP_DISPATCH(fp_fused_layers_kernel, f0, a, blocks, stream);
   PN2_RETURN_LAUNCH();
 }
 
@@ -624,6 +747,10 @@ int pn2_fp_fused(const float* xyz1, const float* xyz2, const float* points1, int
   if (m == 0 && C2 > 0) return PN2_EINVAL;  // nothing to interpolate from
   return pn2::fp_launch(xyz1, xyz2, nullptr, nullptr, nullptr, points1, C1, points2, C2, B, n,
                         m, out, (hipStream_t)stream);
+}
+
+int pn2_fp_fused_layers(const pn2_fp_layer* layers, int nlayers, int B, pn2_stream_t stream) {
+  return pn2::fp_layers_launch(layers, nlayers, B, (hipStream_t)stream);
 }
 
 int pn2_fp_apply(const float* dist, const int32_t* idx, const void* unknown_grid,

@@ -1,0 +1,298 @@
+// Ball query + fused group/centre/concat of SEVERAL set-abstraction layers in ONE launch.
+//
+// Per layer the result is exactly pn2_ball_query followed by pn2_group_concat
+// (tf_grouping_g.cu:3-36 then :40-57 and pointnet_util.py:39-56 / :186-193): the same
+// membership test (d2 < T with T = pn2_ball_threshold(radius), tf_grouping_g.cu:24-25), the
+// first nsample hits in index order, empty slots repeating the first hit (:26-29),
+// pts_cnt = hits capped at nsample (:34), and the grouped rows xyz[idx] - new_xyz (one fp32
+// subtraction, pointnet_util.py:40) concatenated with points[idx].
+//
+// Why one kernel: SA2..SA4 of the SSG stack (and the MSG radii of a level) all wait for the
+// same sampler and each is a small launch (5-20 us). As two launches per layer they were six
+// back-to-back kernels on one side lane, each paying a launch gap; here they are one grid.
+// Fusing the query with the grouping also drops the idx round trip: the wave that found a
+// query's neighbours writes that query's grouped rows from the hits it holds in LDS, reading
+// neighbour coordinates from the LDS copy of the cloud it just scanned.
+//
+// Layout: workgroup = (layer, cloud, tile of queries), 4 waves, one wave per query. The
+// cloud's xyz (N <= kSgCap points) is staged in LDS as SoA. A query's output block
+// (nsample rows x Cout floats) is contiguous in HBM, so the wave streams it with 16-byte
+// stores (64 lanes x 4 consecutive floats; when nsample*Cout % 4 == 0 and the block is 16 B
+// aligned) -- the gathers behind it hit L2 (a cloud's feature rows are shared by its tiles,
+// which the XCD-aware order keeps on one XCD).
+#include "common.h"
+
+namespace pn2 {
+namespace {
+
+constexpr int kSgBlock = 256;
+constexpr int kSgWaves = kSgBlock / kWave;
+constexpr int kSgCap = 1024;    // points per cloud staged in LDS
+constexpr int kSgMaxNs = 128;   // nsample
+constexpr int kSgUnroll = 4;    // 64-point steps per scan iteration
+constexpr int kSgHits = 2048;   // hit slots per workgroup: qpb * nsample
+constexpr int kSgMaxQpb = 64;   // queries per workgroup
+// A/B knobs (tools/bench_layers.py): vector groups in flight per thread, 16-byte feature
+// loads where a group is four feature channels of one row, output bytes per workgroup
+#ifndef PN2_SG_U
+#define PN2_SG_U 2
+#endif
+#ifndef PN2_SG_VLOAD
+#define PN2_SG_VLOAD 1
+#endif
+// diagnostic builds only (results wrong): skip the scan (hits = the first ns points) or the
+// grouped-row writes, to split the kernel's time between its phases
+#ifndef PN2_SG_SKIP
+#define PN2_SG_SKIP 0
+#endif
+#ifndef PN2_SG_SPLIT_KB
+#define PN2_SG_SPLIT_KB 8
+#endif
+#ifndef PN2_SG_SPLIT_STAGE
+#define PN2_SG_SPLIT_STAGE 4096
+#endif
+#ifndef PN2_SG_TILE_KB
+#define PN2_SG_TILE_KB 32
+#endif
+
+enum SgLayout : int {
+  PN2_SG_POINTS_ONLY = 0,  // out = points[idx]                       (Cout = C)
+  PN2_SG_XYZ_ONLY = 1,     // out = xyz[idx] - new_xyz                (Cout = 3)
+  PN2_SG_XYZ_FIRST = 2,    // out = [xyz[idx] - new_xyz, points[idx]] (Cout = 3 + C)
+  PN2_SG_XYZ_LAST = 3,     // out = [points[idx], xyz[idx] - new_xyz] (Cout = C + 3)
+};
+
+struct SgLayer {
+  const float* xyz;
+  const float* points;
+  const float* new_xyz;
+  int32_t* idx;
+  int32_t* cnt;
+  float* grouped_xyz;
+  float* out;
+  int N, C, M, ns, Cout, layout, qpb, tiles;  // workgroups per cloud = tiles * parts
+  int parts, chunk;  // a query split over `parts` workgroups of `chunk` elements each
+  float thresh;
+  FastDiv div_cout, div_ns;
+  int vec;  // 16 B stores of 4 consecutive floats
+};
+
+struct SgArgs {
+  SgLayer l[PN2_SA_MAX_LAYERS];
+  int first[PN2_SA_MAX_LAYERS + 1];  // first logical block of each layer
+  int nlayers;
+};
+
+// out element c of a grouped row: xyz channel (>= 0) or -1 for a feature channel, and the
+// feature channel (SSG [xyz, points], MSG [points, xyz], xyz only, points only)
+PN2_DEV int xyz_channel(int layout, int c, int C, int& cp) {
+  cp = c;
+  if (layout == PN2_SG_XYZ_ONLY) return c;
+  if (layout == PN2_SG_XYZ_FIRST) {
+    if (c < 3) return c;
+    cp = c - 3;
+    return -1;
+  }
+  if (layout == PN2_SG_XYZ_LAST) return c >= C ? c - C : -1;
+  return -1;
+}
+
+__global__ __launch_bounds__(kSgBlock) void ball_group_layers_kernel(SgArgs a) {
+  __shared__ float sx[kSgCap], sy[kSgCap], sz[kSgCap];
+  __shared__ int s_hit[kSgHits];          // the tile's rows: query qi's hits at qi*ns ..
+  __shared__ float s_q[3 * kSgMaxQpb];    // the tile's query centres
+  const int total = a.first[a.nlayers];
+  const int L = xcd_block((int)blockIdx.x, total);
+  if (L >= total) return;  // padding blocks (before any barrier)
+  int li = 0;
+  while (li + 1 < a.nlayers && L >= a.first[li + 1]) ++li;
+  const SgLayer& g = a.l[li];
+  const int local = L - a.first[li];
+  const int per_cloud = g.tiles * g.parts;
+  const int b = local / per_cloud;
+  const int tile = (local - b * per_cloud) / g.parts;
+  const int part = local - b * per_cloud - tile * g.parts;
+  const int t = threadIdx.x, lane = t & (kWave - 1), w = t / kWave;
+  const int N = g.N, C = g.C, M = g.M, ns = g.ns, Cout = g.Cout, layout = g.layout;
+  const int q0 = tile * g.qpb, nq = min(g.qpb, M - q0);
+  const float* __restrict__ P = g.xyz + (size_t)b * N * 3;
+  for (int e = t; e < N; e += kSgBlock) {
+    sx[e] = P[3 * e + 0];
+    sy[e] = P[3 * e + 1];
+    sz[e] = P[3 * e + 2];
+  }
+  const float* __restrict__ Q = g.new_xyz + ((size_t)b * M + q0) * 3;
+  for (int e = t; e < 3 * nq; e += kSgBlock) s_q[e] = Q[e];
+  __syncthreads();
+  // ---- phase 1: one wave per query, the ball query (tf_grouping_g.cu:15-33) into s_hit
+  const uint64_t lower = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  for (int qi = w; qi < nq; qi += kSgWaves) {
+    const float qx = s_q[3 * qi + 0], qy = s_q[3 * qi + 1], qz = s_q[3 * qi + 2];
+    int* hit = s_hit + qi * ns;
+    int cnt = 0, first = 0;
+    if constexpr (PN2_SG_SKIP == 1) cnt = ns;
+    for (int base = 0; base < N && cnt < ns; base += kWave * kSgUnroll) {
+      bool h[kSgUnroll];
+#pragma unroll
+      for (int u = 0; u < kSgUnroll; ++u) {
+        const int k = base + u * kWave + lane;
+        h[u] = k < N && sqdist(qx, qy, qz, sx[k], sy[k], sz[k]) < g.thresh;
+      }
+#pragma unroll
+      for (int u = 0; u < kSgUnroll; ++u) {
+        const uint64_t mask = __ballot(h[u]);
+        if (mask != 0ull && cnt < ns) {
+          if (cnt == 0) first = base + u * kWave + (__ffsll((unsigned long long)mask) - 1);
+          const int pos = cnt + __popcll(mask & lower);
+          if (h[u] && pos < ns) hit[pos] = base + u * kWave + lane;
+          cnt += __popcll(mask);
+        }
+      }
+    }
+    if (cnt > ns) cnt = ns;
+    // the hits other lanes of this wave wrote are visible before the fill reads them
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const size_t gq = (size_t)b * M + q0 + qi;
+    int32_t* __restrict__ row = g.idx + gq * ns;
+    for (int p = lane; p < ns; p += kWave) {
+      const int v = p < cnt ? hit[p] : first;  // :26-29 (0 when no hit)
+      hit[p] = v;
+      if (part == 0) row[p] = v;
+    }
+    if (lane == 0 && part == 0) g.cnt[gq] = cnt;
+  }
+  __syncthreads();
+  // ---- phase 2: the tile's grouped rows (nq * ns rows of Cout floats) are ONE contiguous
+  // range of the output: the whole workgroup streams it, U vector groups in flight per thread
+  const size_t r_base = ((size_t)b * M + q0) * ns;  // first output row of the tile
+  float* __restrict__ O = g.out + r_base * Cout;
+  float* __restrict__ GX = g.grouped_xyz ? g.grouped_xyz + r_base * 3 : nullptr;
+  const float* __restrict__ F = g.points ? g.points + (size_t)b * N * C : nullptr;
+  // this workgroup's elements of the tile: all, or part `part` of a split query
+  const int e_beg = part * g.chunk;
+  const int E = PN2_SG_SKIP == 2 ? 0 : min(nq * ns * Cout, e_beg + g.chunk);
+  auto value = [&](int e) -> float {
+    const int r = (int)fdiv((uint32_t)e, g.div_cout);  // row of the tile
+    const int c = e - r * Cout;
+    const int qi = (int)fdiv((uint32_t)r, g.div_ns);
+    const int i = s_hit[r];
+    int cp;
+    const int cx = xyz_channel(layout, c, C, cp);
+    if (cx >= 0) {
+      const float s = cx == 0 ? sx[i] : (cx == 1 ? sy[i] : sz[i]);
+      const float v = s - s_q[3 * qi + cx];  // pointnet_util.py:40
+      if (GX) GX[(size_t)r * 3 + cx] = v;
+      return v;
+    }
+    return F[(size_t)i * C + cp];
+  };
+  if (g.vec) {
+    constexpr int U = PN2_SG_U;
+    for (int e0 = e_beg + t * 4; e0 < E; e0 += kSgBlock * 4 * U) {
+      float4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int e = e0 + u * kSgBlock * 4;
+        v[u] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        if (e >= E) continue;
+        if constexpr (PN2_SG_VLOAD) {
+          // four feature channels of one row: one 16-byte load (dword-aligned rows of C
+          // floats; gfx950 global loads need only dword alignment)
+          const int r = (int)fdiv((uint32_t)e, g.div_cout);
+          const int c = e - r * Cout;
+          const int f0 = layout == PN2_SG_XYZ_FIRST ? 3 : 0;
+          const int f1 = layout == PN2_SG_XYZ_LAST || layout == PN2_SG_POINTS_ONLY ? C : Cout;
+          if (layout != PN2_SG_XYZ_ONLY && c >= f0 && c + 4 <= f1) {
+            const float* src = F + (size_t)s_hit[r] * C + (c - f0);
+            typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
+            const f4u x = *reinterpret_cast<const f4u*>(src);
+            v[u] = make_float4(x[0], x[1], x[2], x[3]);
+            continue;
+          }
+        }
+        v[u] = make_float4(value(e), value(e + 1), value(e + 2), value(e + 3));
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int e = e0 + u * kSgBlock * 4;
+        if (e < E) *reinterpret_cast<float4*>(O + e) = v[u];
+      }
+    }
+  } else {
+    for (int e = e_beg + t; e < E; e += kSgBlock) O[e] = value(e);
+  }
+}
+
+}  // namespace
+}  // namespace pn2
+
+extern "C" {
+
+int pn2_ball_group_layers(const pn2_sa_layer* layers, int nlayers, int B, pn2_stream_t stream) {
+  if (!layers || nlayers < 1 || nlayers > PN2_SA_MAX_LAYERS || B < 0 || B > 65535)
+    return PN2_EINVAL;
+  pn2::SgArgs a{};
+  a.nlayers = nlayers;
+  long long blocks = 0;
+  for (int i = 0; i < nlayers; ++i) {
+    const pn2_sa_layer& s = layers[i];
+    pn2::SgLayer& g = a.l[i];
+    if (!(s.radius > 0.0f) || s.nsample <= 0 || s.nsample > pn2::kSgMaxNs || s.N < 0 ||
+        s.N > pn2::kSgCap || s.M < 0 || s.C < 0)
+      return PN2_EINVAL;
+    using namespace pn2;
+    int layout, Cout;
+    if (!s.points || s.C == 0) { layout = PN2_SG_XYZ_ONLY; Cout = 3; }
+    else if (!(s.flags & PN2_USE_XYZ)) { layout = PN2_SG_POINTS_ONLY; Cout = s.C; }
+    else { layout = (s.flags & PN2_XYZ_LAST) ? PN2_SG_XYZ_LAST : PN2_SG_XYZ_FIRST; Cout = s.C + 3; }
+    if ((long long)B * s.M > 0) {
+      if (!s.xyz || !s.new_xyz || !s.idx || !s.pts_cnt || !s.new_points) return PN2_EINVAL;
+      if (s.N == 0) return PN2_EINVAL;  // nothing to group from
+    }
+    g.xyz = s.xyz;
+    g.points = layout == PN2_SG_XYZ_ONLY ? nullptr : s.points;
+    g.new_xyz = s.new_xyz;
+    g.idx = s.idx;
+    g.cnt = s.pts_cnt;
+    g.grouped_xyz = layout == PN2_SG_XYZ_ONLY ? nullptr : s.grouped_xyz;
+    g.out = s.new_points;
+    g.N = s.N; g.C = layout == PN2_SG_XYZ_ONLY ? 0 : s.C; g.M = s.M; g.ns = s.nsample;
+    g.Cout = Cout; g.layout = layout;
+    g.thresh = pn2_ball_threshold(s.radius);
+    g.div_cout = pn2::make_fastdiv((uint32_t)Cout);
+    g.vec = (s.nsample * Cout) % 4 == 0 && ((uintptr_t)s.new_points & 15) == 0;
+    // work per workgroup: ~PN2_SG_TILE_KB of output over whole queries; a query of many
+    // channels on a small cloud (cheap to stage and scan again) is split over several
+    // workgroups of ~PN2_SG_SPLIT_KB each, so the grid has enough waves to hide the gathers
+    const long long per_q = (long long)s.nsample * Cout * 4;
+    long long qpb = (PN2_SG_TILE_KB * 1024 + per_q / 2) / per_q;
+    if (qpb < 1) qpb = 1;
+    if (qpb > pn2::kSgMaxQpb) qpb = pn2::kSgMaxQpb;
+    if (qpb * s.nsample > pn2::kSgHits) qpb = pn2::kSgHits / s.nsample;
+    long long parts = 1;
+    if (s.N * 12 <= PN2_SG_SPLIT_STAGE && per_q > PN2_SG_SPLIT_KB * 1024) {
+      qpb = 1;
+      parts = (per_q + PN2_SG_SPLIT_KB * 1024 - 1) / (PN2_SG_SPLIT_KB * 1024);
+    }
+    const long long E = qpb * s.nsample * Cout;
+    g.chunk = (int)(((E + parts - 1) / parts + 3) / 4 * 4);
+    g.parts = (int)((E + g.chunk - 1) / g.chunk);
+    // 32-bit FastDiv of tile elements by Cout and of tile rows by nsample stays exact
+    if (E * (long long)Cout >= (1LL << 32)) return PN2_EINVAL;
+    g.qpb = (int)qpb;
+    g.div_ns = pn2::make_fastdiv((uint32_t)s.nsample);
+    g.tiles = s.M > 0 ? (int)((s.M + qpb - 1) / qpb) : 0;
+    a.first[i] = (int)blocks;
+    blocks += (long long)B * g.tiles * g.parts;
+    if (blocks >= (1LL << 31) - 8) return PN2_EINVAL;
+  }
+  a.first[nlayers] = (int)blocks;
+  if (blocks == 0) return PN2_OK;
+  hipLaunchKernelGGL(pn2::ball_group_layers_kernel, dim3(pn2::xcd_grid(blocks)),
+                     dim3(pn2::kSgBlock), 0, (hipStream_t)stream, a);
+  PN2_RETURN_LAUNCH();
+}
+
+}  // extern "C"

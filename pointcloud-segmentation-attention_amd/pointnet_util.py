@@ -6,8 +6,10 @@ The geometric halves of the SA / FP layers:
   sample_and_group          pointnet_util.py:16-58    FPS + gather + ball query + fused group
   sample_and_group_all      pointnet_util.py:61-87
   sample_and_group_msg      pointnet_util.py:180-193  one FPS, several (radius, nsample) scales
+  ball_group_layers         several layers' query_ball_point + group_concat, one launch
   group_pool                pointnet_util.py:130-145  max / avg / weighted_avg / max_and_avg
   fp_interpolate            pointnet_util.py:218-228  three_nn + IDW + interpolate + concat
+  fp_interpolate_layers     several FP layers' fp_interpolate, one launch
 
 The whole layers, shared MLP included (tf_util.py for the parameters):
 
@@ -23,8 +25,9 @@ reference's registered gradients.
 import torch
 
 from . import tf_grouping, tf_interpolate, tf_sampling, tf_util
-from ._lib import (POOL_MODES, PN2_POOL_NONE, PN2_USE_XYZ, PN2_XYZ_LAST, InvalidArgumentError,
-                   check, device_tensor, lib, ptr, stream_of)
+from ._lib import (POOL_MODES, PN2_FP_MAX_LAYERS, PN2_POOL_NONE, PN2_SA_MAX_LAYERS, PN2_USE_XYZ,
+                   PN2_XYZ_LAST, FpLayer, InvalidArgumentError, SaLayer, check, device_tensor, lib,
+                   ptr, stream_of)
 
 
 def _is_empty_points(points):
@@ -67,6 +70,52 @@ def group_concat(xyz, points, new_xyz, idx, use_xyz=True, xyz_last=False, want_g
     if points is None and want_grouped_xyz:
         grouped_xyz = new_points  # identical values (pointnet_util.py:56)
     return new_points, grouped_xyz
+
+
+BALL_GROUP_MAX_POINTS = 1024  # pn2_ball_group_layers stages each cloud in LDS
+BALL_GROUP_MAX_NSAMPLE = 128
+
+
+def ball_group_layers(layers, use_xyz=True, xyz_last=False):
+    """query_ball_point followed by group_concat (want_grouped_xyz=False) for several layers
+    in ONE launch (pn2_ball_group_layers): layers = [(radius, nsample, xyz, points, new_xyz)],
+    every cloud at most BALL_GROUP_MAX_POINTS points. Returns [(idx, pts_cnt, new_points)],
+    bit-identical to the separate ops (tf_grouping_g.cu:3-57, pointnet_util.py:38-56)."""
+    if not 1 <= len(layers) <= PN2_SA_MAX_LAYERS:
+        raise InvalidArgumentError(f"ball_group_layers: 1..{PN2_SA_MAX_LAYERS} layers")
+    flags = (PN2_USE_XYZ if use_xyz else 0) | (PN2_XYZ_LAST if xyz_last else 0)
+    arr = (SaLayer * len(layers))()
+    outs, keep, B = [], [], None
+    for a, (radius, nsample, xyz, points, new_xyz) in zip(arr, layers):
+        xyz = device_tensor(xyz, "xyz", torch.float32)
+        new_xyz = device_tensor(new_xyz, "new_xyz", torch.float32)
+        if B is None:
+            B = int(xyz.shape[0])
+        N, M, ns = int(xyz.shape[1]), int(new_xyz.shape[1]), int(nsample)
+        if int(xyz.shape[0]) != B or int(new_xyz.shape[0]) != B:
+            raise InvalidArgumentError("ball_group_layers: every layer needs the same batch")
+        if N > BALL_GROUP_MAX_POINTS or not 0 < ns <= BALL_GROUP_MAX_NSAMPLE or not radius > 0:
+            raise InvalidArgumentError("ball_group_layers: N <= 1024, 0 < nsample <= 128, "
+                                       "radius > 0")
+        if _is_empty_points(points):
+            points, C, Cout = None, 0, 3
+        else:
+            points = device_tensor(points, "points", torch.float32)
+            if tuple(points.shape[:2]) != (B, N):
+                raise InvalidArgumentError("ball_group_layers: points (B,N,C) for xyz (B,N,3)")
+            C = int(points.shape[2])
+            Cout = C + 3 if use_xyz else C
+        idx = torch.empty((B, M, ns), dtype=torch.int32, device=xyz.device)
+        cnt = torch.empty((B, M), dtype=torch.int32, device=xyz.device)
+        new_points = torch.empty((B, M, ns, Cout), dtype=torch.float32, device=xyz.device)
+        a.xyz, a.points, a.new_xyz = ptr(xyz), ptr(points), ptr(new_xyz)
+        a.N, a.C, a.M, a.nsample, a.radius, a.flags = N, C, M, ns, float(radius), flags
+        a.idx, a.pts_cnt, a.grouped_xyz, a.new_points = ptr(idx), ptr(cnt), None, ptr(new_points)
+        keep += [xyz, points, new_xyz]
+        outs.append((idx, cnt, new_points))
+    check(lib().pn2_ball_group_layers(arr, len(layers), B, stream_of(keep[0])),
+          "ball_group_layers")
+    return outs
 
 
 def sample_and_group(npoint, radius, nsample, xyz, points, knn=False, use_xyz=True):
@@ -182,6 +231,40 @@ def fp_interpolate(xyz1, xyz2, points1, points2, known_grid=None, unknown_grid=N
         check(lib().pn2_fp_fused(ptr(xyz1), ptr(xyz2), ptr(points1), C1, ptr(points2), C2, B, n,
                                  m, ptr(out), stream_of(xyz1)), "fp_interpolate")
     return (out, nn) if return_nn else out
+
+
+def fp_interpolate_layers(layers):
+    """fp_interpolate (fused search path, no grid) of several FP layers in ONE launch
+    (pn2_fp_fused_layers): layers = [(xyz1, xyz2, points1, points2)] with the same batch.
+    Returns [out (B, n, C2 + C1)], bit-identical to fp_interpolate per layer."""
+    if not 1 <= len(layers) <= PN2_FP_MAX_LAYERS:
+        raise InvalidArgumentError(f"fp_interpolate_layers: 1..{PN2_FP_MAX_LAYERS} layers")
+    arr = (FpLayer * len(layers))()
+    outs, keep, B = [], [], None
+    for a, (xyz1, xyz2, points1, points2) in zip(arr, layers):
+        xyz1 = device_tensor(xyz1, "xyz1", torch.float32)
+        xyz2 = device_tensor(xyz2, "xyz2", torch.float32)
+        points2 = device_tensor(points2, "points2", torch.float32)
+        if B is None:
+            B = int(xyz1.shape[0])
+        n, m, C2 = int(xyz1.shape[1]), int(xyz2.shape[1]), int(points2.shape[2])
+        if int(xyz1.shape[0]) != B or int(xyz2.shape[0]) != B or tuple(points2.shape[:2]) != (B, m):
+            raise InvalidArgumentError("fp_interpolate_layers: xyz1 (B,n,3), xyz2 (B,m,3), "
+                                       "points2 (B,m,C2) with one batch size")
+        C1 = 0
+        if points1 is not None:
+            points1 = device_tensor(points1, "points1", torch.float32)
+            if tuple(points1.shape[:2]) != (B, n):
+                raise InvalidArgumentError("fp_interpolate_layers: points1 (B,n,C1)")
+            C1 = int(points1.shape[2])
+        out = torch.empty((B, n, C2 + C1), dtype=torch.float32, device=xyz1.device)
+        a.xyz1, a.xyz2, a.points1, a.points2 = ptr(xyz1), ptr(xyz2), ptr(points1), ptr(points2)
+        a.C1, a.C2, a.n, a.m, a.out = C1, C2, n, m, ptr(out)
+        keep += [xyz1, xyz2, points1, points2]
+        outs.append(out)
+    check(lib().pn2_fp_fused_layers(arr, len(layers), B, stream_of(keep[0])),
+          "fp_interpolate_layers")
+    return outs
 
 
 # ---------------------------------------------------------------- whole SA / FP layers -----

@@ -305,11 +305,36 @@ class Step:
             sampled = ("fps1", "fps234", "fps234", "fps234")
         tasks.append(Task("sa1", 1, (sampled[0],), sa(0)))
         tasks.append(Task("fp4", 2, (sampled[0],) + grid_dep, fp(0)))
-        for i in (1, 2, 3):
-            tasks.append(Task(f"sa{i + 1}", lane["sa234"], (sampled[i],), sa(i)))
-        tasks.append(Task("fp3", lane["fp123"], (sampled[1],), fp(1)))
-        tasks.append(Task("fp2", lane["fp123"], (sampled[2],), fp(2)))
-        tasks.append(Task("fp1", lane["fp123"], (sampled[3],), fp(3)))
+        if npoints[0] <= pointnet_util.BALL_GROUP_MAX_POINTS and sampled[1:] == ("fps234",) * 3:
+            # SA2..SA4 wait for the same sampler launch: their three ball queries and groupings
+            # run as ONE kernel (pn2_ball_group_layers) instead of six launches on the lane
+            def sa234():
+                specs = [(SSG_SA[i][1], SSG_SA[i][2], v["xyz"][i], points[i], v["xyz"][i + 1])
+                         for i in (1, 2, 3)]
+                for i, (idx, _, new_points) in zip((1, 2, 3),
+                                                   pointnet_util.ball_group_layers(specs)):
+                    v["bq"][i], v["sa"][i] = idx, new_points
+                if "attn" in inp and attn_lane is None:
+                    for i in (1, 2, 3):
+                        att(i)()
+            tasks.append(Task("sa234", lane["sa234"], (sampled[1],), sa234))
+        else:
+            for i in (1, 2, 3):
+                tasks.append(Task(f"sa{i + 1}", lane["sa234"], (sampled[i],), sa(i)))
+        small = [not tf_interpolate.use_grid(SSG_SA[i - 1][0] if i else int(inp["xyz"].shape[1]),
+                                             SSG_SA[i][0]) for i in (1, 2, 3)]
+        if all(small) and sampled[1:] == ("fps234",) * 3:
+            # FP3, FP2, FP1 wait for the same sampler launch: one kernel (pn2_fp_fused_layers)
+            def fp123():
+                outs = pointnet_util.fp_interpolate_layers(
+                    [(v["xyz"][i], v["xyz"][i + 1], points[i], fp_feat[3 - i]) for i in (1, 2, 3)])
+                for i, o in zip((1, 2, 3), outs):
+                    v["fp"][3 - i], v["nn"][3 - i] = o, None
+            tasks.append(Task("fp123", lane["fp123"], (sampled[1],), fp123))
+        else:
+            tasks.append(Task("fp3", lane["fp123"], (sampled[1],), fp(1)))
+            tasks.append(Task("fp2", lane["fp123"], (sampled[2],), fp(2)))
+            tasks.append(Task("fp1", lane["fp123"], (sampled[3],), fp(3)))
         if attn_lane is not None:
             for i in range(4):
                 tasks.append(Task(f"att{i + 1}", attn_lane, (), att(i)))

@@ -39,7 +39,9 @@ def test_latency_of_the_sa1_sampler(bench):
         v["rounds"] * v["floor_round_cycles"]
     assert abs(v["floor_launch_cycles"] - want) < 1e-6
     assert 0 < v["frac_pick"] <= 1 and 0 < v["frac_round"] <= 1
-    assert "rounds" not in bench.sa1_latency("cfg5", 1.3, 512, 16384)  # a different sampler
+    m = bench.sa1_latency("cfg5", 0.36, 512, 16384)  # the MSG sampler: its own stamps
+    assert m["source"].endswith("msg_cull_stamps.json") and m["rounds"] > 0
+    assert 0 < m["frac_pick"] <= 1 and m["floor_launch_ms"] < 0.36
 
 
 def test_cpu_baseline_leg(bench):

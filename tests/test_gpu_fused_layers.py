@@ -1,0 +1,123 @@
+"""GPU parity of the multi-layer launches against the oracle, bit for bit:
+
+* pointnet_util.ball_group_layers (pn2_ball_group_layers): several layers' query_ball_point +
+  group_concat in one kernel == oracle.ball_query + oracle.group_concat per layer
+  (tf_grouping_g.cu:3-57, pointnet_util.py:38-56 / :186-193);
+* pointnet_util.fp_interpolate_layers (pn2_fp_fused_layers): several FP layers' three_nn +
+  IDW + three_interpolate + concat in one kernel == pointnet_util.fp_interpolate per layer
+  (itself pinned to the oracle in test_gpu_parity.py::test_fp_fused).
+"""
+import importlib
+
+import numpy as np
+import pytest
+
+from conftest import PKG_NAME, gpu_available
+
+pytestmark = [pytest.mark.gpu,
+              pytest.mark.skipif(not gpu_available(), reason="needs an MI355X")]
+
+
+@pytest.fixture(scope="module")
+def env():
+    import torch
+
+    from oracle import oracle as O
+    O.set_threads(16)
+    pkg = importlib.import_module(PKG_NAME)
+    return pkg, O, torch, torch.device("cuda:0")
+
+
+def _bits(a):
+    return np.ascontiguousarray(a, np.float32).view(np.int32)
+
+
+def _layer(pkg, O, kind, B, N, M, C, seed):
+    if kind == "grid":  # integer lattice: exact distances on the radius
+        g = np.stack(np.meshgrid(*[np.arange(8)] * 3, indexing="ij"), -1).reshape(-1, 3)
+        rng = np.random.default_rng(seed)
+        x = np.stack([g[rng.integers(0, len(g), N)] for _ in range(B)]).astype(np.float32)
+        q = x[:, :M].copy()
+    else:
+        x = pkg.synth.batch(range(seed, seed + B), N, kind)[0]
+        q = O.gather_point(x, O.fps(x, M))
+    q[:, :1] = 50.0  # a query with no hit at all (idx 0, pts_cnt 0)
+    pts = pkg.synth.features_uniform(seed + 7, (B, N, C)) if C else None
+    return x, pts, q
+
+
+# (kind, N, M, C, radius, nsample) per layer; one list = one launch
+LAUNCHES = [
+    # the SSG stack's SA2..SA4 at cfg2 shapes
+    [("scannet", 1024, 256, 64, 0.2, 32), ("scannet", 256, 64, 128, 0.4, 32),
+     ("scannet", 64, 16, 256, 0.8, 32)],
+    # cfg3 features (C = 9 at SA1-like widths), and an odd Cout (scalar stores)
+    [("scannet", 1000, 100, 9, 0.2, 32), ("uniform", 300, 50, 2, 0.05, 3)],
+    # MSG level-2 radii (ns up to 128), no features, a lattice
+    [("scannet", 512, 128, 0, 0.2, 32), ("scannet", 512, 128, 0, 0.4, 64),
+     ("scannet", 512, 128, 0, 0.8, 128), ("grid", 700, 90, 5, 1.0, 16)],
+    # one layer, one point per cloud
+    [("uniform", 1, 4, 3, 0.5, 8)],
+]
+
+
+@pytest.mark.parametrize("li", range(len(LAUNCHES)))
+@pytest.mark.parametrize("use_xyz,xyz_last", [(True, False), (True, True), (False, False)])
+def test_ball_group_layers(env, li, use_xyz, xyz_last):
+    pkg, O, torch, dev = env
+    B = 3
+    t = lambda a: None if a is None else torch.from_numpy(a).to(dev)  # noqa: E731
+    specs, refs = [], []
+    for j, (kind, N, M, C, r, ns) in enumerate(LAUNCHES[li]):
+        if not use_xyz and C == 0:
+            C = 4  # points only needs points
+        x, pts, q = _layer(pkg, O, kind, B, N, M, C, 10 * li + j)
+        specs.append((r, ns, t(x), t(pts), t(q)))
+        ridx, rcnt = O.ball_query(x, q, r, ns)
+        rnp, _ = O.group_concat(x, pts, q, ridx, use_xyz=use_xyz, xyz_last=xyz_last)
+        refs.append((ridx, rcnt, rnp))
+    got = pkg.pointnet_util.ball_group_layers(specs, use_xyz=use_xyz, xyz_last=xyz_last)
+    for (idx, cnt, new_points), (ridx, rcnt, rnp) in zip(got, refs):
+        assert np.array_equal(cnt.cpu().numpy(), rcnt)
+        assert np.array_equal(idx.cpu().numpy(), ridx)
+        assert np.array_equal(_bits(new_points.cpu().numpy()), _bits(rnp))
+
+
+def test_ball_group_layers_rejects(env):
+    pkg, O, torch, dev = env
+    x = torch.zeros((2, 2000, 3), device=dev)
+    q = torch.zeros((2, 10, 3), device=dev)
+    with pytest.raises(pkg.tf_grouping.InvalidArgumentError):
+        pkg.pointnet_util.ball_group_layers([(0.1, 8, x, None, q)])  # N > 1024
+    x = torch.zeros((2, 100, 3), device=dev)
+    with pytest.raises(pkg.tf_grouping.InvalidArgumentError):
+        pkg.pointnet_util.ball_group_layers([(0.1, 129, x, None, q)])  # nsample > 128
+    with pytest.raises(pkg.tf_grouping.InvalidArgumentError):
+        pkg.pointnet_util.ball_group_layers([(0.1, 8, x, None, q[:1])])  # batch mismatch
+
+
+FP_LAUNCHES = [
+    # the SSG stack's FP3, FP2, FP1 at cfg2 shapes: (n, m, C1, C2)
+    [(1024, 256, 64, 256), (256, 64, 128, 256), (64, 16, 256, 512)],
+    # no points1, odd widths (scalar columns: another kernel variant, its own launch), m < 3
+    [(500, 100, 0, 32), (300, 37, 5, 7), (40, 2, 4, 8)],
+    [(1, 1, 4, 4)],
+]
+
+
+@pytest.mark.parametrize("li", range(len(FP_LAUNCHES)))
+def test_fp_interpolate_layers(env, li):
+    pkg, O, torch, dev = env
+    B = 3
+    t = lambda a: None if a is None else torch.from_numpy(a).to(dev)  # noqa: E731
+    layers = []
+    for j, (n, m, C1, C2) in enumerate(FP_LAUNCHES[li]):
+        x1 = pkg.synth.batch(range(j, j + B), n, "scannet")[0]
+        x2 = x1[:, :m].copy() + np.float32(1e-3)
+        p1 = pkg.synth.features_uniform(40 + j, (B, n, C1)) if C1 else None
+        p2 = pkg.synth.features_uniform(50 + j, (B, m, C2))
+        layers.append((t(x1), t(x2), t(p1), t(p2)))
+    got = pkg.pointnet_util.fp_interpolate_layers(layers)
+    for out, (x1, x2, p1, p2) in zip(got, layers):
+        ref = pkg.pointnet_util.fp_interpolate(x1, x2, p1, p2)
+        assert torch.equal(out.view(torch.int32), ref.view(torch.int32))

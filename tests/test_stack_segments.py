@@ -40,4 +40,4 @@ def test_ssg_side_lanes_are_three_segments():
     step = pkg.stack.Step(inp, overlap=True, chain_lane=0)
     step.overlap = True
     keys = [pkg.stack.Step.segment_key(s) for s in step.segments()]
-    assert keys == ["grid1", "fps1", "fps234", "sa1+sa2+sa3+sa4", "fp4+fp3+fp2+fp1"]
+    assert keys == ["grid1", "fps1", "fps234", "sa1+sa234", "fp4+fp123"]
