@@ -31,64 +31,115 @@ PN2_DEV float dot4(float4 q, float4 k) {  // (1x4)·(4x1) of tf.matmul, summed l
   return s;
 }
 
-// NS = nsample (power of two). LPH lanes per head, KPL pseudo-keys per lane.
-template <int NS>
-__global__ __launch_bounds__(kBlock) void attn_reduce_kernel(const float* __restrict__ Q,
-                                                             const float* __restrict__ K,
-                                                             const float* __restrict__ V, int G,
-                                                             int C, int steps, FastDiv div_steps,
-                                                             float* __restrict__ out) {
+// Segment reductions over LPH = 8..64 lanes with DPP / permlane exchanges (no LDS crossbar
+// round trip per step, unlike ds_bpermute shuffles): quad xor1 / xor2, row_half_mirror,
+// row_mirror, then the gfx950 row swaps. Every lane of a segment ends with the same value.
+template <int CTRL>
+PN2_DEV float dppf(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+template <int SEG, bool MAX>
+PN2_DEV float seg_reduce(float v) {
+  auto op = [](float a, float b) { return MAX ? fmaxf(a, b) : a + b; };
+  v = op(v, dppf<kDppXor1>(v));
+  v = op(v, dppf<kDppXor2>(v));
+  if constexpr (SEG >= 8) v = op(v, dppf<kDppHalfMirror>(v));
+  if constexpr (SEG >= 16) v = op(v, dppf<kDppMirror>(v));
+  if constexpr (SEG >= 32) {
+    const int u = __float_as_int(v);
+    auto x = __builtin_amdgcn_permlane16_swap(u, u, false, false);
+    v = op(__int_as_float((int)x[0]), __int_as_float((int)x[1]));
+  }
+  if constexpr (SEG >= 64) {
+    const int u = __float_as_int(v);
+    auto x = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+    v = op(__int_as_float((int)x[0]), __int_as_float((int)x[1]));
+  }
+  return v;
+}
+
+// One attention reduction: G groups of ns = NS pseudo-keys, C channels, `steps` wave tasks
+// (head groups) per group.
+struct AttnLayer {
+  const float* Q;
+  const float* K;
+  const float* V;
+  float* out;
+  int G, C, steps;
+  FastDiv div_steps;
+};
+
+// NS = nsample (power of two). LPH lanes per head, KPL pseudo-keys per lane, HPW heads per
+// wave task; a wave keeps TIF tasks in flight (their K / V loads issued before any reduction).
+template <int NS, int TIF>
+__global__ __launch_bounds__(kBlock) void attn_reduce_kernel(AttnLayer L) {
   constexpr int LPH = NS < kWave ? NS : kWave;
   constexpr int KPL = NS / LPH;
   constexpr int HPW = kWave / LPH;  // heads per wave step
   const int lane = lane_id();
   const int hl = lane / LPH, sl = lane % LPH;
-  const int H = C / 4;
-  const long long tasks = (long long)G * steps;
+  const long long tasks = (long long)L.G * L.steps;
   const long long nwaves = (long long)gridDim.x * kWavesPerBlock;
-  for (long long task = (long long)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave; task < tasks;
-       task += nwaves) {
-    const uint32_t g = fdiv((uint32_t)task, div_steps);
-    const int step = (int)((uint32_t)task - g * (uint32_t)steps);
-    const int h = step * HPW + hl;
-    const bool valid = h < H;
-    const int hh = valid ? h : 0;
-    const float4 q = *reinterpret_cast<const float4*>(Q + (size_t)g * C + 4 * hh);
-    const float* Kh = K + (size_t)g * NS * C + (size_t)hh * 4 * NS;  // reshape quirk (:35-36)
-    const float* Vh = V + (size_t)g * NS * C + (size_t)hh * 4 * NS;
-    float4 v[KPL];
-    float sc[KPL];
-    float mx = -__builtin_inff();
+  for (long long t0 = (long long)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave; t0 < tasks;
+       t0 += nwaves * TIF) {
+    float4 q[TIF], k[TIF][KPL], v[TIF][KPL];
+    float* op[TIF];
+    bool ok[TIF];
 #pragma unroll
-    for (int kk = 0; kk < KPL; ++kk) {
-      const int s = sl + kk * LPH;
-      const float4 k = *reinterpret_cast<const float4*>(Kh + 4 * s);
-      v[kk] = *reinterpret_cast<const float4*>(Vh + 4 * s);
-      sc[kk] = dot4(q, k) / 2.0f;  // / tf.sqrt(key_dim = 4)  (:38)
-      mx = fmaxf(mx, sc[kk]);
-    }
-    mx = seg_max<LPH>(mx);  // softmax over the ns pseudo-keys (:39)
-    float sum = 0.0f;
+    for (int i = 0; i < TIF; ++i) {
+      long long task = t0 + i * nwaves;
+      ok[i] = task < tasks;
+      task = ok[i] ? task : t0;
+      const uint32_t lt = (uint32_t)task;
+      const uint32_t g = fdiv(lt, L.div_steps);
+      const int step = (int)(lt - g * (uint32_t)L.steps);
+      const int H = L.C / 4;
+      const int h = step * HPW + hl;
+      ok[i] = ok[i] && h < H;
+      const int hh = h < H ? h : 0;
+      q[i] = *reinterpret_cast<const float4*>(L.Q + (size_t)g * L.C + 4 * hh);
+      const float* Kh = L.K + (size_t)g * NS * L.C + (size_t)hh * 4 * NS;  // reshape quirk (:35-36)
+      const float* Vh = L.V + (size_t)g * NS * L.C + (size_t)hh * 4 * NS;
 #pragma unroll
-    for (int kk = 0; kk < KPL; ++kk) {
-      sc[kk] = expf(sc[kk] - mx);
-      sum = sum + sc[kk];
+      for (int kk = 0; kk < KPL; ++kk) {
+        const int s = sl + kk * LPH;
+        k[i][kk] = *reinterpret_cast<const float4*>(Kh + 4 * s);
+        v[i][kk] = *reinterpret_cast<const float4*>(Vh + 4 * s);
+      }
+      op[i] = L.out + (size_t)g * L.C + 4 * h;
     }
-    sum = seg_sum<LPH>(sum);
-    float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-    for (int kk = 0; kk < KPL; ++kk) {
-      const float a = sc[kk] / sum;
-      o.x = o.x + a * v[kk].x;  // aᵀ·V_h (:40)
-      o.y = o.y + a * v[kk].y;
-      o.z = o.z + a * v[kk].z;
-      o.w = o.w + a * v[kk].w;
+    for (int i = 0; i < TIF; ++i) {
+      float sc[KPL];
+      float mx = -__builtin_inff();
+#pragma unroll
+      for (int kk = 0; kk < KPL; ++kk) {
+        sc[kk] = dot4(q[i], k[i][kk]) / 2.0f;  // / tf.sqrt(key_dim = 4)  (:38)
+        mx = fmaxf(mx, sc[kk]);
+      }
+      mx = seg_reduce<LPH, true>(mx);  // softmax over the ns pseudo-keys (:39)
+      float sum = 0.0f;
+#pragma unroll
+      for (int kk = 0; kk < KPL; ++kk) {
+        sc[kk] = expf(sc[kk] - mx);
+        sum = sum + sc[kk];
+      }
+      sum = seg_reduce<LPH, false>(sum);
+      float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int kk = 0; kk < KPL; ++kk) {
+        const float w = sc[kk] / sum;
+        o.x = o.x + w * v[i][kk].x;  // aᵀ·V_h (:40)
+        o.y = o.y + w * v[i][kk].y;
+        o.z = o.z + w * v[i][kk].z;
+        o.w = o.w + w * v[i][kk].w;
+      }
+      o.x = seg_reduce<LPH, false>(o.x);
+      o.y = seg_reduce<LPH, false>(o.y);
+      o.z = seg_reduce<LPH, false>(o.z);
+      o.w = seg_reduce<LPH, false>(o.w);
+      if (sl == 0 && ok[i]) *reinterpret_cast<float4*>(op[i]) = o;  // (:42)
     }
-    o.x = seg_sum<LPH>(o.x);
-    o.y = seg_sum<LPH>(o.y);
-    o.z = seg_sum<LPH>(o.z);
-    o.w = seg_sum<LPH>(o.w);
-    if (sl == 0 && valid) *reinterpret_cast<float4*>(out + (size_t)g * C + 4 * h) = o;  // (:42)
   }
 }
 
@@ -243,15 +294,25 @@ unsigned grid_for(long long waves) {
 }
 
 template <int NS>
-void launch_attn(const float* Q, const float* K, const float* V, int G, int C, float* out,
-                 hipStream_t s) {
+void launch_attn(AttnLayer& L, hipStream_t s) {
   constexpr int LPH = NS < kWave ? NS : kWave;
   constexpr int HPW = kWave / LPH;
-  const int H = C / 4;
-  const int steps = (H + HPW - 1) / HPW;
-  hipLaunchKernelGGL((attn_reduce_kernel<NS>), dim3(grid_for((long long)G * steps)),
-                     dim3(kBlock), 0, s, Q, K, V, G, C, steps, make_fastdiv((uint32_t)steps),
-                     out);
+  L.steps = (L.C / 4 + HPW - 1) / HPW;
+  L.div_steps = make_fastdiv((uint32_t)L.steps);
+  constexpr int TIF = 2;
+  const long long tasks = (long long)L.G * L.steps;
+  hipLaunchKernelGGL((attn_reduce_kernel<NS, TIF>), dim3(grid_for((tasks + TIF - 1) / TIF)),
+                     dim3(kBlock), 0, s, L);
+}
+
+int attn_launch(AttnLayer& a, int ns, hipStream_t s) {
+  if (ns == 8) launch_attn<8>(a, s);
+  else if (ns == 16) launch_attn<16>(a, s);
+  else if (ns == 32) launch_attn<32>(a, s);
+  else if (ns == 64) launch_attn<64>(a, s);
+  else if (ns == 128) launch_attn<128>(a, s);
+  else return PN2_EINVAL;
+  return PN2_OK;
 }
 
 }  // namespace
@@ -269,12 +330,8 @@ int pn2_attn_reduce(const float* Q, const float* K, const float* V, int B, int M
   hipStream_t s = (hipStream_t)stream;
   const long long steps_max = (long long)C / 4;  // worst case HPW = 1
   const bool small_tasks = G * steps_max * steps_max < (1LL << 32);  // FastDiv exactness
-  if (small_tasks && ns == 8) pn2::launch_attn<8>(Q, K, V, (int)G, C, out, s);
-  else if (small_tasks && ns == 16) pn2::launch_attn<16>(Q, K, V, (int)G, C, out, s);
-  else if (small_tasks && ns == 32) pn2::launch_attn<32>(Q, K, V, (int)G, C, out, s);
-  else if (small_tasks && ns == 64) pn2::launch_attn<64>(Q, K, V, (int)G, C, out, s);
-  else if (small_tasks && ns == 128) pn2::launch_attn<128>(Q, K, V, (int)G, C, out, s);
-  else
+  pn2::AttnLayer a{Q, K, V, out, (int)G, C, 0, {}};
+  if (!small_tasks || pn2::attn_launch(a, ns, s) != PN2_OK)
     hipLaunchKernelGGL(pn2::attn_reduce_generic_kernel,
                        dim3(pn2::grid_for(G * (C / 4))), dim3(pn2::kBlock), 0, s, Q, K, V,
                        (int)G, ns, C, out);

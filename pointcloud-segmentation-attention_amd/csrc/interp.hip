@@ -514,16 +514,22 @@ constexpr int kFpMaxLayers = PN2_FP_MAX_LAYERS;
 struct FpLayers {
   FpLayer l[kFpMaxLayers];
   int first[kFpMaxLayers + 1];
-  int nlayers;
+  int nlayers, B;
 };
 template <int V2, int V1, bool PRE, int UN>
 __global__ __launch_bounds__(kNNBlock) void fp_fused_layers_kernel(FpLayers a) {
-  const int total = a.first[a.nlayers];
+  // cloud-major: cloud b's blocks of every layer are contiguous (each XCD gets whole clouds
+  // and the same mix of layers); first[] = each layer's first block within a cloud
+  const int per_cloud_all = a.first[a.nlayers];
+  const int total = per_cloud_all * a.B;
   const int L = xcd_block(blockIdx.x, total);
   if (L >= total) return;
+  const int b = L / per_cloud_all;
+  const int lc = L - b * per_cloud_all;
   int li = 0;
-  while (li + 1 < a.nlayers && L >= a.first[li + 1]) ++li;
-  fp_fused_body<V2, V1, PRE, UN>(a.l[li], L - a.first[li]);
+  while (li + 1 < a.nlayers && lc >= a.first[li + 1]) ++li;
+  const int per_cloud = a.first[li + 1] - a.first[li];
+  fp_fused_body<V2, V1, PRE, UN>(a.l[li], b * per_cloud + (lc - a.first[li]));
 }
 
 // Largest batch chunk whose 32-bit row arithmetic stays exact (rows*n < 2^32, see FastDiv).
@@ -649,13 +655,14 @@ int fp_layers_launch(const pn2_fp_layer* layers, int nlayers, int B, hipStream_t
     }
     a.l[nl] = f.p;
     a.first[nl] = (int)blocks;
-    blocks += f.blocks;
+    blocks += f.blocks / B;  // per cloud
     ++nl;
   }
   if (nl == 0) return PN2_OK;
   a.first[nl] = (int)blocks;
   a.nlayers = nl;
-  PN2_FP_DISPATCH(fp_fused_layers_kernel, f0, a, blocks, stream);
+  a.B = B;
+  PN2_FP_DISPATCH(fp_fused_layers_kernel, f0, a, blocks * B, stream);
   PN2_RETURN_LAUNCH();
 }
 

@@ -46,7 +46,7 @@ constexpr int kSgMaxQpb = 64;   // queries per workgroup
 #define PN2_SG_SKIP 0
 #endif
 #ifndef PN2_SG_SPLIT_KB
-#define PN2_SG_SPLIT_KB 8
+#define PN2_SG_SPLIT_KB 24
 #endif
 #ifndef PN2_SG_SPLIT_STAGE
 #define PN2_SG_SPLIT_STAGE 4096
@@ -79,8 +79,8 @@ struct SgLayer {
 
 struct SgArgs {
   SgLayer l[PN2_SA_MAX_LAYERS];
-  int first[PN2_SA_MAX_LAYERS + 1];  // first logical block of each layer
-  int nlayers;
+  int first[PN2_SA_MAX_LAYERS + 1];  // first block of each layer within a cloud's range
+  int nlayers, B;
 };
 
 // out element c of a grouped row: xyz channel (>= 0) or -1 for a feature channel, and the
@@ -101,17 +101,21 @@ __global__ __launch_bounds__(kSgBlock) void ball_group_layers_kernel(SgArgs a) {
   __shared__ float sx[kSgCap], sy[kSgCap], sz[kSgCap];
   __shared__ int s_hit[kSgHits];          // the tile's rows: query qi's hits at qi*ns ..
   __shared__ float s_q[3 * kSgMaxQpb];    // the tile's query centres
-  const int total = a.first[a.nlayers];
+  // logical blocks cloud-major: cloud b's blocks of every layer are one contiguous range, so
+  // the XCD-aware order gives each XCD whole clouds (their rows in one L2) and every XCD the
+  // same mix of layers
+  const int per_cloud_all = a.first[a.nlayers];
+  const int total = per_cloud_all * a.B;
   const int L = xcd_block((int)blockIdx.x, total);
   if (L >= total) return;  // padding blocks (before any barrier)
+  const int b = L / per_cloud_all;
+  const int lc = L - b * per_cloud_all;
   int li = 0;
-  while (li + 1 < a.nlayers && L >= a.first[li + 1]) ++li;
+  while (li + 1 < a.nlayers && lc >= a.first[li + 1]) ++li;
   const SgLayer& g = a.l[li];
-  const int local = L - a.first[li];
-  const int per_cloud = g.tiles * g.parts;
-  const int b = local / per_cloud;
-  const int tile = (local - b * per_cloud) / g.parts;
-  const int part = local - b * per_cloud - tile * g.parts;
+  const int local = lc - a.first[li];
+  const int tile = local / g.parts;
+  const int part = local - tile * g.parts;
   const int t = threadIdx.x, lane = t & (kWave - 1), w = t / kWave;
   const int N = g.N, C = g.C, M = g.M, ns = g.ns, Cout = g.Cout, layout = g.layout;
   const int q0 = tile * g.qpb, nq = min(g.qpb, M - q0);
@@ -285,12 +289,13 @@ int pn2_ball_group_layers(const pn2_sa_layer* layers, int nlayers, int B, pn2_st
     g.div_ns = pn2::make_fastdiv((uint32_t)s.nsample);
     g.tiles = s.M > 0 ? (int)((s.M + qpb - 1) / qpb) : 0;
     a.first[i] = (int)blocks;
-    blocks += (long long)B * g.tiles * g.parts;
-    if (blocks >= (1LL << 31) - 8) return PN2_EINVAL;
+    blocks += (long long)g.tiles * g.parts;  // per cloud
+    if (blocks * B >= (1LL << 31) - 8) return PN2_EINVAL;
   }
   a.first[nlayers] = (int)blocks;
-  if (blocks == 0) return PN2_OK;
-  hipLaunchKernelGGL(pn2::ball_group_layers_kernel, dim3(pn2::xcd_grid(blocks)),
+  a.B = B;
+  if (blocks * B == 0) return PN2_OK;
+  hipLaunchKernelGGL(pn2::ball_group_layers_kernel, dim3(pn2::xcd_grid(blocks * B)),
                      dim3(pn2::kSgBlock), 0, (hipStream_t)stream, a);
   PN2_RETURN_LAUNCH();
 }

@@ -121,3 +121,4 @@ def test_fp_interpolate_layers(env, li):
     for out, (x1, x2, p1, p2) in zip(got, layers):
         ref = pkg.pointnet_util.fp_interpolate(x1, x2, p1, p2)
         assert torch.equal(out.view(torch.int32), ref.view(torch.int32))
+

@@ -10,9 +10,10 @@ pkg = importlib.import_module("pointcloud-segmentation-attention_amd")
 
 @pytest.mark.parametrize("config", ["cfg2", "cfg3", "cfg5"])
 @pytest.mark.parametrize("chain_lane", [3, 0])
-def test_segments_respect_dependencies(config, chain_lane):
+@pytest.mark.parametrize("layout", ["a", "b", "d"])
+def test_segments_respect_dependencies(config, chain_lane, layout):
     inp = pkg.stack.make_inputs(config, [0, 1], "cpu")
-    step = pkg.stack.Step(inp, overlap=True, chain_lane=chain_lane)
+    step = pkg.stack.Step(inp, overlap=True, chain_lane=chain_lane, layout=layout)
     step.overlap = True  # the GPU schedule (lane 3 in use with chain_lane 0), planned on the CPU
     step.tasks = step._tasks_ssg() if step.kind == "ssg" else step._tasks_msg()
     segs = step.segments()
