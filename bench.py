@@ -29,9 +29,12 @@ DEFAULT_HW_QUEUES = 4
 # profiles/r3/plan/): sampler streams (consecutive steps' samplers run concurrently, one
 # workgroup per cloud each), side-lane layout (stack.side_layout), hardware queues (one per
 # stream: samplers + side lanes) and buffer sets (how far the host may run ahead).
-LAYOUTS = {"cfg2": {"lanes": 3, "side": "b", "queues": 6, "sets": 9},
-           "cfg3": {"lanes": 2, "side": "a", "queues": 5, "sets": 6},
-           "cfg5": {"lanes": 5, "side": "a", "queues": 8, "sets": 10}}
+# chain: the later samplers (SA2.. chain) behind SA1 on its sampler stream, or on a stream of
+# their own (profiles/r3/chainown: cfg2 65.6k -> 69.8k, cfg3 50.7k -> 54.3k clouds/s; cfg5 no
+# gain).
+LAYOUTS = {"cfg2": {"lanes": 3, "side": "b", "queues": 7, "sets": 9, "chain": "own"},
+           "cfg3": {"lanes": 2, "side": "a", "queues": 6, "sets": 6, "chain": "own"},
+           "cfg5": {"lanes": 5, "side": "a", "queues": 8, "sets": 10, "chain": "behind"}}
 
 PKG = "pointcloud-segmentation-attention_amd"
 METRIC = "8192-pt clouds/sec through SA+FP layers, 1/2/4/8 MI355X; HBM GB/s vs peak"
@@ -309,6 +312,10 @@ def main():
     ap.add_argument("--side-layout", choices=["a", "b", "c", "d"], default=None,
                     help="side-lane layout with several sampler streams (stack.side_layout; "
                          "default: the config's LAYOUTS entry)")
+    ap.add_argument("--chain", choices=["own", "behind"], default=None,
+                    help="with several sampler streams: the later samplers (SA2.. chain) on a "
+                         "stream of their own or behind SA1 on its sampler stream (default: the "
+                         "config's LAYOUTS entry)")
     ap.add_argument("--private-side", action="store_true",
                     help="every buffer set gets its own side streams (side work of consecutive "
                          "steps runs concurrently; needs 1 + 2 x sets + sampler lanes - 1 "
@@ -357,6 +364,8 @@ def main():
         args.sets = 3 if args.model else lay["sets"]
     if args.side_layout is None:
         args.side_layout = lay["side"]
+    if args.chain is None:
+        args.chain = lay["chain"]
     if args.hw_queues is None and not args.model and args.sampler_lanes == lay["lanes"]:
         args.hw_queues = lay["queues"]  # one queue per stream (the box's default is 4)
     if args.hw_queues is not None:
@@ -416,7 +425,8 @@ def main():
                                       sampler_lanes=1 if model else args.sampler_lanes,
                                       private_streams=model or args.private_side,
                                       native_plan=not args.no_native_plan,
-                                      only=args.diag_only, layout=args.side_layout)
+                                      only=args.diag_only, layout=args.side_layout,
+                                      chain_own=args.chain == "own")
         else:
             step = pkg.stack.Step(inp, overlap=overlap)
             graph = None if args.eager else pkg.stack.GraphStep(inp, overlap=overlap)
@@ -522,7 +532,9 @@ def main():
                        "lane0_priority": prio0,
                        "streams": (("SA1 sampler + 3 side streams" if args.sampler_lanes <= 1 or args.model
                                     else f"{args.sampler_lanes} sampler streams (consecutive steps' "
-                                    f"samplers concurrent; SA2.. samplers behind SA1) + side streams "
+                                    f"samplers concurrent; SA2.. samplers "
+                                    + ("on their own stream" if args.chain == "own" else "behind SA1")
+                                    + ") + side streams "
                                     f"(layout {args.side_layout})"
                                     + (" per buffer set" if args.private_side else ""))
                                    if overlap else "one stream")

@@ -194,6 +194,8 @@ class Step:
 
     def __init__(self, inp, overlap=True, streams=None, chain_lane=3, layout="a"):
         # chain_lane: the lane of the later samplers (SA2..SA4 / MSG SA2); 0 = behind the SA1
+        # sampler on its stream; -1 = a lane of their own after the side lanes (both: several
+        # sampler streams, Pipeline)
         # sampler on its stream (Pipeline with several sampler lanes); layout: side_layout()
         self.chain_lane = chain_lane if overlap else 0
         self.layout = layout
@@ -235,9 +237,12 @@ class Step:
         # with the later samplers behind SA1 on its stream (chain_lane 0: several sampler
         # streams), lane 3 is free: the attention reductions (they read only their resident
         # inputs) run there instead of inside lane 1's SA tasks
-        multi = self.chain_lane == 0 and self.overlap
+        multi = self.chain_lane <= 0 and self.overlap
         attn_lane = 3 if (multi and "attn" in inp) else None
         lane = side_layout(multi, attn_lane is not None, self.layout)
+        chain_lane = self.chain_lane
+        if chain_lane < 0:  # the later samplers on a lane after every side lane
+            chain_lane = 1 + max([2] + list(lane.values()) + ([attn_lane] if attn_lane else []))
         tasks = []
         if big:  # the SA1 grid over the input cloud (also orders FP4's neighbour search)
             tasks.append(Task("grid1", 1, (), lambda: v.__setitem__(
@@ -294,14 +299,14 @@ class Step:
             tasks.append(Task("fps1", 0, (), lambda: tf_sampling.farthest_point_sample_chain(
                 npoints[:1], xyz, out=v["chain"][:1]), direct=True,
                 chain=(npoints[:1], xyz, v["chain"][:1])))
-            tasks.append(Task("fps234", self.chain_lane, ("fps1",), lambda: tf_sampling.farthest_point_sample_chain(
+            tasks.append(Task("fps234", chain_lane, ("fps1",), lambda: tf_sampling.farthest_point_sample_chain(
                 npoints[1:], v["xyz"][1], out=v["chain"][1:]), direct=True,
                 chain=(npoints[1:], v["xyz"][1], v["chain"][1:])))
             sampled = ("fps1", "fps234", "fps234", "fps234")
         else:
             # lane 0: SA1's sampler alone; lane 3: SA2..SA4's samplers as one task
             tasks.append(Task("fps1", 0, (), fps(0)))
-            tasks.append(Task("fps234", self.chain_lane, ("fps1",), lambda: [fps(i)() for i in (1, 2, 3)]))
+            tasks.append(Task("fps234", chain_lane, ("fps1",), lambda: [fps(i)() for i in (1, 2, 3)]))
             sampled = ("fps1", "fps234", "fps234", "fps234")
         tasks.append(Task("sa1", 1, (sampled[0],), sa(0)))
         tasks.append(Task("fp4", 2, (sampled[0],) + grid_dep, fp(0)))
@@ -453,12 +458,13 @@ class Step:
             if i == 0:
                 tasks.append(Task("fps1", 0, (), fps(0), direct=True, chain=spec))
             else:
-                tasks.append(Task(f"fps{i + 1}", self.chain_lane, (f"fps{i}",), fps(i), direct=True,
+                chain_lane = 4 if self.chain_lane < 0 else self.chain_lane  # after the radii
+                tasks.append(Task(f"fps{i + 1}", chain_lane, (f"fps{i}",), fps(i), direct=True,
                                   chain=spec))
             for r in range(len(MSG_SA[i][1])):
                 # radius r on lane 1 + r when lane 3 is free (chain_lane 0), else radius 0 on
                 # lane 1 and the others on lane 2
-                lane = 1 + r if self.chain_lane == 0 and self.overlap else 1 + min(r, 1)
+                lane = 1 + r if self.chain_lane <= 0 and self.overlap else 1 + min(r, 1)
                 tasks.append(Task(f"sa{i + 1}_{r}", lane, (f"fps{i + 1}",), grp(i, r)))
         return tasks
 
@@ -766,7 +772,7 @@ class Pipeline:
     1 + 2 + (sampler_lanes - 1) <= GPU_MAX_HW_QUEUES."""
 
     def __init__(self, inp, graphs=True, overlap=True, nsets=3, private_streams=False,
-                 sampler_lanes=1, native_plan=True, only=None, layout="a"):
+                 sampler_lanes=1, native_plan=True, only=None, layout="a", chain_own=False):
         # private_streams: every buffer set gets its own side streams, so the side lanes of
         # consecutive steps overlap each other too (the whole-model step, whose lane-1 chain
         # of SA/FP layers is longer than a sampler period; the geometric step once its
@@ -782,7 +788,8 @@ class Pipeline:
             return [None] + [side_stream(dev, (i, lane)) for lane in range(1, NSIDE + 1)]
 
         multi = sampler_lanes > 1 and overlap and inp["xyz"].is_cuda
-        chain_lane = 0 if multi else 3
+        # chain_own: the later samplers on a stream of their own instead of behind SA1
+        chain_lane = (-1 if chain_own else 0) if multi else 3
         self.lane0 = [None]
         if multi:
             # queues go to streams in order of first use: the extra sampler streams now, then

@@ -127,20 +127,22 @@ def _poison_sampled(pipe, torch):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("lanes,native,layout", [(1, False, "a"), (1, True, "a"), (2, True, "a"),
-                                                 (3, True, "b")])
+@pytest.mark.parametrize("lanes,native,layout,own", [(1, False, "a", False), (1, True, "a", False),
+                                                     (2, True, "a", False), (3, True, "b", False),
+                                                     (3, True, "b", True)])
 @pytest.mark.parametrize("config,B", CONFIGS)
-def test_pipeline_full_size(env, config, B, lanes, native, layout):
+def test_pipeline_full_size(env, config, B, lanes, native, layout, own):
     """What bench.py times: the software-pipelined hipGraph steps over 3 buffer sets, at the
     BASELINE batch, after several rotations, with one, two or three sampler streams
     (consecutive steps' samplers concurrent), enqueued by the Python task loop or by the native
-    plan (include/pn2plan.h), side layouts a and b (stack.side_layout). The sampled coordinates
+    plan (include/pn2plan.h), side layouts a and b (stack.side_layout), the later samplers
+    behind SA1 or on a stream of their own (chain_own). The sampled coordinates
     of every set are poisoned before the last three steps (a missing wait then shows), and the
     last two steps' outputs (one per sampler stream) are compared with the oracle."""
     pkg, O, torch, dev = env
     inp = pkg.stack.make_inputs(config, list(range(100, 100 + B)), dev)
     pipe = pkg.stack.Pipeline(inp, graphs=True, nsets=3, sampler_lanes=lanes, native_plan=native,
-                              layout=layout)
+                              layout=layout, chain_own=own)
     assert len(pipe.lane0) == lanes
     assert pipe.native_plan == native
     for _ in range(7):
