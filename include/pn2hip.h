@@ -184,6 +184,13 @@ int pn2_grid_build(const float* xyz, int B, int N, float cell_edge, void* grid,
                    size_t grid_bytes, pn2_stream_t stream);
 int pn2_ball_query_grid(const void* grid, const float* xyz2, int B, int N, int M, float radius,
                         int nsample, int32_t* idx, int32_t* pts_cnt, pn2_stream_t stream);
+/* pn2_ball_query_grid plus the grouping of an xyz-only layer in the same kernel:
+ * grouped_xyz (B,M,nsample,3) = xyz1[idx] - xyz2, i.e. pn2_group_concat with points = NULL
+ * (pointnet_util.py:39-40, 55-56), bit for bit. xyz1 (B,N,3) is the cloud the grid was built
+ * over. */
+int pn2_ball_group_xyz_grid(const void* grid, const float* xyz1, const float* xyz2, int B, int N,
+                            int M, float radius, int nsample, int32_t* idx, int32_t* pts_cnt,
+                            float* grouped_xyz, pn2_stream_t stream);
 
 /* ---- k nearest neighbours ---------------------------------------------------------- *
  * pn2_select_top_k: select_top_k / SelectionSort (tf_grouping.py:22-31, tf_grouping_g.cu:

@@ -168,11 +168,14 @@ __global__ __launch_bounds__(kBuildBlock) void grid_build_kernel(const float* __
   }
 }
 
-template <int BLOCK>
+// GROUP: also the grouped coordinates gxyz (B,M,ns,3) = xyz1[idx] - xyz2 (pn2_group_concat
+// with no points, pointnet_util.py:39-40): each lane writes the rows of the hits it ranks, so
+// the SA1 grouping of an xyz-only layer needs no launch of its own.
+template <int BLOCK, bool GROUP>
 __global__ __launch_bounds__(BLOCK) void ball_query_grid_kernel(
     const char* __restrict__ grid, const float* __restrict__ xyz2, int N, int M, float radius,
     float thresh, int ns, int qpb, int words, int gx, int nblk, int32_t* __restrict__ idx,
-    int32_t* __restrict__ pts_cnt) {
+    int32_t* __restrict__ pts_cnt, const float* __restrict__ xyz1, float* __restrict__ gxyz) {
   constexpr int NW = BLOCK / kWave;
   extern __shared__ uint32_t bits[];  // NW x words
   // XCD-aware order (common.h): each XCD takes a contiguous range of (cloud, query chunk)
@@ -225,18 +228,33 @@ __global__ __launch_bounds__(BLOCK) void ball_query_grid_kernel(
     const int total = __shfl(incl, kWave - 1, kWave);
     const int cnt = min(total, ns);
     int32_t* __restrict__ row = idx + ((size_t)b * M + q) * ns;
+    float* __restrict__ grow = GROUP ? gxyz + ((size_t)b * M + q) * ns * 3 : nullptr;
+    const float* __restrict__ X1 = GROUP ? xyz1 + (size_t)b * N * 3 : nullptr;
     int rank = incl - pop;
     for (int j = 0; j < wpl && rank < ns; ++j) {
       const int wi = lane * wpl + j;
       uint32_t v = wi < words ? mine[wi] : 0u;
       while (v && rank < ns) {
-        row[rank++] = 32 * wi + __builtin_ctz(v);
+        const int k = 32 * wi + __builtin_ctz(v);
+        if constexpr (GROUP) {
+          grow[3 * rank + 0] = X1[3 * k + 0] - qx;  // pointnet_util.py:40
+          grow[3 * rank + 1] = X1[3 * k + 1] - qy;
+          grow[3 * rank + 2] = X1[3 * k + 2] - qz;
+        }
+        row[rank++] = k;
         v &= v - 1u;
       }
     }
     const uint64_t has = __ballot(pop > 0);
     const int first = has ? __shfl(myfirst, __ffsll((unsigned long long)has) - 1, kWave) : 0;
-    for (int p = cnt + lane; p < ns; p += kWave) row[p] = first;  // :26-29 (0 when no hit)
+    for (int p = cnt + lane; p < ns; p += kWave) {
+      row[p] = first;  // :26-29 (0 when no hit)
+      if constexpr (GROUP) {
+        grow[3 * p + 0] = X1[3 * first + 0] - qx;
+        grow[3 * p + 1] = X1[3 * first + 1] - qy;
+        grow[3 * p + 2] = X1[3 * first + 2] - qz;
+      }
+    }
     if (lane == 0) pts_cnt[(size_t)b * M + q] = cnt;
   }
 }
@@ -264,11 +282,14 @@ int pn2_grid_build(const float* xyz, int B, int N, float cell_edge, void* grid,
   PN2_RETURN_LAUNCH();
 }
 
-int pn2_ball_query_grid(const void* grid, const float* xyz2, int B, int N, int M, float radius,
-                        int nsample, int32_t* idx, int32_t* pts_cnt, pn2_stream_t stream) {
+namespace {
+int ball_query_grid(const void* grid, const float* xyz2, int B, int N, int M, float radius,
+                    int nsample, int32_t* idx, int32_t* pts_cnt, const float* xyz1, float* gxyz,
+                    hipStream_t stream) {
   if (!(radius > 0.0f) || nsample <= 0 || B < 0 || N < 0 || M < 0) return PN2_EINVAL;
   if ((long long)B * M == 0) return PN2_OK;
   if (!grid || !xyz2 || !idx || !pts_cnt || B > 65535) return PN2_EINVAL;
+  if (gxyz && !xyz1) return PN2_EINVAL;
   const int words = (N + 31) / 32;
   if (words > pn2::kMaxBitWords) return PN2_EINVAL;
   constexpr int BLOCK = 256, NW = BLOCK / pn2::kWave;
@@ -280,11 +301,32 @@ int pn2_ball_query_grid(const void* grid, const float* xyz2, int B, int N, int M
   const size_t lds = (size_t)NW * (words > 0 ? words : 1) * 4;
   const long long nblk = (long long)gx * B;
   if (nblk > INT32_MAX - pn2::kXcds) return PN2_EINVAL;
-  hipLaunchKernelGGL((pn2::ball_query_grid_kernel<BLOCK>), dim3(pn2::xcd_grid(nblk)), dim3(BLOCK),
-                     lds, (hipStream_t)stream, (const char*)grid, xyz2, N, M, radius,
-                     pn2_ball_threshold(radius), nsample, (int)qpb, words, (int)gx, (int)nblk,
-                     idx, pts_cnt);
+  if (gxyz)
+    hipLaunchKernelGGL((pn2::ball_query_grid_kernel<BLOCK, true>), dim3(pn2::xcd_grid(nblk)),
+                       dim3(BLOCK), lds, stream, (const char*)grid, xyz2, N, M, radius,
+                       pn2_ball_threshold(radius), nsample, (int)qpb, words, (int)gx, (int)nblk,
+                       idx, pts_cnt, xyz1, gxyz);
+  else
+    hipLaunchKernelGGL((pn2::ball_query_grid_kernel<BLOCK, false>), dim3(pn2::xcd_grid(nblk)),
+                       dim3(BLOCK), lds, stream, (const char*)grid, xyz2, N, M, radius,
+                       pn2_ball_threshold(radius), nsample, (int)qpb, words, (int)gx, (int)nblk,
+                       idx, pts_cnt, nullptr, nullptr);
   PN2_RETURN_LAUNCH();
+}
+}  // namespace
+
+int pn2_ball_query_grid(const void* grid, const float* xyz2, int B, int N, int M, float radius,
+                        int nsample, int32_t* idx, int32_t* pts_cnt, pn2_stream_t stream) {
+  return ball_query_grid(grid, xyz2, B, N, M, radius, nsample, idx, pts_cnt, nullptr, nullptr,
+                         (hipStream_t)stream);
+}
+
+int pn2_ball_group_xyz_grid(const void* grid, const float* xyz1, const float* xyz2, int B, int N,
+                            int M, float radius, int nsample, int32_t* idx, int32_t* pts_cnt,
+                            float* grouped_xyz, pn2_stream_t stream) {
+  if (!grouped_xyz) return PN2_EINVAL;
+  return ball_query_grid(grid, xyz2, B, N, M, radius, nsample, idx, pts_cnt, xyz1, grouped_xyz,
+                         (hipStream_t)stream);
 }
 
 }  // extern "C"

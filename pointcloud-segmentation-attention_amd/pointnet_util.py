@@ -72,6 +72,26 @@ def group_concat(xyz, points, new_xyz, idx, use_xyz=True, xyz_last=False, want_g
     return new_points, grouped_xyz
 
 
+def ball_group_xyz(radius, nsample, xyz, new_xyz, grid):
+    """query_ball_point over `grid` (a tf_grouping.BallGrid built over xyz) and the grouping of
+    an xyz-only layer (group_concat with points None: xyz[idx] - new_xyz, pointnet_util.py:
+    39-40, 55-56) in ONE kernel (pn2_ball_group_xyz_grid). Returns (idx, pts_cnt, grouped)."""
+    xyz = device_tensor(xyz, "xyz", torch.float32)
+    new_xyz = device_tensor(new_xyz, "new_xyz", torch.float32)
+    if not grid.matches(xyz):
+        raise InvalidArgumentError("ball_group_xyz: the grid was built over a different xyz")
+    B, N, M, ns = int(xyz.shape[0]), int(xyz.shape[1]), int(new_xyz.shape[1]), int(nsample)
+    if int(new_xyz.shape[0]) != B:
+        raise InvalidArgumentError("ball_group_xyz: xyz and new_xyz need the same batch")
+    idx = torch.empty((B, M, ns), dtype=torch.int32, device=xyz.device)
+    cnt = torch.empty((B, M), dtype=torch.int32, device=xyz.device)
+    grouped = torch.empty((B, M, ns, 3), dtype=torch.float32, device=xyz.device)
+    check(lib().pn2_ball_group_xyz_grid(ptr(grid.buf), ptr(xyz), ptr(new_xyz), B, N, M,
+                                        float(radius), ns, ptr(idx), ptr(cnt), ptr(grouped),
+                                        stream_of(xyz)), "ball_group_xyz")
+    return idx, cnt, grouped
+
+
 BALL_GROUP_MAX_POINTS = 1024  # pn2_ball_group_layers stages each cloud in LDS
 BALL_GROUP_MAX_NSAMPLE = 128
 

@@ -258,11 +258,16 @@ class Step:
             def f():
                 _, radius, nsample, _ = SSG_SA[i]
                 xyz, new_xyz = v["xyz"][i], v["xyz"][i + 1]
-                idx, _ = tf_grouping.query_ball_point(radius, nsample, xyz, new_xyz,
-                                                      grid=v.get("grid1") if i == 0 else None)
+                if i == 0 and points[0] is None and v.get("grid1") is not None:
+                    # xyz-only SA1 (cfg2): query and grouping in one kernel
+                    idx, _, new_points = pointnet_util.ball_group_xyz(radius, nsample, xyz,
+                                                                      new_xyz, v["grid1"])
+                else:
+                    idx, _ = tf_grouping.query_ball_point(radius, nsample, xyz, new_xyz,
+                                                          grid=v.get("grid1") if i == 0 else None)
+                    new_points, _ = pointnet_util.group_concat(xyz, points[i], new_xyz, idx,
+                                                               want_grouped_xyz=False)
                 v["bq"][i] = idx
-                new_points, _ = pointnet_util.group_concat(xyz, points[i], new_xyz, idx,
-                                                           want_grouped_xyz=False)
                 v["sa"][i] = new_points
                 if "attn" in inp and attn_lane is None:
                     att(i)()
@@ -444,11 +449,17 @@ class Step:
                 radius, nsample = MSG_SA[i][1][r], MSG_SA[i][2][r]
                 points = None if i == 0 else inp["sa_out"][0]
                 xyz, new_xyz = v["xyz"][i], v["xyz"][i + 1]
-                idx, _ = tf_grouping.query_ball_point(radius, nsample, xyz, new_xyz)
+                if points is None and int(xyz.shape[1]) >= tf_grouping.GRID_MIN_POINTS:
+                    # xyz-only level (SA1): grid query and grouping in one kernel
+                    grid = tf_grouping.BallGrid(xyz, radius)
+                    idx, _, v["gp"][(i, r)] = pointnet_util.ball_group_xyz(
+                        radius, nsample, xyz, new_xyz, grid)
+                else:
+                    idx, _ = tf_grouping.query_ball_point(radius, nsample, xyz, new_xyz)
+                    v["gp"][(i, r)] = pointnet_util.group_concat(xyz, points, new_xyz, idx,
+                                                                 xyz_last=True,
+                                                                 want_grouped_xyz=False)[0]
                 v["bq"][(i, r)] = idx
-                v["gp"][(i, r)] = pointnet_util.group_concat(xyz, points, new_xyz, idx,
-                                                             xyz_last=True,
-                                                             want_grouped_xyz=False)[0]
             return f
 
         for i in range(len(MSG_SA)):

@@ -122,3 +122,27 @@ def test_fp_interpolate_layers(env, li):
         ref = pkg.pointnet_util.fp_interpolate(x1, x2, p1, p2)
         assert torch.equal(out.view(torch.int32), ref.view(torch.int32))
 
+
+
+GROUP_XYZ_CASES = [
+    ("scannet", 2, 8192, 1024, 0.1, 32),   # cfg2 SA1
+    ("scannet", 1, 16384, 512, 0.4, 128),  # cfg5 SA1, largest radius
+    ("scannet", 1, 16384, 512, 0.1, 16),
+    ("grid", 2, 4096, 500, 1.0, 16),       # exact lattice distances at the radius
+]
+
+
+@pytest.mark.parametrize("kind,B,N,M,r,ns", GROUP_XYZ_CASES)
+def test_ball_group_xyz(env, kind, B, N, M, r, ns):
+    """pointnet_util.ball_group_xyz (pn2_ball_group_xyz_grid) == oracle ball_query +
+    group_concat of an xyz-only layer, bit for bit, including a query with no hit."""
+    pkg, O, torch, dev = env
+    x, _, q = _layer(pkg, O, kind, B, N, M, 0, 3)
+    xt, qt = torch.from_numpy(x).to(dev), torch.from_numpy(q).to(dev)
+    grid = pkg.tf_grouping.BallGrid(xt, r)
+    idx, cnt, grouped = pkg.pointnet_util.ball_group_xyz(r, ns, xt, qt, grid)
+    ridx, rcnt = O.ball_query(x, q, r, ns)
+    rg, _ = O.group_concat(x, None, q, ridx)
+    assert np.array_equal(cnt.cpu().numpy(), rcnt)
+    assert np.array_equal(idx.cpu().numpy(), ridx)
+    assert np.array_equal(_bits(grouped.cpu().numpy()), _bits(rg))
