@@ -316,6 +316,9 @@ def main():
                     help="with several sampler streams: the later samplers (SA2.. chain) on a "
                          "stream of their own or behind SA1 on its sampler stream (default: the "
                          "config's LAYOUTS entry)")
+    ap.add_argument("--cu-partition", type=int, default=None, metavar="CUS",
+                    help="run the samplers on CUS CUs and the side lanes on the others "
+                         "(CU-masked streams; default: the config's LAYOUTS entry, 0 = off)")
     ap.add_argument("--private-side", action="store_true",
                     help="every buffer set gets its own side streams (side work of consecutive "
                          "steps runs concurrently; needs 1 + 2 x sets + sampler lanes - 1 "
@@ -366,6 +369,8 @@ def main():
         args.side_layout = lay["side"]
     if args.chain is None:
         args.chain = lay["chain"]
+    if args.cu_partition is None:
+        args.cu_partition = 0 if args.model else lay.get("cu", 0)
     if args.hw_queues is None and not args.model and args.sampler_lanes == lay["lanes"]:
         args.hw_queues = lay["queues"]  # one queue per stream (the box's default is 4)
     if args.hw_queues is not None:
@@ -421,6 +426,10 @@ def main():
         overlap = not args.no_overlap
         pipelined = overlap and not args.no_pipeline
         if pipelined:
+            if not model and args.sampler_lanes > 1:
+                # CU-masked sampler and side streams (stack.set_cu_partition), before any
+                # stream of the pipeline exists
+                pkg.stack.set_cu_partition(dev, args.cu_partition)
             pipe = pkg.stack.Pipeline(inp, graphs=not args.eager, nsets=args.sets,
                                       sampler_lanes=1 if model else args.sampler_lanes,
                                       private_streams=model or args.private_side,
@@ -529,6 +538,9 @@ def main():
                         + ("; one native plan call per step (include/pn2plan.h)"
                            if pipelined and not args.no_native_plan else "")),
                        "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "0")),
+                       "cu_partition": (f"samplers on {args.cu_partition} CUs, side lanes on "
+                                        "the others" if args.cu_partition and not args.model
+                                        and args.sampler_lanes > 1 else "none"),
                        "lane0_priority": prio0,
                        "streams": (("SA1 sampler + 3 side streams" if args.sampler_lanes <= 1 or args.model
                                     else f"{args.sampler_lanes} sampler streams (consecutive steps' "

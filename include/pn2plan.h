@@ -55,6 +55,12 @@ int pn2_plan_launch(pn2_plan* plan);
  * be NULL) */
 int pn2_plan_launch_timed(pn2_plan* plan, void* ev_start, void* ev_end);
 
+/* A stream whose kernels run only on the CUs set in `mask` (bit i of word i / 32 = CU i;
+ * hipExtStreamCreateWithCUMask), so the latency-bound samplers and the side lanes can be
+ * given disjoint CUs. 0 and *stream, or the HIP error. Destroy with pn2_stream_destroy. */
+int pn2_stream_create_cu_mask(const uint32_t* mask, int words, pn2_stream_t* stream);
+int pn2_stream_destroy(pn2_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -137,6 +137,8 @@ SIGNATURES = {
     "pn2_plan_size": (_I, [_P]),
     "pn2_plan_launch": (_I, [_P]),
     "pn2_plan_launch_timed": (_I, [_P, _P, _P]),
+    "pn2_stream_create_cu_mask": (_I, [_P, _I, _P]),
+    "pn2_stream_destroy": (_I, [_P]),
 }
 
 _lib = None

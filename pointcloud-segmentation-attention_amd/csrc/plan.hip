@@ -146,4 +146,20 @@ int pn2_plan_launch_timed(pn2_plan* plan, void* ev_start, void* ev_end) {
   return launch(plan, ev_start, ev_end);
 }
 
+// CU-partitioned streams (hipExtStreamCreateWithCUMask): `mask` holds one bit per CU (bit i of
+// word i / 32 = CU i). Returns 0 and the new stream, or the HIP error.
+int pn2_stream_create_cu_mask(const uint32_t* mask, int words, pn2_stream_t* stream) {
+  if (!mask || words <= 0 || !stream) return PN2_EINVAL;
+  hipStream_t s = nullptr;
+  const hipError_t e = hipExtStreamCreateWithCUMask(&s, (uint32_t)words, mask);
+  if (e != hipSuccess) return (int)e;
+  *stream = (pn2_stream_t)s;
+  return PN2_OK;
+}
+
+int pn2_stream_destroy(pn2_stream_t stream) {
+  const hipError_t e = hipStreamDestroy((hipStream_t)stream);
+  return e == hipSuccess ? PN2_OK : (int)e;
+}
+
 }  // extern "C"

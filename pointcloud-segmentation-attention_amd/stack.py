@@ -123,16 +123,52 @@ def make_inputs(config, cloud_ids, device, seed=1234, model=False):
 
 
 _SIDE = {}
+_CU_PART = {}  # device -> {"sampler": mask words, "side": mask words} (set_cu_partition)
 
 
-def side_stream(dev, lane):
+def set_cu_partition(dev, sampler_cus=64):
+    """Give the latency-bound samplers (SA1 streams and the later-sampler chain) and the side
+    lanes DISJOINT CUs: streams created from now on (side_stream, Pipeline's sampler streams)
+    are CU-masked (include/pn2plan.h pn2_stream_create_cu_mask). The sampler part is 8
+    consecutive CU bits out of every 32, so it spreads evenly over the XCDs whichever way the
+    bits map onto them; sampler_cus = 0 turns the partition off for new streams."""
+    key = str(torch.device(dev))
+    if not sampler_cus:
+        _CU_PART.pop(key, None)
+        return
+    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+    per32 = max(1, min(31, round(32 * sampler_cus / ncu)))
+    words = (ncu + 31) // 32
+    samp = [0] * words
+    side = [0] * words
+    for i in range(ncu):
+        if i % 32 < per32:
+            samp[i // 32] |= 1 << (i % 32)
+        else:
+            side[i // 32] |= 1 << (i % 32)
+    _CU_PART[key] = {"sampler": samp, "side": side}
+
+
+def _masked_stream(dev, part):
+    import ctypes
+    from ._lib import check, lib
+    words = _CU_PART[str(torch.device(dev))][part]
+    arr = (ctypes.c_uint32 * len(words))(*words)
+    h = ctypes.c_void_p()
+    with torch.cuda.device(dev):
+        check(lib().pn2_stream_create_cu_mask(arr, len(words), ctypes.byref(h)), "cu mask stream")
+    return torch.cuda.ExternalStream(h.value, device=dev)
+
+
+def side_stream(dev, lane, part="side"):
     """The process-wide side stream of `lane` on `dev`: every Step shares them, so the
     sampler chain (the current stream) and the side lanes stay on distinct hardware queues
     (HIP gives each new stream a new hardware queue up to GPU_MAX_HW_QUEUES, then shares the
     least-used ones): the first Step creates lanes 1-3 before any other stream exists."""
     key = (str(dev), lane)
     if key not in _SIDE:
-        _SIDE[key] = torch.cuda.Stream(device=dev)
+        masked = str(torch.device(dev)) in _CU_PART
+        _SIDE[key] = _masked_stream(dev, part) if masked else torch.cuda.Stream(device=dev)
     return _SIDE[key]
 
 
@@ -212,8 +248,12 @@ class Step:
         self.nlanes = 1 + max(t.lane for t in self.tasks)
         if self.overlap:
             dev = inp["xyz"].device
+            # the later samplers' own lane (chain "own") counts as a sampler under a CU
+            # partition (set_cu_partition)
+            samp = {t.lane for t in self.tasks if t.direct and t.lane > 0}
             self.streams = [None] + (list(streams[1:self.nlanes]) if streams else
-                                     [side_stream(dev, lane) for lane in range(1, self.nlanes)])
+                                     [side_stream(dev, lane, "sampler" if lane in samp else "side")
+                                      for lane in range(1, self.nlanes)])
             # HIP binds a stream to a hardware queue when the stream is first used: use the
             # lanes now, in order, so that they (not the warm-up or capture streams made later)
             # get the queues the current stream does not hold
@@ -805,10 +845,14 @@ class Pipeline:
         if multi:
             # queues go to streams in order of first use: the extra sampler streams now, then
             # each set's side lanes when its Step is built (Step.__init__ touches them in
-            # order), all before the sets' warm-up and capture streams
+            # order), all before the sets' warm-up and capture streams. Under a CU partition
+            # (set_cu_partition) every sampler lane is a masked stream, the first one too.
             cur = torch.cuda.current_stream(dev)
-            for i in range(1, sampler_lanes):
-                st = side_stream(dev, ("sampler", i))
+            part = str(torch.device(dev)) in _CU_PART
+            if part:
+                self.lane0 = []
+            for i in range(0 if part else 1, sampler_lanes):
+                st = side_stream(dev, ("sampler", i), "sampler")
                 st.wait_stream(cur)
                 self.lane0.append(st)
         # native_plan: a graph step is enqueued by ONE call into the C++ executor

@@ -127,11 +127,11 @@ def _poison_sampled(pipe, torch):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("lanes,native,layout,own", [(1, False, "a", False), (1, True, "a", False),
-                                                     (2, True, "a", False), (3, True, "b", False),
-                                                     (3, True, "b", True)])
+@pytest.mark.parametrize("lanes,native,layout,own,cus", [
+    (1, False, "a", False, 0), (1, True, "a", False, 0), (2, True, "a", False, 0),
+    (3, True, "b", False, 0), (3, True, "b", True, 0), (3, True, "b", True, 64)])
 @pytest.mark.parametrize("config,B", CONFIGS)
-def test_pipeline_full_size(env, config, B, lanes, native, layout, own):
+def test_pipeline_full_size(env, config, B, lanes, native, layout, own, cus):
     """What bench.py times: the software-pipelined hipGraph steps over 3 buffer sets, at the
     BASELINE batch, after several rotations, with one, two or three sampler streams
     (consecutive steps' samplers concurrent), enqueued by the Python task loop or by the native
@@ -141,6 +141,10 @@ def test_pipeline_full_size(env, config, B, lanes, native, layout, own):
     last two steps' outputs (one per sampler stream) are compared with the oracle."""
     pkg, O, torch, dev = env
     inp = pkg.stack.make_inputs(config, list(range(100, 100 + B)), dev)
+    pkg.stack.set_cu_partition(dev, cus)  # CU-masked sampler / side streams (cus > 0)
+    saved = dict(pkg.stack._SIDE)
+    if cus:
+        pkg.stack._SIDE.clear()  # fresh (masked) streams for this pipeline
     pipe = pkg.stack.Pipeline(inp, graphs=True, nsets=3, sampler_lanes=lanes, native_plan=native,
                               layout=layout, chain_own=own)
     assert len(pipe.lane0) == lanes
@@ -155,6 +159,10 @@ def test_pipeline_full_size(env, config, B, lanes, native, layout, own):
     torch.cuda.synchronize()
     if native:
         assert all(getattr(s, "plans", None) for s in pipe.sets), "a set ran without its plan"
+    pkg.stack.set_cu_partition(dev, 0)
+    if cus:
+        pkg.stack._SIDE.clear()
+        pkg.stack._SIDE.update(saved)
     for back in (1, 2):
         s = pipe.sets[(pipe.k - back) % len(pipe.sets)]
         check_step(O, config, inp, s.outs if back > 1 else outs, s.intermediates())
