@@ -14,12 +14,11 @@
 // query's neighbours writes that query's grouped rows from the hits it holds in LDS, reading
 // neighbour coordinates from the LDS copy of the cloud it just scanned.
 //
-// Layout: workgroup = (layer, cloud, tile of queries), 4 waves, one wave per query. The
-// cloud's xyz (N <= kSgCap points) is staged in LDS as SoA. A query's output block
-// (nsample rows x Cout floats) is contiguous in HBM, so the wave streams it with 16-byte
-// stores (64 lanes x 4 consecutive floats; when nsample*Cout % 4 == 0 and the block is 16 B
-// aligned) -- the gathers behind it hit L2 (a cloud's feature rows are shared by its tiles,
-// which the XCD-aware order keeps on one XCD).
+// Layout: workgroup = (cloud, layer, tile of queries), 4 waves. The cloud's xyz (N <= kSgCap
+// points) is staged in LDS as SoA; one wave per query scans it into an LDS hit row. The tile's
+// grouped rows are one contiguous output range, streamed by the whole workgroup with four
+// elements' gathers in flight per thread (they hit L2: a cloud's feature rows are shared by
+// its tiles, which the cloud-major XCD-aware order keeps on one XCD).
 #include "common.h"
 
 namespace pn2 {
@@ -32,14 +31,7 @@ constexpr int kSgMaxNs = 128;   // nsample
 constexpr int kSgUnroll = 4;    // 64-point steps per scan iteration
 constexpr int kSgHits = 2048;   // hit slots per workgroup: qpb * nsample
 constexpr int kSgMaxQpb = 64;   // queries per workgroup
-// A/B knobs (tools/bench_layers.py): vector groups in flight per thread, 16-byte feature
-// loads where a group is four feature channels of one row, output bytes per workgroup
-#ifndef PN2_SG_U
-#define PN2_SG_U 2
-#endif
-#ifndef PN2_SG_VLOAD
-#define PN2_SG_VLOAD 1
-#endif
+// A/B knobs (tools/bench_layers.py): output bytes per workgroup, query splitting
 // diagnostic builds only (results wrong): skip the scan (hits = the first ns points) or the
 // grouped-row writes, to split the kernel's time between its phases
 #ifndef PN2_SG_SKIP
@@ -74,7 +66,6 @@ struct SgLayer {
   int parts, chunk;  // a query split over `parts` workgroups of `chunk` elements each
   float thresh;
   FastDiv div_cout, div_ns;
-  int vec;  // 16 B stores of 4 consecutive floats
 };
 
 struct SgArgs {
@@ -169,7 +160,9 @@ __global__ __launch_bounds__(kSgBlock) void ball_group_layers_kernel(SgArgs a) {
   }
   __syncthreads();
   // ---- phase 2: the tile's grouped rows (nq * ns rows of Cout floats) are ONE contiguous
-  // range of the output: the whole workgroup streams it, U vector groups in flight per thread
+  // range of the output: the whole workgroup streams it, one float per lane per element and
+  // four elements' loads in flight before any store (16-byte stores and loads of four
+  // channels measured 3 % slower: profiles/r3/sgs)
   const size_t r_base = ((size_t)b * M + q0) * ns;  // first output row of the tile
   float* __restrict__ O = g.out + r_base * Cout;
   float* __restrict__ GX = g.grouped_xyz ? g.grouped_xyz + r_base * 3 : nullptr;
@@ -192,40 +185,19 @@ __global__ __launch_bounds__(kSgBlock) void ball_group_layers_kernel(SgArgs a) {
     }
     return F[(size_t)i * C + cp];
   };
-  if (g.vec) {
-    constexpr int U = PN2_SG_U;
-    for (int e0 = e_beg + t * 4; e0 < E; e0 += kSgBlock * 4 * U) {
-      float4 v[U];
+  constexpr int U = 4;
+  for (int e0 = e_beg + t; e0 < E; e0 += kSgBlock * U) {
+    float v[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int e = e0 + u * kSgBlock * 4;
-        v[u] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        if (e >= E) continue;
-        if constexpr (PN2_SG_VLOAD) {
-          // four feature channels of one row: one 16-byte load (dword-aligned rows of C
-          // floats; gfx950 global loads need only dword alignment)
-          const int r = (int)fdiv((uint32_t)e, g.div_cout);
-          const int c = e - r * Cout;
-          const int f0 = layout == PN2_SG_XYZ_FIRST ? 3 : 0;
-          const int f1 = layout == PN2_SG_XYZ_LAST || layout == PN2_SG_POINTS_ONLY ? C : Cout;
-          if (layout != PN2_SG_XYZ_ONLY && c >= f0 && c + 4 <= f1) {
-            const float* src = F + (size_t)s_hit[r] * C + (c - f0);
-            typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
-            const f4u x = *reinterpret_cast<const f4u*>(src);
-            v[u] = make_float4(x[0], x[1], x[2], x[3]);
-            continue;
-          }
-        }
-        v[u] = make_float4(value(e), value(e + 1), value(e + 2), value(e + 3));
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int e = e0 + u * kSgBlock * 4;
-        if (e < E) *reinterpret_cast<float4*>(O + e) = v[u];
-      }
+    for (int u = 0; u < U; ++u) {
+      const int e = e0 + u * kSgBlock;
+      v[u] = e < E ? value(e) : 0.0f;
     }
-  } else {
-    for (int e = e_beg + t; e < E; e += kSgBlock) O[e] = value(e);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = e0 + u * kSgBlock;
+      if (e < E) O[e] = v[u];
+    }
   }
 }
 
@@ -266,7 +238,6 @@ int pn2_ball_group_layers(const pn2_sa_layer* layers, int nlayers, int B, pn2_st
     g.Cout = Cout; g.layout = layout;
     g.thresh = pn2_ball_threshold(s.radius);
     g.div_cout = pn2::make_fastdiv((uint32_t)Cout);
-    g.vec = (s.nsample * Cout) % 4 == 0 && ((uintptr_t)s.new_points & 15) == 0;
     // work per workgroup: ~PN2_SG_TILE_KB of output over whole queries; a query of many
     // channels on a small cloud (cheap to stage and scan again) is split over several
     // workgroups of ~PN2_SG_SPLIT_KB each, so the grid has enough waves to hide the gathers
