@@ -456,6 +456,8 @@ def main():
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
               for _ in range(steps)]
         barrier()
+        if pipelined:
+            pipe.host_wait_s = pipe.host_launch_s = 0.0
         t0 = time.perf_counter()
         outs = None
         timed_k = [] if args.diag_only == "side" else \
@@ -469,11 +471,16 @@ def main():
         timed = [ev[k] for k in timed_k]
         fps_ms = (sum(a.elapsed_time(b) for a, b in timed) / len(timed)  # SA1 sampler, per launch
                   if timed else float("nan"))
+        if pipelined:  # host time per step: waiting for a free buffer set / enqueueing a step
+            host["wait_ms_per_step"] = pipe.host_wait_s / steps * 1e3
+            host["enqueue_ms_per_step"] = pipe.host_launch_s / steps * 1e3
         return elapsed, fps_ms, outs
 
     overlap = not args.no_overlap
     pipelined = overlap and not args.no_pipeline
+    host = {}
     elapsed, fps_ms, outs, prio0 = measure(args.model, args.steps, args.warmup)
+    host_geom = dict(host)
     # per-cloud output checksums, gathered (outside the timed region) so ranks can be compared
     sums = pkg.shard.gather_checksums(pkg.shard.cloud_checksums(outs, B))
     e2e = None
@@ -559,6 +566,7 @@ def main():
                 note="the SA1 sampler is a chain of M-1 dependent picks on one CU per cloud: "
                      "its bound is latency (floor from tools/ubench/pick_floor.hip, "
                      "roofline.latency); the HBM figures (roofline.hbm) are structurally low"),
+            "host": host_geom or None,
             "step_hbm": {"algorithmic_bytes": step_bytes,
                          "achieved_GBps": step_bytes * world / (elapsed / args.steps) / 1e9,
                          "frac": step_bytes * world / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBPS},

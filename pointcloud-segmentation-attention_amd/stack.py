@@ -21,6 +21,8 @@ every FP layer as one fused interpolation + MLP kernel, and the conv1d head (fc1
 norm, dropout = identity at inference, fc2 to 21 classes) fused into FP4's MLP. Weights are
 the reference initialisers (tf_util.ParamStore, fixed seed).
 """
+import time
+
 import torch
 
 from . import attention_layer, pointnet_util, synth, tf_grouping, tf_interpolate, tf_sampling, \
@@ -866,6 +868,7 @@ class Pipeline:
                                            chain_lane=chain_lane, layout=layout))
         self.sets = [mk(i) for i in range(nsets)]
         self.k = 0
+        self.host_wait_s = self.host_launch_s = 0.0  # host wait for a set / enqueue time
 
     def run(self, sampler_events=None):
         st = self.lane0[self.k % len(self.lane0)]
@@ -877,16 +880,23 @@ class Pipeline:
     def _run(self, sampler_events):
         s = self.sets[self.k % len(self.sets)]
         self.k += 1
-        if isinstance(s, GraphStep):
-            if s.step.ran and s.step.overlap:
-                s.step.lane_done[1].synchronize()  # this set's previous side work
-            else:
-                s.step.join()
-            if self.native_plan:
-                return s.replay_plan(sampler_events)
-            return s.replay(sampler_events, join=False)
-        s.join()
-        return s.run(sampler_events, join=False)
+        t0 = time.perf_counter()
+        try:
+            if isinstance(s, GraphStep):
+                if s.step.ran and s.step.overlap:
+                    s.step.lane_done[1].synchronize()  # this set's previous side work
+                else:
+                    s.step.join()
+                t1 = time.perf_counter()
+                self.host_wait_s += t1 - t0
+                t0 = t1
+                if self.native_plan:
+                    return s.replay_plan(sampler_events)
+                return s.replay(sampler_events, join=False)
+            s.join()
+            return s.run(sampler_events, join=False)
+        finally:  # host time of the enqueue (bench.py reports both per step)
+            self.host_launch_s += time.perf_counter() - t0
 
     def join(self):
         """Wait for everything enqueued; returns the outputs of the last step run."""
