@@ -9,7 +9,7 @@ pkg = importlib.import_module("pointcloud-segmentation-attention_amd")
 
 
 @pytest.mark.parametrize("config", ["cfg2", "cfg3", "cfg5"])
-@pytest.mark.parametrize("chain_lane", [3, 0])
+@pytest.mark.parametrize("chain_lane", [3, 0, -1])
 @pytest.mark.parametrize("layout", ["a", "b", "d"])
 def test_segments_respect_dependencies(config, chain_lane, layout):
     inp = pkg.stack.make_inputs(config, [0, 1], "cpu")
@@ -42,3 +42,19 @@ def test_ssg_side_lanes_are_three_segments():
     step.overlap = True
     keys = [pkg.stack.Step.segment_key(s) for s in step.segments()]
     assert keys == ["grid1", "fps1", "fps234", "sa1+sa234", "fp4+fp123"]
+
+
+@pytest.mark.parametrize("config,layout,want", [("cfg2", "b", 4), ("cfg2", "a", 3),
+                                                 ("cfg3", "a", 4), ("cfg2", "d", 5),
+                                                 ("cfg5", "a", 4)])
+def test_chain_own_lane_follows_the_side_lanes(config, layout, want):
+    """chain_lane -1 (bench.py --chain own): the later samplers get the lane after every side
+    lane, and nothing else runs there."""
+    inp = pkg.stack.make_inputs(config, [0], "cpu")
+    step = pkg.stack.Step(inp, overlap=True, chain_lane=-1, layout=layout)
+    step.overlap = True
+    step.tasks = step._tasks_ssg() if step.kind == "ssg" else step._tasks_msg()
+    chain = [t for t in step.tasks if t.direct and t.name != "fps1"]
+    assert chain and all(t.lane == want for t in chain)
+    assert all(t.lane != want for t in step.tasks if not t.direct)
+    assert max(t.lane for t in step.tasks) == want
