@@ -21,6 +21,7 @@ every FP layer as one fused interpolation + MLP kernel, and the conv1d head (fc1
 norm, dropout = identity at inference, fc2 to 21 classes) fused into FP4's MLP. Weights are
 the reference initialisers (tf_util.ParamStore, fixed seed).
 """
+import os
 import time
 
 import torch
@@ -125,6 +126,10 @@ def make_inputs(config, cloud_ids, device, seed=1234, model=False):
 
 
 _SIDE = {}
+# LANE_JOIN (A/B, PN2_LANE_JOIN=1): lanes 2.. hand their end to lane 1 with cross-queue waits
+# and one event marks a step's end; otherwise every lane records its own end event and the
+# host waits for all of them (no wait packets on the side queues)
+LANE_JOIN = os.environ.get("PN2_LANE_JOIN") == "1"
 _CU_PART = {}  # device -> {"sampler": mask words, "side": mask words} (set_cu_partition)
 
 
@@ -593,13 +598,33 @@ class Step:
                 done[t.name].record(st)
             elif timed:
                 sampler_events[1].record(st)
-        # the step's side work is complete when lane 1 is: lanes 2.. hand their last work to it
-        # (off the critical chain), so the chain waits on ONE event before reusing buffers
+        # every lane records its own end; the host (Pipeline) and join() wait for all of them
         for lane in range(2, self.nlanes):
             self.lane_done[lane].record(self.streams[lane])
-            self.streams[1].wait_event(self.lane_done[lane])
+            if LANE_JOIN:
+                self.streams[1].wait_event(self.lane_done[lane])
         self.lane_done[1].record(self.streams[1])
         return self.join() if join else None
+
+    def done_lanes(self):
+        """The lanes whose end events mark the end of the step's side work."""
+        return [1] if LANE_JOIN else list(range(1, self.nlanes))
+
+    def _needed_waits(self, waits):
+        """`waits` minus the events another waited task already implies (its own cross-lane
+        waits reach them): each wait packet stalls the side queue, so fewer is faster."""
+        deps = {t.name: t.deps for t in self.tasks}
+
+        def closure(n, seen):
+            for d in deps.get(n, ()):
+                if d not in seen:
+                    seen.add(d)
+                    closure(d, seen)
+            return seen
+        implied = set()
+        for w in waits:
+            implied |= closure(w, set())
+        return [w for w in waits if w not in implied]
 
     def restrict(self, only):
         """DIAGNOSTIC (bench.py --diag-only; never a measured step): keep only the samplers
@@ -679,7 +704,7 @@ class Step:
                 for d in t.deps:
                     if lane_of[d] != lane and d not in waits:
                         waits.append(d)
-            for d in waits:
+            for d in self._needed_waits(waits):
                 plan.wait(st, self.done[d])
             if seg[0].direct:
                 if seg[0].chain is None:
@@ -692,9 +717,10 @@ class Step:
             for t in seg:
                 if any(t.name in u.deps and u.lane != lane for u in self.tasks):
                     plan.record(self.done[t.name], st)
-        for lane in range(2, self.nlanes):
+        for lane in range(2, self.nlanes):  # as run(): each lane records its own end
             plan.record(self.lane_done[lane], self.streams[lane])
-            plan.wait(self.streams[1], self.lane_done[lane])
+            if LANE_JOIN:
+                plan.wait(self.streams[1], self.lane_done[lane])
         plan.record(self.lane_done[1], self.streams[1])
 
     def join(self):
@@ -705,7 +731,8 @@ class Step:
         outs = self.outputs()
         if self.overlap:
             main = torch.cuda.current_stream(self.inp["xyz"].device)
-            main.wait_event(self.lane_done[1])
+            for lane in self.done_lanes():
+                main.wait_event(self.lane_done[lane])
             if not torch.cuda.is_current_stream_capturing():
                 for o in outs:  # made on side streams, consumed on the current stream from here
                     o.record_stream(main)
@@ -884,7 +911,8 @@ class Pipeline:
         try:
             if isinstance(s, GraphStep):
                 if s.step.ran and s.step.overlap:
-                    s.step.lane_done[1].synchronize()  # this set's previous side work
+                    for lane in s.step.done_lanes():  # this set's previous side work
+                        s.step.lane_done[lane].synchronize()
                 else:
                     s.step.join()
                 t1 = time.perf_counter()
