@@ -130,9 +130,6 @@ _SIDE = {}
 # and one event marks a step's end; otherwise every lane records its own end event and the
 # host waits for all of them (no wait packets on the side queues)
 LANE_JOIN = os.environ.get("PN2_LANE_JOIN") == "1"
-# GRID_SHARED: FP4 waits for lane 1's input grid; PN2_GRID_SHARED=0 (A/B): FP4's lane builds
-# its own copy instead
-GRID_SHARED = os.environ.get("PN2_GRID_SHARED", "1") != "0"
 _CU_PART = {}  # device -> {"sampler": mask words, "side": mask words} (set_cu_partition)
 
 
@@ -331,10 +328,9 @@ class Step:
         def fp(i):
             def f():
                 k = 3 - i  # the FP layer whose coarse level (i+1) just became available
-                ugrid = v.get("grid1b", v.get("grid1")) if i == 0 else None
                 v["fp"][k], v["nn"][k] = pointnet_util.fp_interpolate(
                     v["xyz"][i], v["xyz"][i + 1], points[i], fp_feat[k],
-                    unknown_grid=ugrid, return_nn=True)
+                    unknown_grid=v.get("grid1") if i == 0 else None, return_nn=True)
             return f
 
         npoints = [sa_[0] for sa_ in SSG_SA]
@@ -365,12 +361,6 @@ class Step:
             tasks.append(Task("fps234", chain_lane, ("fps1",), lambda: [fps(i)() for i in (1, 2, 3)]))
             sampled = ("fps1", "fps234", "fps234", "fps234")
         tasks.append(Task("sa1", 1, (sampled[0],), sa(0)))
-        if big and multi and not GRID_SHARED:
-            # FP4's lane builds its own copy of the input grid (it only orders the unknowns):
-            # a wait on lane 1's grid would hold FP4 behind lane 1's previous step (§3.6b)
-            tasks.append(Task("grid1b", 2, (), lambda: v.__setitem__(
-                "grid1b", tf_grouping.BallGrid(inp["xyz"], SSG_SA[0][1]))))
-            grid_dep = ()
         tasks.append(Task("fp4", 2, (sampled[0],) + grid_dep, fp(0)))
         if npoints[0] <= pointnet_util.BALL_GROUP_MAX_POINTS and sampled[1:] == ("fps234",) * 3:
             # SA2..SA4 wait for the same sampler launch: their three ball queries and groupings
