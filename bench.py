@@ -195,6 +195,33 @@ def sa1_latency(config, fps_ms, M1, N):
     return out
 
 
+def verify_sets(config, runs, threads):
+    """The CHECKER (outside every timed region): each buffer set's last step -- its inputs,
+    outputs and index intermediates -- against the oracle (oracle/pn2_oracle.c, the C
+    restatement pinned to the reference's own code) with north_star's bars: bit-exact indices
+    and copies, 1e-5 for interpolated features and the attention reduction."""
+    from oracle import oracle as O
+    O.set_threads(threads)
+    fails, clouds, t0 = [], 0, time.perf_counter()
+    for inp, outs, inter in runs:
+        np_inp = dict(inp)
+        np_inp["xyz"] = inp["xyz"].cpu().numpy()
+        np_inp["feats"] = None if inp["feats"] is None else inp["feats"].cpu().numpy()
+        for k in ("sa_out", "fp_out"):
+            if k in inp:
+                np_inp[k] = [t.cpu().numpy() for t in inp[k]]
+        if "attn" in inp:
+            np_inp["attn"] = [tuple(t.cpu().numpy() for t in qkv) for qkv in inp["attn"]]
+        fails += O.compare_stack(np_inp, config, [o.cpu().numpy() for o in outs],
+                                 {k: v.cpu().numpy() for k, v in inter.items()})
+        clouds += int(inp["B"])
+    return {"sets": len(runs), "clouds": clouds, "failures": fails[:8],
+            "seconds": time.perf_counter() - t0, "threads": threads,
+            "checker": "oracle.compare_stack: every output and index intermediate of each "
+                       "buffer set's last step vs oracle/pn2_oracle.c (bit-exact indices and "
+                       "copies; rtol=atol=1e-5 interpolated features / attention)"}
+
+
 def _e2e_child(args, e2e):
     """The whole-model measurement in a child process (`bench.py --model`, same config, queues
     and steps). HIP maps streams to hardware queues round-robin in creation order, so in the
@@ -266,12 +293,22 @@ def dry_run(args):
         dist.barrier()
     elapsed = pkg.shard.max_over_ranks(time.perf_counter() - t0)
     sums = pkg.shard.gather_checksums(pkg.shard.cloud_checksums(outs, B))
+    # what each rank would run: its shard of every buffer set, and the hardware-queue setting
+    # its HIP runtime would start with (bench.py sets it before anything touches the GPU)
+    mine = {"rank": rank, "ids": ids, "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"),
+            "set_ids": [pkg.shard.set_ids(rank, world, B, i) for i in range(args.sets)]}
+    ranks = [None] * world
+    if world > 1:
+        dist.all_gather_object(ranks, mine)
+    else:
+        ranks = [mine]
     if rank == 0:
         print(json.dumps({"metric": METRIC, "value": None, "unit": "clouds/s", "n_gpus": world,
                           "dry_run": True, "clouds": world * B, "clouds_per_rank": B,
                           "elapsed_max_over_ranks": elapsed,
                           "checksum": float(sums.sum().item()),
                           "per_cloud_checksums": [float(x) for x in sums.tolist()],
+                          "ranks": ranks, "sets": args.sets,
                           "config": {"config": args.config, "clouds_per_gpu": B,
                                      "global_batch": world * B,
                                      "parallelism": f"dp{world} (batch split)"}}), flush=True)
@@ -348,6 +385,11 @@ def main():
     ap.add_argument("--e2e-steps", type=int, default=20,
                     help="after the geometric measurement, time this many whole-model steps "
                          "(reported as 'e2e'; 0 = skip)")
+    ap.add_argument("--no-verify", action="store_true",
+                    help="skip the post-run oracle check of every buffer set's last step (the "
+                         "line's `verified` is then null)")
+    ap.add_argument("--latency-reps", type=int, default=10,
+                    help="un-pipelined single steps timed after the run (latency_ms_per_batch)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher / rank plumbing only, on the CPU over gloo: every rank builds "
                          "its shard's synthetic inputs and checksums them per cloud; max-over-"
@@ -358,8 +400,6 @@ def main():
         # one process per GPU: start the ranks as children BEFORE anything touches the GPU
         # (this process never initialises HIP), and exit with the launcher's status
         sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
-    if args.dry_run:
-        return dry_run(args)
     lay = LAYOUTS[args.config]
     if args.sampler_lanes is None:
         args.sampler_lanes = 1 if args.model else lay["lanes"]
@@ -377,6 +417,8 @@ def main():
         os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, max(1, args.hw_queues)))
     else:
         os.environ.setdefault("GPU_MAX_HW_QUEUES", str(DEFAULT_HW_QUEUES))
+    if args.dry_run:  # (after the queue setting: every rank reports what HIP would see)
+        return dry_run(args)
 
     import torch
     import torch.distributed as dist
@@ -419,12 +461,20 @@ def main():
             return _measure(model, steps, warmup) + (prio,)
 
     def _measure(model, steps, warmup):
-        """W warm-up steps, then K timed steps between barrier + synchronize; returns
-        (max-over-ranks elapsed seconds, mean SA1-sampler ms, last outputs)."""
-        inp = pkg.stack.make_inputs(args.config, ids, dev, model=model)
-        torch.cuda.synchronize()
+        """W warm-up steps, then K timed steps between barrier + synchronize; then, outside the
+        timed region, the sampler fault word, the oracle check of every buffer set's last step
+        and the latency of one un-pipelined step. Returns (max-over-ranks elapsed seconds, mean
+        SA1-sampler ms, last outputs, post-run checks)."""
         overlap = not args.no_overlap
         pipelined = overlap and not args.no_pipeline
+        # every buffer set holds its own clouds (shard.set_ids): consecutive pipelined steps
+        # sample different clouds, never one input replayed
+        set_inputs = ([pkg.stack.make_inputs(args.config, pkg.shard.set_ids(rank, world, B, i),
+                                             dev, model=model) for i in range(max(2, args.sets))]
+                      if pipelined else None)
+        inp = set_inputs[0] if pipelined else pkg.stack.make_inputs(args.config, ids, dev,
+                                                                     model=model)
+        torch.cuda.synchronize()
         if pipelined:
             if not model and args.sampler_lanes > 1:
                 # CU-masked sampler and side streams (stack.set_cu_partition), before any
@@ -435,7 +485,7 @@ def main():
                                       private_streams=model or args.private_side,
                                       native_plan=not args.no_native_plan,
                                       only=args.diag_only, layout=args.side_layout,
-                                      chain_own=args.chain == "own")
+                                      chain_own=args.chain == "own", set_inputs=set_inputs)
         else:
             step = pkg.stack.Step(inp, overlap=overlap)
             graph = None if args.eager else pkg.stack.GraphStep(inp, overlap=overlap)
@@ -474,12 +524,38 @@ def main():
         if pipelined:  # host time per step: waiting for a free buffer set / enqueueing a step
             host["wait_ms_per_step"] = pipe.host_wait_s / steps * 1e3
             host["enqueue_ms_per_step"] = pipe.host_launch_s / steps * 1e3
-        return elapsed, fps_ms, outs
+        post = {}
+        # the sampler fault word (include/pn2hip.h pn2_fault_status) after the timed steps:
+        # a fault raises here, so a fast but wrong line is never printed
+        post["fault_status"] = pipe.check_faults() if pipelined else \
+            pkg._lib.check_device_faults(dev) or 0
+        if not model and args.diag_only is None and not args.no_verify:
+            runs = (pipe.outputs_by_set() if pipelined else
+                    [(inp, (graph.step if graph is not None else step).outputs(),
+                      (graph.step if graph is not None else step).intermediates())])
+            threads = max(1, (args.cpu_threads or _cpu_share()) // world)
+            post["verify"] = verify_sets(args.config, runs, threads)
+            ok = pkg.shard.min_over_ranks(0.0 if post["verify"]["failures"] else 1.0, dev)
+            post["verified"] = ok == 1.0
+        # one step alone, enqueued and joined (no pipelining): the latency of one batch
+        lat = []
+        for _ in range(args.latency_reps):
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            run_step()
+            finish()
+            torch.cuda.synchronize()
+            lat.append(time.perf_counter() - t1)
+        if lat:
+            lat.sort()
+            post["latency_ms_per_batch"] = pkg.shard.max_over_ranks(lat[len(lat) // 2], dev) * 1e3
+            post["latency_ms_per_batch_min"] = lat[0] * 1e3
+        return elapsed, fps_ms, outs, post
 
     overlap = not args.no_overlap
     pipelined = overlap and not args.no_pipeline
     host = {}
-    elapsed, fps_ms, outs, prio0 = measure(args.model, args.steps, args.warmup)
+    elapsed, fps_ms, outs, post, prio0 = measure(args.model, args.steps, args.warmup)
     host_geom = dict(host)
     # per-cloud output checksums, gathered (outside the timed region) so ranks can be compared
     sums = pkg.shard.gather_checksums(pkg.shard.cloud_checksums(outs, B))
@@ -490,7 +566,7 @@ def main():
         if not child:
             # after the geometric step: the stream-to-queue mapping is round-robin in creation
             # order, and creating the model's streams first cost the geometric step 29 %
-            e_el, e_fps, e_outs, e_prio = measure(True, args.e2e_steps, min(args.warmup, 5))
+            e_el, e_fps, e_outs, _, e_prio = measure(True, args.e2e_steps, min(args.warmup, 5))
             e_sums = pkg.shard.gather_checksums(pkg.shard.cloud_checksums(e_outs, B))
             e2e.update({"value": world * B * args.e2e_steps / e_el, "unit": "clouds/s",
                         "ms_per_step": e_el / args.e2e_steps * 1e3, "steps": args.e2e_steps,
@@ -557,7 +633,8 @@ def main():
                                     f"(layout {args.side_layout})"
                                     + (" per buffer set" if args.private_side else ""))
                                    if overlap else "one stream")
-                       + (f", steps software-pipelined over {args.sets} buffer sets" if pipelined else "")},
+                       + (f", steps software-pipelined over {args.sets} buffer sets, each set "
+                          "its own clouds" if pipelined else "")},
             "roofline": dict(
                 {"kernel": f"SA1 sampler (FPS + gather fused): {B} clouds x {N} pts -> {M1}, "
                            "one workgroup per cloud"},
@@ -571,6 +648,13 @@ def main():
                          "achieved_GBps": step_bytes * world / (elapsed / args.steps) / 1e9,
                          "frac": step_bytes * world / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBPS},
             "checksum": float(sums.sum().item()),
+            "verified": post.get("verified"),
+            "verify": post.get("verify"),
+            "fault_status": post.get("fault_status"),
+            "latency_ms_per_batch": post.get("latency_ms_per_batch"),
+            "latency_ms_per_batch_min": post.get("latency_ms_per_batch_min"),
+            "latency_note": "one B-cloud step enqueued and joined alone (no pipelining), host "
+                            f"clock, median of {args.latency_reps}, max over ranks",
         }
         if e2e is not None:
             result["e2e"] = e2e

@@ -48,8 +48,11 @@ int pn2_plan_mark_timed(pn2_plan* plan);
 /* number of operations in the plan */
 int pn2_plan_size(const pn2_plan* plan);
 
-/* enqueue every operation in order; returns 0, or the first failing operation's status
- * (a hipError_t, PN2_EINVAL, or PN2_EFAULT from a sampler fault stored earlier) and stops */
+/* enqueue every operation in order; returns 0, or PN2_EFAULT (and enqueues nothing) when an
+ * earlier sampler launch stored a fault (the fault word is read and cleared once, before the
+ * first operation; the plan's own sampler launches do not read it, so a step is never left
+ * half enqueued by a fault), or the first failing operation's status (a hipError_t or
+ * PN2_EINVAL) and stops */
 int pn2_plan_launch(pn2_plan* plan);
 /* the same with the marked operation bracketed by records of ev_start / ev_end (either may
  * be NULL) */

@@ -446,6 +446,54 @@ def run_stack_cpu(inp_np, config, intermediates=False):
     return (outs, labels, inter) if intermediates else outs
 
 
+def _bits32(a):
+    return np.ascontiguousarray(a, np.float32).view(np.int32)
+
+
+def compare_stack(inp_np, config, outs, inter, rtol=1e-5, atol=1e-5):
+    """The CHECKER of a step (tests/, bench.py's `verified` field): every output and index
+    intermediate of one step (numpy arrays, Step.outputs() / Step.intermediates() order and
+    names) against run_stack_cpu on the same inputs, each with the bar north_star sets --
+    bit-exact for indices and copies, rtol = atol = 1e-5 for the interpolated FP columns and the
+    attention reduction. Returns a list of failure strings (empty = parity)."""
+    ref, labels, rinter = run_stack_cpu(inp_np, config, intermediates=True)
+    bad = []
+    if len(outs) != len(ref):
+        return [f"{len(outs)} outputs, oracle has {len(ref)}"]
+
+    def exact(name, g, r):
+        if g.shape != r.shape:
+            bad.append(f"{name}: shape {g.shape} vs {r.shape}")
+            return
+        d = (g != r) if (g.dtype == np.int32 or r.dtype == np.int32) else (_bits32(g) != _bits32(r))
+        if d.any():
+            bad.append(f"{name}: {int(d.sum())} of {d.size} values differ (bit-exact bar)")
+
+    def close(name, g, r):
+        if g.shape != r.shape:
+            bad.append(f"{name}: shape {g.shape} vs {r.shape}")
+        elif not np.allclose(g, r, rtol=rtol, atol=atol):
+            err = np.abs(g.astype(np.float64) - r) - atol - rtol * np.abs(r)
+            bad.append(f"{name}: {int((err > 0).sum())} values outside rtol=atol=1e-5")
+
+    for g, r, (name, how) in zip(outs, ref, labels):
+        if how is None:
+            exact(name, g, r)
+        elif how == "tol":
+            close(name, g, r)
+        else:  # FP output: [interpolated (C2 columns), points1 copy]
+            close(name + "[:C2] interpolated", g[..., :how], r[..., :how])
+            exact(name + "[C2:] points1 copy", g[..., how:], r[..., how:])
+    if not inter:
+        bad.append("the step recorded no intermediates")
+    for name, t in inter.items():
+        exact(name, t, rinter[name])
+    for name in rinter:
+        if name.startswith(("fps", "bq")) and name not in inter:
+            bad.append(f"{name} missing from the step's intermediates")
+    return bad
+
+
 # ---------------------------------------------------------------- scene crops (numpy)
 # data_transformation.py:70-154 (get_subset) restated in numpy with TF's float32 semantics, for
 # caller-supplied random draws (test infrastructure: the crop sampler kernels' bar). TensorFlow

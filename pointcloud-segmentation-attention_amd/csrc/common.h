@@ -160,6 +160,12 @@ PN2_DEV uint32_t fdiv(uint32_t n, FastDiv f) { return f.d == 1 ? n : __umulhi(n,
 // pn2_fps_chain's argument check (fps.hip), shared with the plan executor (plan.hip)
 int fps_chain_check(const float* xyz, int B, int N, int nstages, const int* npoint,
                     int32_t* const* idx, float* const* new_xyz);
+// pn2_fps_chain without the stored-fault report (the plan executor takes the fault word once,
+// before it enqueues anything, so a plan never stops part-way through a step)
+int fps_chain_launch(const float* xyz, int B, int N, int nstages, const int* npoint,
+                     int32_t* const* idx, float* const* new_xyz, hipStream_t s, bool take);
+// a fault stored by an earlier sampler launch, cleared (0: none)
+int fps_take_fault();
 
 }  // namespace pn2
 

@@ -196,7 +196,7 @@ __global__ __launch_bounds__(kChainBlock) void fps_chain_kernel(const float* __r
 }
 
 int fps_impl(const float* xyz, int B, int N, int M, int32_t* idx, float* nx, void* ws,
-             size_t ws_bytes, hipStream_t s, int sched = PN2_FPS_AUTO) {
+             size_t ws_bytes, hipStream_t s, int sched = PN2_FPS_AUTO, bool take = true) {
   if (B < 0 || N < 0 || M <= 0 || (B > 0 && (!xyz || !idx))) return PN2_EINVAL;
   // schedules other than AUTO exist only where the culled sampler runs (4096 < N <= 16384;
   // the 128-entry variant up to 8192 points)
@@ -204,7 +204,7 @@ int fps_impl(const float* xyz, int B, int N, int M, int32_t* idx, float* nx, voi
     return PN2_EINVAL;
   if (sched != PN2_FPS_AUTO && (N <= 4096 || N > kMaxRegPoints)) return PN2_EINVAL;
   if (sched == PN2_FPS_HOTCULL_K128 && N > 8192) return PN2_EINVAL;
-  if (take_fault()) return PN2_EFAULT;
+  if (take && take_fault()) return PN2_EFAULT;
   if (B == 0) return PN2_OK;
   if (N == 0) {
     const int total = B * M;
@@ -262,6 +262,36 @@ int fps_chain_check(const float* xyz, int B, int N, int nstages, const int* npoi
   if (B > 0 && (!xyz || B > 65535)) return PN2_EINVAL;
   return PN2_OK;
 }
+int fps_take_fault() { return take_fault(); }
+
+int fps_chain_launch(const float* xyz, int B, int N, int nstages, const int* npoint,
+                     int32_t* const* idx, float* const* new_xyz, hipStream_t s, bool take) {
+  const int rc0 = fps_chain_check(xyz, B, N, nstages, npoint, idx, new_xyz);
+  if (rc0 != PN2_OK || B == 0) return rc0;
+  int first = 0;  // first stage of the fused tail
+  if (N > kChainNext) {  // the big first stage as its own sampler launch
+    const int rc = fps_impl(xyz, B, N, npoint[0], idx[0], new_xyz[0], nullptr, 0, s,
+                            PN2_FPS_AUTO, take);
+    if (rc != PN2_OK) return rc;
+    if (nstages == 1) return PN2_OK;
+    xyz = new_xyz[0];
+    N = npoint[0];
+    first = 1;
+  }
+  FpsChain c;
+  c.stages = nstages - first;
+  int n = N;
+  for (int i = 0; i < kChainMax; ++i) {
+    const bool on = i < c.stages;
+    c.n[i] = on ? n : 0;
+    c.m[i] = on ? npoint[first + i] : 0;
+    c.idx[i] = on ? idx[first + i] : nullptr;
+    c.nx[i] = on ? new_xyz[first + i] : nullptr;
+    if (on) n = c.m[i];
+  }
+  hipLaunchKernelGGL(fps_chain_kernel, dim3(B), dim3(kChainBlock), 0, s, xyz, c);
+  PN2_RETURN_LAUNCH();
+}
 }  // namespace pn2
 
 extern "C" {
@@ -282,31 +312,8 @@ int pn2_fps_gather_sched(const float* xyz, int B, int N, int npoint, int32_t* id
 
 int pn2_fps_chain(const float* xyz, int B, int N, int nstages, const int* npoint,
                   int32_t* const* idx, float* const* new_xyz, pn2_stream_t stream) {
-  const int rc0 = pn2::fps_chain_check(xyz, B, N, nstages, npoint, idx, new_xyz);
-  if (rc0 != PN2_OK || B == 0) return rc0;
-  hipStream_t s = (hipStream_t)stream;
-  int first = 0;  // first stage of the fused tail
-  if (N > pn2::kChainNext) {  // the big first stage as its own sampler launch
-    const int rc = pn2::fps_impl(xyz, B, N, npoint[0], idx[0], new_xyz[0], nullptr, 0, s);
-    if (rc != PN2_OK) return rc;
-    if (nstages == 1) return PN2_OK;
-    xyz = new_xyz[0];
-    N = npoint[0];
-    first = 1;
-  }
-  pn2::FpsChain c;
-  c.stages = nstages - first;
-  int n = N;
-  for (int i = 0; i < pn2::kChainMax; ++i) {
-    const bool on = i < c.stages;
-    c.n[i] = on ? n : 0;
-    c.m[i] = on ? npoint[first + i] : 0;
-    c.idx[i] = on ? idx[first + i] : nullptr;
-    c.nx[i] = on ? new_xyz[first + i] : nullptr;
-    if (on) n = c.m[i];
-  }
-  hipLaunchKernelGGL(pn2::fps_chain_kernel, dim3(B), dim3(pn2::kChainBlock), 0, s, xyz, c);
-  PN2_RETURN_LAUNCH();
+  return pn2::fps_chain_launch(xyz, B, N, nstages, npoint, idx, new_xyz, (hipStream_t)stream,
+                               true);
 }
 
 size_t pn2_fps_workspace_size(int B, int N) {

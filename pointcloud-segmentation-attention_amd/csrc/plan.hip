@@ -47,14 +47,18 @@ int run_op(const Op& o) {
     case kWait:
       return (int)hipStreamWaitEvent(o.stream, (hipEvent_t)o.handle, 0);
     case kFpsChain:
-      return pn2_fps_chain(o.xyz, o.B, o.N, o.nstages, o.npoint, o.idx, o.nx,
-                           (pn2_stream_t)o.stream);
+      return pn2::fps_chain_launch(o.xyz, o.B, o.N, o.nstages, o.npoint, o.idx, o.nx, o.stream,
+                                   false);
   }
   return PN2_EINVAL;
 }
 
 int launch(pn2_plan* p, void* ev0, void* ev1) {
   if (!p) return PN2_EINVAL;
+  // a sampler fault stored by an earlier launch is reported here, once, before anything of
+  // this step is enqueued: the plan's own sampler launches do not look at the fault word, so
+  // a step is enqueued whole or not at all (its events then still describe the previous step)
+  if (pn2::fps_take_fault()) return PN2_EFAULT;
   const int n = (int)p->ops.size();
   for (int i = 0; i < n; ++i) {
     const Op& o = p->ops[i];

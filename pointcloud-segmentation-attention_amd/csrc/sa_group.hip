@@ -199,6 +199,17 @@ __global__ __launch_bounds__(kSgBlock) void ball_group_layers_kernel(SgArgs a) {
       if (e < E) O[e] = v[u];
     }
   }
+  // points-only rows carry no xyz channel: grouped_xyz (still an output of sample_and_group,
+  // pointnet_util.py:58) gets its own pass over the tile, by the query's first part
+  if (GX && layout == PN2_SG_POINTS_ONLY && part == 0 && PN2_SG_SKIP != 2) {
+    for (int e = t; e < nq * ns * 3; e += kSgBlock) {
+      const int r = e / 3, cx = e - 3 * (e / 3);
+      const int qi = (int)fdiv((uint32_t)r, g.div_ns);
+      const int i = s_hit[r];
+      const float s = cx == 0 ? sx[i] : (cx == 1 ? sy[i] : sz[i]);
+      GX[e] = s - s_q[3 * qi + cx];  // pointnet_util.py:40
+    }
+  }
 }
 
 }  // namespace
@@ -232,7 +243,7 @@ int pn2_ball_group_layers(const pn2_sa_layer* layers, int nlayers, int B, pn2_st
     g.new_xyz = s.new_xyz;
     g.idx = s.idx;
     g.cnt = s.pts_cnt;
-    g.grouped_xyz = layout == PN2_SG_XYZ_ONLY ? nullptr : s.grouped_xyz;
+    g.grouped_xyz = s.grouped_xyz;  // written in every layout (= out when xyz-only)
     g.out = s.new_points;
     g.N = s.N; g.C = layout == PN2_SG_XYZ_ONLY ? 0 : s.C; g.M = s.M; g.ns = s.nsample;
     g.Cout = Cout; g.layout = layout;

@@ -96,11 +96,12 @@ BALL_GROUP_MAX_POINTS = 1024  # pn2_ball_group_layers stages each cloud in LDS
 BALL_GROUP_MAX_NSAMPLE = 128
 
 
-def ball_group_layers(layers, use_xyz=True, xyz_last=False):
-    """query_ball_point followed by group_concat (want_grouped_xyz=False) for several layers
-    in ONE launch (pn2_ball_group_layers): layers = [(radius, nsample, xyz, points, new_xyz)],
-    every cloud at most BALL_GROUP_MAX_POINTS points. Returns [(idx, pts_cnt, new_points)],
-    bit-identical to the separate ops (tf_grouping_g.cu:3-57, pointnet_util.py:38-56)."""
+def ball_group_layers(layers, use_xyz=True, xyz_last=False, want_grouped_xyz=False):
+    """query_ball_point followed by group_concat for several layers in ONE launch
+    (pn2_ball_group_layers): layers = [(radius, nsample, xyz, points, new_xyz)], every cloud at
+    most BALL_GROUP_MAX_POINTS points. Returns [(idx, pts_cnt, new_points)], plus grouped_xyz
+    (B, M, nsample, 3) as a 4th element with want_grouped_xyz, bit-identical to the separate
+    ops (tf_grouping_g.cu:3-57, pointnet_util.py:38-58)."""
     if not 1 <= len(layers) <= PN2_SA_MAX_LAYERS:
         raise InvalidArgumentError(f"ball_group_layers: 1..{PN2_SA_MAX_LAYERS} layers")
     flags = (PN2_USE_XYZ if use_xyz else 0) | (PN2_XYZ_LAST if xyz_last else 0)
@@ -128,11 +129,13 @@ def ball_group_layers(layers, use_xyz=True, xyz_last=False):
         idx = torch.empty((B, M, ns), dtype=torch.int32, device=xyz.device)
         cnt = torch.empty((B, M), dtype=torch.int32, device=xyz.device)
         new_points = torch.empty((B, M, ns, Cout), dtype=torch.float32, device=xyz.device)
+        gxyz = (torch.empty((B, M, ns, 3), dtype=torch.float32, device=xyz.device)
+                if want_grouped_xyz else None)
         a.xyz, a.points, a.new_xyz = ptr(xyz), ptr(points), ptr(new_xyz)
         a.N, a.C, a.M, a.nsample, a.radius, a.flags = N, C, M, ns, float(radius), flags
-        a.idx, a.pts_cnt, a.grouped_xyz, a.new_points = ptr(idx), ptr(cnt), None, ptr(new_points)
+        a.idx, a.pts_cnt, a.grouped_xyz, a.new_points = ptr(idx), ptr(cnt), ptr(gxyz), ptr(new_points)
         keep += [xyz, points, new_xyz]
-        outs.append((idx, cnt, new_points))
+        outs.append((idx, cnt, new_points) + ((gxyz,) if want_grouped_xyz else ()))
     check(lib().pn2_ball_group_layers(arr, len(layers), B, stream_of(keep[0])),
           "ball_group_layers")
     return outs

@@ -14,6 +14,23 @@ def shard_ids(rank, world, per_rank):
     return list(range(rank * per_rank, (rank + 1) * per_rank))
 
 
+def set_ids(rank, world, per_rank, set_index):
+    """Global cloud ids of buffer set `set_index` on `rank`: the pipelined bench rotates over
+    several buffer sets, each holding its own clouds, so set i of every rank is a contiguous
+    global batch of world * per_rank clouds after the i batches before it."""
+    return [set_index * world * per_rank + c for c in shard_ids(rank, world, per_rank)]
+
+
+def min_over_ranks(value, device="cpu"):
+    """all_reduce(MIN) of one float (e.g. a 0/1 parity flag) across ranks."""
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return float(value)
+    t = torch.tensor([float(value)], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+    return float(t.item())
+
+
 def max_over_ranks(value, device="cpu"):
     """all_reduce(MAX) of one float (the elapsed time) across ranks."""
     import torch.distributed as dist

@@ -21,6 +21,7 @@ every FP layer as one fused interpolation + MLP kernel, and the conv1d head (fc1
 norm, dropout = identity at inference, fc2 to 21 classes) fused into FP4's MLP. Weights are
 the reference initialisers (tf_util.ParamStore, fixed seed).
 """
+import math
 import os
 import time
 
@@ -39,6 +40,7 @@ SSG_FP_MLP = ((256, 256), (256, 256), (256, 128), (128, 128, 128))
 NUM_CLASSES = 21  # ScanNet (pointnet2_sem_seg_attention.py:17)
 
 NSIDE = 4  # side streams of the whole-model step (the geometric steps use 3)
+MAX_LANES = 8  # lanes of any step layout (0 = the sampler stream)
 
 CONFIGS = {
     # name: (points per cloud, kind, with_features, attention)
@@ -238,8 +240,7 @@ class Step:
     def __init__(self, inp, overlap=True, streams=None, chain_lane=3, layout="a"):
         # chain_lane: the lane of the later samplers (SA2..SA4 / MSG SA2); 0 = behind the SA1
         # sampler on its stream; -1 = a lane of their own after the side lanes (both: several
-        # sampler streams, Pipeline)
-        # sampler on its stream (Pipeline with several sampler lanes); layout: side_layout()
+        # sampler streams, Pipeline); layout: side_layout()
         self.chain_lane = chain_lane if overlap else 0
         self.layout = layout
         self.inp = inp
@@ -258,6 +259,9 @@ class Step:
             # the later samplers' own lane (chain "own") counts as a sampler under a CU
             # partition (set_cu_partition)
             samp = {t.lane for t in self.tasks if t.direct and t.lane > 0}
+            if streams and len(streams) < self.nlanes:
+                raise ValueError(f"this step layout uses {self.nlanes} lanes, {len(streams)} "
+                                 "streams given")
             self.streams = [None] + (list(streams[1:self.nlanes]) if streams else
                                      [side_stream(dev, lane, "sampler" if lane in samp else "side")
                                       for lane in range(1, self.nlanes)])
@@ -811,10 +815,10 @@ class GraphStep:
                       launch=lambda t: t.fn() if t.direct else self.graphs[t.name].replay())
         return self.outs
 
-    def replay_plan(self, sampler_events=None):
-        """replay(join=False) through a native plan (one host call for the whole step): the
-        plan for the current stream as lane 0 is recorded at its first use."""
-        main = torch.cuda.current_stream(self.step.inp["xyz"].device)
+    def plan_for(self, main):
+        """The native plan of this step with `main` as lane 0, recorded at the first request
+        (Pipeline records every (set, sampler stream) pair it will use up front, so no plan is
+        built inside a timed region)."""
         if not hasattr(self, "plans"):
             self.plans = {}
         p = self.plans.get(main.cuda_stream)
@@ -823,7 +827,13 @@ class GraphStep:
             p = Plan()
             self.step.emit_plan(p, self.graphs, main)
             self.plans[main.cuda_stream] = p
-        p.launch(sampler_events)
+        return p
+
+    def replay_plan(self, sampler_events=None):
+        """replay(join=False) through a native plan (one host call for the whole step) for the
+        current stream as lane 0."""
+        main = torch.cuda.current_stream(self.step.inp["xyz"].device)
+        self.plan_for(main).launch(sampler_events)
         self.step.ran = True
         return self.outs
 
@@ -852,7 +862,10 @@ class Pipeline:
     1 + 2 + (sampler_lanes - 1) <= GPU_MAX_HW_QUEUES."""
 
     def __init__(self, inp, graphs=True, overlap=True, nsets=3, private_streams=False,
-                 sampler_lanes=1, native_plan=True, only=None, layout="a", chain_own=False):
+                 sampler_lanes=1, native_plan=True, only=None, layout="a", chain_own=False,
+                 set_inputs=None):
+        # set_inputs: one make_inputs() dict per buffer set (distinct clouds per set: the
+        # steps of a pipelined run then sample different clouds); None = every set reads `inp`
         # private_streams: every buffer set gets its own side streams, so the side lanes of
         # consecutive steps overlap each other too (the whole-model step, whose lane-1 chain
         # of SA/FP layers is longer than a sampler period; the geometric step once its
@@ -865,7 +878,9 @@ class Pipeline:
         def streams(i):  # set 0 keeps the process-wide side streams
             if i == 0 or not private:
                 return None
-            return [None] + [side_stream(dev, (i, lane)) for lane in range(1, NSIDE + 1)]
+            # every lane a step of any layout can use (side lanes, attention, the later
+            # samplers' own lane); a stream takes a hardware queue only when first used
+            return [None] + [side_stream(dev, (i, lane)) for lane in range(1, MAX_LANES)]
 
         multi = sampler_lanes > 1 and overlap and inp["xyz"].is_cuda
         # chain_own: the later samplers on a stream of their own instead of behind SA1
@@ -889,13 +904,25 @@ class Pipeline:
         # Python loop
         self.native_plan = native_plan and graphs and overlap and inp["xyz"].is_cuda
         # only: DIAGNOSTIC restriction of every step to its samplers or its side work
-        mk = (lambda i: GraphStep(inp, overlap=overlap, streams=streams(i), chain_lane=chain_lane,
-                                  segments=self.native_plan, only=only, layout=layout)) \
-            if graphs else (lambda i: Step(inp, overlap=overlap, streams=streams(i),
+        if set_inputs is not None and len(set_inputs) != nsets:
+            raise ValueError(f"set_inputs: {len(set_inputs)} input dicts for {nsets} sets")
+        inps = list(set_inputs) if set_inputs is not None else [inp] * nsets
+        mk = (lambda i: GraphStep(inps[i], overlap=overlap, streams=streams(i),
+                                  chain_lane=chain_lane, segments=self.native_plan, only=only,
+                                  layout=layout)) \
+            if graphs else (lambda i: Step(inps[i], overlap=overlap, streams=streams(i),
                                            chain_lane=chain_lane, layout=layout))
         self.sets = [mk(i) for i in range(nsets)]
+        self.inputs = inps
         self.k = 0
         self.host_wait_s = self.host_launch_s = 0.0  # host wait for a set / enqueue time
+        if self.native_plan:
+            # every (set, sampler stream) pair the rotation will meet gets its plan now, not at
+            # its first replay (which could fall inside a timed region)
+            nl = len(self.lane0)
+            for k in range(nsets * nl // math.gcd(nsets, nl)):
+                st = self.lane0[k % nl] or torch.cuda.current_stream(dev)
+                self.sets[k % nsets].plan_for(st)
 
     def run(self, sampler_events=None):
         st = self.lane0[self.k % len(self.lane0)]
@@ -927,10 +954,51 @@ class Pipeline:
             self.host_launch_s += time.perf_counter() - t0
 
     def join(self):
-        """Wait for everything enqueued; returns the outputs of the last step run."""
+        """Wait for everything enqueued; returns the outputs of the last step run. Raises
+        RuntimeError if a sampler launch that has already completed stored a fault (the host
+        sees the fault word once the launch is done; check_faults() synchronises first)."""
         for s in self.sets:
             s.join()
-        return self.sets[(self.k - 1) % len(self.sets)].join()
+        out = self.sets[(self.k - 1) % len(self.sets)].join()
+        _raise_fault(_lib_fault_status(clear=True))
+        return out
+
+    def check_faults(self):
+        """Synchronise with every set's enqueued work, then return the sampler fault word
+        (include/pn2hip.h pn2_fault_status; 0 = no fault) and clear it, raising RuntimeError
+        when it is set (Pn2RuntimeError): the indices of the step whose sampler faulted are not
+        to be trusted."""
+        for s in self.sets:
+            st = s.step if isinstance(s, GraphStep) else s
+            if st.ran and st.overlap:
+                for lane in range(1, st.nlanes):
+                    st.lane_done[lane].synchronize()
+        torch.cuda.synchronize(self.inputs[0]["xyz"].device)
+        code = _lib_fault_status(clear=True)
+        _raise_fault(code)
+        return code
+
+    def outputs_by_set(self):
+        """(inputs, outputs, intermediates) of every set's last step, after join()."""
+        res = []
+        for s, inp in zip(self.sets, self.inputs):
+            st = s.step if isinstance(s, GraphStep) else s
+            if st.ran:
+                res.append((inp, st.outputs(), st.intermediates()))
+        return res
+
+
+def _lib_fault_status(clear):
+    from ._lib import lib
+    return int(lib().pn2_fault_status(1 if clear else 0))
+
+
+def _raise_fault(code):
+    if code:
+        from ._lib import Pn2RuntimeError
+        raise Pn2RuntimeError(f"sampler fault {code} (pn2_fault_status; PN2_FAULT_FPS_POLL = 1: a "
+                              "culled sampler's cold waves ran past their poll bound): the "
+                              "indices of the step it sampled are not valid")
 
 
 def sa_fp_bytes(config, B):

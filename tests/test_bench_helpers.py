@@ -1,6 +1,7 @@
 """bench.py's inputs that do not need a GPU: the committed PMC summary behind roofline.traffic,
 the committed stamp summary behind roofline.latency, and the CPU baseline leg (a short
 sample)."""
+import importlib
 import importlib.util
 import os
 
@@ -50,3 +51,37 @@ def test_cpu_baseline_leg(bench):
     assert r["unit"] == "clouds/s"
     assert r["value_all_cores_at_measured_efficiency"] == pytest.approx(
         r["value_all_cores_extrapolated"] * r["scaling_efficiency_1_to_threads"])
+
+
+@pytest.mark.parametrize("config", ["cfg2", "cfg3"])
+def test_verify_checker_catches_a_wrong_step(bench, config):
+    """bench.py's `verified` field: the checker passes the oracle's own outputs and fails a
+    step whose one index, one copied float or one interpolated value is off."""
+    import numpy as np
+    import torch
+
+    from oracle import oracle as O
+    pkg = importlib.import_module("pointcloud-segmentation-attention_amd")
+    inp = pkg.stack.make_inputs(config, [5], "cpu")
+    np_inp = dict(inp, xyz=inp["xyz"].numpy(), feats=None if inp["feats"] is None else
+                  inp["feats"].numpy(), sa_out=[t.numpy() for t in inp["sa_out"]],
+                  fp_out=[t.numpy() for t in inp["fp_out"]])
+    if "attn" in inp:
+        np_inp["attn"] = [tuple(t.numpy() for t in q) for q in inp["attn"]]
+    ref, _, inter = O.run_stack_cpu(np_inp, config, intermediates=True)
+    T = lambda a: torch.from_numpy(np.array(a))  # noqa: E731
+    good = bench.verify_sets(config, [(inp, [T(r) for r in ref],
+                                       {k: T(v) for k, v in inter.items()})], 2)
+    assert good["failures"] == [] and good["clouds"] == 1
+    bad_idx = {k: T(v) for k, v in inter.items()}
+    bad_idx["bq2.idx"][0, 3, 5] += 1
+    bad_copy = [T(r) for r in ref]
+    bad_copy[0].view(-1)[17] = float(np.nextafter(np.float32(bad_copy[0].view(-1)[17]),
+                                                   np.float32(9)))
+    bad_fp = [T(r) for r in ref]
+    bad_fp[-1][0, 0, 0] += 1e-3
+    for outs, it, what in ((ref, bad_idx, "bq2.idx"), (bad_copy, inter, "sa1.new_points"),
+                           (bad_fp, inter, "fp4.out")):
+        r = bench.verify_sets(config, [(inp, [T(o) for o in outs],
+                                        {k: T(v) for k, v in it.items()})], 2)
+        assert r["failures"] and what in r["failures"][0], r["failures"]

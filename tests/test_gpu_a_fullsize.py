@@ -140,15 +140,21 @@ def test_pipeline_full_size(env, config, B, lanes, native, layout, own, cus):
     of every set are poisoned before the last three steps (a missing wait then shows), and the
     last two steps' outputs (one per sampler stream) are compared with the oracle."""
     pkg, O, torch, dev = env
-    inp = pkg.stack.make_inputs(config, list(range(100, 100 + B)), dev)
+    # every set its own clouds (as bench.py runs it): a set that read another set's buffers
+    # would give outputs that match no oracle run
+    sets = [pkg.stack.make_inputs(config, list(range(100 + i * B, 100 + (i + 1) * B)), dev)
+            for i in range(3)]
+    inp = sets[0]
     pkg.stack.set_cu_partition(dev, cus)  # CU-masked sampler / side streams (cus > 0)
     saved = dict(pkg.stack._SIDE)
     if cus:
         pkg.stack._SIDE.clear()  # fresh (masked) streams for this pipeline
     pipe = pkg.stack.Pipeline(inp, graphs=True, nsets=3, sampler_lanes=lanes, native_plan=native,
-                              layout=layout, chain_own=own)
+                              layout=layout, chain_own=own, set_inputs=sets)
     assert len(pipe.lane0) == lanes
     assert pipe.native_plan == native
+    if native:  # every (set, sampler stream) plan exists before the first step
+        assert all(getattr(s, "plans", None) for s in pipe.sets), "plans not built up front"
     for _ in range(7):
         pipe.run()
     pipe.join()
@@ -156,16 +162,22 @@ def test_pipeline_full_size(env, config, B, lanes, native, layout, own, cus):
     for _ in range(3):
         pipe.run()
     outs = pipe.join()
-    torch.cuda.synchronize()
-    if native:
-        assert all(getattr(s, "plans", None) for s in pipe.sets), "a set ran without its plan"
+    assert pipe.check_faults() == 0
     pkg.stack.set_cu_partition(dev, 0)
     if cus:
         pkg.stack._SIDE.clear()
         pkg.stack._SIDE.update(saved)
     for back in (1, 2):
         s = pipe.sets[(pipe.k - back) % len(pipe.sets)]
-        check_step(O, config, inp, s.outs if back > 1 else outs, s.intermediates())
+        check_step(O, config, sets[(pipe.k - back) % 3], s.outs if back > 1 else outs,
+                   s.intermediates())
+    # the checker bench.py's `verified` field runs, over every set
+    runs = pipe.outputs_by_set()
+    assert len(runs) == 3
+    for sinp, souts, sinter in runs:
+        bad = O.compare_stack(_np_inputs(sinp), config, [o.cpu().numpy() for o in souts],
+                              {k: v.cpu().numpy() for k, v in sinter.items()})
+        assert not bad, bad
 
 
 @pytest.mark.timeout(300)

@@ -63,7 +63,10 @@ LAUNCHES = [
 
 @pytest.mark.parametrize("li", range(len(LAUNCHES)))
 @pytest.mark.parametrize("use_xyz,xyz_last", [(True, False), (True, True), (False, False)])
-def test_ball_group_layers(env, li, use_xyz, xyz_last):
+@pytest.mark.parametrize("want_gx", [False, True])
+def test_ball_group_layers(env, li, use_xyz, xyz_last, want_gx):
+    """Every layout (SSG [xyz, points], MSG [points, xyz], points only, xyz only), with and
+    without the grouped_xyz output (written in every layout, as pn2_group_concat does)."""
     pkg, O, torch, dev = env
     B = 3
     t = lambda a: None if a is None else torch.from_numpy(a).to(dev)  # noqa: E731
@@ -74,13 +77,17 @@ def test_ball_group_layers(env, li, use_xyz, xyz_last):
         x, pts, q = _layer(pkg, O, kind, B, N, M, C, 10 * li + j)
         specs.append((r, ns, t(x), t(pts), t(q)))
         ridx, rcnt = O.ball_query(x, q, r, ns)
-        rnp, _ = O.group_concat(x, pts, q, ridx, use_xyz=use_xyz, xyz_last=xyz_last)
-        refs.append((ridx, rcnt, rnp))
-    got = pkg.pointnet_util.ball_group_layers(specs, use_xyz=use_xyz, xyz_last=xyz_last)
-    for (idx, cnt, new_points), (ridx, rcnt, rnp) in zip(got, refs):
+        rnp, rgx = O.group_concat(x, pts, q, ridx, use_xyz=use_xyz, xyz_last=xyz_last)
+        refs.append((ridx, rcnt, rnp, rgx))
+    got = pkg.pointnet_util.ball_group_layers(specs, use_xyz=use_xyz, xyz_last=xyz_last,
+                                              want_grouped_xyz=want_gx)
+    for out, (ridx, rcnt, rnp, rgx) in zip(got, refs):
+        idx, cnt, new_points = out[:3]
         assert np.array_equal(cnt.cpu().numpy(), rcnt)
         assert np.array_equal(idx.cpu().numpy(), ridx)
         assert np.array_equal(_bits(new_points.cpu().numpy()), _bits(rnp))
+        if want_gx:
+            assert np.array_equal(_bits(out[3].cpu().numpy()), _bits(rgx)), "grouped_xyz"
 
 
 def test_ball_group_layers_rejects(env):
