@@ -38,6 +38,8 @@ MSG_SA = ((512, (0.1, 0.2, 0.4), (16, 32, 128), (64, 128, 128)),
 SSG_SA_MLP = ((32, 32, 64), (64, 64, 128), (128, 128, 256), (256, 256, 512))
 SSG_FP_MLP = ((256, 256), (256, 256), (256, 128), (128, 128, 128))
 NUM_CLASSES = 21  # ScanNet (pointnet2_sem_seg_attention.py:17)
+# cell edge of the one grid that serves all of MSG SA1's radii (tools/bench_msg_grid.py)
+MSG_GRID_EDGE = 0.1
 
 NSIDE = 4  # side streams of the whole-model step (the geometric steps use 3)
 MAX_LANES = 8  # lanes of any step layout (0 = the sampler stream)
@@ -495,16 +497,23 @@ class Step:
                                                         out=v["fps_out"][i:i + 1])
             return f
 
+        # the xyz-only level (SA1) is grouped with the grid query: ONE grid over the input
+        # cloud (built on lane 1 while SA1 is sampled) serves all of its radii -- the query's
+        # cell range follows its own radius, whatever the cell edge
+        grid_level = int(xyz0.shape[1]) >= tf_grouping.GRID_MIN_POINTS
+        if grid_level:
+            tasks.append(Task("grid1", 1, (), lambda: v.__setitem__(
+                "grid1", tf_grouping.BallGrid(xyz0, MSG_GRID_EDGE))))
+
         def grp(i, r):
             def f():
                 radius, nsample = MSG_SA[i][1][r], MSG_SA[i][2][r]
                 points = None if i == 0 else inp["sa_out"][0]
                 xyz, new_xyz = v["xyz"][i], v["xyz"][i + 1]
-                if points is None and int(xyz.shape[1]) >= tf_grouping.GRID_MIN_POINTS:
+                if i == 0 and grid_level:
                     # xyz-only level (SA1): grid query and grouping in one kernel
-                    grid = tf_grouping.BallGrid(xyz, radius)
                     idx, _, v["gp"][(i, r)] = pointnet_util.ball_group_xyz(
-                        radius, nsample, xyz, new_xyz, grid)
+                        radius, nsample, xyz, new_xyz, v["grid1"])
                 else:
                     idx, _ = tf_grouping.query_ball_point(radius, nsample, xyz, new_xyz)
                     v["gp"][(i, r)] = pointnet_util.group_concat(xyz, points, new_xyz, idx,
@@ -527,7 +536,8 @@ class Step:
                 # radius r on lane 1 + r when lane 3 is free (chain_lane 0), else radius 0 on
                 # lane 1 and the others on lane 2
                 lane = 1 + r if self.chain_lane <= 0 and self.overlap else 1 + min(r, 1)
-                tasks.append(Task(f"sa{i + 1}_{r}", lane, (f"fps{i + 1}",), grp(i, r)))
+                deps = (f"fps{i + 1}",) + (("grid1",) if i == 0 and grid_level else ())
+                tasks.append(Task(f"sa{i + 1}_{r}", lane, deps, grp(i, r)))
         return tasks
 
     def outputs(self):
