@@ -9,15 +9,16 @@
 // per iteration and a ballot/DPP argmax whose lane order IS the reference's tie order — see
 // fps_v9_kernel in fps_kernels.h. gather_point is fused (thread 0 writes new_xyz,
 // pointnet_util.py:34). Clouds beyond kMaxRegPoints keep the running min in a caller-provided
-// workspace (fps_ws_kernel). Measured variants live in tools/fps_lab.
+// workspace (fps_ws_kernel). The measured variants (a lab library of rounds 1-2, since removed
+// from the tree) and their numbers are in DESIGN.md §3.1 and profiles/r1/.
 #include <mutex>
 
 #include "fps_kernels.h"
 #include "fps_cull.h"
 
 // Code placement of the SA1 (256 x 32) sampler's iteration loop. The loop runs ~6 % slower
-// when it starts at an address = 0 mod 8 than at 4 mod 8 (tools/pad_fps.py,
-// profiles/r1/pad_fps.log). tools/place_sa1_loop.py compiles this file, reads where the
+// when it starts at an address = 0 mod 8 than at 4 mod 8 (a round-1 padding sweep, since
+// removed; its log: profiles/r1/pad_fps.log). tools/place_sa1_loop.py compiles this file, reads where the
 // loop landed and writes build/sa1_pad.h: the number of s_nop placed before the loop (run
 // once per launch) that moves it to the measured best offset.
 #ifndef PN2_SA1_PAD
@@ -212,7 +213,7 @@ int fps_impl(const float* xyz, int B, int N, int M, int32_t* idx, float* nx, voi
                        nx);
     PN2_RETURN_LAUNCH();
   }
-  // launch table measured on MI355X (tools/tune_fps.py, B = 16 ScanNet crops,
+  // launch table measured on MI355X (round-1 sweep, B = 16 ScanNet crops,
   // profiles/r1/tune_fps.jsonl; lane-resolve variants: profiles/r1/tune_fps_lres.jsonl)
   if (N <= 64) launch_v9<64, 1, 1>(xyz, B, N, M, idx, nx, s);
   else if (N <= 128) launch_v9<64, 2, 2>(xyz, B, N, M, idx, nx, s);

@@ -1,5 +1,5 @@
 // Device-side building blocks of the gfx950 farthest-point sampler, shared by the
-// production dispatch (fps.hip) and the variant lab (tools/fps_lab/fps_lab.hip).
+// production dispatch (fps.hip) (and, in rounds 1-2, a variant lab since removed).
 // Reference: farthestpointsamplingKernel, pointnet2_tensorflow/tf_ops/sampling/
 // tf_sampling_g.cu:105-170 (tie rule :146-163).
 #pragma once
@@ -97,7 +97,7 @@ struct Lay9 {
 // the waves' entries. Three rotating slots: slot (j+1) % 3 is cleared by thread 0 before
 // iteration j's barrier, after every read of it (iteration j-2, before barrier j-1).
 // PAD >= 0: that many s_nop right before the iteration loop, shifting the loop's code address
-// by 4 * PAD bytes (code-placement experiments, tools/pad_fps.py; the product uses PAD = -1).
+// by 4 * PAD bytes (code-placement experiments, profiles/r1/pad_fps.log; the product uses PAD = -1).
 template <int BLOCK, int PPT, int G, bool STAMP = false, bool LRES = false, bool ATOM = false,
           int PAD = -1>
 PN2_DEV void fps_v9_body(const float* P, int N, int M, const float* CXYZ, int32_t* I, float* NX,

@@ -28,6 +28,9 @@ namespace pn2 {
 namespace {
 
 constexpr int kBuildBlock = 1024;
+#ifndef PN2_GQ_FLAT
+#define PN2_GQ_FLAT 1
+#endif
 constexpr int kMaxBitWords = 4096;  // bitmask words per wave (N <= 131072)
 constexpr float kAutoPointsPerCell = 2.0f;
 
@@ -255,6 +258,7 @@ __global__ __launch_bounds__(BLOCK) void ball_query_grid_kernel(
     const int x0 = cell_coord(qx - rr, h.ox, h.inv, h.nx), x1 = cell_coord(qx + rr, h.ox, h.inv, h.nx);
     const int y0 = cell_coord(qy - rr, h.oy, h.inv, h.ny), y1 = cell_coord(qy + rr, h.oy, h.inv, h.ny);
     const int z0 = cell_coord(qz - rr, h.oz, h.inv, h.nz), z1 = cell_coord(qz + rr, h.oz, h.inv, h.nz);
+#if !PN2_GQ_FLAT  // A/B: one row at a time (two dependent offset loads per row)
     for (int z = z0; z <= z1; ++z) {
       for (int y = y0; y <= y1; ++y) {
         const int row = (z * h.ny + y) * h.nx;
@@ -268,6 +272,49 @@ __global__ __launch_bounds__(BLOCK) void ball_query_grid_kernel(
         }
       }
     }
+#else
+    // the cell range as rows (z, y) of contiguous cells x0..x1: the sorted-point ranges of up
+    // to 64 rows are fetched at once (lane j: row r0 + j), then the wave walks the
+    // concatenation of those ranges 64 points at a time -- one dependent memory trip per 64
+    // points, where a loop over the rows made two per row (its offsets) plus one per row's
+    // points, most rows holding a few points
+    const int nyr = y1 - y0 + 1;
+    const int nrows = (z1 - z0 + 1) * nyr;
+    for (int r0 = 0; r0 < nrows; r0 += kWave) {
+      int beg = 0, len = 0;
+      const int r = r0 + lane;
+      if (r < nrows) {
+        const int zr = r / nyr;
+        const int row = ((z0 + zr) * h.ny + y0 + (r - zr * nyr)) * h.nx;
+        beg = off[row + x0];
+        len = off[row + x1 + 1] - beg;  // cells x0..x1 of a row are contiguous
+      }
+      const int incl = wave_incl_scan(len, lane);
+      const int total = __builtin_amdgcn_readlane(incl, kWave - 1);
+      const int excl = incl - len;
+      for (int i0 = 0; i0 < total; i0 += kWave) {
+        // the rows overlapping [i0, i0 + 64): each lane takes the last one starting at or
+        // before its position (empty rows never qualify)
+        const int i = i0 + lane;
+        uint64_t span = __ballot(len > 0 && incl > i0 && excl < i0 + kWave);
+        int base = 0;
+        while (span) {
+          const int j = (int)__builtin_ctzll(span);
+          span &= span - 1;
+          const int ej = __builtin_amdgcn_readlane(excl, j);
+          const int bj = __builtin_amdgcn_readlane(beg, j);
+          base = ej <= i ? bj - ej : base;
+        }
+        if (i < total) {
+          const float4 p = pts[base + i];
+          if (sqdist(qx, qy, qz, p.x, p.y, p.z) < thresh) {  // tf_grouping_g.cu:24-25
+            const int k = __float_as_int(p.w);
+            atomicOr(&mine[k >> 5], 1u << (k & 31));
+          }
+        }
+      }
+    }
+#endif
     // hits in index order: lane l owns bitmask words [l*wpl, (l+1)*wpl)
     int pop = 0, myfirst = -1;
     for (int j = 0; j < wpl; ++j) {

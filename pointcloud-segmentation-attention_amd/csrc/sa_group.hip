@@ -43,6 +43,9 @@ constexpr int kSgMaxQpb = 64;   // queries per workgroup
 #ifndef PN2_SG_SPLIT_STAGE
 #define PN2_SG_SPLIT_STAGE 4096
 #endif
+#ifndef PN2_SG_U  // elements whose gathers are in flight per thread before its stores
+#define PN2_SG_U 4
+#endif
 #ifndef PN2_SG_TILE_KB
 #define PN2_SG_TILE_KB 32
 #endif
@@ -185,7 +188,7 @@ __global__ __launch_bounds__(kSgBlock) void ball_group_layers_kernel(SgArgs a) {
     }
     return F[(size_t)i * C + cp];
   };
-  constexpr int U = 4;
+  constexpr int U = PN2_SG_U;
   for (int e0 = e_beg + t; e0 < E; e0 += kSgBlock * U) {
     float v[U];
 #pragma unroll
