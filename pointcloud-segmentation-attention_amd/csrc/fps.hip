@@ -169,18 +169,20 @@ struct FpsChain {
 
 // one stage (N <= kChainNext) for one cloud: the configuration fps_impl uses for this N
 PN2_DEV void chain_stage(const float* P, int N, int M, const float* CXYZ, int32_t* I, float* NX,
-                         float* SNEXT, uint2 (*red)[8]) {
+                         float* SNEXT, uint2 (*red)[8], FpsSlot (*wslot)[8]) {
   const bool w0 = threadIdx.x < kWave;
+  constexpr bool WC = PN2_FPS_WCOORD;  // winner coordinates carried (fps_kernels.h)
   if (N <= 64) { if (w0) fps_v9_body<64, 1, 1>(P, N, M, CXYZ, I, NX, SNEXT, red); }
   else if (N <= 128) { if (w0) fps_v9_body<64, 2, 2>(P, N, M, CXYZ, I, NX, SNEXT, red); }
-  else if (N <= 256) { if (w0) fps_v9_body<64, 4, 4, false, true>(P, N, M, CXYZ, I, NX, SNEXT, red); }
-  else if (N <= 512) { if (w0) fps_v9_body<64, 8, 4, false, true>(P, N, M, CXYZ, I, NX, SNEXT, red); }
-  else fps_v9_body<256, 4, 2, false, true>(P, N, M, CXYZ, I, NX, SNEXT, red);
+  else if (N <= 256) { if (w0) fps_v9_body<64, 4, 4, false, true, false, -1, WC>(P, N, M, CXYZ, I, NX, SNEXT, red, wslot); }
+  else if (N <= 512) { if (w0) fps_v9_body<64, 8, 4, false, true, false, -1, WC>(P, N, M, CXYZ, I, NX, SNEXT, red, wslot); }
+  else fps_v9_body<256, 4, 2, false, true, false, -1, WC>(P, N, M, CXYZ, I, NX, SNEXT, red, wslot);
 }
 
 __global__ __launch_bounds__(kChainBlock) void fps_chain_kernel(const float* __restrict__ xyz,
                                                                 FpsChain c) {
   __shared__ uint2 red[2][8];
+  __shared__ FpsSlot wslot[2][8];
   __shared__ float sxyz[3 * kChainNext];
   __shared__ float snew[2][3 * kChainNext];
   const int b = blockIdx.x;
@@ -191,7 +193,7 @@ __global__ __launch_bounds__(kChainBlock) void fps_chain_kernel(const float* __r
     const float* cxyz = i == 0 ? sxyz : snew[(i - 1) & 1];
     float* next = i + 1 < c.stages ? snew[i & 1] : nullptr;
     chain_stage(cxyz, c.n[i], c.m[i], cxyz, c.idx[i] + (size_t)b * c.m[i],
-                c.nx[i] + (size_t)b * c.m[i] * 3, next, red);
+                c.nx[i] + (size_t)b * c.m[i] * 3, next, red, wslot);
     __syncthreads();  // stage i's LDS output complete before stage i+1 reads it
   }
 }

@@ -98,10 +98,23 @@ struct Lay9 {
 // iteration j's barrier, after every read of it (iteration j-2, before barrier j-1).
 // PAD >= 0: that many s_nop right before the iteration loop, shifting the loop's code address
 // by 4 * PAD bytes (code-placement experiments, profiles/r1/pad_fps.log; the product uses PAD = -1).
+// WC (with LRES, not ATOM): the winner's coordinates travel with its index instead of being
+// read back from CXYZ after the argmax: every lane selects its own candidate's coordinates
+// beside the wave max, the wave winner's come out of v_readlane, and with several waves they
+// ride in the LDS slot next to (max, index) -- one LDS round trip less on the pick's
+// dependency chain. The coordinates are the same floats (loaded from CXYZ at setup).
+#ifndef PN2_FPS_WCOORD
+#define PN2_FPS_WCOORD 1
+#endif
+struct FpsSlot {  // one wave's published winner (WC): max, index, coordinates
+  uint32_t km, k;
+  float x, y, z, pad0, pad1, pad2;
+};
 template <int BLOCK, int PPT, int G, bool STAMP = false, bool LRES = false, bool ATOM = false,
-          int PAD = -1>
+          int PAD = -1, bool WC = false>
 PN2_DEV void fps_v9_body(const float* P, int N, int M, const float* CXYZ, int32_t* I, float* NX,
-                         float* SNEXT, uint2 (*red)[8]) {
+                         float* SNEXT, uint2 (*red)[8], FpsSlot (*wslot)[8] = nullptr) {
+  static_assert(!WC || (LRES && !ATOM), "WC needs the lane resolve and the slot block step");
   unsigned long long st_acc[6] = {0, 0, 0, 0, 0, 0}, st_prev = 0;
   using Lay = Lay9<BLOCK, PPT>;
   constexpr int NW = BLOCK / kWave;
@@ -217,6 +230,22 @@ PN2_DEV void fps_v9_body(const float* P, int N, int M, const float* CXYZ, int32_
       ls = bg * G + r;
     }
     PN2_STAMP(0)
+    float wx = 0.0f, wy = 0.0f, wz = 0.0f;  // WC: this lane's candidate's coordinates
+    if constexpr (WC) {
+#pragma unroll
+      for (int q = 0; q < PPT; ++q) {
+        const bool sel = ls == q;
+        if constexpr (PK) {
+          wx = sel ? vx[q / 2][q % 2] : wx;
+          wy = sel ? vy[q / 2][q % 2] : wy;
+          wz = sel ? vz[q / 2][q % 2] : wz;
+        } else {
+          wx = sel ? px[q] : wx;
+          wy = sel ? py[q] : wy;
+          wz = sel ? pz[q] : wz;
+        }
+      }
+    }
     const uint32_t km = wave_max_u32(hi);
     PN2_STAMP(1)
     const uint64_t hold = __builtin_amdgcn_ballot_w64(hi == km);
@@ -240,7 +269,33 @@ PN2_DEV void fps_v9_body(const float* P, int N, int M, const float* CXYZ, int32_
     }
     int old = Lay::point(w * kWave + L, sq);
     PN2_STAMP(2)
-    if constexpr (NW > 1 && ATOM) {
+    if constexpr (WC) {
+      cx = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__float_as_int(wx), L));
+      cy = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__float_as_int(wy), L));
+      cz = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__float_as_int(wz), L));
+      if constexpr (NW > 1) {
+        if (lane == 0) {
+          FpsSlot sl;
+          sl.km = km;
+          sl.k = (uint32_t)old;
+          sl.x = cx; sl.y = cy; sl.z = cz;
+          sl.pad0 = sl.pad1 = sl.pad2 = 0.0f;
+          wslot[j & 1][w] = sl;
+        }
+        __syncthreads();
+        PN2_STAMP(3)
+        const FpsSlot r = (lane & 7) < NW ? wslot[j & 1][lane & 7] : FpsSlot{};
+        uint32_t bm = max_dpp_u32<kDppXor1>(r.km);
+        bm = max_dpp_u32<kDppXor2>(bm);
+        bm = max_dpp_u32<kDppHalfMirror>(bm);
+        const uint64_t wins = __builtin_amdgcn_ballot_w64(r.km == bm) & 0xFFull;
+        const int wi = (int)__builtin_amdgcn_readfirstlane((int)__builtin_ctzll(wins));
+        old = __builtin_amdgcn_readlane((int)r.k, wi);
+        cx = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__float_as_int(r.x), wi));
+        cy = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__float_as_int(r.y), wi));
+        cz = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__float_as_int(r.z), wi));
+      }
+    } else if constexpr (NW > 1 && ATOM) {
       const int sl = j % 3;
       if (lane == 0) atomicMax(&aslot[sl], ((unsigned long long)km << 32) | tie_low(old));
       if (t == 0) aslot[sl == 2 ? 0 : sl + 1] = 0ull;
@@ -260,7 +315,9 @@ PN2_DEV void fps_v9_body(const float* P, int N, int M, const float* CXYZ, int32_
       old = __builtin_amdgcn_readlane((int)r.y, wi);
     }
     PN2_STAMP(4)
-    cx = CXYZ[3 * old + 0]; cy = CXYZ[3 * old + 1]; cz = CXYZ[3 * old + 2];
+    if constexpr (!WC) {
+      cx = CXYZ[3 * old + 0]; cy = CXYZ[3 * old + 1]; cz = CXYZ[3 * old + 2];
+    }
     if (t == 0) {
       I[j] = old;
       if (NX) { NX[3 * j + 0] = cx; NX[3 * j + 1] = cy; NX[3 * j + 2] = cz; }
@@ -279,7 +336,9 @@ template <int BLOCK, int PPT, int G, bool XYZ_LDS, bool STAMP = false, bool LRES
 __global__ __launch_bounds__(BLOCK) void fps_v9_kernel(const float* __restrict__ xyz, int N,
                                                        int M, int32_t* __restrict__ idx,
                                                        float* __restrict__ new_xyz) {
+  constexpr bool WC = PN2_FPS_WCOORD && LRES && !ATOM;
   __shared__ uint2 red[2][8];
+  __shared__ FpsSlot wslot[WC ? 2 : 1][8];
   __shared__ float sxyz[XYZ_LDS ? 3 * BLOCK * PPT : 1];
   const int b = blockIdx.x;
   const float* __restrict__ P = xyz + (size_t)b * N * 3;
@@ -287,9 +346,9 @@ __global__ __launch_bounds__(BLOCK) void fps_v9_kernel(const float* __restrict__
     for (int e = threadIdx.x; e < 3 * N; e += BLOCK) sxyz[e] = P[e];
     __syncthreads();
   }
-  fps_v9_body<BLOCK, PPT, G, STAMP, LRES, ATOM, PAD>(
+  fps_v9_body<BLOCK, PPT, G, STAMP, LRES, ATOM, PAD, WC>(
       P, N, M, XYZ_LDS ? sxyz : P, idx + (size_t)b * M,
-      new_xyz ? new_xyz + (size_t)b * M * 3 : nullptr, nullptr, red);
+      new_xyz ? new_xyz + (size_t)b * M * 3 : nullptr, nullptr, red, WC ? wslot : nullptr);
 }
 
 template <int BLOCK, int PPT, int G, bool LRES = false, bool ATOM = false, int PAD = -1>

@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 OUT=gpurun_out/r4/check
 mkdir -p $OUT
 B=pointcloud-segmentation-attention_amd/csrc/build
-timeout -k 10 600 python3 -u -m pytest -x -q --timeout 280 --timeout-method thread -m gpu tests/test_gpu_a_fullsize.py tests/test_gpu_fused_layers.py > $OUT/pytest.log 2>&1 || { tail -30 $OUT/pytest.log; exit 1; }
+timeout -k 10 600 python3 -u -m pytest -x -q --timeout 280 --timeout-method thread -m gpu tests/test_gpu_a_fullsize.py tests/test_gpu_fused_layers.py tests/test_gpu_parity.py -k "fps or chain or grid or ball or pipeline or stack or golden or group" > $OUT/pytest.log 2>&1 || { tail -30 $OUT/pytest.log; exit 1; }
 tail -1 $OUT/pytest.log
 timeout -k 10 120 python3 tools/bench_msg_grid.py > $OUT/msg_grid_flat.json 2>&1 || { tail -20 $OUT/msg_grid_flat.json; exit 1; }
 PN2HIP_LIB=$B/libpn2hip_v_gqrows.so timeout -k 10 120 python3 tools/bench_msg_grid.py > $OUT/msg_grid_rows.json 2>&1 || { tail -20 $OUT/msg_grid_rows.json; exit 1; }
@@ -31,3 +31,6 @@ timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/trace_cfg
 T=$(find $OUT/trace_cfg2 -name "*kernel_trace.csv" | head -1)
 python3 tools/critical_path.py $T --out $OUT/critical_path_cfg2.txt | head -8
 python3 tools/lane_report.py $T > $OUT/lanes_cfg2.txt; head -30 $OUT/lanes_cfg2.txt
+timeout -k 10 120 python3 tools/bench_chain.py > $OUT/chain_wc1.json 2>&1 || { tail -20 $OUT/chain_wc1.json; exit 1; }
+PN2HIP_LIB=$B/libpn2hip_v_wc0.so timeout -k 10 120 python3 tools/bench_chain.py > $OUT/chain_wc0.json 2>&1 || { tail -20 $OUT/chain_wc0.json; exit 1; }
+cat $OUT/chain_wc1.json $OUT/chain_wc0.json

@@ -35,4 +35,10 @@ for m in npts:
 for i, m in enumerate(npts):
     res[f"stage{i + 1}_us"] = timeit(lambda i=i, m=m: ts.farthest_point_sample_and_gather(m, ins[i]))
 res["stages_sum_us"] = sum(res[f"stage{i + 1}_us"] for i in range(4))
+# what the pipelined step launches on its chain lane: SA2..SA4's samplers fused (fps234)
+res["tail_234_us"] = timeit(lambda: ts.farthest_point_sample_chain(npts[1:], ins[1]))
+# index-exact against the stage-by-stage samplers
+for (i_, x_), m, src in zip(ts.farthest_point_sample_chain(npts[1:], ins[1]), npts[1:], ins[1:]):
+    ri, rx = ts.farthest_point_sample_and_gather(m, src)
+    assert torch.equal(i_, ri) and torch.equal(x_, rx), "fused tail differs from the stages"
 print(json.dumps({k: round(v, 1) for k, v in res.items()}))
