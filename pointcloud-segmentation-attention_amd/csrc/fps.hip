@@ -157,7 +157,10 @@ int take_fault() {
 // fused kernel's SA1 loop ran ~4% behind the same loop in its own kernel, more than the
 // launch it saved -- profiles/r1/chain_split.log.)
 constexpr int kChainMax = 4;
-constexpr int kChainBlock = 256;
+#ifndef PN2_CHAIN_BLOCK  // A/B: threads of the chain workgroup (its 1024-point stage: 1024 / BLOCK per lane)
+#define PN2_CHAIN_BLOCK 256
+#endif
+constexpr int kChainBlock = PN2_CHAIN_BLOCK;
 constexpr int kChainNext = 1024;  // points per fused stage (LDS: input copy + 2 hand-over arrays)
 
 struct FpsChain {
@@ -176,6 +179,10 @@ PN2_DEV void chain_stage(const float* P, int N, int M, const float* CXYZ, int32_
   else if (N <= 128) { if (w0) fps_v9_body<64, 2, 2>(P, N, M, CXYZ, I, NX, SNEXT, red); }
   else if (N <= 256) { if (w0) fps_v9_body<64, 4, 4, false, true, false, -1, WC>(P, N, M, CXYZ, I, NX, SNEXT, red, wslot); }
   else if (N <= 512) { if (w0) fps_v9_body<64, 8, 4, false, true, false, -1, WC>(P, N, M, CXYZ, I, NX, SNEXT, red, wslot); }
+  else if constexpr (kChainBlock == 128)
+    fps_v9_body<128, 8, 4, false, true, false, -1, WC>(P, N, M, CXYZ, I, NX, SNEXT, red, wslot);
+  else if constexpr (kChainBlock == 512)
+    fps_v9_body<512, 2, 2, false, true, false, -1, WC>(P, N, M, CXYZ, I, NX, SNEXT, red, wslot);
   else fps_v9_body<256, 4, 2, false, true, false, -1, WC>(P, N, M, CXYZ, I, NX, SNEXT, red, wslot);
 }
 

@@ -25,7 +25,13 @@ enum Layout : int {
 };
 
 constexpr int kBlock = 256;
-constexpr int kTileElems = 2048;  // output floats per workgroup tile
+#ifndef PN2_GC_TILE  // A/B knobs (tools/bench_group.py): output floats per workgroup tile,
+#define PN2_GC_TILE 2048  // elements whose gathers a thread has in flight before its stores
+#endif
+#ifndef PN2_GC_U
+#define PN2_GC_U 4
+#endif
+constexpr int kTileElems = PN2_GC_TILE;  // output floats per workgroup tile
 
 // Tile = `rows` consecutive output rows (rows*Cout <= max(kTileElems, Cout)).
 __global__ __launch_bounds__(kBlock) void group_concat_kernel(
@@ -36,7 +42,7 @@ __global__ __launch_bounds__(kBlock) void group_concat_kernel(
   // the tile's neighbour indices are staged in LDS first (one coalesced load per row), and a
   // thread then issues the gathers of kU elements before it stores any: one element at a time
   // made each element two dependent memory trips (idx, then the gather), latency-bound
-  constexpr int kU = 4;
+  constexpr int kU = PN2_GC_U;
   __shared__ int s_idx[kTileElems];
   // XCD-aware order (common.h): each XCD takes a contiguous range of tiles, so the rows of a
   // cloud's xyz / points are fetched into one L2, not into all eight

@@ -34,3 +34,12 @@ python3 tools/lane_report.py $T > $OUT/lanes_cfg2.txt; head -30 $OUT/lanes_cfg2.
 timeout -k 10 120 python3 tools/bench_chain.py > $OUT/chain_wc1.json 2>&1 || { tail -20 $OUT/chain_wc1.json; exit 1; }
 PN2HIP_LIB=$B/libpn2hip_v_wc0.so timeout -k 10 120 python3 tools/bench_chain.py > $OUT/chain_wc0.json 2>&1 || { tail -20 $OUT/chain_wc0.json; exit 1; }
 cat $OUT/chain_wc1.json $OUT/chain_wc0.json
+for v in cb128 cb512; do
+  PN2HIP_LIB=$B/libpn2hip_v_$v.so timeout -k 10 120 python3 tools/bench_chain.py > $OUT/chain_$v.json 2>&1 || { tail -20 $OUT/chain_$v.json; exit 1; }
+  echo $v; cat $OUT/chain_$v.json
+done
+for v in main gcu8 gcu8t4k gcu16t4k; do
+  L=""; [ $v != main ] && L=$B/libpn2hip_v_$v.so
+  PN2HIP_LIB=$L timeout -k 10 120 python3 tools/bench_group.py > $OUT/group_$v.json 2>&1 || { tail -20 $OUT/group_$v.json; exit 1; }
+  echo $v; cat $OUT/group_$v.json
+done
