@@ -522,6 +522,18 @@ class Step:
                 v["bq"][(i, r)] = idx
             return f
 
+        def grp_all(i):
+            # every radius of a level whose input fits the multi-layer kernel (N <= 1024: SA2)
+            # as ONE launch (pn2_ball_group_layers, MSG [points, xyz] order)
+            def f():
+                points = inp["sa_out"][0]
+                specs = [(MSG_SA[i][1][r], MSG_SA[i][2][r], v["xyz"][i], points, v["xyz"][i + 1])
+                         for r in range(len(MSG_SA[i][1]))]
+                for r, (idx, _, new_points) in enumerate(
+                        pointnet_util.ball_group_layers(specs, xyz_last=True)):
+                    v["bq"][(i, r)], v["gp"][(i, r)] = idx, new_points
+            return f
+
         for i in range(len(MSG_SA)):
             # lane 0: SA1's sampler only; the later samplers run on lane 3 after it; radius 0's
             # grouping on lane 1, the other radii on lane 2
@@ -532,6 +544,10 @@ class Step:
                 chain_lane = 4 if self.chain_lane < 0 else self.chain_lane  # after the radii
                 tasks.append(Task(f"fps{i + 1}", chain_lane, (f"fps{i}",), fps(i), direct=True,
                                   chain=spec))
+            if i > 0 and MSG_SA[i - 1][0] <= pointnet_util.BALL_GROUP_MAX_POINTS \
+                    and max(MSG_SA[i][2]) <= pointnet_util.BALL_GROUP_MAX_NSAMPLE:
+                tasks.append(Task(f"sa{i + 1}", 2, (f"fps{i + 1}",), grp_all(i)))
+                continue
             for r in range(len(MSG_SA[i][1])):
                 # radius r on lane 1 + r when lane 3 is free (chain_lane 0), else radius 0 on
                 # lane 1 and the others on lane 2
