@@ -46,6 +46,10 @@ constexpr int kSgMaxQpb = 64;   // queries per workgroup
 #ifndef PN2_SG_U  // elements whose gathers are in flight per thread before its stores
 #define PN2_SG_U 4
 #endif
+#ifndef PN2_SG_VEC  // A/B: the vector write phase (ball_group_layers_kernel, below)
+#define PN2_SG_VEC 0
+#endif
+constexpr int kSgVecFloats = 4096;  // the vector write phase's LDS staging chunk (16 KB)
 #ifndef PN2_SG_TILE_KB
 #define PN2_SG_TILE_KB 32
 #endif
@@ -67,8 +71,9 @@ struct SgLayer {
   float* out;
   int N, C, M, ns, Cout, layout, qpb, tiles;  // workgroups per cloud = tiles * parts
   int parts, chunk;  // a query split over `parts` workgroups of `chunk` elements each
+  int vec;           // the vector write phase applies (PN2_SG_VEC builds; host-checked)
   float thresh;
-  FastDiv div_cout, div_ns;
+  FastDiv div_cout, div_ns, div_c4;
 };
 
 struct SgArgs {
@@ -95,6 +100,7 @@ __global__ __launch_bounds__(kSgBlock) void ball_group_layers_kernel(SgArgs a) {
   __shared__ float sx[kSgCap], sy[kSgCap], sz[kSgCap];
   __shared__ int s_hit[kSgHits];          // the tile's rows: query qi's hits at qi*ns ..
   __shared__ float s_q[3 * kSgMaxQpb];    // the tile's query centres
+  __shared__ float4 s_out4[PN2_SG_VEC ? kSgVecFloats / 4 : 1];  // vector phase: chunk image
   // logical blocks cloud-major: cloud b's blocks of every layer are one contiguous range, so
   // the XCD-aware order gives each XCD whole clouds (their rows in one L2) and every XCD the
   // same mix of layers
@@ -170,6 +176,66 @@ __global__ __launch_bounds__(kSgBlock) void ball_group_layers_kernel(SgArgs a) {
   float* __restrict__ O = g.out + r_base * Cout;
   float* __restrict__ GX = g.grouped_xyz ? g.grouped_xyz + r_base * 3 : nullptr;
   const float* __restrict__ F = g.points ? g.points + (size_t)b * N * C : nullptr;
+  if constexpr (PN2_SG_VEC) {
+    if (g.vec) {
+      // ---- phase 2, vector form: the tile's rows go out in chunks of CH rows through LDS.
+      // Feature columns are gathered as float4 (a points row is 16-B aligned: C % 4 == 0) and
+      // the xyz columns computed from the LDS cloud copy, both into the chunk's row-major
+      // image; then the chunk leaves as aligned float4 stores (CH, the tile's first row and
+      // ns are multiples of 4, so every chunk starts on a 16-B boundary of the output). One
+      // gather round trip per chunk instead of one per four elements of each thread.
+      float* s_out = reinterpret_cast<float*>(s_out4);
+      const int C4 = C >> 2;
+      const int foff = layout == PN2_SG_XYZ_FIRST ? 3 : 0;  // first feature column
+      const int xoff = layout == PN2_SG_XYZ_LAST ? C : 0;   // first xyz column
+      const bool has_xyz = layout != PN2_SG_POINTS_ONLY;
+      const int CH = (kSgVecFloats / Cout) & ~3;  // >= 4 (host: Cout <= kSgVecFloats / 4)
+      const int R = nq * ns;
+      const float4* __restrict__ F4 = reinterpret_cast<const float4*>(F);
+      for (int c0 = 0; c0 < R; c0 += CH) {
+        const int nr = min(CH, R - c0);
+        const int nf = nr * C4;
+        constexpr int UV = 4;
+        for (int f0 = t; f0 < nf; f0 += kSgBlock * UV) {
+          float4 v[UV];
+          int dst[UV];
+#pragma unroll
+          for (int u = 0; u < UV; ++u) {
+            const int f = min(f0 + u * kSgBlock, nf - 1);  // (a surplus lane reloads the last)
+            const int rr = (int)fdiv((uint32_t)f, g.div_c4);
+            const int cc = f - rr * C4;
+            v[u] = F4[(size_t)s_hit[c0 + rr] * C4 + cc];
+            dst[u] = rr * Cout + foff + 4 * cc;
+          }
+#pragma unroll
+          for (int u = 0; u < UV; ++u) {
+            if (f0 + u * kSgBlock < nf) {
+              s_out[dst[u]] = v[u].x;
+              s_out[dst[u] + 1] = v[u].y;
+              s_out[dst[u] + 2] = v[u].z;
+              s_out[dst[u] + 3] = v[u].w;
+            }
+          }
+        }
+        if (has_xyz) {
+          for (int e = t; e < nr * 3; e += kSgBlock) {
+            const int rr = e / 3, cx = e - 3 * rr;
+            const int r = c0 + rr;
+            const int qi = (int)fdiv((uint32_t)r, g.div_ns);
+            const int i = s_hit[r];
+            const float sv = cx == 0 ? sx[i] : (cx == 1 ? sy[i] : sz[i]);
+            s_out[rr * Cout + xoff + cx] = sv - s_q[3 * qi + cx];  // pointnet_util.py:40
+          }
+        }
+        __syncthreads();
+        float4* __restrict__ O4 = reinterpret_cast<float4*>(O + (size_t)c0 * Cout);
+        const int n4 = (nr * Cout) >> 2;  // nr % 4 == 0
+        for (int k = t; k < n4; k += kSgBlock) O4[k] = s_out4[k];
+        __syncthreads();  // the image is free for the next chunk
+      }
+      return;
+    }
+  }
   // this workgroup's elements of the tile: all, or part `part` of a split query
   const int e_beg = part * g.chunk;
   const int E = PN2_SG_SKIP == 2 ? 0 : min(nq * ns * Cout, e_beg + g.chunk);
@@ -273,6 +339,13 @@ int pn2_ball_group_layers(const pn2_sa_layer* layers, int nlayers, int B, pn2_st
     g.qpb = (int)qpb;
     g.div_ns = pn2::make_fastdiv((uint32_t)s.nsample);
     g.tiles = s.M > 0 ? (int)((s.M + qpb - 1) / qpb) : 0;
+    // the vector write phase (PN2_SG_VEC builds): float4 feature rows, whole queries per
+    // workgroup, 16-B aligned buffers, ns % 4 == 0 (chunks start on 16-B boundaries), no
+    // grouped_xyz output, at least 4 rows per LDS chunk
+    g.div_c4 = pn2::make_fastdiv((uint32_t)(s.C / 4 > 0 ? s.C / 4 : 1));
+    g.vec = PN2_SG_VEC && layout != PN2_SG_XYZ_ONLY && s.C % 4 == 0 && s.nsample % 4 == 0 &&
+            g.parts == 1 && !s.grouped_xyz && 4 * Cout <= pn2::kSgVecFloats &&
+            (((uintptr_t)s.points | (uintptr_t)s.new_points) & 15) == 0;
     a.first[i] = (int)blocks;
     blocks += (long long)g.tiles * g.parts;  // per cloud
     if (blocks * B >= (1LL << 31) - 8) return PN2_EINVAL;

@@ -13,7 +13,9 @@ tail -1 $OUT/pytest.log
 timeout -k 10 120 python3 tools/bench_msg_grid.py > $OUT/msg_grid_flat.json 2>&1 || { tail -20 $OUT/msg_grid_flat.json; exit 1; }
 PN2HIP_LIB=$B/libpn2hip_v_gqrows.so timeout -k 10 120 python3 tools/bench_msg_grid.py > $OUT/msg_grid_rows.json 2>&1 || { tail -20 $OUT/msg_grid_rows.json; exit 1; }
 paste $OUT/msg_grid_flat.json $OUT/msg_grid_rows.json
-for v in main u8 u16; do
+PN2HIP_LIB=$B/libpn2hip_sg_vec.so timeout -k 10 300 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_fused_layers.py -k ball_group_layers > $OUT/pytest_sgvec.log 2>&1 || { tail -30 $OUT/pytest_sgvec.log; exit 1; }
+tail -1 $OUT/pytest_sgvec.log
+for v in main u8 u16 vec vecu8; do
   L=""; [ $v != main ] && L=$B/libpn2hip_sg_$v.so
   PN2HIP_LIB=$L timeout -k 10 120 python3 tools/bench_layers.py > $OUT/layers_$v.json 2>&1 || { tail -20 $OUT/layers_$v.json; exit 1; }
   echo $v; cat $OUT/layers_$v.json
