@@ -349,7 +349,7 @@ def main():
     ap.add_argument("--side-layout", choices=["a", "b", "c", "d"], default=None,
                     help="side-lane layout with several sampler streams (stack.side_layout; "
                          "default: the config's LAYOUTS entry)")
-    ap.add_argument("--chain", choices=["own", "behind"], default=None,
+    ap.add_argument("--chain", choices=["own", "own2", "behind"], default=None,
                     help="with several sampler streams: the later samplers (SA2.. chain) on a "
                          "stream of their own or behind SA1 on its sampler stream (default: the "
                          "config's LAYOUTS entry)")
@@ -485,7 +485,9 @@ def main():
                                       private_streams=model or args.private_side,
                                       native_plan=not args.no_native_plan,
                                       only=args.diag_only, layout=args.side_layout,
-                                      chain_own=args.chain == "own", set_inputs=set_inputs)
+                                      chain_own=args.chain in ("own", "own2"),
+                                      chain_streams=2 if args.chain == "own2" else 1,
+                                      set_inputs=set_inputs)
         else:
             step = pkg.stack.Step(inp, overlap=overlap)
             graph = None if args.eager else pkg.stack.GraphStep(inp, overlap=overlap)
@@ -628,7 +630,9 @@ def main():
                        "streams": (("SA1 sampler + 3 side streams" if args.sampler_lanes <= 1 or args.model
                                     else f"{args.sampler_lanes} sampler streams (consecutive steps' "
                                     f"samplers concurrent; SA2.. samplers "
-                                    + ("on their own stream" if args.chain == "own" else "behind SA1")
+                                    + ({"own": "on their own stream", "own2": "on two streams of "
+                                        "their own, alternating by buffer set"}.get(args.chain,
+                                                                                 "behind SA1"))
                                     + ") + side streams "
                                     f"(layout {args.side_layout})"
                                     + (" per buffer set" if args.private_side else ""))

@@ -294,8 +294,10 @@ class Step:
         attn_lane = 3 if (multi and "attn" in inp) else None
         lane = side_layout(multi, attn_lane is not None, self.layout)
         chain_lane = self.chain_lane
-        if chain_lane < 0:  # the later samplers on a lane after every side lane
-            chain_lane = 1 + max([2] + list(lane.values()) + ([attn_lane] if attn_lane else []))
+        if chain_lane < 0:  # the later samplers on a lane after every side lane (-1: the
+            # first such lane, -2: the second, ... -- Pipeline's chain_streams)
+            chain_lane = max([2] + list(lane.values()) + ([attn_lane] if attn_lane else [])) \
+                - chain_lane
         tasks = []
         if big:  # the SA1 grid over the input cloud (also orders FP4's neighbour search)
             tasks.append(Task("grid1", 1, (), lambda: v.__setitem__(
@@ -541,7 +543,7 @@ class Step:
             if i == 0:
                 tasks.append(Task("fps1", 0, (), fps(0), direct=True, chain=spec))
             else:
-                chain_lane = 4 if self.chain_lane < 0 else self.chain_lane  # after the radii
+                chain_lane = 3 - self.chain_lane if self.chain_lane < 0 else self.chain_lane  # after the radii
                 tasks.append(Task(f"fps{i + 1}", chain_lane, (f"fps{i}",), fps(i), direct=True,
                                   chain=spec))
             if i > 0 and MSG_SA[i - 1][0] <= pointnet_util.BALL_GROUP_MAX_POINTS \
@@ -889,7 +891,10 @@ class Pipeline:
 
     def __init__(self, inp, graphs=True, overlap=True, nsets=3, private_streams=False,
                  sampler_lanes=1, native_plan=True, only=None, layout="a", chain_own=False,
-                 set_inputs=None):
+                 set_inputs=None, chain_streams=1):
+        # chain_streams (with chain_own): the later samplers of set i run on chain stream
+        # i % chain_streams, so consecutive steps' chains can overlap (one shared chain stream
+        # runs one chain per step back to back: its launch time bounds the step)
         # set_inputs: one make_inputs() dict per buffer set (distinct clouds per set: the
         # steps of a pipelined run then sample different clouds); None = every set reads `inp`
         # private_streams: every buffer set gets its own side streams, so the side lanes of
@@ -933,11 +938,13 @@ class Pipeline:
         if set_inputs is not None and len(set_inputs) != nsets:
             raise ValueError(f"set_inputs: {len(set_inputs)} input dicts for {nsets} sets")
         inps = list(set_inputs) if set_inputs is not None else [inp] * nsets
+        cl = (lambda i: chain_lane - (i % max(1, chain_streams)) if chain_lane < 0
+              else chain_lane)
         mk = (lambda i: GraphStep(inps[i], overlap=overlap, streams=streams(i),
-                                  chain_lane=chain_lane, segments=self.native_plan, only=only,
+                                  chain_lane=cl(i), segments=self.native_plan, only=only,
                                   layout=layout)) \
             if graphs else (lambda i: Step(inps[i], overlap=overlap, streams=streams(i),
-                                           chain_lane=chain_lane, layout=layout))
+                                           chain_lane=cl(i), layout=layout))
         self.sets = [mk(i) for i in range(nsets)]
         self.inputs = inps
         self.k = 0

@@ -47,11 +47,14 @@ def test_ssg_side_lanes_are_three_segments():
 @pytest.mark.parametrize("config,layout,want", [("cfg2", "b", 4), ("cfg2", "a", 3),
                                                  ("cfg3", "a", 4), ("cfg2", "d", 5),
                                                  ("cfg5", "a", 4)])
-def test_chain_own_lane_follows_the_side_lanes(config, layout, want):
+@pytest.mark.parametrize("nth", [1, 2])
+def test_chain_own_lane_follows_the_side_lanes(config, layout, want, nth):
     """chain_lane -1 (bench.py --chain own): the later samplers get the lane after every side
-    lane, and nothing else runs there."""
+    lane, and nothing else runs there; -2 (the second chain stream of --chain own2) the lane
+    after that."""
+    want += nth - 1
     inp = pkg.stack.make_inputs(config, [0], "cpu")
-    step = pkg.stack.Step(inp, overlap=True, chain_lane=-1, layout=layout)
+    step = pkg.stack.Step(inp, overlap=True, chain_lane=-nth, layout=layout)
     step.overlap = True
     step.tasks = step._tasks_ssg() if step.kind == "ssg" else step._tasks_msg()
     chain = [t for t in step.tasks if t.direct and t.name != "fps1"]
