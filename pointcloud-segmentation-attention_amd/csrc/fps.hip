@@ -174,7 +174,7 @@ struct FpsChain {
 PN2_DEV void chain_stage(const float* P, int N, int M, const float* CXYZ, int32_t* I, float* NX,
                          float* SNEXT, uint2 (*red)[8], FpsSlot (*wslot)[8]) {
   const bool w0 = threadIdx.x < kWave;
-  constexpr bool WC = PN2_FPS_WCOORD;  // winner coordinates carried (fps_kernels.h)
+  constexpr bool WC = PN2_FPS_WCOORD;  // winner coordinates carried (fps_kernels.h; <= 8 slots)
   if (N <= 64) { if (w0) fps_v9_body<64, 1, 1>(P, N, M, CXYZ, I, NX, SNEXT, red); }
   else if (N <= 128) { if (w0) fps_v9_body<64, 2, 2>(P, N, M, CXYZ, I, NX, SNEXT, red); }
   else if (N <= 256) { if (w0) fps_v9_body<64, 4, 4, false, true, false, -1, WC>(P, N, M, CXYZ, I, NX, SNEXT, red, wslot); }

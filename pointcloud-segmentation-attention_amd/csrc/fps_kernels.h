@@ -336,7 +336,8 @@ template <int BLOCK, int PPT, int G, bool XYZ_LDS, bool STAMP = false, bool LRES
 __global__ __launch_bounds__(BLOCK) void fps_v9_kernel(const float* __restrict__ xyz, int N,
                                                        int M, int32_t* __restrict__ idx,
                                                        float* __restrict__ new_xyz) {
-  constexpr bool WC = PN2_FPS_WCOORD && LRES && !ATOM;
+  // (the per-lane select costs 3 VALU per slot: only for a few slots per lane)
+  constexpr bool WC = PN2_FPS_WCOORD && LRES && !ATOM && PPT <= 8;
   __shared__ uint2 red[2][8];
   __shared__ FpsSlot wslot[WC ? 2 : 1][8];
   __shared__ float sxyz[XYZ_LDS ? 3 * BLOCK * PPT : 1];

@@ -69,7 +69,7 @@ def test_verify_checker_catches_a_wrong_step(bench, config):
     if "attn" in inp:
         np_inp["attn"] = [tuple(t.numpy() for t in q) for q in inp["attn"]]
     ref, _, inter = O.run_stack_cpu(np_inp, config, intermediates=True)
-    T = lambda a: torch.from_numpy(np.array(a))  # noqa: E731
+    T = lambda a: torch.tensor(a.numpy() if torch.is_tensor(a) else a)  # noqa: E731
     good = bench.verify_sets(config, [(inp, [T(r) for r in ref],
                                        {k: T(v) for k, v in inter.items()})], 2)
     assert good["failures"] == [] and good["clouds"] == 1
