@@ -7,6 +7,20 @@ export TMPDIR=/tmp
 OUT=gpurun_out/r4/ab
 mkdir -p $OUT
 B=pointcloud-segmentation-attention_amd/csrc/build
+run() {  # name, bench args
+  n=$1; shift
+  timeout -k 10 300 python3 bench.py --no-cpu-baseline --e2e-steps 0 "$@" > $OUT/b_$n.json 2> $OUT/b_$n.err || { tail -20 $OUT/b_$n.err; exit 1; }
+  python3 -c "import json; d=json.load(open('$OUT/b_$n.json')); print('$n', round(d['value']), round(d['ms_per_step'],4), round(d['roofline']['avg_launch_ms'],4), d['verified'], d['latency_ms_per_batch'], d['host'])"
+}
+run default
+run cup64 --cu-partition 64
+run cup80 --cu-partition 80
+run cup96 --cu-partition 96
+run l4cup80 --sampler-lanes 4 --hw-queues 8 --sets 12 --cu-partition 80
+run own2cup80 --chain own2 --hw-queues 8 --cu-partition 80
+run drv_default --steps 20 --warmup 5
+run drv_cup64 --steps 20 --warmup 5 --cu-partition 64
+run drv_cup80 --steps 20 --warmup 5 --cu-partition 80
 PN2HIP_LIB=$B/libpn2hip_sg_vec.so timeout -k 10 300 python3 -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_fused_layers.py -k ball_group_layers > $OUT/pytest_sgvec.log 2>&1 || { tail -30 $OUT/pytest_sgvec.log; exit 1; }
 tail -1 $OUT/pytest_sgvec.log
 timeout -k 10 120 python3 tools/bench_msg_grid.py > $OUT/msg_grid_flat.json 2>&1 || { tail -20 $OUT/msg_grid_flat.json; exit 1; }
@@ -27,15 +41,3 @@ for v in main gcu8 gcu8t4k gcu16t4k; do
   PN2HIP_LIB=$L timeout -k 10 120 python3 tools/bench_group.py > $OUT/group_$v.json 2>&1 || { tail -20 $OUT/group_$v.json; exit 1; }
   echo $v; tail -1 $OUT/group_$v.json
 done
-run() {  # name, bench args
-  n=$1; shift
-  timeout -k 10 300 python3 bench.py --no-cpu-baseline --e2e-steps 0 "$@" > $OUT/b_$n.json 2> $OUT/b_$n.err || { tail -20 $OUT/b_$n.err; exit 1; }
-  python3 -c "import json; d=json.load(open('$OUT/b_$n.json')); print('$n', round(d['value']), round(d['ms_per_step'],4), round(d['roofline']['avg_launch_ms'],4), d['verified'], d['latency_ms_per_batch'], d['host'])"
-}
-run default
-run own2 --chain own2 --hw-queues 8
-run l4 --sampler-lanes 4 --hw-queues 8 --sets 12
-run l4own2 --sampler-lanes 4 --chain own2 --hw-queues 9 --sets 12
-run drv_default --steps 20 --warmup 5
-run drv_own2 --steps 20 --warmup 5 --chain own2 --hw-queues 8
-run drv_l4 --steps 20 --warmup 5 --sampler-lanes 4 --hw-queues 8 --sets 12
