@@ -375,6 +375,10 @@ def main():
     ap.add_argument("--hw-queues", type=int, default=None,
                     help="GPU_MAX_HW_QUEUES for this process (default: the environment's, else "
                          f"{DEFAULT_HW_QUEUES}; <= 32)")
+    ap.add_argument("--sampler-priority", choices=["default", "high"], default=None,
+                    help="stream priority of every sampler stream (lane 0, the extra sampler "
+                         "streams, the later samplers' own stream); default: the config's "
+                         "LAYOUTS entry")
     ap.add_argument("--lane0-priority", choices=["auto", "default", "high"], default="auto",
                     help="stream priority of lane 0 (the SA1 sampler chain); auto = default "
                          "for the geometric step, high for the whole model")
@@ -411,6 +415,8 @@ def main():
         args.chain = lay["chain"]
     if args.cu_partition is None:
         args.cu_partition = 0 if args.model else lay.get("cu", 0)
+    if args.sampler_priority is None:
+        args.sampler_priority = lay.get("prio", "default")
     if args.hw_queues is None and not args.model and args.sampler_lanes == lay["lanes"]:
         args.hw_queues = lay["queues"]  # one queue per stream (the box's default is 4)
     if args.hw_queues is not None:
@@ -454,7 +460,7 @@ def main():
     def measure(model, steps, warmup):
         prio = args.lane0_priority
         if prio == "auto":
-            prio = "high" if model else "default"
+            prio = "high" if (model or args.sampler_priority == "high") else "default"
         lane0 = (torch.cuda.Stream(device=dev, priority=-1) if prio == "high"
                  else torch.cuda.current_stream(dev))
         with torch.cuda.stream(lane0):
@@ -480,6 +486,7 @@ def main():
                 # CU-masked sampler and side streams (stack.set_cu_partition), before any
                 # stream of the pipeline exists
                 pkg.stack.set_cu_partition(dev, args.cu_partition)
+                pkg.stack.set_sampler_priority(dev, args.sampler_priority == "high")
             pipe = pkg.stack.Pipeline(inp, graphs=not args.eager, nsets=args.sets,
                                       sampler_lanes=1 if model else args.sampler_lanes,
                                       private_streams=model or args.private_side,
@@ -627,6 +634,7 @@ def main():
                                         "the others" if args.cu_partition and not args.model
                                         and args.sampler_lanes > 1 else "none"),
                        "lane0_priority": prio0,
+                       "sampler_priority": args.sampler_priority,
                        "streams": (("SA1 sampler + 3 side streams" if args.sampler_lanes <= 1 or args.model
                                     else f"{args.sampler_lanes} sampler streams (consecutive steps' "
                                     f"samplers concurrent; SA2.. samplers "

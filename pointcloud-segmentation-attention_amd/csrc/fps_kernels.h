@@ -103,8 +103,8 @@ struct Lay9 {
 // beside the wave max, the wave winner's come out of v_readlane, and with several waves they
 // ride in the LDS slot next to (max, index) -- one LDS round trip less on the pick's
 // dependency chain. The coordinates are the same floats (loaded from CXYZ at setup).
-#ifndef PN2_FPS_WCOORD
-#define PN2_FPS_WCOORD 1
+#ifndef PN2_FPS_WCOORD  // measured: no gain standalone, the fused SA2-4 chain 126 -> 156 us: off
+#define PN2_FPS_WCOORD 0
 #endif
 struct FpsSlot {  // one wave's published winner (WC): max, index, coordinates
   uint32_t km, k;

@@ -31,6 +31,11 @@ constexpr int kBuildBlock = 1024;
 #ifndef PN2_GQ_FLAT
 #define PN2_GQ_FLAT 1
 #endif
+// rows of at least this many points on average are walked one by one (tools/bench_msg_grid.py:
+// the flattened walk won on short rows, lost at r = 0.4 on r-sized cells)
+#ifndef PN2_GQ_LONG_ROWS
+#define PN2_GQ_LONG_ROWS 24
+#endif
 constexpr int kMaxBitWords = 4096;  // bitmask words per wave (N <= 131072)
 constexpr float kAutoPointsPerCell = 2.0f;
 
@@ -292,6 +297,22 @@ __global__ __launch_bounds__(BLOCK) void ball_query_grid_kernel(
       const int incl = wave_incl_scan(len, lane);
       const int total = __builtin_amdgcn_readlane(incl, kWave - 1);
       const int excl = incl - len;
+      const int nr = min(kWave, nrows - r0);
+      if (total >= PN2_GQ_LONG_ROWS * nr) {
+        // long rows (a large radius over small cells): row by row, offsets already in hand
+        for (int j = 0; j < nr; ++j) {
+          const int bj = __builtin_amdgcn_readlane(beg, j);
+          const int lj = __builtin_amdgcn_readlane(len, j);
+          for (int i = lane; i < lj; i += kWave) {
+            const float4 p = pts[bj + i];
+            if (sqdist(qx, qy, qz, p.x, p.y, p.z) < thresh) {  // tf_grouping_g.cu:24-25
+              const int k = __float_as_int(p.w);
+              atomicOr(&mine[k >> 5], 1u << (k & 31));
+            }
+          }
+        }
+        continue;
+      }
       for (int i0 = 0; i0 < total; i0 += kWave) {
         // the rows overlapping [i0, i0 + 64): each lane takes the last one starting at or
         // before its position (empty rows never qualify)

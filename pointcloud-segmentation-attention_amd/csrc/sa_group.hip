@@ -46,8 +46,8 @@ constexpr int kSgMaxQpb = 64;   // queries per workgroup
 #ifndef PN2_SG_U  // elements whose gathers are in flight per thread before its stores
 #define PN2_SG_U 4
 #endif
-#ifndef PN2_SG_VEC  // A/B: the vector write phase (ball_group_layers_kernel, below)
-#define PN2_SG_VEC 0
+#ifndef PN2_SG_VEC  // the vector write phase (ball_group_layers_kernel, below); 0 = A/B off
+#define PN2_SG_VEC 1
 #endif
 constexpr int kSgVecFloats = 4096;  // the vector write phase's LDS staging chunk (16 KB)
 #ifndef PN2_SG_TILE_KB
@@ -190,10 +190,14 @@ __global__ __launch_bounds__(kSgBlock) void ball_group_layers_kernel(SgArgs a) {
       const int xoff = layout == PN2_SG_XYZ_LAST ? C : 0;   // first xyz column
       const bool has_xyz = layout != PN2_SG_POINTS_ONLY;
       const int CH = (kSgVecFloats / Cout) & ~3;  // >= 4 (host: Cout <= kSgVecFloats / 4)
+      // this workgroup's rows of the tile: all, or part `part` of a query split over
+      // g.parts workgroups (row ranges of a multiple of 4 rows)
       const int R = nq * ns;
+      const int RP = (((R + g.parts - 1) / g.parts) + 3) & ~3;
+      const int rbeg = part * RP, rend = min(R, rbeg + RP);
       const float4* __restrict__ F4 = reinterpret_cast<const float4*>(F);
-      for (int c0 = 0; c0 < R; c0 += CH) {
-        const int nr = min(CH, R - c0);
+      for (int c0 = rbeg; c0 < rend; c0 += CH) {
+        const int nr = min(CH, rend - c0);
         const int nf = nr * C4;
         constexpr int UV = 4;
         for (int f0 = t; f0 < nf; f0 += kSgBlock * UV) {
@@ -229,7 +233,7 @@ __global__ __launch_bounds__(kSgBlock) void ball_group_layers_kernel(SgArgs a) {
         }
         __syncthreads();
         float4* __restrict__ O4 = reinterpret_cast<float4*>(O + (size_t)c0 * Cout);
-        const int n4 = (nr * Cout) >> 2;  // nr % 4 == 0
+        const int n4 = (nr * Cout) >> 2;  // nr % 4 == 0 (R, RP and CH are multiples of 4)
         for (int k = t; k < n4; k += kSgBlock) O4[k] = s_out4[k];
         __syncthreads();  // the image is free for the next chunk
       }
@@ -344,7 +348,7 @@ int pn2_ball_group_layers(const pn2_sa_layer* layers, int nlayers, int B, pn2_st
     // grouped_xyz output, at least 4 rows per LDS chunk
     g.div_c4 = pn2::make_fastdiv((uint32_t)(s.C / 4 > 0 ? s.C / 4 : 1));
     g.vec = PN2_SG_VEC && layout != PN2_SG_XYZ_ONLY && s.C % 4 == 0 && s.nsample % 4 == 0 &&
-            g.parts == 1 && !s.grouped_xyz && 4 * Cout <= pn2::kSgVecFloats &&
+            !s.grouped_xyz && 4 * Cout <= pn2::kSgVecFloats &&
             (((uintptr_t)s.points | (uintptr_t)s.new_points) & 15) == 0;
     a.first[i] = (int)blocks;
     blocks += (long long)g.tiles * g.parts;  // per cloud

@@ -171,6 +171,21 @@ def _masked_stream(dev, part):
     return torch.cuda.ExternalStream(h.value, device=dev)
 
 
+_SAMPLER_PRIO = set()  # devices whose sampler streams are created with high priority
+
+
+def set_sampler_priority(dev, high=True):
+    """Streams created from now on for the samplers (Pipeline's extra sampler streams, the
+    later samplers' own lane) get high priority: when a CU drains, the dispatcher then
+    serves a waiting sampler workgroup (which needs a whole CU: 16 waves x 128 VGPRs, 150 KB
+    of LDS) before the side lanes' workgroups refill it."""
+    key = str(torch.device(dev))
+    if high:
+        _SAMPLER_PRIO.add(key)
+    else:
+        _SAMPLER_PRIO.discard(key)
+
+
 def side_stream(dev, lane, part="side"):
     """The process-wide side stream of `lane` on `dev`: every Step shares them, so the
     sampler chain (the current stream) and the side lanes stay on distinct hardware queues
@@ -179,7 +194,9 @@ def side_stream(dev, lane, part="side"):
     key = (str(dev), lane)
     if key not in _SIDE:
         masked = str(torch.device(dev)) in _CU_PART
-        _SIDE[key] = _masked_stream(dev, part) if masked else torch.cuda.Stream(device=dev)
+        prio = -1 if (part == "sampler" and str(torch.device(dev)) in _SAMPLER_PRIO) else 0
+        _SIDE[key] = _masked_stream(dev, part) if masked else \
+            torch.cuda.Stream(device=dev, priority=prio)
     return _SIDE[key]
 
 
