@@ -81,6 +81,8 @@ typedef void* pn2_stream_t; /* hipStream_t */
 #define PN2_FPS_AUTO 0           /* the library's choice by N (what pn2_fps* run)            */
 #define PN2_FPS_BLOCKSCAN 1      /* one block-wide argmax per pick (the v9 register sampler) */
 #define PN2_FPS_HOTCULL_K128 6   /* culled hot-set sampler with 128 hot entries, N <= 8192  */
+#define PN2_FPS_HOTCULL_LEAN 7   /* culled hot-set sampler, cloud left in L2 (~57 KB LDS), N <= 8192 */
+#define PN2_FPS_HOTCULL_LDS 8    /* culled hot-set sampler with the cloud's LDS copy, N <= 8192 */
 
 /* flags of pn2_group_concat / pn2_sample_and_group */
 #define PN2_USE_XYZ 1  /* concat the centred xyz with the grouped features (use_xyz=True)      */

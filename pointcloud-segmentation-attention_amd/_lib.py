@@ -19,6 +19,7 @@ PN2_EINVAL = -22
 PN2_EFAULT = -14
 PN2_FAULT_FPS_POLL = 1
 PN2_FPS_AUTO, PN2_FPS_BLOCKSCAN, PN2_FPS_HOTCULL_K128 = 0, 1, 6
+PN2_FPS_HOTCULL_LEAN, PN2_FPS_HOTCULL_LDS = 7, 8
 PN2_USE_XYZ = 1
 PN2_XYZ_LAST = 2
 POOL_MODES = {"max": 0, "avg": 1, "weighted_avg": 2, "max_and_avg": 3}

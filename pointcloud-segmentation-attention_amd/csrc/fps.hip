@@ -111,6 +111,9 @@ __global__ void gather_point_grad_kernel(const float* __restrict__ out_g,
 }
 
 constexpr int kMaxRegPoints = 1024 * 16;
+#ifndef PN2_FPS_LEAN  // AUTO at the SA1 size runs the lean-LDS culled sampler (fps_cull.h)
+#define PN2_FPS_LEAN 0
+#endif
 
 // ---- device fault word ------------------------------------------------------------------
 // A kernel that finds a broken invariant (the culled sampler's cold waves waiting past their
@@ -210,10 +213,13 @@ int fps_impl(const float* xyz, int B, int N, int M, int32_t* idx, float* nx, voi
   if (B < 0 || N < 0 || M <= 0 || (B > 0 && (!xyz || !idx))) return PN2_EINVAL;
   // schedules other than AUTO exist only where the culled sampler runs (4096 < N <= 16384;
   // the 128-entry variant up to 8192 points)
-  if (sched != PN2_FPS_AUTO && sched != PN2_FPS_BLOCKSCAN && sched != PN2_FPS_HOTCULL_K128)
+  if (sched != PN2_FPS_AUTO && sched != PN2_FPS_BLOCKSCAN && sched != PN2_FPS_HOTCULL_K128 &&
+      sched != PN2_FPS_HOTCULL_LEAN && sched != PN2_FPS_HOTCULL_LDS)
     return PN2_EINVAL;
   if (sched != PN2_FPS_AUTO && (N <= 4096 || N > kMaxRegPoints)) return PN2_EINVAL;
-  if (sched == PN2_FPS_HOTCULL_K128 && N > 8192) return PN2_EINVAL;
+  if ((sched == PN2_FPS_HOTCULL_K128 || sched == PN2_FPS_HOTCULL_LEAN ||
+       sched == PN2_FPS_HOTCULL_LDS) && N > 8192)
+    return PN2_EINVAL;
   if (take && take_fault()) return PN2_EFAULT;
   if (B == 0) return PN2_OK;
   if (N == 0) {
@@ -234,10 +240,15 @@ int fps_impl(const float* xyz, int B, int N, int M, int32_t* idx, float* nx, voi
   else if (N <= 8192) {
     // culled hot-set sampler (fps_cull.h; 0.40 vs 0.71 ms at B = 16); the v9
     // block-scan sampler stays selectable for A/B timing and parity cross-checks
+    // (the lean-LDS form, PN2_FPS_HOTCULL_LEAN, leaves the cloud in L2 so the workgroup fits
+    // a CU that side-lane work partly occupies: fps_cull.h LEAN)
+    const bool lean = sched == PN2_FPS_HOTCULL_LEAN || (sched == PN2_FPS_AUTO && PN2_FPS_LEAN);
     if (sched == PN2_FPS_BLOCKSCAN)
       launch_v9<256, 32, 4, true, false, PN2_SA1_PAD>(xyz, B, N, M, idx, nx, s);
     else if (sched == PN2_FPS_HOTCULL_K128)
       launch_hotcull<16, 9, 3, 2>(xyz, B, N, M, idx, nx, fault_word_dev(), s);
+    else if (lean)
+      launch_hotcull<16, 9, 3, 4, 8192, 1, true>(xyz, B, N, M, idx, nx, fault_word_dev(), s);
     else
       launch_hotcull<16, 9, 3, 4>(xyz, B, N, M, idx, nx, fault_word_dev(), s);
   }

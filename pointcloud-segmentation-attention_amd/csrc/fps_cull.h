@@ -239,11 +239,18 @@ PN2_DEV void hot_update(int (&hv)[2 * HP], const hf2 (&hx)[HP], const hf2 (&hy)[
 #define PN2_FPS_POLL_LIMIT (1 << 22)
 #endif
 
-template <int NW, int PPT, int NPTS, bool STAMP = false, int PRIO = 0, int HQ = 2, int PPC = 1>
-__global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __restrict__ xyz, int N,
-                                                           int M, int32_t* __restrict__ idx,
-                                                           float* __restrict__ new_xyz,
-                                                           int* __restrict__ fault) {
+// LEAN (N <= 8192, one point per lane per cell): the cloud is NOT copied to LDS. Its
+// coordinates are read from global memory (L2) at setup, the cold lanes keep x, y, z of their
+// points in VGPRs, and a hot entry carries its point's coordinates (the hot wave reads no
+// coordinate at a round start); the batch buffer and the hot set live in the sort histogram's
+// LDS once the sort is done. ~53 KB of LDS instead of ~155 KB: with fewer VGPRs too
+// (fps_hotcull_lean_kernel), a CU that side-lane workgroups partly occupy can still take a
+// sampler workgroup (the 155 KB / 128-VGPR workgroup waits for a CU to drain completely).
+template <int NW, int PPT, int NPTS, bool STAMP = false, int PRIO = 0, int HQ = 2, int PPC = 1,
+          bool LEAN = false>
+__device__ __attribute__((always_inline)) inline void hotcull_body(
+    const float* __restrict__ xyz, int N, int M, int32_t* __restrict__ idx,
+    float* __restrict__ new_xyz, int* __restrict__ fault) {
   constexpr int BLOCK = 64 * NW;
   constexpr int NCW = NW - 1;  // cold waves
   constexpr int NCELL = NCW * PPT;
@@ -263,13 +270,21 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
 
   // the cloud's coordinates: an LDS copy when it fits beside the rest (NPTS <= 8192),
   // otherwise read from global memory (L2) -- only at setup and once per round
-  constexpr bool XYZ_LDS = NPTS <= 8192;
+  static_assert(!LEAN || (PPC == 1 && NPTS <= 8192), "LEAN: one point per lane per cell");
+  constexpr bool XYZ_LDS = NPTS <= 8192 && !LEAN;
   __shared__ __attribute__((aligned(16))) float sxyz[XYZ_LDS ? 3 * NPTS : 4];
   __shared__ int sperm[NPTS];         // sorted position -> point index
-  __shared__ uint32_t shist[NBK];     // bucket counts, then offsets
+  // bucket counts, then offsets; LEAN: then the batch buffer and the hot set (below)
+  constexpr int kLeanWords = (K + 1) * 4 + K * 4 + K;
+  __shared__ __attribute__((aligned(16))) uint32_t shist[LEAN && kLeanWords > NBK ? kLeanWords : NBK];
   __shared__ float4 scell[2 * NCELL]; // cell boxes (lo, hi)
-  __shared__ float4 scl[K + 1];       // centres of the current batch (x, y, z, idx)
-  __shared__ uint2 sh[K];             // hot entries (running min bits, point index)
+  __shared__ float4 scl_[LEAN ? 1 : K + 1];  // centres of the current batch (x, y, z, idx)
+  __shared__ uint2 sh_[LEAN ? 1 : K];        // hot entries (running min bits, point index)
+  float4* const scl = LEAN ? reinterpret_cast<float4*>(shist) : scl_;
+  uint2* const sh = sh_;
+  // LEAN hot entries: (running min bits, point index, x, y) and z
+  uint4* const shx = reinterpret_cast<uint4*>(shist) + (K + 1);
+  float* const shz = reinterpret_cast<float*>(shist) + (K + 1) * 4 + K * 4;
   __shared__ uint64_t swk[NW];        // per-wave (value + 1, ~key) of the exact argmax
   __shared__ float sbox[NW][8];
   __shared__ int swmax[NW];
@@ -278,7 +293,7 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
   // without the LDS copy (NPTS > 8192) the cold points' z coordinates live in the freed LDS
   // instead of VGPRs (at 16 waves the kernel is held to 128 VGPRs): lane-consecutive, so a
   // cold wave's read of one slot is conflict-free
-  constexpr bool ZLDS = !XYZ_LDS;
+  constexpr bool ZLDS = !XYZ_LDS && !LEAN;
   __shared__ float scz[ZLDS ? NCW * PPT * PPC * kWave : 1];
 
   const int b = blockIdx.x;
@@ -581,8 +596,15 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
               const uint64_t m = __builtin_amdgcn_ballot_w64(tb[e] > T);
               const uint32_t below = __builtin_amdgcn_mbcnt_hi(
                   (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-              if (tb[e] > T)
-                sh[base + (int)below] = make_uint2((uint32_t)tb[e], (uint32_t)sperm[spos(s, h)]);
+              if (tb[e] > T) {
+                if constexpr (LEAN) {
+                  shx[base + (int)below] = make_uint4((uint32_t)tb[e], (uint32_t)sperm[spos(s, h)],
+                                                      __float_as_uint(px[e]), __float_as_uint(py[e]));
+                  shz[base + (int)below] = pz[e];
+                } else {
+                  sh[base + (int)below] = make_uint2((uint32_t)tb[e], (uint32_t)sperm[spos(s, h)]);
+                }
+              }
               base += __builtin_popcountll(m);
             }
           }
@@ -652,12 +674,22 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
         static_assert(HQ == 2 || HQ == 4, "hot entries per lane");
         int hv[HQ], hk[HQ];
         uint32_t hkey[HQ];
+        float qx[HQ], qy[HQ], qz[HQ];  // LEAN: the entries' coordinates, carried in the set
 #pragma unroll
         for (int q = 0; q < HQ; ++q) {
           const int e = lane + q * kWave;
-          const uint2 en = e < nh ? sh[e] : make_uint2(0xFFFFFFFFu, 0u);
-          hv[q] = (int)en.x;
-          hk[q] = (int)en.y;
+          if constexpr (LEAN) {
+            const uint4 en = e < nh ? shx[e] : make_uint4(0xFFFFFFFFu, 0u, 0u, 0u);
+            qz[q] = e < nh ? shz[e] : 0.0f;
+            hv[q] = (int)en.x;
+            hk[q] = (int)en.y;
+            qx[q] = __uint_as_float(en.z);
+            qy[q] = __uint_as_float(en.w);
+          } else {
+            const uint2 en = e < nh ? sh[e] : make_uint2(0xFFFFFFFFu, 0u);
+            hv[q] = (int)en.x;
+            hk[q] = (int)en.y;
+          }
           hkey[q] = hv[q] >= 0 ? cull_key(hk[q]) : 0xFFFFFFFFu;
         }
         // a lane's entries in tie order (odd-even transposition sort by key): then a tournament
@@ -671,6 +703,11 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
               const uint32_t y = hkey[q];
               hv[q] = hv[q + 1]; hk[q] = hk[q + 1]; hkey[q] = hkey[q + 1];
               hv[q + 1] = v; hk[q + 1] = k; hkey[q + 1] = y;
+              if constexpr (LEAN) {
+                const float ax = qx[q], ay = qy[q], az = qz[q];
+                qx[q] = qx[q + 1]; qy[q] = qy[q + 1]; qz[q] = qz[q + 1];
+                qx[q + 1] = ax; qy[q + 1] = ay; qz[q + 1] = az;
+              }
             }
           }
         }
@@ -678,9 +715,9 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
         f2 hx[HP], hy[HP], hz[HP];
 #pragma unroll
         for (int q = 0; q < HQ; ++q) {
-          hx[q / 2][q % 2] = X[3 * hk[q]];
-          hy[q / 2][q % 2] = X[3 * hk[q] + 1];
-          hz[q / 2][q % 2] = X[3 * hk[q] + 2];
+          hx[q / 2][q % 2] = LEAN ? qx[q] : X[3 * hk[q]];
+          hy[q / 2][q % 2] = LEAN ? qy[q] : X[3 * hk[q] + 1];
+          hz[q / 2][q % 2] = LEAN ? qz[q] : X[3 * hk[q] + 2];
         }
         const int lim = min(K, M - j);
         int jj = 0;
@@ -903,11 +940,38 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
   }
 }
 
-template <int NW, int PPT, int PRIO = 0, int HQ = 2, int NPTS = 8192, int PPC = 1>
+template <int NW, int PPT, int NPTS, bool STAMP = false, int PRIO = 0, int HQ = 2, int PPC = 1,
+          bool LEAN = false>
+__global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __restrict__ xyz, int N,
+                                                           int M, int32_t* __restrict__ idx,
+                                                           float* __restrict__ new_xyz,
+                                                           int* __restrict__ fault) {
+  hotcull_body<NW, PPT, NPTS, STAMP, PRIO, HQ, PPC, LEAN>(xyz, N, M, idx, new_xyz, fault);
+}
+
+// The lean-LDS form held to PN2_FPS_LEAN_WPE waves per SIMD's worth of VGPRs (16 waves need 4
+// per SIMD; 5 leaves each SIMD ~100 VGPRs for a side-lane wave beside the sampler)
+#ifndef PN2_FPS_LEAN_WPE
+#define PN2_FPS_LEAN_WPE 4
+#endif
+template <int NW, int PPT, int NPTS, int PRIO, int HQ>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(PN2_FPS_LEAN_WPE)))
+void fps_hotcull_lean_kernel(const float* __restrict__ xyz, int N, int M,
+                             int32_t* __restrict__ idx, float* __restrict__ new_xyz,
+                             int* __restrict__ fault) {
+  hotcull_body<NW, PPT, NPTS, false, PRIO, HQ, 1, true>(xyz, N, M, idx, new_xyz, fault);
+}
+
+template <int NW, int PPT, int PRIO = 0, int HQ = 2, int NPTS = 8192, int PPC = 1,
+          bool LEAN = false>
 void launch_hotcull(const float* xyz, int B, int N, int M, int32_t* idx, float* nx, int* fault,
                     hipStream_t s) {
-  hipLaunchKernelGGL((fps_hotcull_kernel<NW, PPT, NPTS, false, PRIO, HQ, PPC>), dim3(B),
-                     dim3(64 * NW), 0, s, xyz, N, M, idx, nx, fault);
+  if constexpr (LEAN)
+    hipLaunchKernelGGL((fps_hotcull_lean_kernel<NW, PPT, NPTS, PRIO, HQ>), dim3(B), dim3(64 * NW),
+                       0, s, xyz, N, M, idx, nx, fault);
+  else
+    hipLaunchKernelGGL((fps_hotcull_kernel<NW, PPT, NPTS, false, PRIO, HQ, PPC>), dim3(B),
+                       dim3(64 * NW), 0, s, xyz, N, M, idx, nx, fault);
 }
 
 }  // namespace

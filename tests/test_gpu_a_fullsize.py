@@ -239,7 +239,8 @@ def _cloud(pkg, kind, B, N, seed=0):
 
 # SA1-size clouds (4096 < N <= 8192) run the culled hot-set sampler by default; every schedule
 # pn2_fps_gather_sched offers there (PN2_FPS_AUTO, PN2_FPS_BLOCKSCAN = the v9 block scan,
-# PN2_FPS_HOTCULL_K128 = the culled sampler with 128 hot entries) must give the oracle's
+# PN2_FPS_HOTCULL_K128 = the culled sampler with 128 hot entries, PN2_FPS_HOTCULL_LEAN = its
+# lean-LDS form, PN2_FPS_HOTCULL_LDS = its LDS-copy form) must give the oracle's
 # indices: ScanNet crops with duplicates, uniform, the integer lattice (exact ties everywhere),
 # npoint beyond the distinct points, npoint > N, tiny npoint, odd N.
 SAMPLER_CASES = [
@@ -269,7 +270,7 @@ def _sched(pkg, torch, x, M, sched):
 
 
 @pytest.mark.parametrize("sched,kind,B,N,M",
-                         [(s,) + c for s in (0, 1, 6) for c in SAMPLER_CASES]
+                         [(s,) + c for s in (0, 1, 6, 7, 8) for c in SAMPLER_CASES]
                          + [(s,) + c for s in (0, 1) for c in MSG_SAMPLER_CASES])
 def test_fps_sampler_schedules(env, sched, kind, B, N, M):
     pkg, O, torch, dev = env
@@ -291,6 +292,8 @@ def test_fps_schedule_rejections(env):
     L = pkg._lib
     x = torch.from_numpy(_cloud(pkg, "scannet", 1, 16384)).to(dev)
     assert _sched(pkg, torch, x, 64, L.PN2_FPS_HOTCULL_K128)[0] == L.PN2_EINVAL
+    assert _sched(pkg, torch, x, 64, L.PN2_FPS_HOTCULL_LEAN)[0] == L.PN2_EINVAL
+    assert _sched(pkg, torch, x, 64, L.PN2_FPS_HOTCULL_LDS)[0] == L.PN2_EINVAL
     assert _sched(pkg, torch, x[:, :4096].contiguous(), 64, L.PN2_FPS_BLOCKSCAN)[0] == L.PN2_EINVAL
     assert _sched(pkg, torch, x, 64, 5)[0] == L.PN2_EINVAL
     assert _sched(pkg, torch, x, 64, L.PN2_FPS_AUTO)[0] == 0
