@@ -39,7 +39,7 @@ SSG_SA_MLP = ((32, 32, 64), (64, 64, 128), (128, 128, 256), (256, 256, 512))
 SSG_FP_MLP = ((256, 256), (256, 256), (256, 128), (128, 128, 128))
 NUM_CLASSES = 21  # ScanNet (pointnet2_sem_seg_attention.py:17)
 # cell edge of the one grid that serves all of MSG SA1's radii (tools/bench_msg_grid.py)
-MSG_GRID_EDGE = 0.1
+MSG_GRID_EDGE = 0.2  # 105 us for the three radii vs 110 at 0.1, 122 at 0.4 (profiles/r4/ab2)
 
 NSIDE = 4  # side streams of the whole-model step (the geometric steps use 3)
 MAX_LANES = 8  # lanes of any step layout (0 = the sampler stream)
@@ -134,6 +134,9 @@ _SIDE = {}
 # and one event marks a step's end; otherwise every lane records its own end event and the
 # host waits for all of them (no wait packets on the side queues)
 LANE_JOIN = os.environ.get("PN2_LANE_JOIN") == "1"
+# SEG_MERGE (A/B, PN2_SEG_MERGE=1): a lane's consecutive tasks share one launch segment even
+# when a later task waits for another producer (the segment then waits for all of them first)
+SEG_MERGE = os.environ.get("PN2_SEG_MERGE") == "1"
 _CU_PART = {}  # device -> {"sampler": mask words, "side": mask words} (set_cu_partition)
 
 
@@ -692,8 +695,10 @@ class Step:
         earlier than a task would have, only later, so a consumer still cannot run before its
         producer -- and releases its tasks' events at its end. Returned in an order in which
         every segment comes after the segments it waits for and after the earlier segments of
-        its lane (the host enqueues waits after the records they refer to). On the SSG step
-        the side lanes become three segments: [grid1], [sa1..sa4], [fp4..fp1]."""
+        its lane (the host enqueues waits after the records they refer to). A task whose
+        cross-lane waits the open segment does not already imply starts a new segment, so no
+        task waits for a producer it does not need. On the SSG step the side lanes become
+        [grid1], [sa1], [sa2..sa4], [fp4], [fp3..fp1]."""
         lane_of = {t.name: (t.lane if self.overlap else 0) for t in self.tasks}
         xdeps = {t.name: any(t.name in u.deps and lane_of[u.name] != lane_of[t.name]
                              for u in self.tasks) for t in self.tasks}
@@ -701,6 +706,17 @@ class Step:
         # the whole-model step keeps one segment per task: its lane-1 chain of SA and FP
         # layers waits for each neighbour search separately, not for all of them up front
         merge = "model" not in self.inp
+        deps_of = {t.name: t.deps for t in self.tasks}
+
+        def closure(names):
+            seen, todo = set(), list(names)
+            while todo:
+                n = todo.pop()
+                if n not in seen:
+                    seen.add(n)
+                    todo.extend(deps_of.get(n, ()))
+            return seen
+        seg_waits = {}  # open segment's lane -> what its up-front waits already imply
         for t in self.tasks:
             lane = lane_of[t.name]
             if t.direct or not merge:
@@ -708,10 +724,19 @@ class Step:
                 segs.append([t])
                 continue
             cur = open_seg.get(lane)
+            xd = {d for d in t.deps if lane_of[d] != lane}
+            # a task that would add a wait to the open segment starts its own (unless
+            # PN2_SEG_MERGE=1, the round-3 rule): otherwise the segment's earlier tasks would
+            # wait for it too (SA1's grouping behind the later samplers' chain)
+            if cur is not None and not SEG_MERGE and not xd <= seg_waits[lane]:
+                del open_seg[lane]
+                cur = None
             if cur is None:
                 cur = open_seg[lane] = []
                 segs.append(cur)
+                seg_waits[lane] = set()
             cur.append(t)
+            seg_waits[lane] |= closure(xd)
             if xdeps[t.name]:
                 del open_seg[lane]
         seg_of = {t.name: i for i, seg in enumerate(segs) for t in seg}

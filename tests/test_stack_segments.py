@@ -36,12 +36,13 @@ def test_segments_respect_dependencies(config, chain_lane, layout):
         assert [n for n in names if n in order] == order
 
 
-def test_ssg_side_lanes_are_three_segments():
+def test_ssg_side_lane_segments():
     inp = pkg.stack.make_inputs("cfg2", [0], "cpu")
     step = pkg.stack.Step(inp, overlap=True, chain_lane=0)
     step.overlap = True
     keys = [pkg.stack.Step.segment_key(s) for s in step.segments()]
-    assert keys == ["grid1", "fps1", "fps234", "sa1+sa234", "fp4+fp123"]
+    # SA1's grouping waits for the SA1 sampler only, not for the later samplers' chain
+    assert keys == ["grid1", "fps1", "fps234", "sa1", "fp4", "sa234", "fp123"]
 
 
 @pytest.mark.parametrize("config,layout,want", [("cfg2", "b", 4), ("cfg2", "a", 3),

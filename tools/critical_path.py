@@ -70,16 +70,22 @@ def main():
     for (t, q), lst in streams.items():
         by_task[t].append(lst)
     for t, lsts in by_task.items():
+        if t == "grid":
+            continue
         allk = sorted([k for lst in lsts for k in lst], key=lambda k: k["s"])
         allk = [k for k in allk if k["e"] >= first]
-        if t == "grid":  # two builds a step (SA1 ball-query grid, FP4 known grid), by queue
-            for lst in lsts:
-                lst = [k for k in lst if k["e"] >= first]
-                for j, k in enumerate(lst):
-                    k["step"] = j
-        else:
-            for j, k in enumerate(allk):
-                k["step"] = j
+        for j, k in enumerate(allk):
+            k["step"] = j
+    # a grid build belongs to the step of the next kernel on its queue (SA1's ball-query grid
+    # before that step's SA1 grouping, FP4's known grid before its three_nn)
+    byq0 = defaultdict(list)
+    for k in ks:
+        byq0[k["q"]].append(k)
+    for q, lst in byq0.items():
+        lst.sort(key=lambda k: k["s"])
+        for a_, b_ in zip(lst, lst[1:]):
+            if a_["task"] == "grid" and "step" in b_:
+                a_["step"] = b_["step"]
     steps = defaultdict(dict)
     for k in ks:
         if "step" in k:
