@@ -389,6 +389,10 @@ def main():
     ap.add_argument("--e2e-steps", type=int, default=20,
                     help="after the geometric measurement, time this many whole-model steps "
                          "(reported as 'e2e'; 0 = skip)")
+    ap.add_argument("--timeline", default=None, metavar="PATH",
+                    help="DIAGNOSTIC: bracket every timed sampler with events and write, per "
+                         "step, the host's wait / enqueue times and the GPU times of the sampler "
+                         "and of each side lane's end (relative to one base event) to PATH (JSON)")
     ap.add_argument("--no-verify", action="store_true",
                     help="skip the post-run oracle check of every buffer set's last step (the "
                          "line's `verified` is then null)")
@@ -517,10 +521,13 @@ def main():
         barrier()
         if pipelined:
             pipe.host_wait_s = pipe.host_launch_s = 0.0
+            if args.timeline and not model:
+                pipe.start_trace()
         t0 = time.perf_counter()
         outs = None
+        every = 1 if (args.timeline and pipelined and not model) else args.time_every
         timed_k = [] if args.diag_only == "side" else \
-            [k for k in range(steps) if k % args.time_every == 0]
+            [k for k in range(steps) if k % every == 0]
         for k in range(steps):
             outs = run_step(ev[k] if k in timed_k else None)
         outs = finish() or outs
@@ -533,6 +540,9 @@ def main():
         if pipelined:  # host time per step: waiting for a free buffer set / enqueueing a step
             host["wait_ms_per_step"] = pipe.host_wait_s / steps * 1e3
             host["enqueue_ms_per_step"] = pipe.host_launch_s / steps * 1e3
+            if getattr(pipe, "trace", None) is not None:
+                with open(args.timeline, "w") as fh:
+                    json.dump({"elapsed_ms": elapsed * 1e3, "steps": pipe.finish_trace()}, fh)
         post = {}
         # the sampler fault word (include/pn2hip.h pn2_fault_status) after the timed steps:
         # a fault raises here, so a fast but wrong line is never printed

@@ -1006,10 +1006,45 @@ class Pipeline:
                 return self._run(sampler_events)
         return self._run(sampler_events)
 
+    def start_trace(self):
+        """DIAGNOSTIC (bench.py --timeline): from now on every step records its host times
+        (wait for the set, enqueue) and, once its set is reused (or at finish_trace), the GPU
+        times of its lane ends relative to a base event; sampler events passed to run() are
+        read the same way. No cost when not started."""
+        self.trace = []
+        self.trace_base = torch.cuda.Event(enable_timing=True)
+        self.trace_base.record()
+        self.trace_t0 = time.perf_counter()
+        self._last_of_set = {}
+
+    def _trace_done(self, si):
+        # the set's previous step: its lane-end events are complete (synchronised or joined)
+        j = self._last_of_set.get(si)
+        if j is None:
+            return
+        st = self.sets[si].step if isinstance(self.sets[si], GraphStep) else self.sets[si]
+        rec = self.trace[j]
+        rec["lane_end_ms"] = {lane: self.trace_base.elapsed_time(st.lane_done[lane])
+                              for lane in st.done_lanes()}
+        ev = rec.pop("_events", None)
+        if ev is not None:
+            rec["sampler_ms"] = [self.trace_base.elapsed_time(ev[0]),
+                                 self.trace_base.elapsed_time(ev[1])]
+
+    def finish_trace(self):
+        """Synchronise and complete the records of the last steps; returns the list."""
+        torch.cuda.synchronize()
+        for si in range(len(self.sets)):
+            self._trace_done(si)
+        out, self.trace = self.trace, None
+        return out
+
     def _run(self, sampler_events):
-        s = self.sets[self.k % len(self.sets)]
+        si = self.k % len(self.sets)
+        s = self.sets[si]
         self.k += 1
         t0 = time.perf_counter()
+        tr = getattr(self, "trace", None)
         try:
             if isinstance(s, GraphStep):
                 if s.step.ran and s.step.overlap:
@@ -1019,6 +1054,12 @@ class Pipeline:
                     s.step.join()
                 t1 = time.perf_counter()
                 self.host_wait_s += t1 - t0
+                if tr is not None:
+                    self._trace_done(si)
+                    tr.append({"k": self.k - 1, "set": si,
+                               "host_ms": [(t0 - self.trace_t0) * 1e3, (t1 - self.trace_t0) * 1e3],
+                               "_events": sampler_events})
+                    self._last_of_set[si] = len(tr) - 1
                 t0 = t1
                 if self.native_plan:
                     return s.replay_plan(sampler_events)
@@ -1026,7 +1067,10 @@ class Pipeline:
             s.join()
             return s.run(sampler_events, join=False)
         finally:  # host time of the enqueue (bench.py reports both per step)
-            self.host_launch_s += time.perf_counter() - t0
+            t2 = time.perf_counter()
+            self.host_launch_s += t2 - t0
+            if tr is not None and tr and "host_ms" in tr[-1] and len(tr[-1]["host_ms"]) == 2:
+                tr[-1]["host_ms"].append((t2 - self.trace_t0) * 1e3)
 
     def join(self):
         """Wait for everything enqueued; returns the outputs of the last step run. Raises

@@ -24,3 +24,7 @@ run cfg3 --config cfg3
 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $OUT/trace_cfg2 -o run -- python3 bench.py --steps 200 --warmup 20 --no-cpu-baseline --e2e-steps 0 --no-verify --latency-reps 5 > $OUT/trace_cfg2.log 2>&1 || { tail -20 $OUT/trace_cfg2.log; exit 1; }
 T=$(find $OUT/trace_cfg2 -name "*kernel_trace.csv" | head -1)
 python3 tools/critical_path.py $T --out $OUT/critical_path_cfg2.txt | head -12
+timeout -k 10 300 python3 bench.py --no-cpu-baseline --e2e-steps 0 --steps 200 --timeline $OUT/timeline_200.json > $OUT/b_tl200.json 2> $OUT/b_tl200.err || { tail -20 $OUT/b_tl200.err; exit 1; }
+python3 tools/timeline_report.py $OUT/timeline_200.json | tee $OUT/timeline_200.txt
+timeout -k 10 300 python3 bench.py --no-cpu-baseline --e2e-steps 0 --steps 20 --warmup 5 --timeline $OUT/timeline_20.json > $OUT/b_tl20.json 2> $OUT/b_tl20.err || { tail -20 $OUT/b_tl20.err; exit 1; }
+python3 tools/timeline_report.py $OUT/timeline_20.json --skip 0 --show 20 | tee $OUT/timeline_20.txt
