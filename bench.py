@@ -486,6 +486,7 @@ def main():
                                                                      model=model)
         torch.cuda.synchronize()
         if pipelined:
+            pkg.stack.TIMING_EVENTS = bool(args.timeline) and not model
             if not model and args.sampler_lanes > 1:
                 # CU-masked sampler and side streams (stack.set_cu_partition), before any
                 # stream of the pipeline exists

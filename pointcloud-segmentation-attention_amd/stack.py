@@ -137,6 +137,8 @@ LANE_JOIN = os.environ.get("PN2_LANE_JOIN") == "1"
 # SEG_MERGE (A/B, PN2_SEG_MERGE=1): a lane's consecutive tasks share one launch segment even
 # when a later task waits for another producer (the segment then waits for all of them first)
 SEG_MERGE = os.environ.get("PN2_SEG_MERGE") == "1"
+# lane-end events with timing (DIAGNOSTIC: bench.py --timeline sets it before the pipeline)
+TIMING_EVENTS = False
 _CU_PART = {}  # device -> {"sampler": mask words, "side": mask words} (set_cu_partition)
 
 
@@ -294,7 +296,9 @@ class Step:
             for st in self.streams[1:]:
                 st.wait_stream(main)
             self.done = {t.name: torch.cuda.Event() for t in self.tasks}
-            self.lane_done = [torch.cuda.Event() for _ in range(self.nlanes)]
+            # (timing-enabled under bench.py --timeline, which reads their GPU times)
+            self.lane_done = [torch.cuda.Event(enable_timing=TIMING_EVENTS)
+                              for _ in range(self.nlanes)]
 
     # ------------------------------------------------------------------ task lists
     def _tasks_ssg(self):
