@@ -12,3 +12,5 @@ python3 tools/timeline_report.py $OUT/timeline_20_$n.json --skip 0 --show 20 | t
 done
 timeout -k 10 300 python3 bench.py --no-cpu-baseline --e2e-steps 0 --steps 200 --timeline $OUT/timeline_200.json > $OUT/b_tl200.json 2> $OUT/b_tl200.err || { tail -20 $OUT/b_tl200.err; exit 1; }
 python3 tools/timeline_report.py $OUT/timeline_200.json | tee $OUT/timeline_200.txt
+timeout -k 10 120 python3 tools/cu_mask_probe.py > $OUT/cu_mask_probe.json 2>&1 || { tail -20 $OUT/cu_mask_probe.json; exit 1; }
+cat $OUT/cu_mask_probe.json
