@@ -375,6 +375,9 @@ def main():
     ap.add_argument("--hw-queues", type=int, default=None,
                     help="GPU_MAX_HW_QUEUES for this process (default: the environment's, else "
                          f"{DEFAULT_HW_QUEUES}; <= 32)")
+    ap.add_argument("--alt-lanes", default=None,
+                    help="comma list of side lanes whose work of every other buffer set runs on a "
+                         "second stream (e.g. 2 = FP4's lane); default: the config's LAYOUTS entry")
     ap.add_argument("--sampler-priority", choices=["default", "high"], default=None,
                     help="stream priority of every sampler stream (lane 0, the extra sampler "
                          "streams, the later samplers' own stream); default: the config's "
@@ -421,6 +424,9 @@ def main():
         args.cu_partition = 0 if args.model else lay.get("cu", 0)
     if args.sampler_priority is None:
         args.sampler_priority = lay.get("prio", "default")
+    if args.alt_lanes is None:
+        args.alt_lanes = lay.get("alt", "")
+    alt_lanes = tuple(int(x) for x in args.alt_lanes.split(",") if x.strip())
     if args.hw_queues is None and not args.model and args.sampler_lanes == lay["lanes"]:
         args.hw_queues = lay["queues"]  # one queue per stream (the box's default is 4)
     if args.hw_queues is not None:
@@ -499,7 +505,8 @@ def main():
                                       only=args.diag_only, layout=args.side_layout,
                                       chain_own=args.chain in ("own", "own2"),
                                       chain_streams=2 if args.chain == "own2" else 1,
-                                      set_inputs=set_inputs)
+                                      set_inputs=set_inputs,
+                                      alt_lanes=() if model else alt_lanes)
         else:
             step = pkg.stack.Step(inp, overlap=overlap)
             graph = None if args.eager else pkg.stack.GraphStep(inp, overlap=overlap)
@@ -646,6 +653,7 @@ def main():
                                         and args.sampler_lanes > 1 else "none"),
                        "lane0_priority": prio0,
                        "sampler_priority": args.sampler_priority,
+                       "alt_lanes": list(alt_lanes),
                        "streams": (("SA1 sampler + 3 side streams" if args.sampler_lanes <= 1 or args.model
                                     else f"{args.sampler_lanes} sampler streams (consecutive steps' "
                                     f"samplers concurrent; SA2.. samplers "

@@ -261,7 +261,7 @@ class Step:
 
     SAMPLER = "fps1"
 
-    def __init__(self, inp, overlap=True, streams=None, chain_lane=3, layout="a"):
+    def __init__(self, inp, overlap=True, streams=None, chain_lane=3, layout="a", alt_lanes=()):
         # chain_lane: the lane of the later samplers (SA2..SA4 / MSG SA2); 0 = behind the SA1
         # sampler on its stream; -1 = a lane of their own after the side lanes (both: several
         # sampler streams, Pipeline); layout: side_layout()
@@ -277,6 +277,14 @@ class Step:
             self.tasks = self._tasks_ssg() if self.kind == "ssg" else self._tasks_msg()
         self.ran = False
         self.synced_inputs = False
+        if alt_lanes:
+            # this step's tasks of the side lanes in alt_lanes run on lanes of their own after
+            # every other lane (Pipeline gives them to every other buffer set: consecutive
+            # steps' work of a saturated lane then runs on two queues)
+            top = 1 + max(t.lane for t in self.tasks)
+            remap = {L: top + j for j, L in enumerate(sorted(alt_lanes))}
+            for t in self.tasks:
+                t.lane = remap.get(t.lane, t.lane)
         self.nlanes = 1 + max(t.lane for t in self.tasks)
         if self.overlap:
             dev = inp["xyz"].device
@@ -831,11 +839,11 @@ class GraphStep:
     eager step. Inputs stay resident, outputs are overwritten in place at every replay."""
 
     def __init__(self, inp, warmup=2, overlap=True, streams=None, chain_lane=3, segments=False,
-                 only=None, layout="a"):
+                 only=None, layout="a", alt_lanes=()):
         # segments: capture one graph per launch segment (Step.segments(), for a native plan:
         # replay_plan) instead of one per task (replay)
         self.step = Step(inp, overlap=overlap, streams=streams, chain_lane=chain_lane,
-                         layout=layout)
+                         layout=layout, alt_lanes=alt_lanes)
         self.segmented = segments and self.step.overlap
         dev = inp["xyz"].device
         warm = side_stream(dev, "warm")
@@ -937,7 +945,7 @@ class Pipeline:
 
     def __init__(self, inp, graphs=True, overlap=True, nsets=3, private_streams=False,
                  sampler_lanes=1, native_plan=True, only=None, layout="a", chain_own=False,
-                 set_inputs=None, chain_streams=1):
+                 set_inputs=None, chain_streams=1, alt_lanes=()):
         # chain_streams (with chain_own): the later samplers of set i run on chain stream
         # i % chain_streams, so consecutive steps' chains can overlap (one shared chain stream
         # runs one chain per step back to back: its launch time bounds the step)
@@ -986,11 +994,13 @@ class Pipeline:
         inps = list(set_inputs) if set_inputs is not None else [inp] * nsets
         cl = (lambda i: chain_lane - (i % max(1, chain_streams)) if chain_lane < 0
               else chain_lane)
+        # alt_lanes: side lanes whose work of every other buffer set runs on a second stream
+        al = (lambda i: tuple(alt_lanes) if i % 2 else ())
         mk = (lambda i: GraphStep(inps[i], overlap=overlap, streams=streams(i),
                                   chain_lane=cl(i), segments=self.native_plan, only=only,
-                                  layout=layout)) \
+                                  layout=layout, alt_lanes=al(i))) \
             if graphs else (lambda i: Step(inps[i], overlap=overlap, streams=streams(i),
-                                           chain_lane=cl(i), layout=layout))
+                                           chain_lane=cl(i), layout=layout, alt_lanes=al(i)))
         self.sets = [mk(i) for i in range(nsets)]
         self.inputs = inps
         self.k = 0
