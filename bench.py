@@ -654,6 +654,8 @@ def main():
                        "lane0_priority": prio0,
                        "sampler_priority": args.sampler_priority,
                        "alt_lanes": list(alt_lanes),
+                       **({"DIAGNOSTIC_dup_tasks": sorted(pkg.stack.DUP_TASKS)}
+                          if pkg.stack.DUP_TASKS else {}),
                        "streams": (("SA1 sampler + 3 side streams" if args.sampler_lanes <= 1 or args.model
                                     else f"{args.sampler_lanes} sampler streams (consecutive steps' "
                                     f"samplers concurrent; SA2.. samplers "

@@ -139,6 +139,10 @@ LANE_JOIN = os.environ.get("PN2_LANE_JOIN") == "1"
 SEG_MERGE = os.environ.get("PN2_SEG_MERGE") == "1"
 # lane-end events with timing (DIAGNOSTIC: bench.py --timeline sets it before the pipeline)
 TIMING_EVENTS = False
+# DIAGNOSTIC (PN2_DUP_TASKS=sa1,fp4,...): the named tasks run twice in their captured graph
+# (same inputs, same results), so a bench run prices one extra copy of each -- its marginal
+# cost in the pipelined step (scripts/r4_dup.sh). Never set by the product.
+DUP_TASKS = frozenset(t for t in os.environ.get("PN2_DUP_TASKS", "").split(",") if t)
 _CU_PART = {}  # device -> {"sampler": mask words, "side": mask words} (set_cu_partition)
 
 
@@ -872,6 +876,8 @@ class GraphStep:
             with torch.cuda.graph(g, pool=pools[lane], stream=cap):
                 for t in ts:
                     t.fn()
+                    if t.name in DUP_TASKS:
+                        t.fn()
             st.wait_stream(cap)
             self.graphs[key] = g
 
