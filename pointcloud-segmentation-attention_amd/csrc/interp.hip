@@ -177,21 +177,29 @@ PN2_DEV bool box_certifies(const GridHdr& h, float px, float py, float pz, int x
   return gap > 0.0f && d3 < gap * gap * 0.9999f;
 }
 
-// G lanes per unknown point (1, or 4 = a quad); BLOCK / G unknowns per workgroup
-template <int BLOCK, bool LDS, int G>
+#ifndef PN2_NN_ROWS
+#define PN2_NN_ROWS 1  // row blocks per workgroup (one staging of the known grid serves K)
+#endif
+#ifndef PN2_NN_LDS
+#define PN2_NN_LDS 1  // 0: the search reads the known grid from L2 (A/B builds)
+#endif
+
+// G lanes per unknown point (1, or 4 = a quad); BLOCK / G unknowns per row block, K row
+// blocks of one cloud per workgroup
+template <int BLOCK, bool LDS, int G, int K>
 __global__ __launch_bounds__(BLOCK) void three_nn_grid_kernel(
     const void* __restrict__ kgrid, int m, const void* __restrict__ ugrid,
     const float* __restrict__ xyz1, int n, int B, float* __restrict__ dist,
     int32_t* __restrict__ idx) {
   static_assert(G == 1 || G == 4, "one lane or a quad per unknown");
-  constexpr int QPB = BLOCK / G;  // unknowns per workgroup
+  constexpr int QPB = BLOCK / G;  // unknowns per row block
   extern __shared__ float4 s_pts[];  // LDS: m sorted known points, then ncell+1 offsets
-  // logical block (cloud b, row block x), XCD-aware: the blocks of a cloud share one L2
-  const int R = (n + QPB - 1) / QPB;
+  // logical block (cloud b, block x of K row blocks), XCD-aware: the blocks of a cloud share
+  // one L2
+  const int R = (n + QPB * K - 1) / (QPB * K);
   const int Lg = xcd_block(blockIdx.x, R * B);
   if (Lg >= R * B) return;
   const int b = Lg / R;
-  const int i = (Lg - b * R) * QPB + (int)threadIdx.x / G;
   const int q = (int)threadIdx.x & (G - 1);
   const GridView g = grid_view(kgrid, b, m);
   const GridHdr& h = g.h;
@@ -207,62 +215,67 @@ __global__ __launch_bounds__(BLOCK) void three_nn_grid_kernel(
     pts = s_pts;
     off = s_off;
   }
-  if (i >= n) return;  // no barriers below; a quad's lanes share i
-  float px, py, pz;
-  int u;
-  if (ugrid) {
-    const float4 U = grid_view(ugrid, b, n).pts[i];
-    px = U.x; py = U.y; pz = U.z;
-    u = __float_as_int(U.w);
-  } else {
-    const float* U = xyz1 + ((size_t)b * n + i) * 3;
-    px = U[0]; py = U[1]; pz = U[2];
-    u = i;
-  }
-  Best3 best;
-  best3_init(best);
-  auto visit = [&](int lo, int hi) {  // sorted points [lo, hi), this lane's share
-    for (int e = lo + q; e < hi; e += G) {
-      const float4 p = pts[e];
-      best3_insert_lex(best, sqdist(p.x, p.y, p.z, px, py, pz), __float_as_int(p.w));
+  const float4* __restrict__ upts = ugrid ? grid_view(ugrid, b, n).pts : nullptr;
+  for (int kb = 0; kb < K; ++kb) {  // no barriers below; a quad's lanes share i
+    const int i = ((Lg - b * R) * K + kb) * QPB + (int)threadIdx.x / G;
+    if (i >= n) break;
+    float px, py, pz;
+    int u;
+    if (upts) {
+      const float4 U = upts[i];
+      px = U.x; py = U.y; pz = U.z;
+      u = __float_as_int(U.w);
+    } else {
+      const float* U = xyz1 + ((size_t)b * n + i) * 3;
+      px = U[0]; py = U[1]; pz = U[2];
+      u = i;
     }
-  };
-  auto merged = [&]() {  // the quad's top 3 (every lane of the quad gets the same)
-    Best3 mb = best;
-    if constexpr (G == 4) {
-      best3_merge_xor(mb, 1);
-      best3_merge_xor(mb, 2);
-    }
-    return mb;
-  };
-  const int cx = cell_coord(px, h.ox, h.inv, h.nx);
-  const int cy = cell_coord(py, h.oy, h.inv, h.ny);
-  const int cz = cell_coord(pz, h.oz, h.inv, h.nz);
-  Best3 res;
-  for (int s = 0;; ++s) {
-    const int xl = cx - s, xh = cx + s, yl = cy - s, yh = cy + s, zl = cz - s, zh = cz + s;
-    const int x0 = max(xl, 0), x1 = min(xh, h.nx - 1);
-    for (int z = max(zl, 0); z <= min(zh, h.nz - 1); ++z) {
-      for (int y = max(yl, 0); y <= min(yh, h.ny - 1); ++y) {
-        const int row = (z * h.ny + y) * h.nx;
-        if (s == 0 || z == zl || z == zh || y == yl || y == yh) {
-          visit(off[row + x0], off[row + x1 + 1]);  // a face row: all of x0..x1
-        } else {
-          if (xl >= 0) visit(off[row + xl], off[row + xl + 1]);
-          if (xh < h.nx) visit(off[row + xh], off[row + xh + 1]);
+    Best3 best;
+    best3_init(best);
+    auto visit = [&](int lo, int hi) {  // sorted points [lo, hi), this lane's share
+      for (int e = lo + q; e < hi; e += G) {
+        const float4 p = pts[e];
+        best3_insert_lex(best, sqdist(p.x, p.y, p.z, px, py, pz), __float_as_int(p.w));
+      }
+    };
+    auto merged = [&]() {  // the quad's top 3 (every lane of the quad gets the same)
+      Best3 mb = best;
+      if constexpr (G == 4) {
+        best3_merge_xor(mb, 1);
+        best3_merge_xor(mb, 2);
+      }
+      return mb;
+    };
+    const int cx = cell_coord(px, h.ox, h.inv, h.nx);
+    const int cy = cell_coord(py, h.oy, h.inv, h.ny);
+    const int cz = cell_coord(pz, h.oz, h.inv, h.nz);
+    Best3 res;
+    for (int s = 0;; ++s) {
+      const int xl = cx - s, xh = cx + s, yl = cy - s, yh = cy + s, zl = cz - s, zh = cz + s;
+      const int x0 = max(xl, 0), x1 = min(xh, h.nx - 1);
+      for (int z = max(zl, 0); z <= min(zh, h.nz - 1); ++z) {
+        for (int y = max(yl, 0); y <= min(yh, h.ny - 1); ++y) {
+          const int row = (z * h.ny + y) * h.nx;
+          if (s == 0 || z == zl || z == zh || y == yl || y == yh) {
+            visit(off[row + x0], off[row + x1 + 1]);  // a face row: all of x0..x1
+          } else {
+            if (xl >= 0) visit(off[row + xl], off[row + xl + 1]);
+            if (xh < h.nx) visit(off[row + xh], off[row + xh + 1]);
+          }
         }
       }
+      res = merged();
+      if (xl <= 0 && yl <= 0 && zl <= 0 && xh >= h.nx - 1 && yh >= h.ny - 1 && zh >= h.nz - 1)
+        break;  // every cell visited
+      if (box_certifies(h, px, py, pz, xl, xh, yl, yh, zl, zh, res.d3)) break;
     }
-    res = merged();
-    if (xl <= 0 && yl <= 0 && zl <= 0 && xh >= h.nx - 1 && yh >= h.ny - 1 && zh >= h.nz - 1)
-      break;  // every cell visited
-    if (box_certifies(h, px, py, pz, xl, xh, yl, yh, zl, zh, res.d3)) break;
+    if (q == 0) {
+      float* D = dist + ((size_t)b * n + u) * 3;
+      int32_t* I = idx + ((size_t)b * n + u) * 3;
+      D[0] = res.d1; D[1] = res.d2; D[2] = res.d3;
+      I[0] = res.i1; I[1] = res.i2; I[2] = res.i3;
+    }
   }
-  if (q != 0) return;
-  float* D = dist + ((size_t)b * n + u) * 3;
-  int32_t* I = idx + ((size_t)b * n + u) * 3;
-  D[0] = res.d1; D[1] = res.d2; D[2] = res.d3;
-  I[0] = res.i1; I[1] = res.i2; I[2] = res.i3;
 }
 
 __global__ void idw_kernel(const float* __restrict__ dist, int total, float* __restrict__ weight) {
@@ -783,12 +796,13 @@ int pn2_three_nn_grid(const void* known_grid, const void* unknown_grid, const fl
   // explicit-edge one may have up to kGridCap and is read from global memory
   const size_t lds = (size_t)m * 16 + (size_t)(std::max(m, pn2::kAutoMinCells) + 1) * 4;
   constexpr int G = PN2_NN_QUAD ? 4 : 1;
-  const dim3 grid(pn2::xcd_grid((long long)((n + BLOCK / G - 1) / (BLOCK / G)) * B));
-  if (lds <= 64 * 1024)
-    hipLaunchKernelGGL((pn2::three_nn_grid_kernel<BLOCK, true, G>), grid, dim3(BLOCK), lds,
+  constexpr int K = PN2_NN_ROWS;
+  const dim3 grid(pn2::xcd_grid((long long)((n + BLOCK / G * K - 1) / (BLOCK / G * K)) * B));
+  if (PN2_NN_LDS && lds <= 64 * 1024)
+    hipLaunchKernelGGL((pn2::three_nn_grid_kernel<BLOCK, true, G, K>), grid, dim3(BLOCK), lds,
                        (hipStream_t)stream, known_grid, m, unknown_grid, xyz1, n, B, dist, idx);
   else
-    hipLaunchKernelGGL((pn2::three_nn_grid_kernel<BLOCK, false, G>), grid, dim3(BLOCK), 0,
+    hipLaunchKernelGGL((pn2::three_nn_grid_kernel<BLOCK, false, G, K>), grid, dim3(BLOCK), 0,
                        (hipStream_t)stream, known_grid, m, unknown_grid, xyz1, n, B, dist, idx);
   PN2_RETURN_LAUNCH();
 }

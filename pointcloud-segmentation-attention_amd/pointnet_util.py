@@ -241,19 +241,42 @@ def fp_interpolate(xyz1, xyz2, points1, points2, known_grid=None, unknown_grid=N
         C1 = int(points1.shape[2])
     else:
         C1 = 0
-    out = torch.empty((B, n, C2 + C1), dtype=torch.float32, device=xyz1.device)
     nn = None
     if known_grid is not None or tf_interpolate.use_grid(n, m):
-        dist, idx = tf_interpolate.three_nn(xyz1, xyz2, known_grid, unknown_grid)
-        check(lib().pn2_fp_apply(ptr(dist), ptr(idx),
-                                 None if unknown_grid is None else ptr(unknown_grid.buf),
-                                 ptr(points1), C1, ptr(points2), C2, B, n, m, ptr(out),
-                                 stream_of(xyz1)), "fp_interpolate")
-        nn = (dist, idx)
+        nn = tf_interpolate.three_nn(xyz1, xyz2, known_grid, unknown_grid)
+        out = fp_apply(nn, points1, points2, unknown_grid)
     else:
+        out = torch.empty((B, n, C2 + C1), dtype=torch.float32, device=xyz1.device)
         check(lib().pn2_fp_fused(ptr(xyz1), ptr(xyz2), ptr(points1), C1, ptr(points2), C2, B, n,
                                  m, ptr(out), stream_of(xyz1)), "fp_interpolate")
     return (out, nn) if return_nn else out
+
+
+def fp_apply(nn, points1, points2, unknown_grid=None):
+    """The second half of fp_interpolate's grid path (pn2_fp_apply): IDW weights from the
+    three_nn distances, three_interpolate and concat [interpolated, points1] -- nn = (dist, idx)
+    of tf_interpolate.three_nn over the same points (unknown_grid: the grid that search took
+    its unknowns' order from; rows are written in that order). Returns (B, n, C2 + C1)."""
+    dist, idx = nn
+    points2 = device_tensor(points2, "points2", torch.float32)
+    B, n, m, C2 = int(dist.shape[0]), int(dist.shape[1]), int(points2.shape[1]), int(points2.shape[2])
+    if tuple(idx.shape) != (B, n, 3) or tuple(dist.shape) != (B, n, 3) or int(points2.shape[0]) != B:
+        raise InvalidArgumentError("fp_apply: dist / idx (B,n,3), points2 (B,m,C2)")
+    if points1 is not None:
+        points1 = device_tensor(points1, "points1", torch.float32)
+        if tuple(points1.shape[:2]) != (B, n):
+            raise InvalidArgumentError("fp_apply: points1 (B,n,C1)")
+        C1 = int(points1.shape[2])
+    else:
+        C1 = 0
+    if unknown_grid is not None and int(unknown_grid.N) != n:
+        raise InvalidArgumentError("fp_apply: the unknown grid was built over other points")
+    out = torch.empty((B, n, C2 + C1), dtype=torch.float32, device=dist.device)
+    check(lib().pn2_fp_apply(ptr(dist), ptr(idx),
+                             None if unknown_grid is None else ptr(unknown_grid.buf),
+                             ptr(points1), C1, ptr(points2), C2, B, n, m, ptr(out),
+                             stream_of(dist)), "fp_apply")
+    return out
 
 
 def fp_interpolate_layers(layers):
