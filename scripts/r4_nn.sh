@@ -25,5 +25,5 @@ run default "" ""
 run dup_nn4 "" nn4
 run dup_fp4 "" fp4
 for v in nnk2 nnk4 nnk8 nnglob nnglobk4; do run $v $B/libpn2hip_v_$v.so ""; done
-PN2_NN4_LANE=3 run nn4lane3 "" ""
+export PN2_NN4_LANE=3; run nn4lane3 "" ""; unset PN2_NN4_LANE
 run default2 "" ""
