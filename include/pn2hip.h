@@ -26,6 +26,7 @@
  *   sample_and_group     pointnet_util.py:16-58 (SSG), :180-191  → pn2_sample_and_group,
  *                                                                  pn2_group_concat
  *   pointnet_fp_module   pointnet_util.py:218-226 (geometry)     → pn2_fp_fused,
+ *                                                                  pn2_fp_grid_fused,
  *                                                                  pn2_fp_apply
  *   AttentionLayer.call  attention_layer.py:29-45 (reduction)    → pn2_attn_reduce,
  *                                                                  pn2_attn_reduce_grad
@@ -316,6 +317,16 @@ int pn2_three_nn_grid(const void* known_grid, const void* unknown_grid, const fl
 int pn2_fp_apply(const float* dist, const int32_t* idx, const void* unknown_grid,
                  const float* points1, int C1, const float* points2, int C2, int B, int n, int m,
                  float* out, pn2_stream_t stream);
+/* pn2_fp_fused for a large search (FP4: n = 8192 unknowns, m = 1024 known) in ONE launch:
+ * every workgroup sorts the cloud's m known points into a grid in its own LDS (the automatic
+ * edge of pn2_grid_build) and searches it, then writes its rows -- the output of
+ * pn2_grid_build + pn2_three_nn_grid + pn2_fp_apply, bit for bit. 1 <= m <= 4096 (else
+ * PN2_EINVAL: use those three). `unknown_grid` (optional, a grid over the n unknown points)
+ * orders the rows as in pn2_fp_apply; with it xyz1 may be NULL. dist / idx (B,n,3): the
+ * three_nn result as well, or both NULL. C1 + C2 >= 1. */
+int pn2_fp_grid_fused(const float* xyz1, const float* xyz2, const void* unknown_grid,
+                      const float* points1, int C1, const float* points2, int C2, int B, int n,
+                      int m, float* out, float* dist, int32_t* idx, pn2_stream_t stream);
 
 /* ---------------------------------------------------------------- attention / pooling --- */
 

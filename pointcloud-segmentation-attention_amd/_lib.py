@@ -94,6 +94,7 @@ SIGNATURES = {
     "pn2_ball_group_xyz_grid": (_I, [_P, _P, _P, _I, _I, _I, _F, _I, _P, _P, _P, _P]),
     "pn2_three_nn_grid": (_I, [_P, _P, _P, _I, _I, _I, _P, _P, _P]),
     "pn2_fp_apply": (_I, [_P, _P, _P, _P, _I, _P, _I, _I, _I, _I, _P, _P]),
+    "pn2_fp_grid_fused": (_I, [_P, _P, _P, _P, _I, _P, _I, _I, _I, _I, _P, _P, _P, _P]),
     "pn2_group_point": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _P]),
     "pn2_group_point_grad": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _P]),
     "pn2_group_concat": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P]),

@@ -6,6 +6,8 @@
 // k = the point's index in the input. Cells are ordered x fastest, so the cells x0..x1 of one
 // (y, z) row are one contiguous range of the sorted points.
 #pragma once
+#include <math.h>
+
 #include "common.h"
 
 namespace pn2 {
@@ -43,6 +45,68 @@ PN2_DEV int cell_coord(float v, float o, float inv, int n) {
   float f = floorf((v - o) * inv);
   f = fminf(fmaxf(f, 0.0f), (float)(n - 1));
   return (int)f;
+}
+
+constexpr float kAutoPointsPerCell = 2.0f;
+
+PN2_DEV float wave_min_f(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, kWave));
+  return v;
+}
+PN2_DEV float wave_max_f(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, kWave));
+  return v;
+}
+PN2_DEV int wave_incl_scan(int v, int lane) {
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const int u = __shfl_up(v, o, kWave);
+    if (lane >= o) v += u;
+  }
+  return v;
+}
+
+// The grid's header for bbox [lo, hi] of N points (an empty / NaN-only axis as lo = hi = 0).
+// One thread computes it: pn2_grid_build's workgroup, or each workgroup of the fused FP
+// search (interp.hip), which builds a cloud's grid of known points in its own LDS.
+PN2_DEV GridHdr grid_dims(const float lo[3], const float hi[3], int N, float edge) {
+  GridHdr h;
+  // cell edge: the caller's, or ~kAutoPointsPerCell points per cell of the bbox volume
+  // (then also at most max(N, 64) cells, which bounds the grid's size for LDS staging);
+  // grown by 1.25x until the cells fit kGridCap;
+  // degenerate extents (inf / NaN coordinates) fall back to one cell (inv = 0)
+  float c = edge;
+  if (!(c > 0.0f)) {
+    const float ext = fmaxf(fmaxf(hi[0] - lo[0], hi[1] - lo[1]), hi[2] - lo[2]);
+    const double cells = fmax((double)N / kAutoPointsPerCell, 1.0);
+    double e = cbrt((double)(hi[0] - lo[0]) * (hi[1] - lo[1]) * (hi[2] - lo[2]) / cells);
+    if (!(e > 0.0)) e = (double)ext / cbrt(cells);
+    c = (float)e;
+    if (!(c > 0.0f)) c = 1.0f;  // all points identical: any edge gives one cell
+  }
+  int n[3] = {1, 1, 1};
+  bool ok = false;
+  for (int it = 0; it < 400 && !ok; ++it) {
+    double cells = 1.0, d[3];
+    for (int a = 0; a < 3; ++a) {
+      d[a] = floor((double)(hi[a] - lo[a]) / (double)c) + 1.0;
+      cells *= d[a];
+    }
+    if (cells <= (double)kGridCap && (edge > 0.0f || cells <= fmax((double)N, (double)kAutoMinCells))) {
+      for (int a = 0; a < 3; ++a) n[a] = (int)d[a];
+      ok = true;
+    } else {
+      c *= 1.25f;
+    }
+  }
+  if (!ok) { n[0] = n[1] = n[2] = 1; c = INFINITY; }
+  h.ox = lo[0]; h.oy = lo[1]; h.oz = lo[2];
+  h.inv = ok ? 1.0f / c : 0.0f;
+  h.nx = n[0]; h.ny = n[1]; h.nz = n[2];
+  h.ncell = n[0] * n[1] * n[2];
+  return h;
 }
 
 }  // namespace pn2

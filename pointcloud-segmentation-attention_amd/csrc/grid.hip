@@ -37,27 +37,6 @@ constexpr int kBuildBlock = 1024;
 #define PN2_GQ_LONG_ROWS 24
 #endif
 constexpr int kMaxBitWords = 4096;  // bitmask words per wave (N <= 131072)
-constexpr float kAutoPointsPerCell = 2.0f;
-
-PN2_DEV float wave_min_f(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, kWave));
-  return v;
-}
-PN2_DEV float wave_max_f(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, kWave));
-  return v;
-}
-PN2_DEV int wave_incl_scan(int v, int lane) {
-#pragma unroll
-  for (int o = 1; o < kWave; o <<= 1) {
-    const int u = __shfl_up(v, o, kWave);
-    if (lane >= o) v += u;
-  }
-  return v;
-}
-
 // The cloud's points are read ONCE into registers (PPT per thread, every load issued before
 // the first is used): the bounding box, the count and the scatter all work from them. The
 // first version looped over the cloud three times from memory with one dependent load trip per
@@ -132,39 +111,7 @@ __global__ __launch_bounds__(kBuildBlock) void grid_build_kernel(const float* __
       for (int i = 1; i < NW; ++i) { lo[a] = fminf(lo[a], red[a][i]); hi[a] = fmaxf(hi[a], red[3 + a][i]); }
       if (!(hi[a] >= lo[a])) { lo[a] = 0.0f; hi[a] = 0.0f; }  // N == 0 or NaN-only axis
     }
-    // cell edge: the caller's, or ~kAutoPointsPerCell points per cell of the bbox volume
-    // (then also at most max(N, 64) cells, which bounds the grid's size for LDS staging);
-    // grown by 1.25x until the cells fit kGridCap;
-    // degenerate extents (inf / NaN coordinates) fall back to one cell (inv = 0)
-    float c = edge;
-    if (!(c > 0.0f)) {
-      const float ext = fmaxf(fmaxf(hi[0] - lo[0], hi[1] - lo[1]), hi[2] - lo[2]);
-      const double cells = fmax((double)N / kAutoPointsPerCell, 1.0);
-      double e = cbrt((double)(hi[0] - lo[0]) * (hi[1] - lo[1]) * (hi[2] - lo[2]) / cells);
-      if (!(e > 0.0)) e = (double)ext / cbrt(cells);
-      c = (float)e;
-      if (!(c > 0.0f)) c = 1.0f;  // all points identical: any edge gives one cell
-    }
-    int n[3] = {1, 1, 1};
-    bool ok = false;
-    for (int it = 0; it < 400 && !ok; ++it) {
-      double cells = 1.0, d[3];
-      for (int a = 0; a < 3; ++a) {
-        d[a] = floor((double)(hi[a] - lo[a]) / (double)c) + 1.0;
-        cells *= d[a];
-      }
-      if (cells <= (double)kGridCap && (edge > 0.0f || cells <= fmax((double)N, (double)kAutoMinCells))) {
-        for (int a = 0; a < 3; ++a) n[a] = (int)d[a];
-        ok = true;
-      } else {
-        c *= 1.25f;
-      }
-    }
-    if (!ok) { n[0] = n[1] = n[2] = 1; c = INFINITY; }
-    sh.ox = lo[0]; sh.oy = lo[1]; sh.oz = lo[2];
-    sh.inv = ok ? 1.0f / c : 0.0f;
-    sh.nx = n[0]; sh.ny = n[1]; sh.nz = n[2];
-    sh.ncell = n[0] * n[1] * n[2];
+    sh = grid_dims(lo, hi, N, edge);
     *(GridHdr*)G = sh;
   }
   __syncthreads();

@@ -177,6 +177,55 @@ PN2_DEV bool box_certifies(const GridHdr& h, float px, float py, float pz, int x
   return gap > 0.0f && d3 < gap * gap * 0.9999f;
 }
 
+// The three nearest known points of (px, py, pz) over a grid's sorted points (pts, off: in
+// LDS or global memory), lexicographic in (d, k): cubic shells of cells around the point's
+// cell until the certificate holds; G lanes (lane q of them) split each shell's cells and
+// merge their lists at its end, so all G return the same result.
+template <int G>
+PN2_DEV Best3 grid_nn3(const GridHdr& h, const float4* __restrict__ pts,
+                       const int* __restrict__ off, float px, float py, float pz, int q) {
+  Best3 best;
+  best3_init(best);
+  auto visit = [&](int lo, int hi) {  // sorted points [lo, hi), this lane's share
+    for (int e = lo + q; e < hi; e += G) {
+      const float4 p = pts[e];
+      best3_insert_lex(best, sqdist(p.x, p.y, p.z, px, py, pz), __float_as_int(p.w));
+    }
+  };
+  auto merged = [&]() {  // the quad's top 3 (every lane of the quad gets the same)
+    Best3 mb = best;
+    if constexpr (G == 4) {
+      best3_merge_xor(mb, 1);
+      best3_merge_xor(mb, 2);
+    }
+    return mb;
+  };
+  const int cx = cell_coord(px, h.ox, h.inv, h.nx);
+  const int cy = cell_coord(py, h.oy, h.inv, h.ny);
+  const int cz = cell_coord(pz, h.oz, h.inv, h.nz);
+  Best3 res;
+  for (int s = 0;; ++s) {
+    const int xl = cx - s, xh = cx + s, yl = cy - s, yh = cy + s, zl = cz - s, zh = cz + s;
+    const int x0 = max(xl, 0), x1 = min(xh, h.nx - 1);
+    for (int z = max(zl, 0); z <= min(zh, h.nz - 1); ++z) {
+      for (int y = max(yl, 0); y <= min(yh, h.ny - 1); ++y) {
+        const int row = (z * h.ny + y) * h.nx;
+        if (s == 0 || z == zl || z == zh || y == yl || y == yh) {
+          visit(off[row + x0], off[row + x1 + 1]);  // a face row: all of x0..x1
+        } else {
+          if (xl >= 0) visit(off[row + xl], off[row + xl + 1]);
+          if (xh < h.nx) visit(off[row + xh], off[row + xh + 1]);
+        }
+      }
+    }
+    res = merged();
+    if (xl <= 0 && yl <= 0 && zl <= 0 && xh >= h.nx - 1 && yh >= h.ny - 1 && zh >= h.nz - 1)
+      break;  // every cell visited
+    if (box_certifies(h, px, py, pz, xl, xh, yl, yh, zl, zh, res.d3)) break;
+  }
+  return res;
+}
+
 #ifndef PN2_NN_ROWS
 #define PN2_NN_ROWS 1  // row blocks per workgroup (one staging of the known grid serves K)
 #endif
@@ -230,45 +279,7 @@ __global__ __launch_bounds__(BLOCK) void three_nn_grid_kernel(
       px = U[0]; py = U[1]; pz = U[2];
       u = i;
     }
-    Best3 best;
-    best3_init(best);
-    auto visit = [&](int lo, int hi) {  // sorted points [lo, hi), this lane's share
-      for (int e = lo + q; e < hi; e += G) {
-        const float4 p = pts[e];
-        best3_insert_lex(best, sqdist(p.x, p.y, p.z, px, py, pz), __float_as_int(p.w));
-      }
-    };
-    auto merged = [&]() {  // the quad's top 3 (every lane of the quad gets the same)
-      Best3 mb = best;
-      if constexpr (G == 4) {
-        best3_merge_xor(mb, 1);
-        best3_merge_xor(mb, 2);
-      }
-      return mb;
-    };
-    const int cx = cell_coord(px, h.ox, h.inv, h.nx);
-    const int cy = cell_coord(py, h.oy, h.inv, h.ny);
-    const int cz = cell_coord(pz, h.oz, h.inv, h.nz);
-    Best3 res;
-    for (int s = 0;; ++s) {
-      const int xl = cx - s, xh = cx + s, yl = cy - s, yh = cy + s, zl = cz - s, zh = cz + s;
-      const int x0 = max(xl, 0), x1 = min(xh, h.nx - 1);
-      for (int z = max(zl, 0); z <= min(zh, h.nz - 1); ++z) {
-        for (int y = max(yl, 0); y <= min(yh, h.ny - 1); ++y) {
-          const int row = (z * h.ny + y) * h.nx;
-          if (s == 0 || z == zl || z == zh || y == yl || y == yh) {
-            visit(off[row + x0], off[row + x1 + 1]);  // a face row: all of x0..x1
-          } else {
-            if (xl >= 0) visit(off[row + xl], off[row + xl + 1]);
-            if (xh < h.nx) visit(off[row + xh], off[row + xh + 1]);
-          }
-        }
-      }
-      res = merged();
-      if (xl <= 0 && yl <= 0 && zl <= 0 && xh >= h.nx - 1 && yh >= h.ny - 1 && zh >= h.nz - 1)
-        break;  // every cell visited
-      if (box_certifies(h, px, py, pz, xl, xh, yl, yh, zl, zh, res.d3)) break;
-    }
+    const Best3 res = grid_nn3<G>(h, pts, off, px, py, pz, q);
     if (q == 0) {
       float* D = dist + ((size_t)b * n + u) * 3;
       int32_t* I = idx + ((size_t)b * n + u) * 3;
@@ -351,54 +362,17 @@ struct FpLayer {
   FastDiv div_cw;
 };
 
+// The output rows j0 .. j0 + 63 of cloud b, column slice zb, from the rows' three neighbours
+// and IDW weights (s_idx / s_w by row of the workgroup; PRE: output row s_row[rl], else
+// j0 + rl): interpolated columns ((p1*w1)+(p2*w2))+(p3*w3), then the points1 concat.
 template <int V2, int V1, bool PRE, int UN>
-PN2_DEV void fp_fused_body(const FpLayer& p, int Lg) {
-  __shared__ float4 sk[PRE ? 1 : kNNTile];
-  __shared__ int4 s_idx[kNNRows];
-  __shared__ float4 s_w[kNNRows];
-  __shared__ int s_row[PRE ? kNNRows : 1];
-  const float* __restrict__ xyz1 = p.xyz1;
-  const float* __restrict__ xyz2 = p.xyz2;
-  const float* __restrict__ pdist = p.pdist;
-  const int32_t* __restrict__ pidx = p.pidx;
-  const void* __restrict__ ugrid = p.ugrid;
+PN2_DEV void fp_write_rows(const FpLayer& p, int b, int zb, int j0, const int4* s_idx,
+                           const float4* s_w, const int* s_row) {
   const float* __restrict__ points1 = p.points1;
   const float* __restrict__ points2 = p.points2;
   float* __restrict__ out = p.out;
-  const int C1 = p.C1, C2 = p.C2, n = p.n, m = p.m, cw = p.cw, Z = p.Z;
+  const int C1 = p.C1, C2 = p.C2, n = p.n, m = p.m, cw = p.cw;
   const FastDiv div_cw = p.div_cw;
-  const int R = (n + kNNRows - 1) / kNNRows;
-  const int b = Lg / (R * Z);
-  const int zb = (Lg - b * R * Z) / R;
-  const int j0 = (Lg - b * R * Z - zb * R) * kNNRows;
-  if constexpr (PRE) {
-    int jj = j0 + (int)threadIdx.x;
-    if (threadIdx.x < kNNRows && jj < n) {
-      if (ugrid) jj = __float_as_int(grid_view(ugrid, b, n).pts[jj].w);
-      s_row[threadIdx.x] = jj;
-      const float* D = pdist + ((size_t)b * n + jj) * 3;
-      const int32_t* I = pidx + ((size_t)b * n + jj) * 3;
-      float w1, w2, w3;
-      idw(D[0], D[1], D[2], w1, w2, w3);
-      s_idx[threadIdx.x] = make_int4(I[0], I[1], I[2], 0);
-      s_w[threadIdx.x] = make_float4(w1, w2, w3, 0.0f);
-    }
-  } else {
-    const int jl = threadIdx.x / kNNGroup;
-    const int j = j0 + jl;
-    const bool valid = j < n;
-    const float* U = xyz1 + ((size_t)b * n + (valid ? j : 0)) * 3;
-    Best3 best;
-    best3_init(best);
-    scan_known(xyz2 + (size_t)b * m * 3, m, U[0], U[1], U[2], sk, best);
-    if ((threadIdx.x & (kNNGroup - 1)) == 0) {
-      float w1, w2, w3;
-      idw(best.d1, best.d2, best.d3, w1, w2, w3);
-      s_idx[jl] = make_int4(best.i1, best.i2, best.i3, 0);
-      s_w[jl] = make_float4(w1, w2, w3, 0.0f);
-    }
-  }
-  __syncthreads();
   const int Cout = C2 + C1;             // floats
   // columns: c2v interpolated ones of V2 floats, then c1v concat ones of V1 floats
   const int c2v = C2 / V2, coutv = c2v + C1 / V1;
@@ -507,6 +481,53 @@ PN2_DEV void fp_fused_body(const FpLayer& p, int Lg) {
   }
 }
 
+template <int V2, int V1, bool PRE, int UN>
+PN2_DEV void fp_fused_body(const FpLayer& p, int Lg) {
+  __shared__ float4 sk[PRE ? 1 : kNNTile];
+  __shared__ int4 s_idx[kNNRows];
+  __shared__ float4 s_w[kNNRows];
+  __shared__ int s_row[PRE ? kNNRows : 1];
+  const float* __restrict__ xyz1 = p.xyz1;
+  const float* __restrict__ xyz2 = p.xyz2;
+  const float* __restrict__ pdist = p.pdist;
+  const int32_t* __restrict__ pidx = p.pidx;
+  const void* __restrict__ ugrid = p.ugrid;
+  const int n = p.n, m = p.m, Z = p.Z;
+  const int R = (n + kNNRows - 1) / kNNRows;
+  const int b = Lg / (R * Z);
+  const int zb = (Lg - b * R * Z) / R;
+  const int j0 = (Lg - b * R * Z - zb * R) * kNNRows;
+  if constexpr (PRE) {
+    int jj = j0 + (int)threadIdx.x;
+    if (threadIdx.x < kNNRows && jj < n) {
+      if (ugrid) jj = __float_as_int(grid_view(ugrid, b, n).pts[jj].w);
+      s_row[threadIdx.x] = jj;
+      const float* D = pdist + ((size_t)b * n + jj) * 3;
+      const int32_t* I = pidx + ((size_t)b * n + jj) * 3;
+      float w1, w2, w3;
+      idw(D[0], D[1], D[2], w1, w2, w3);
+      s_idx[threadIdx.x] = make_int4(I[0], I[1], I[2], 0);
+      s_w[threadIdx.x] = make_float4(w1, w2, w3, 0.0f);
+    }
+  } else {
+    const int jl = threadIdx.x / kNNGroup;
+    const int j = j0 + jl;
+    const bool valid = j < n;
+    const float* U = xyz1 + ((size_t)b * n + (valid ? j : 0)) * 3;
+    Best3 best;
+    best3_init(best);
+    scan_known(xyz2 + (size_t)b * m * 3, m, U[0], U[1], U[2], sk, best);
+    if ((threadIdx.x & (kNNGroup - 1)) == 0) {
+      float w1, w2, w3;
+      idw(best.d1, best.d2, best.d3, w1, w2, w3);
+      s_idx[jl] = make_int4(best.i1, best.i2, best.i3, 0);
+      s_w[jl] = make_float4(w1, w2, w3, 0.0f);
+    }
+  }
+  __syncthreads();
+  fp_write_rows<V2, V1, PRE, UN>(p, b, zb, j0, s_idx, s_w, s_row);
+}
+
 // Workgroup (x, b, z) of one layer: unknown points [64x, 64x+64) of cloud b, columns
 // [z*cw, (z+1)*cw) of the Cout = C2 + C1 concat row (V2- / V1-float columns). PRE: the three
 // neighbours come from a previous three_nn (pdist, pidx) instead of the scan; with `ugrid` (a
@@ -519,6 +540,151 @@ __global__ __launch_bounds__(kNNBlock) void fp_fused_kernel(FpLayer p) {
   const int Lg = xcd_block(blockIdx.x, total);
   if (Lg >= total) return;
   fp_fused_body<V2, V1, PRE, UN>(p, Lg);
+}
+
+// pointnet_fp_module geometry over a grid of the KNOWN points that every workgroup builds in
+// its own LDS (FP4: the m = 1024 FPS centres of an 8192-point cloud). One launch does what
+// pn2_grid_build + pn2_three_nn_grid + pn2_fp_apply did in three, each waiting for the one
+// before: per workgroup (cloud b, unknowns j0 .. j0 + 63 in `ugrid` order, all columns),
+//   1. the bbox of the cloud's known points and the grid's header (grid_dims, the automatic
+//      edge of pn2_grid_build: ~2 points per cell, at most max(m, 64) cells);
+//   2. a counting sort of the known points into cells, in LDS (the order inside a cell is
+//      the order of the atomics -- the (d, k)-lexicographic search does not depend on it);
+//   3. the quad search (grid_nn3) of each unknown, its IDW weights, optionally dist / idx;
+//   4. the rows (fp_write_rows).
+// A cloud's 128 workgroups each redo steps 1-2 over 12 KB of L2-resident points, which costs
+// less than the launch and the dependency they replace. Bit-identical to the three-launch path.
+constexpr int kFpGridMaxKnown = 4096;  // LDS: m float4 + (max(m, 64) + 1) offsets <= 80 KB
+
+inline size_t fp_grid_lds(int m) {
+  return (size_t)m * 16 + (size_t)((m > kAutoMinCells ? m : kAutoMinCells) + 1) * 4;
+}
+
+template <int V2, int V1, int UN>
+__global__ __launch_bounds__(kNNBlock) void fp_grid_fused_kernel(FpLayer p, float* __restrict__ dist,
+                                                              int32_t* __restrict__ idx) {
+  constexpr int NW = kNNBlock / kWave;
+  extern __shared__ float4 s_pts[];  // m known points sorted by cell, then ncell + 1 offsets
+  __shared__ int4 s_idx[kNNRows];
+  __shared__ float4 s_w[kNNRows];
+  __shared__ int s_row[kNNRows];
+  __shared__ float red[6][NW];
+  __shared__ int wsum[NW];
+  __shared__ GridHdr sh;
+  const int n = p.n, m = p.m;
+  const int R = (n + kNNRows - 1) / kNNRows;
+  const int total = R * p.B;
+  const int Lg = xcd_block(blockIdx.x, total);
+  if (Lg >= total) return;
+  const int b = Lg / R;
+  const int j0 = (Lg - b * R) * kNNRows;
+  const int t = threadIdx.x, lane = t & (kWave - 1), w = t / kWave;
+  const float* __restrict__ K = p.xyz2 + (size_t)b * m * 3;
+  int* s_off = (int*)(s_pts + m);
+
+  // 1. bounding box -> header
+  float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+  for (int k = t; k < m; k += kNNBlock) {
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      const float v = K[3 * k + a];
+      mn[a] = fminf(mn[a], v);
+      mx[a] = fmaxf(mx[a], v);
+    }
+  }
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    mn[a] = wave_min_f(mn[a]);
+    mx[a] = wave_max_f(mx[a]);
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int a = 0; a < 3; ++a) { red[a][w] = mn[a]; red[3 + a][w] = mx[a]; }
+  }
+  __syncthreads();
+  if (t == 0) {
+    float lo[3], hi[3];
+    for (int a = 0; a < 3; ++a) {
+      lo[a] = red[a][0];
+      hi[a] = red[3 + a][0];
+      for (int i = 1; i < NW; ++i) { lo[a] = fminf(lo[a], red[a][i]); hi[a] = fmaxf(hi[a], red[3 + a][i]); }
+      if (!(hi[a] >= lo[a])) { lo[a] = 0.0f; hi[a] = 0.0f; }  // NaN-only axis
+    }
+    sh = grid_dims(lo, hi, m, 0.0f);
+  }
+  __syncthreads();
+  const GridHdr h = sh;
+  auto cell_at = [&](float x, float y, float z) {
+    const int ix = cell_coord(x, h.ox, h.inv, h.nx);
+    const int iy = cell_coord(y, h.oy, h.inv, h.ny);
+    const int iz = cell_coord(z, h.oz, h.inv, h.nz);
+    return (iz * h.ny + iy) * h.nx + ix;
+  };
+
+  // 2. counting sort: counts at s_off[1 + c], exclusive scan in place, then the scatter uses
+  // s_off[1 + c] as cell c's cursor, which leaves it at cell c's end = cell c+1's start
+  for (int i = t; i <= h.ncell; i += kNNBlock) s_off[i] = 0;
+  __syncthreads();
+  for (int k = t; k < m; k += kNNBlock)
+    atomicAdd(&s_off[1 + cell_at(K[3 * k + 0], K[3 * k + 1], K[3 * k + 2])], 1);
+  __syncthreads();
+  {
+    const int per = (h.ncell + kNNBlock - 1) / kNNBlock;
+    const int s0 = t * per, s1 = min(s0 + per, h.ncell);
+    int sum = 0;
+    for (int i = s0; i < s1; ++i) sum += s_off[1 + i];
+    const int incl = wave_incl_scan(sum, lane);
+    if (lane == kWave - 1) wsum[w] = incl;
+    __syncthreads();
+    int base = incl - sum;
+    for (int i = 0; i < w; ++i) base += wsum[i];
+    for (int i = s0; i < s1; ++i) {
+      const int c = s_off[1 + i];
+      s_off[1 + i] = base;
+      base += c;
+    }
+  }
+  __syncthreads();
+  for (int k = t; k < m; k += kNNBlock) {
+    const float x = K[3 * k + 0], y = K[3 * k + 1], z = K[3 * k + 2];
+    const int pos = atomicAdd(&s_off[1 + cell_at(x, y, z)], 1);
+    s_pts[pos] = make_float4(x, y, z, __int_as_float(k));
+  }
+  __syncthreads();
+
+  // 3. the search, a quad per unknown (the quad's lanes share j)
+  const int jl = t / kNNGroup, q = t & (kNNGroup - 1);
+  const int j = j0 + jl;
+  if (j < n) {
+    float px, py, pz;
+    int u;
+    if (p.ugrid) {
+      const float4 U = grid_view(p.ugrid, b, n).pts[j];
+      px = U.x; py = U.y; pz = U.z;
+      u = __float_as_int(U.w);
+    } else {
+      const float* U = p.xyz1 + ((size_t)b * n + j) * 3;
+      px = U[0]; py = U[1]; pz = U[2];
+      u = j;
+    }
+    const Best3 res = grid_nn3<kNNGroup>(h, s_pts, s_off, px, py, pz, q);
+    if (q == 0) {
+      float w1, w2, w3;
+      idw(res.d1, res.d2, res.d3, w1, w2, w3);
+      s_row[jl] = u;
+      s_idx[jl] = make_int4(res.i1, res.i2, res.i3, 0);
+      s_w[jl] = make_float4(w1, w2, w3, 0.0f);
+      if (dist) {
+        float* D = dist + ((size_t)b * n + u) * 3;
+        int32_t* I = idx + ((size_t)b * n + u) * 3;
+        D[0] = res.d1; D[1] = res.d2; D[2] = res.d3;
+        I[0] = res.i1; I[1] = res.i2; I[2] = res.i3;
+      }
+    }
+  }
+  __syncthreads();
+  // 4. the rows
+  fp_write_rows<V2, V1, true, UN>(p, b, 0, j0, s_idx, s_w, s_row);
 }
 
 // Several FP layers in one launch (the FP layers that wait for the same sampler): logical
@@ -577,7 +743,7 @@ struct FpPlan {
 // The search (xyz1, xyz2) or precomputed neighbours (pdist, pidx).
 int fp_plan(const float* xyz1, const float* xyz2, const float* pdist, const int32_t* pidx,
             const void* ugrid, const float* points1, int C1, const float* points2, int C2,
-            int B, int n, int m, float* out, FpPlan& f) {
+            int B, int n, int m, float* out, FpPlan& f, bool split = true) {
   const bool pre = pdist != nullptr;
   // interpolated columns of 4 floats when C2 % 4 == 0 (16 B aligned loads and, on rows that
   // start 16 B aligned, stores); concat columns of 4 when C1 % 4 == 0 as well
@@ -588,7 +754,7 @@ int fp_plan(const float* xyz1, const float* xyz2, const float* pdist, const int3
   // split the channels over grid.z until ~2 workgroups per CU, keeping >= 16 vector columns
   // per workgroup and (search variant) not re-running a long known-point scan too often
   int zsplit = 1;
-  while ((long long)row_blocks * B * zsplit < PN2_FP_MIN_BLOCKS &&
+  while (split && (long long)row_blocks * B * zsplit < PN2_FP_MIN_BLOCKS &&
          coutv / (zsplit * 2) >= PN2_FP_MIN_COLS &&
          (pre || (long long)m * zsplit * 2 <= PN2_FP_SCAN_BUDGET))
     zsplit *= 2;
@@ -637,6 +803,29 @@ int fp_launch(const float* xyz1, const float* xyz2, const float* pdist, const in
   const int rc = fp_plan(xyz1, xyz2, pdist, pidx, ugrid, points1, C1, points2, C2, B, n, m, out, f);
   if (rc != PN2_OK) return rc;
   PN2_FP_DISPATCH(fp_fused_kernel, f, f.p, f.blocks, stream);
+  PN2_RETURN_LAUNCH();
+}
+
+// pn2_fp_grid_fused: one workgroup per 64 unknowns and all columns (no channel split: each
+// workgroup searches its rows once)
+int fp_grid_launch(const float* xyz1, const float* xyz2, const void* ugrid, const float* points1,
+                   int C1, const float* points2, int C2, int B, int n, int m, float* out,
+                   float* dist, int32_t* idx, hipStream_t stream) {
+  FpPlan f;
+  const int rc = fp_plan(xyz1, xyz2, nullptr, nullptr, ugrid, points1, C1, points2, C2, B, n, m,
+                         out, f, /*split=*/false);
+  if (rc != PN2_OK) return rc;
+  const dim3 grid(xcd_grid(f.blocks)), blk(kNNBlock);
+  const size_t lds = fp_grid_lds(m);
+  const int un = fp_unroll();
+#define PN2_FPG(V2, V1)                                                                        \
+  if (un == 1) hipLaunchKernelGGL((fp_grid_fused_kernel<V2, V1, 1>), grid, blk, lds, stream, f.p, dist, idx); \
+  else if (un == 4) hipLaunchKernelGGL((fp_grid_fused_kernel<V2, V1, 4>), grid, blk, lds, stream, f.p, dist, idx); \
+  else hipLaunchKernelGGL((fp_grid_fused_kernel<V2, V1, 2>), grid, blk, lds, stream, f.p, dist, idx)
+  if (f.v1) { PN2_FPG(4, 4); }
+  else if (f.v2) { PN2_FPG(4, 1); }
+  else { PN2_FPG(1, 1); }
+#undef PN2_FPG
   PN2_RETURN_LAUNCH();
 }
 
@@ -783,6 +972,21 @@ int pn2_fp_apply(const float* dist, const int32_t* idx, const void* unknown_grid
   if (m == 0 && C2 > 0) return PN2_EINVAL;
   return pn2::fp_launch(nullptr, nullptr, dist, idx, unknown_grid, points1, C1, points2, C2, B,
                         n, m, out, (hipStream_t)stream);
+}
+
+int pn2_fp_grid_fused(const float* xyz1, const float* xyz2, const void* unknown_grid,
+                      const float* points1, int C1, const float* points2, int C2, int B, int n,
+                      int m, float* out, float* dist, int32_t* idx, pn2_stream_t stream) {
+  if (B < 0 || n < 0 || m < 1 || m > pn2::kFpGridMaxKnown || C1 < 0 || C2 < 0 || B > 65535)
+    return PN2_EINVAL;
+  if (!points1 && C1 != 0) return PN2_EINVAL;
+  if ((dist == nullptr) != (idx == nullptr)) return PN2_EINVAL;
+  if ((long long)B * n == 0) return PN2_OK;
+  if (C1 + C2 == 0) return dist ? PN2_EINVAL : PN2_OK;  // (the search alone: pn2_three_nn_grid)
+  if (!xyz2 || (!xyz1 && !unknown_grid) || !out || (C2 > 0 && !points2))
+    return PN2_EINVAL;
+  return pn2::fp_grid_launch(xyz1, xyz2, unknown_grid, points1, C1, points2, C2, B, n, m, out,
+                             dist, idx, (hipStream_t)stream);
 }
 
 int pn2_three_nn_grid(const void* known_grid, const void* unknown_grid, const float* xyz1,

@@ -217,12 +217,16 @@ def group_pool(new_points, pooling="max", grouped_xyz=None):
     return out
 
 
+FP_GRID_MAX_KNOWN = 4096  # pn2_fp_grid_fused's LDS bound on m
+
+
 def fp_interpolate(xyz1, xyz2, points1, points2, known_grid=None, unknown_grid=None,
                    return_nn=False):
     """Geometry of pointnet_fp_module (pointnet_util.py:218-228), before its MLP:
     three_nn, IDW weights, three_interpolate and concat [interpolated, points1].
     Returns (B, n, C2 + C1). known_grid / unknown_grid: optional grid.PointGrid over xyz2 /
-    xyz1 for the neighbour search (built here when the search is large).
+    xyz1 for the neighbour search. A large search without a known grid (FP4) is ONE launch,
+    pn2_fp_grid_fused, whose workgroups grid the known points in LDS themselves.
     return_nn: also return the three_nn (dist, idx) the layer used, or None when the search
     ran fused inside the interpolation kernel (pn2_fp_fused keeps them in registers)."""
     xyz1 = device_tensor(xyz1, "xyz1", torch.float32)
@@ -242,7 +246,21 @@ def fp_interpolate(xyz1, xyz2, points1, points2, known_grid=None, unknown_grid=N
     else:
         C1 = 0
     nn = None
-    if known_grid is not None or tf_interpolate.use_grid(n, m):
+    if known_grid is None and tf_interpolate.use_grid(n, m) and m <= FP_GRID_MAX_KNOWN \
+            and C1 + C2 > 0:
+        # one launch: each workgroup grids the known points in LDS, searches, writes its rows
+        if unknown_grid is not None and not unknown_grid.matches(xyz1):
+            raise InvalidArgumentError("fp_interpolate: the unknown grid was built over other points")
+        out = torch.empty((B, n, C2 + C1), dtype=torch.float32, device=xyz1.device)
+        if return_nn:
+            nn = (torch.empty((B, n, 3), dtype=torch.float32, device=xyz1.device),
+                  torch.empty((B, n, 3), dtype=torch.int32, device=xyz1.device))
+        check(lib().pn2_fp_grid_fused(ptr(xyz1), ptr(xyz2),
+                                      None if unknown_grid is None else ptr(unknown_grid.buf),
+                                      ptr(points1), C1, ptr(points2), C2, B, n, m, ptr(out),
+                                      ptr(nn[0]) if nn else None, ptr(nn[1]) if nn else None,
+                                      stream_of(xyz1)), "fp_interpolate")
+    elif known_grid is not None or tf_interpolate.use_grid(n, m):
         nn = tf_interpolate.three_nn(xyz1, xyz2, known_grid, unknown_grid)
         out = fp_apply(nn, points1, points2, unknown_grid)
     else:

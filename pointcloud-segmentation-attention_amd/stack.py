@@ -139,8 +139,10 @@ LANE_JOIN = os.environ.get("PN2_LANE_JOIN") == "1"
 SEG_MERGE = os.environ.get("PN2_SEG_MERGE") == "1"
 # lane-end events with timing (DIAGNOSTIC: bench.py --timeline sets it before the pipeline)
 TIMING_EVENTS = False
-# NN4_LANE (A/B, PN2_NN4_LANE=n): the lane of FP4's neighbour search on the SSG step (2: with
-# its interpolation)
+# FP4_SPLIT (A/B, PN2_FP4_SPLIT=1): FP4 as the round-3 launches (grid build, three_nn over it,
+# then the interpolation: tasks nn4 and fp4) instead of one pn2_fp_grid_fused launch;
+# NN4_LANE (PN2_NN4_LANE=n): then the lane of nn4 (2: with the interpolation)
+FP4_SPLIT = os.environ.get("PN2_FP4_SPLIT") == "1"
 NN4_LANE = int(os.environ.get("PN2_NN4_LANE", "2"))
 # DIAGNOSTIC (PN2_DUP_TASKS=sa1,fp4,...): the named tasks run twice in their captured graph
 # (same inputs, same results), so a bench run prices one extra copy of each -- its marginal
@@ -408,9 +410,9 @@ class Step:
             tasks.append(Task("fps234", chain_lane, ("fps1",), lambda: [fps(i)() for i in (1, 2, 3)]))
             sampled = ("fps1", "fps234", "fps234", "fps234")
         tasks.append(Task("sa1", 1, (sampled[0],), sa(0)))
-        if big and tf_interpolate.use_grid(int(inp["xyz"].shape[1]), SSG_SA[0][0]):
-            # FP4 on the SA1 grid: its neighbour search (the known grid's build + the search)
-            # and its interpolation as two tasks of lane 2 (one launch segment)
+        if FP4_SPLIT and big and tf_interpolate.use_grid(int(inp["xyz"].shape[1]), SSG_SA[0][0]):
+            # (A/B) FP4 as three launches: the known grid's build + the search (task nn4),
+            # then the interpolation (task fp4), two tasks of lane 2 (one launch segment)
             def nn4():
                 v["nn"][3] = tf_interpolate.three_nn(v["xyz"][0], v["xyz"][1],
                                                      unknown_grid=v["grid1"])
@@ -730,7 +732,7 @@ class Step:
         its lane (the host enqueues waits after the records they refer to). A task whose
         cross-lane waits the open segment does not already imply starts a new segment, so no
         task waits for a producer it does not need. On the SSG step the side lanes become
-        [grid1], [sa1], [sa2..sa4], [nn4, fp4], [fp3..fp1]."""
+        [grid1], [sa1], [sa2..sa4], [fp4], [fp3..fp1]."""
         lane_of = {t.name: (t.lane if self.overlap else 0) for t in self.tasks}
         xdeps = {t.name: any(t.name in u.deps and lane_of[u.name] != lane_of[t.name]
                              for u in self.tasks) for t in self.tasks}

@@ -100,6 +100,13 @@ def test_grid_contract(pn2):
     assert lib.pn2_three_nn_grid(None, None, None, 1, 10, 10, None, None, None) == E
     assert lib.pn2_three_nn_grid(None, None, None, 0, 10, 10, None, None, None) == 0
     assert lib.pn2_fp_apply(None, None, None, None, 3, None, 4, 1, 4, 4, None, None) == E
+    # pn2_fp_grid_fused: m in [1, 4096], dist and idx together, points1 with C1 > 0
+    assert lib.pn2_fp_grid_fused(None, None, None, None, 0, None, 4, 1, 10, 0, None, None, None, None) == E
+    assert lib.pn2_fp_grid_fused(None, None, None, None, 0, None, 4, 1, 10, 4097, None, None, None, None) == E
+    assert lib.pn2_fp_grid_fused(None, None, None, None, 3, None, 4, 1, 10, 10, None, None, None, None) == E
+    assert lib.pn2_fp_grid_fused(None, None, None, None, 0, None, 4, 1, 10, 10, None, 1, None, None) == E
+    assert lib.pn2_fp_grid_fused(None, None, None, None, 0, None, 4, 1, 10, 10, None, None, None, None) == E
+    assert lib.pn2_fp_grid_fused(None, None, None, None, 0, None, 4, 0, 10, 10, None, None, None, None) == 0
 
 
 def test_fps_workspace_contract(pn2):

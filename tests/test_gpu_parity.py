@@ -391,6 +391,61 @@ def test_three_nn_grid(env, kind, B, n, m):
             assert torch.equal(a, fused)
 
 
+FP_GRID_CASES = NN_GRID_CASES + [("scannet", 1, 8192, 4096)]  # m at the LDS bound
+
+
+@pytest.mark.parametrize("kind,B,n,m", FP_GRID_CASES)
+@pytest.mark.parametrize("C1,C2", [(0, 128), (9, 64), (8, 70)])
+def test_fp_grid_fused(env, kind, B, n, m, C1, C2):
+    """pn2_fp_grid_fused (each workgroup grids the known points in its own LDS, searches and
+    writes its rows) = the oracle's three_nn (dist / idx bit-exact) and the fused scan's rows
+    (pn2_fp_fused, bit for bit), with and without an unknown grid ordering the rows."""
+    pkg, O, torch, dev = env
+    if kind == "fp4":
+        x1 = _cloud(pkg, "scannet", B, n, seed=4)
+        x2 = O.gather_point(x1, O.fps(x1, m))
+    elif kind == "far":
+        x1 = _cloud(pkg, "uniform", B, n, seed=4) * np.float32(20.0) - np.float32(10.0)
+        x2 = _cloud(pkg, "scannet", B, m, seed=6)
+    else:
+        x1 = _cloud(pkg, kind if kind != "dup" else "scannet", B, n, seed=4)
+        x2 = _cloud(pkg, kind, B, m, seed=8)
+        if kind == "grid":
+            x1 = x1 + np.float32(0.5)
+    t1, t2 = torch.from_numpy(x1).to(dev), torch.from_numpy(x2).to(dev)
+    rd, ri = O.three_nn(x1, x2)
+    L = pkg.lib()
+    st = torch.cuda.current_stream().cuda_stream
+    p1 = torch.from_numpy(pkg.synth.features_uniform(1, (B, n, max(C1, 1)))[..., :C1].copy()).to(dev)
+    p2 = torch.from_numpy(pkg.synth.features_uniform(2, (B, m, C2))).to(dev)
+    ref = torch.empty((B, n, C1 + C2), device=dev)
+    if m >= 3:
+        assert L.pn2_fp_fused(t1.data_ptr(), t2.data_ptr(), p1.data_ptr() if C1 else None, C1,
+                              p2.data_ptr(), C2, B, n, m, ref.data_ptr(), st) == 0
+    ug = pkg.grid.PointGrid(t1, 0.1)
+    for u in (None, ug):
+        out = torch.full((B, n, C1 + C2), float("nan"), device=dev)
+        d = torch.empty((B, n, 3), device=dev)
+        i = torch.empty((B, n, 3), dtype=torch.int32, device=dev)
+        assert L.pn2_fp_grid_fused(t1.data_ptr() if u is None else None, t2.data_ptr(),
+                                   None if u is None else u.buf.data_ptr(),
+                                   p1.data_ptr() if C1 else None, C1, p2.data_ptr(), C2, B, n, m,
+                                   out.data_ptr(), d.data_ptr(), i.data_ptr(), st) == 0
+        assert np.array_equal(i.cpu().numpy(), ri)
+        assert np.array_equal(_bits(d.cpu().numpy()), _bits(rd))
+        if m >= 3:
+            assert torch.equal(out, ref)
+        # without the neighbour outputs, through the op wrapper
+        a = pkg.pointnet_util.fp_interpolate(t1, t2, p1 if C1 else None, p2, unknown_grid=u)
+        if m >= 3 and pkg.tf_interpolate.use_grid(n, m):
+            assert torch.equal(a, ref)
+    # m beyond the LDS bound, and one neighbour output without the other
+    assert L.pn2_fp_grid_fused(t1.data_ptr(), t2.data_ptr(), None, 0, None, p2.data_ptr(), C2, B,
+                               n, 4097, out.data_ptr(), None, None, st) == -22
+    assert L.pn2_fp_grid_fused(t1.data_ptr(), t2.data_ptr(), None, 0, None, p2.data_ptr(), C2, B,
+                               n, m, out.data_ptr(), d.data_ptr(), None, st) == -22
+
+
 @pytest.mark.parametrize("C", [1, 16, 128, 512])
 def test_three_interpolate_and_idw(env, C):
     pkg, O, torch, dev = env

@@ -42,7 +42,7 @@ def test_ssg_side_lane_segments():
     step.overlap = True
     keys = [pkg.stack.Step.segment_key(s) for s in step.segments()]
     # SA1's grouping waits for the SA1 sampler only, not for the later samplers' chain
-    assert keys == ["grid1", "fps1", "fps234", "sa1", "nn4+fp4", "sa234", "fp123"]
+    assert keys == ["grid1", "fps1", "fps234", "sa1", "fp4", "sa234", "fp123"]
 
 
 @pytest.mark.parametrize("config,layout,want", [("cfg2", "b", 4), ("cfg2", "a", 3),

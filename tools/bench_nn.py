@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Micro-benchmark of the three_nn paths at FP4 size (B=16, n=8192 cloud points, m=1024 FPS
 centres): brute-force scan, grid search (LDS-staged / global), with and without the unknown
-grid ordering. HIP events, median of 20."""
+grid ordering; FP4 whole as three launches vs pn2_fp_grid_fused. HIP events, median of 20."""
 import importlib
 import json
 import os
@@ -46,6 +46,28 @@ def main():
             r = timeit(lambda: L.pn2_three_nn_grid(kg.buf.data_ptr(), None if u is None else u.buf.data_ptr(), t1.data_ptr(), B, n, m, dist.data_ptr(), idx.data_ptr(), st))
             assert torch.equal(idx, ref[1]) and torch.equal(dist, ref[0])
             res[f"grid edge={edge} {name}"] = r
+    # FP4 whole: grid build + three_nn_grid + fp_apply (three launches) vs pn2_fp_grid_fused
+    p2 = torch.rand((B, m, 128), device=dev)
+    out = torch.empty((B, n, 128), device=dev)
+    out2 = torch.empty((B, n, 128), device=dev)
+
+    def three_launches():
+        kg = pkg.grid.PointGrid(k, 0.0)
+        L.pn2_three_nn_grid(kg.buf.data_ptr(), ug.buf.data_ptr(), t1.data_ptr(), B, n, m,
+                            dist.data_ptr(), idx.data_ptr(), st)
+        L.pn2_fp_apply(dist.data_ptr(), idx.data_ptr(), ug.buf.data_ptr(), None, 0,
+                       p2.data_ptr(), 128, B, n, m, out.data_ptr(), st)
+    res["fp4 three launches"] = timeit(three_launches)
+    res["fp4 apply only"] = timeit(lambda: L.pn2_fp_apply(
+        dist.data_ptr(), idx.data_ptr(), ug.buf.data_ptr(), None, 0, p2.data_ptr(), 128, B, n, m,
+        out.data_ptr(), st))
+    res["fp4 grid fused"] = timeit(lambda: L.pn2_fp_grid_fused(
+        None, k.data_ptr(), ug.buf.data_ptr(), None, 0, p2.data_ptr(), 128, B, n, m,
+        out2.data_ptr(), None, None, st))
+    res["fp4 grid fused +nn"] = timeit(lambda: L.pn2_fp_grid_fused(
+        None, k.data_ptr(), ug.buf.data_ptr(), None, 0, p2.data_ptr(), 128, B, n, m,
+        out2.data_ptr(), dist.data_ptr(), idx.data_ptr(), st))
+    assert torch.equal(out, out2) and torch.equal(idx, ref[1])
     res["build known grid"] = timeit(lambda: pkg.grid.PointGrid(k, 0.0))
     res["build cloud grid"] = timeit(lambda: pkg.grid.PointGrid(t1, 0.1))
     print(json.dumps({k_: round(v, 1) for k_, v in res.items()}, indent=1))
