@@ -440,9 +440,9 @@ def test_fp_grid_fused(env, kind, B, n, m, C1, C2):
         if m >= 3 and pkg.tf_interpolate.use_grid(n, m):
             assert torch.equal(a, ref)
     # m beyond the LDS bound, and one neighbour output without the other
-    assert L.pn2_fp_grid_fused(t1.data_ptr(), t2.data_ptr(), None, 0, None, p2.data_ptr(), C2, B,
+    assert L.pn2_fp_grid_fused(t1.data_ptr(), t2.data_ptr(), None, None, 0, p2.data_ptr(), C2, B,
                                n, 4097, out.data_ptr(), None, None, st) == -22
-    assert L.pn2_fp_grid_fused(t1.data_ptr(), t2.data_ptr(), None, 0, None, p2.data_ptr(), C2, B,
+    assert L.pn2_fp_grid_fused(t1.data_ptr(), t2.data_ptr(), None, None, 0, p2.data_ptr(), C2, B,
                                n, m, out.data_ptr(), d.data_ptr(), None, st) == -22
 
 
