@@ -4,7 +4,7 @@ per step the host's wait for its buffer set and its enqueue, the SA1 sampler's G
 end, and the end of each side lane, on one clock (GPU times relative to a base event recorded
 at the host's time origin, so host and GPU times agree to within the event's latency).
 
-    python tools/timeline_report.py <timeline.json> [--skip 10]"""
+    python tools/timeline_report.py <timeline.json> [--skip 10] [--lanes]"""
 import argparse
 import json
 import statistics
@@ -19,6 +19,9 @@ def main():
     ap.add_argument("path")
     ap.add_argument("--skip", type=int, default=10)
     ap.add_argument("--show", type=int, default=12)
+    ap.add_argument("--lanes", action="store_true",
+                    help="per side lane: median period between consecutive steps' ends and "
+                         "median lag of its end after the SA1 sampler's end")
     a = ap.parse_args()
     d = json.load(open(a.path))
     st = [s for s in d["steps"] if "sampler_ms" in s and "lane_end_ms" in s]
@@ -40,6 +43,13 @@ def main():
           f"{med([r['latency'] for r in body]):.3f}, enqueue -> last lane end "
           f"{med([r['enq_to_end'] for r in body]):.3f}; sampler start to next sampler start "
           f"{med(gaps):.3f}")
+    if a.lanes:
+        sb = st[a.skip:]
+        for L in sorted(sb[0]["lane_end_ms"], key=int):
+            e = [s["lane_end_ms"][L] for s in sb]
+            lag = [s["lane_end_ms"][L] - s["sampler_ms"][1] for s in sb]
+            print(f"lane {L}: period {med([y - x for x, y in zip(e, e[1:])]):.3f} ms, end after "
+                  f"the sampler's {med(lag):.3f} ms")
     print("first steps (ms from the start): k, host wait start, enqueue, sampler start, end, last lane end")
     for s, r in zip(st[:a.show], rows[:a.show]):
         print(f"  {r['k']:3d}  {s['host_ms'][0]:8.3f} {s['host_ms'][1]:8.3f}  "
