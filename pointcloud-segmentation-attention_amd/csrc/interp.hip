@@ -177,22 +177,24 @@ PN2_DEV bool box_certifies(const GridHdr& h, float px, float py, float pz, int x
   return gap > 0.0f && d3 < gap * gap * 0.9999f;
 }
 
+#ifndef PN2_NN_ROWSPLIT
+#define PN2_NN_ROWSPLIT 1  // 0: the G lanes split each row's points (round 3; A/B builds)
+#endif
+
 // The three nearest known points of (px, py, pz) over a grid's sorted points (pts, off: in
 // LDS or global memory), lexicographic in (d, k): cubic shells of cells around the point's
-// cell until the certificate holds; G lanes (lane q of them) split each shell's cells and
-// merge their lists at its end, so all G return the same result.
+// cell until the certificate holds; G lanes (lane q of them) split each shell and merge their
+// lists at its end, so all G return the same result.
+// The split is by ROWS (a shell's (z, y) rows dealt round-robin, each lane walking whole
+// rows): a lane's dependent chain is then its quarter of the rows' offset loads, not every
+// row's (the round-3 split of each row's points left all G lanes loading every row's
+// offsets: 44 dependent round trips per lane at shell 2).
 template <int G>
 PN2_DEV Best3 grid_nn3(const GridHdr& h, const float4* __restrict__ pts,
                        const int* __restrict__ off, float px, float py, float pz, int q) {
   Best3 best;
   best3_init(best);
-  auto visit = [&](int lo, int hi) {  // sorted points [lo, hi), this lane's share
-    for (int e = lo + q; e < hi; e += G) {
-      const float4 p = pts[e];
-      best3_insert_lex(best, sqdist(p.x, p.y, p.z, px, py, pz), __float_as_int(p.w));
-    }
-  };
-  auto merged = [&]() {  // the quad's top 3 (every lane of the quad gets the same)
+  auto merged = [&]() {  // the lanes' top 3 (every lane of the G gets the same)
     Best3 mb = best;
     if constexpr (G == 4) {
       best3_merge_xor(mb, 1);
@@ -207,6 +209,40 @@ PN2_DEV Best3 grid_nn3(const GridHdr& h, const float4* __restrict__ pts,
   for (int s = 0;; ++s) {
     const int xl = cx - s, xh = cx + s, yl = cy - s, yh = cy + s, zl = cz - s, zh = cz + s;
     const int x0 = max(xl, 0), x1 = min(xh, h.nx - 1);
+#if PN2_NN_ROWSPLIT
+    auto visit = [&](int lo, int hi) {  // sorted points [lo, hi), all of them by this lane
+      int e = lo;
+      for (; e + 1 < hi; e += 2) {
+        const float4 a = pts[e], b = pts[e + 1];
+        best3_insert_lex(best, sqdist(a.x, a.y, a.z, px, py, pz), __float_as_int(a.w));
+        best3_insert_lex(best, sqdist(b.x, b.y, b.z, px, py, pz), __float_as_int(b.w));
+      }
+      if (e < hi) {
+        const float4 a = pts[e];
+        best3_insert_lex(best, sqdist(a.x, a.y, a.z, px, py, pz), __float_as_int(a.w));
+      }
+    };
+    const int ylo = max(yl, 0), yhi = min(yh, h.ny - 1), zlo = max(zl, 0), zhi = min(zh, h.nz - 1);
+    const int ny = yhi - ylo + 1;
+    int z = zlo + q / ny, y = ylo + q % ny;  // row q, then every G-th
+    for (; z <= zhi;) {
+      const int row = (z * h.ny + y) * h.nx;
+      if (s == 0 || z == zl || z == zh || y == yl || y == yh) {
+        visit(off[row + x0], off[row + x1 + 1]);  // a face row: all of x0..x1
+      } else {
+        if (xl >= 0) visit(off[row + xl], off[row + xl + 1]);
+        if (xh < h.nx) visit(off[row + xh], off[row + xh + 1]);
+      }
+      y += G;
+      while (y > yhi) { y -= ny; ++z; }
+    }
+#else
+    auto visit = [&](int lo, int hi) {  // sorted points [lo, hi), this lane's share
+      for (int e = lo + q; e < hi; e += G) {
+        const float4 p = pts[e];
+        best3_insert_lex(best, sqdist(p.x, p.y, p.z, px, py, pz), __float_as_int(p.w));
+      }
+    };
     for (int z = max(zl, 0); z <= min(zh, h.nz - 1); ++z) {
       for (int y = max(yl, 0); y <= min(yh, h.ny - 1); ++y) {
         const int row = (z * h.ny + y) * h.nx;
@@ -218,6 +254,7 @@ PN2_DEV Best3 grid_nn3(const GridHdr& h, const float4* __restrict__ pts,
         }
       }
     }
+#endif
     res = merged();
     if (xl <= 0 && yl <= 0 && zl <= 0 && xh >= h.nx - 1 && yh >= h.ny - 1 && zh >= h.nz - 1)
       break;  // every cell visited
