@@ -178,17 +178,17 @@ PN2_DEV bool box_certifies(const GridHdr& h, float px, float py, float pz, int x
 }
 
 #ifndef PN2_NN_ROWSPLIT
-#define PN2_NN_ROWSPLIT 1  // 0: the G lanes split each row's points (round 3; A/B builds)
+#define PN2_NN_ROWSPLIT 0  // 1: the G lanes split a shell's rows (A/B builds)
 #endif
 
 // The three nearest known points of (px, py, pz) over a grid's sorted points (pts, off: in
 // LDS or global memory), lexicographic in (d, k): cubic shells of cells around the point's
-// cell until the certificate holds; G lanes (lane q of them) split each shell and merge their
-// lists at its end, so all G return the same result.
-// The split is by ROWS (a shell's (z, y) rows dealt round-robin, each lane walking whole
-// rows): a lane's dependent chain is then its quarter of the rows' offset loads, not every
-// row's (the round-3 split of each row's points left all G lanes loading every row's
-// offsets: 44 dependent round trips per lane at shell 2).
+// cell until the certificate holds; G lanes (lane q of them) split each row's points and
+// merge their lists at the shell's end, so all G return the same result.
+// (A/B, PN2_NN_ROWSPLIT=1: the G lanes deal a shell's (z, y) rows round-robin, each walking
+// whole rows, so a lane loads a quarter of the rows' offsets -- measured slower, 33 -> 49 us
+// at FP4, tools/bench_nn.py, profiles/r4/rows: the lanes of a wave then run rows of different
+// lengths, and the wave runs the longest.)
 template <int G>
 PN2_DEV Best3 grid_nn3(const GridHdr& h, const float4* __restrict__ pts,
                        const int* __restrict__ off, float px, float py, float pz, int q) {
