@@ -263,6 +263,60 @@ PN2_DEV Best3 grid_nn3(const GridHdr& h, const float4* __restrict__ pts,
   return res;
 }
 
+#ifndef PN2_NN_MARGIN
+#define PN2_NN_MARGIN 0.6f  // the wave box's margin, in cell edges (A/B; 0: the shell walk only)
+#endif
+
+// grid_nn3 for the unknowns of a whole wave (its G-lane groups; `valid`: this group has one),
+// in two passes:
+//   1. the wave's unknowns' bounding box, grown by PN2_NN_MARGIN cell edges, rounded out to
+//      cells: every group scans every known point of that cell box -- the same rows, the same
+//      trip counts and the same LDS addresses (broadcast) for the whole wave, no divergence;
+//   2. a group whose third-nearest distance the box does not certify (box_certifies: every
+//      point outside it is farther) walks the shells (grid_nn3) from scratch.
+// The unknowns of a wave are consecutive in the order of the SA1 grid, so its box is small:
+// at FP4 (ScanNet-like clouds, 16 unknowns a wave, the automatic edge) ~80 candidates per
+// unknown against ~69 for the walk, with none of the walk's per-row overhead or divergence,
+// and ~1 unknown in 10^4 falls back (tools/sim_nn_box.py). Exact either way: the result is
+// the (d, k)-lexicographic top 3 of a point set that provably contains it.
+template <int G>
+PN2_DEV Best3 grid_nn3_wave(const GridHdr& h, const float4* __restrict__ pts,
+                            const int* __restrict__ off, float px, float py, float pz, int q,
+                            bool valid) {
+  const float inf = __builtin_inff();
+  // (every lane takes part in the reductions, before any divergence)
+  const float bx0 = wave_min_f(valid ? px : inf), bx1 = wave_max_f(valid ? px : -inf);
+  const float by0 = wave_min_f(valid ? py : inf), by1 = wave_max_f(valid ? py : -inf);
+  const float bz0 = wave_min_f(valid ? pz : inf), bz1 = wave_max_f(valid ? pz : -inf);
+  Best3 best;
+  best3_init(best);
+  if (!(bx0 <= bx1 && by0 <= by1 && bz0 <= bz1) || PN2_NN_MARGIN <= 0.0f)
+    return valid ? grid_nn3<G>(h, pts, off, px, py, pz, q) : best;  // (NaN box: the walk)
+  const float mg = h.inv > 0.0f ? PN2_NN_MARGIN / h.inv : 0.0f;  // inv = 0: one cell
+  const int cx0 = cell_coord(bx0 - mg, h.ox, h.inv, h.nx), cx1 = cell_coord(bx1 + mg, h.ox, h.inv, h.nx);
+  const int cy0 = cell_coord(by0 - mg, h.oy, h.inv, h.ny), cy1 = cell_coord(by1 + mg, h.oy, h.inv, h.ny);
+  const int cz0 = cell_coord(bz0 - mg, h.oz, h.inv, h.nz), cz1 = cell_coord(bz1 + mg, h.oz, h.inv, h.nz);
+  for (int z = cz0; z <= cz1; ++z) {
+    for (int y = cy0; y <= cy1; ++y) {
+      const int row = (z * h.ny + y) * h.nx;
+      const int hi = off[row + cx1 + 1];
+      for (int e = off[row + cx0] + q; e < hi; e += G) {
+        const float4 p = pts[e];
+        best3_insert_lex(best, sqdist(p.x, p.y, p.z, px, py, pz), __float_as_int(p.w));
+      }
+    }
+  }
+  if constexpr (G == 4) {
+    best3_merge_xor(best, 1);
+    best3_merge_xor(best, 2);
+  }
+  if (!valid) return best;
+  const bool all = cx0 == 0 && cy0 == 0 && cz0 == 0 && cx1 == h.nx - 1 && cy1 == h.ny - 1 &&
+                   cz1 == h.nz - 1;
+  if (all || box_certifies(h, px, py, pz, cx0, cx1, cy0, cy1, cz0, cz1, best.d3)) return best;
+  return grid_nn3<G>(h, pts, off, px, py, pz, q);
+}
+
 #ifndef PN2_NN_ROWS
 #define PN2_NN_ROWS 1  // row blocks per workgroup (one staging of the known grid serves K)
 #endif
@@ -303,21 +357,24 @@ __global__ __launch_bounds__(BLOCK) void three_nn_grid_kernel(
   }
   const float4* __restrict__ upts = ugrid ? grid_view(ugrid, b, n).pts : nullptr;
   for (int kb = 0; kb < K; ++kb) {  // no barriers below; a quad's lanes share i
-    const int i = ((Lg - b * R) * K + kb) * QPB + (int)threadIdx.x / G;
-    if (i >= n) break;
+    const int i0 = ((Lg - b * R) * K + kb) * QPB;
+    if (i0 >= n) break;  // (workgroup-uniform)
+    const int i = i0 + (int)threadIdx.x / G;
+    const bool valid = i < n;
+    const int ic = valid ? i : n - 1;
     float px, py, pz;
     int u;
     if (upts) {
-      const float4 U = upts[i];
+      const float4 U = upts[ic];
       px = U.x; py = U.y; pz = U.z;
       u = __float_as_int(U.w);
     } else {
-      const float* U = xyz1 + ((size_t)b * n + i) * 3;
+      const float* U = xyz1 + ((size_t)b * n + ic) * 3;
       px = U[0]; py = U[1]; pz = U[2];
-      u = i;
+      u = ic;
     }
-    const Best3 res = grid_nn3<G>(h, pts, off, px, py, pz, q);
-    if (q == 0) {
+    const Best3 res = grid_nn3_wave<G>(h, pts, off, px, py, pz, q, valid);
+    if (valid && q == 0) {
       float* D = dist + ((size_t)b * n + u) * 3;
       int32_t* I = idx + ((size_t)b * n + u) * 3;
       D[0] = res.d1; D[1] = res.d2; D[2] = res.d3;
@@ -587,7 +644,7 @@ __global__ __launch_bounds__(kNNBlock) void fp_fused_kernel(FpLayer p) {
 //      edge of pn2_grid_build: ~2 points per cell, at most max(m, 64) cells);
 //   2. a counting sort of the known points into cells, in LDS (the order inside a cell is
 //      the order of the atomics -- the (d, k)-lexicographic search does not depend on it);
-//   3. the quad search (grid_nn3) of each unknown, its IDW weights, optionally dist / idx;
+//   3. the quad search (grid_nn3_wave) of each unknown, its IDW weights, optionally dist / idx;
 //   4. the rows (fp_write_rows).
 // A cloud's 128 workgroups each redo steps 1-2 over 12 KB of L2-resident points, which costs
 // less than the launch and the dependency they replace. Bit-identical to the three-launch path.
@@ -692,20 +749,22 @@ __global__ __launch_bounds__(kNNBlock) void fp_grid_fused_kernel(FpLayer p, floa
   // 3. the search, a quad per unknown (the quad's lanes share j)
   const int jl = t / kNNGroup, q = t & (kNNGroup - 1);
   const int j = j0 + jl;
-  if (j < n) {
+  {
+    const bool valid = j < n;
+    const int jc = valid ? j : n - 1;
     float px, py, pz;
     int u;
     if (p.ugrid) {
-      const float4 U = grid_view(p.ugrid, b, n).pts[j];
+      const float4 U = grid_view(p.ugrid, b, n).pts[jc];
       px = U.x; py = U.y; pz = U.z;
       u = __float_as_int(U.w);
     } else {
-      const float* U = p.xyz1 + ((size_t)b * n + j) * 3;
+      const float* U = p.xyz1 + ((size_t)b * n + jc) * 3;
       px = U[0]; py = U[1]; pz = U[2];
-      u = j;
+      u = jc;
     }
-    const Best3 res = grid_nn3<kNNGroup>(h, s_pts, s_off, px, py, pz, q);
-    if (q == 0) {
+    const Best3 res = grid_nn3_wave<kNNGroup>(h, s_pts, s_off, px, py, pz, q, valid);
+    if (valid && q == 0) {
       float w1, w2, w3;
       idw(res.d1, res.d2, res.d3, w1, w2, w3);
       s_row[jl] = u;
