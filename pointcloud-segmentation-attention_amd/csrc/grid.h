@@ -71,7 +71,9 @@ PN2_DEV int wave_incl_scan(int v, int lane) {
 // The grid's header for bbox [lo, hi] of N points (an empty / NaN-only axis as lo = hi = 0).
 // One thread computes it: pn2_grid_build's workgroup, or each workgroup of the fused FP
 // search (interp.hip), which builds a cloud's grid of known points in its own LDS.
-PN2_DEV GridHdr grid_dims(const float lo[3], const float hi[3], int N, float edge) {
+// ppc: the automatic edge's points per cell (then at most max(N * 2 / ppc, 64) cells).
+PN2_DEV GridHdr grid_dims(const float lo[3], const float hi[3], int N, float edge,
+                          float ppc = kAutoPointsPerCell) {
   GridHdr h;
   // cell edge: the caller's, or ~kAutoPointsPerCell points per cell of the bbox volume
   // (then also at most max(N, 64) cells, which bounds the grid's size for LDS staging);
@@ -80,7 +82,7 @@ PN2_DEV GridHdr grid_dims(const float lo[3], const float hi[3], int N, float edg
   float c = edge;
   if (!(c > 0.0f)) {
     const float ext = fmaxf(fmaxf(hi[0] - lo[0], hi[1] - lo[1]), hi[2] - lo[2]);
-    const double cells = fmax((double)N / kAutoPointsPerCell, 1.0);
+    const double cells = fmax((double)N / ppc, 1.0);
     double e = cbrt((double)(hi[0] - lo[0]) * (hi[1] - lo[1]) * (hi[2] - lo[2]) / cells);
     if (!(e > 0.0)) e = (double)ext / cbrt(cells);
     c = (float)e;
@@ -94,7 +96,8 @@ PN2_DEV GridHdr grid_dims(const float lo[3], const float hi[3], int N, float edg
       d[a] = floor((double)(hi[a] - lo[a]) / (double)c) + 1.0;
       cells *= d[a];
     }
-    if (cells <= (double)kGridCap && (edge > 0.0f || cells <= fmax((double)N, (double)kAutoMinCells))) {
+    if (cells <= (double)kGridCap &&
+        (edge > 0.0f || cells <= fmax(ceil((double)N * kAutoPointsPerCell / ppc), (double)kAutoMinCells))) {
       for (int a = 0; a < 3; ++a) n[a] = (int)d[a];
       ok = true;
     } else {

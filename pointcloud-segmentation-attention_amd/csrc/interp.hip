@@ -264,7 +264,7 @@ PN2_DEV Best3 grid_nn3(const GridHdr& h, const float4* __restrict__ pts,
 }
 
 #ifndef PN2_NN_MARGIN
-#define PN2_NN_MARGIN 0.6f  // the wave box's margin, in cell edges (A/B; 0: the shell walk only)
+#define PN2_NN_MARGIN 0.0f  // > 0: the wave box with this margin, in cell edges (A/B builds)
 #endif
 
 // grid_nn3 for the unknowns of a whole wave (its G-lane groups; `valid`: this group has one),
@@ -279,19 +279,30 @@ PN2_DEV Best3 grid_nn3(const GridHdr& h, const float4* __restrict__ pts,
 // unknown against ~69 for the walk, with none of the walk's per-row overhead or divergence,
 // and ~1 unknown in 10^4 falls back (tools/sim_nn_box.py). Exact either way: the result is
 // the (d, k)-lexicographic top 3 of a point set that provably contains it.
+// MEASURED SLOWER, so off by default (PN2_NN_MARGIN = 0: the shell walk alone): FP4 search
+// 34 -> 44 us standalone at margin 0.6 (43.5 / 45.6 at 0.45 / 0.8), 53 -> 160 us when the
+// unknowns come in input order (each wave's box is then the whole grid); the pipelined step
+// unchanged within noise (profiles/r4/box). The walk's cost is its ~17 inserts per lane, not
+// its row overhead or divergence, and the box scans as many candidates.
 template <int G>
 PN2_DEV Best3 grid_nn3_wave(const GridHdr& h, const float4* __restrict__ pts,
                             const int* __restrict__ off, float px, float py, float pz, int q,
                             bool valid) {
   const float inf = __builtin_inff();
+  if constexpr (!(PN2_NN_MARGIN > 0.0f)) {
+    if (valid) return grid_nn3<G>(h, pts, off, px, py, pz, q);
+    Best3 none;
+    best3_init(none);
+    return none;
+  }
   // (every lane takes part in the reductions, before any divergence)
   const float bx0 = wave_min_f(valid ? px : inf), bx1 = wave_max_f(valid ? px : -inf);
   const float by0 = wave_min_f(valid ? py : inf), by1 = wave_max_f(valid ? py : -inf);
   const float bz0 = wave_min_f(valid ? pz : inf), bz1 = wave_max_f(valid ? pz : -inf);
   Best3 best;
   best3_init(best);
-  if (!(bx0 <= bx1 && by0 <= by1 && bz0 <= bz1) || PN2_NN_MARGIN <= 0.0f)
-    return valid ? grid_nn3<G>(h, pts, off, px, py, pz, q) : best;  // (NaN box: the walk)
+  if (!(bx0 <= bx1 && by0 <= by1 && bz0 <= bz1))
+    return valid ? grid_nn3<G>(h, pts, off, px, py, pz, q) : best;  // (no valid lane)
   const float mg = h.inv > 0.0f ? PN2_NN_MARGIN / h.inv : 0.0f;  // inv = 0: one cell
   const int cx0 = cell_coord(bx0 - mg, h.ox, h.inv, h.nx), cx1 = cell_coord(bx1 + mg, h.ox, h.inv, h.nx);
   const int cy0 = cell_coord(by0 - mg, h.oy, h.inv, h.ny), cy1 = cell_coord(by1 + mg, h.oy, h.inv, h.ny);
@@ -648,10 +659,14 @@ __global__ __launch_bounds__(kNNBlock) void fp_fused_kernel(FpLayer p) {
 //   4. the rows (fp_write_rows).
 // A cloud's 128 workgroups each redo steps 1-2 over 12 KB of L2-resident points, which costs
 // less than the launch and the dependency they replace. Bit-identical to the three-launch path.
-constexpr int kFpGridMaxKnown = 4096;  // LDS: m float4 + (max(m, 64) + 1) offsets <= 80 KB
+constexpr int kFpGridMaxKnown = 4096;  // LDS: m float4 + (max(2m / ppc, 64) + 1) offsets
+#ifndef PN2_FPG_PPC
+#define PN2_FPG_PPC 2.0f  // the LDS grid's points per cell (grid_dims' automatic edge)
+#endif
 
 inline size_t fp_grid_lds(int m) {
-  return (size_t)m * 16 + (size_t)((m > kAutoMinCells ? m : kAutoMinCells) + 1) * 4;
+  const size_t cells = (size_t)ceil((double)m * kAutoPointsPerCell / PN2_FPG_PPC);
+  return (size_t)m * 16 + (std::max(cells, (size_t)kAutoMinCells) + 1) * 4;
 }
 
 template <int V2, int V1, int UN>
@@ -704,7 +719,7 @@ __global__ __launch_bounds__(kNNBlock) void fp_grid_fused_kernel(FpLayer p, floa
       for (int i = 1; i < NW; ++i) { lo[a] = fminf(lo[a], red[a][i]); hi[a] = fmaxf(hi[a], red[3 + a][i]); }
       if (!(hi[a] >= lo[a])) { lo[a] = 0.0f; hi[a] = 0.0f; }  // NaN-only axis
     }
-    sh = grid_dims(lo, hi, m, 0.0f);
+    sh = grid_dims(lo, hi, m, 0.0f, PN2_FPG_PPC);
   }
   __syncthreads();
   const GridHdr h = sh;
