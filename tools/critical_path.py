@@ -26,6 +26,7 @@ from collections import defaultdict
 TASKS = [("fps_hotcull", "fps1"), ("fps_v9", "fps1"), ("fps_chain", "fps234"),
          ("ball_group_layers", "sa234"), ("fp_fused_layers", "fp123"),
          ("ball_query_grid", "sa1"), ("three_nn_grid", "nn4"), ("fp_fused_kernel", "fp4"),
+         ("fp_grid_fused", "fp4"),
          ("grid_build", "grid"), ("group_concat", "grp"), ("attn", "att")]
 # task -> producers on other lanes (grid builds are matched on their own queue)
 DEPS = {"sa1": ["fps1"], "nn4": ["fps1"], "fp4": ["fps1"], "fps234": ["fps1"],
