@@ -189,9 +189,9 @@ PN2_DEV bool box_certifies(const GridHdr& h, float px, float py, float pz, int x
 // whole rows, so a lane loads a quarter of the rows' offsets -- measured slower, 33 -> 49 us
 // at FP4, tools/bench_nn.py, profiles/r4/rows: the lanes of a wave then run rows of different
 // lengths, and the wave runs the longest.)
-template <int G>
+template <int G, typename Off>
 PN2_DEV Best3 grid_nn3(const GridHdr& h, const float4* __restrict__ pts,
-                       const int* __restrict__ off, float px, float py, float pz, int q) {
+                       const Off* __restrict__ off, float px, float py, float pz, int q) {
   Best3 best;
   best3_init(best);
   auto merged = [&]() {  // the lanes' top 3 (every lane of the G gets the same)
@@ -284,13 +284,13 @@ PN2_DEV Best3 grid_nn3(const GridHdr& h, const float4* __restrict__ pts,
 // unknowns come in input order (each wave's box is then the whole grid); the pipelined step
 // unchanged within noise (profiles/r4/box). The walk's cost is its ~17 inserts per lane, not
 // its row overhead or divergence, and the box scans as many candidates.
-template <int G>
+template <int G, typename Off>
 PN2_DEV Best3 grid_nn3_wave(const GridHdr& h, const float4* __restrict__ pts,
-                            const int* __restrict__ off, float px, float py, float pz, int q,
+                            const Off* __restrict__ off, float px, float py, float pz, int q,
                             bool valid) {
   const float inf = __builtin_inff();
   if constexpr (!(PN2_NN_MARGIN > 0.0f)) {
-    if (valid) return grid_nn3<G>(h, pts, off, px, py, pz, q);
+    if (valid) return grid_nn3<G, Off>(h, pts, off, px, py, pz, q);
     Best3 none;
     best3_init(none);
     return none;
@@ -302,7 +302,7 @@ PN2_DEV Best3 grid_nn3_wave(const GridHdr& h, const float4* __restrict__ pts,
   Best3 best;
   best3_init(best);
   if (!(bx0 <= bx1 && by0 <= by1 && bz0 <= bz1))
-    return valid ? grid_nn3<G>(h, pts, off, px, py, pz, q) : best;  // (no valid lane)
+    return valid ? grid_nn3<G, Off>(h, pts, off, px, py, pz, q) : best;  // (no valid lane)
   const float mg = h.inv > 0.0f ? PN2_NN_MARGIN / h.inv : 0.0f;  // inv = 0: one cell
   const int cx0 = cell_coord(bx0 - mg, h.ox, h.inv, h.nx), cx1 = cell_coord(bx1 + mg, h.ox, h.inv, h.nx);
   const int cy0 = cell_coord(by0 - mg, h.oy, h.inv, h.ny), cy1 = cell_coord(by1 + mg, h.oy, h.inv, h.ny);
@@ -325,7 +325,7 @@ PN2_DEV Best3 grid_nn3_wave(const GridHdr& h, const float4* __restrict__ pts,
   const bool all = cx0 == 0 && cy0 == 0 && cz0 == 0 && cx1 == h.nx - 1 && cy1 == h.ny - 1 &&
                    cz1 == h.nz - 1;
   if (all || box_certifies(h, px, py, pz, cx0, cx1, cy0, cy1, cz0, cz1, best.d3)) return best;
-  return grid_nn3<G>(h, pts, off, px, py, pz, q);
+  return grid_nn3<G, Off>(h, pts, off, px, py, pz, q);
 }
 
 #ifndef PN2_NN_ROWS
@@ -384,7 +384,7 @@ __global__ __launch_bounds__(BLOCK) void three_nn_grid_kernel(
       px = U[0]; py = U[1]; pz = U[2];
       u = ic;
     }
-    const Best3 res = grid_nn3_wave<G>(h, pts, off, px, py, pz, q, valid);
+    const Best3 res = grid_nn3_wave<G, int>(h, pts, off, px, py, pz, q, valid);
     if (valid && q == 0) {
       float* D = dist + ((size_t)b * n + u) * 3;
       int32_t* I = idx + ((size_t)b * n + u) * 3;
@@ -467,12 +467,18 @@ struct FpLayer {
   FastDiv div_cw;
 };
 
+// One output row's three neighbours (I.x..z), IDW weights (W.x..z) and row index r.
+struct FpRow {
+  int4 I;
+  float4 W;
+  int r;
+};
+
 // The output rows j0 .. j0 + 63 of cloud b, column slice zb, from the rows' three neighbours
-// and IDW weights (s_idx / s_w by row of the workgroup; PRE: output row s_row[rl], else
-// j0 + rl): interpolated columns ((p1*w1)+(p2*w2))+(p3*w3), then the points1 concat.
-template <int V2, int V1, bool PRE, int UN>
-PN2_DEV void fp_write_rows(const FpLayer& p, int b, int zb, int j0, const int4* s_idx,
-                           const float4* s_w, const int* s_row) {
+// and IDW weights (row(rl) -> FpRow for the workgroup's row rl): interpolated columns
+// ((p1*w1)+(p2*w2))+(p3*w3), then the points1 concat.
+template <int V2, int V1, int UN, typename RowFn>
+PN2_DEV void fp_write_rows(const FpLayer& p, int b, int zb, int j0, RowFn row) {
   const float* __restrict__ points1 = p.points1;
   const float* __restrict__ points2 = p.points2;
   float* __restrict__ out = p.out;
@@ -510,15 +516,14 @@ PN2_DEV void fp_write_rows(const FpLayer& p, int b, int zb, int j0, const int4* 
       int c = cb + ((e < elems ? e : e0) - rl * cw);
       ok[u] = e < elems && c < ce;
       c = min(c, ce - 1);  // (a skipped element still loads from inside the rows)
-      int r;
-      if constexpr (PRE) r = s_row[rl];
-      else r = j0 + rl;
+      const FpRow rw = row(rl);
+      const int r = rw.r;
       cat[u] = c >= c2v;
-      W[u] = s_w[rl];
+      W[u] = rw.W;
       if constexpr (V1 == V2) {
         // one width: no branch; a concat element loads its points1 value three times (same
         // address) and is selected as is
-        const int4 I = s_idx[rl];
+        const int4 I = rw.I;
         const V2T* P1v = reinterpret_cast<const V2T*>(P1);
         const V2T* pa = cat[u] ? P1v + (size_t)r * (C1 / V1) + (c - c2v) : P2 + (size_t)I.x * c2v + c;
         const V2T* pb = cat[u] ? pa : P2 + (size_t)I.y * c2v + c;
@@ -530,7 +535,7 @@ PN2_DEV void fp_write_rows(const FpLayer& p, int b, int zb, int j0, const int4* 
         o[u] = (size_t)r * Cout + (size_t)c * V2;  // (C2 + (c - c2v) V1 = c V2 here)
       } else if (!cat[u]) {
         q[u] = V1T{};
-        const int4 I = s_idx[rl];
+        const int4 I = rw.I;
         a[u] = P2[(size_t)I.x * c2v + c];
         bb[u] = P2[(size_t)I.y * c2v + c];
         cc[u] = P2[(size_t)I.z * c2v + c];
@@ -630,7 +635,10 @@ PN2_DEV void fp_fused_body(const FpLayer& p, int Lg) {
     }
   }
   __syncthreads();
-  fp_write_rows<V2, V1, PRE, UN>(p, b, zb, j0, s_idx, s_w, s_row);
+  fp_write_rows<V2, V1, UN>(p, b, zb, j0, [&](int rl) {
+    if constexpr (PRE) return FpRow{s_idx[rl], s_w[rl], s_row[rl]};
+    else return FpRow{s_idx[rl], s_w[rl], j0 + rl};
+  });
 }
 
 // Workgroup (x, b, z) of one layer: unknown points [64x, 64x+64) of cloud b, columns
@@ -664,22 +672,27 @@ constexpr int kFpGridMaxKnown = 4096;  // LDS: m float4 + (max(2m / ppc, 64) + 1
 #define PN2_FPG_PPC 2.0f  // the LDS grid's points per cell (grid_dims' automatic edge)
 #endif
 
+// dynamic LDS: the m sorted points, then the ncell + 1 cell offsets as uint16 (m <= 4096)
 inline size_t fp_grid_lds(int m) {
   const size_t cells = (size_t)ceil((double)m * kAutoPointsPerCell / PN2_FPG_PPC);
-  return (size_t)m * 16 + (std::max(cells, (size_t)kAutoMinCells) + 1) * 4;
+  return (size_t)m * 16 + ((std::max(cells, (size_t)kAutoMinCells) + 1) * 2 + 3) / 4 * 4;
 }
 
-template <int V2, int V1, int UN>
+// KPT: known points per thread (m <= KPT * kNNBlock), kept in registers between the count
+// and the scatter. LDS at FP4 (m = 1024, B = 16): 16 KB points + 2 KB offsets + 1.75 KB, so
+// 8 workgroups fit a CU (the LDS bound; their 32 waves are the wave bound).
+template <int V2, int V1, int UN, int KPT>
 __global__ __launch_bounds__(kNNBlock) void fp_grid_fused_kernel(FpLayer p, float* __restrict__ dist,
                                                               int32_t* __restrict__ idx) {
   constexpr int NW = kNNBlock / kWave;
   extern __shared__ float4 s_pts[];  // m known points sorted by cell, then ncell + 1 offsets
-  __shared__ int4 s_idx[kNNRows];
-  __shared__ float4 s_w[kNNRows];
-  __shared__ int s_row[kNNRows];
-  __shared__ float red[6][NW];
-  __shared__ int wsum[NW];
-  __shared__ GridHdr sh;
+  __shared__ int4 s_idx[kNNRows];     // the row's three neighbours and its output row
+  __shared__ float s_wv[3][kNNRows];  // the row's IDW weights; before the search: the build's
+                                      // scratch (bbox partials, scan partials, header)
+  float(*red)[NW] = reinterpret_cast<float(*)[NW]>(&s_wv[0][0]);  // [6][NW] <= 64 floats
+  int* wsum = reinterpret_cast<int*>(&s_wv[1][0]);
+  GridHdr* shp = reinterpret_cast<GridHdr*>(&s_wv[2][0]);
+  static_assert(6 * NW <= kNNRows && sizeof(GridHdr) <= kNNRows * 4, "build scratch fits");
   const int n = p.n, m = p.m;
   const int R = (n + kNNRows - 1) / kNNRows;
   const int total = R * p.B;
@@ -689,16 +702,21 @@ __global__ __launch_bounds__(kNNBlock) void fp_grid_fused_kernel(FpLayer p, floa
   const int j0 = (Lg - b * R) * kNNRows;
   const int t = threadIdx.x, lane = t & (kWave - 1), w = t / kWave;
   const float* __restrict__ K = p.xyz2 + (size_t)b * m * 3;
-  int* s_off = (int*)(s_pts + m);
+  uint16_t* s_off = reinterpret_cast<uint16_t*>(s_pts + m);
+  uint32_t* s_cnt = reinterpret_cast<uint32_t*>(s_pts + m);  // the offsets as counter pairs
 
   // 1. bounding box -> header
   float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
-  for (int k = t; k < m; k += kNNBlock) {
 #pragma unroll
-    for (int a = 0; a < 3; ++a) {
-      const float v = K[3 * k + a];
-      mn[a] = fminf(mn[a], v);
-      mx[a] = fmaxf(mx[a], v);
+  for (int i = 0; i < KPT; ++i) {
+    const int k = t + i * kNNBlock;
+    if (k < m) {
+#pragma unroll
+      for (int a = 0; a < 3; ++a) {
+        const float v = K[3 * k + a];
+        mn[a] = fminf(mn[a], v);
+        mx[a] = fmaxf(mx[a], v);
+      }
     }
   }
 #pragma unroll
@@ -719,10 +737,10 @@ __global__ __launch_bounds__(kNNBlock) void fp_grid_fused_kernel(FpLayer p, floa
       for (int i = 1; i < NW; ++i) { lo[a] = fminf(lo[a], red[a][i]); hi[a] = fmaxf(hi[a], red[3 + a][i]); }
       if (!(hi[a] >= lo[a])) { lo[a] = 0.0f; hi[a] = 0.0f; }  // NaN-only axis
     }
-    sh = grid_dims(lo, hi, m, 0.0f, PN2_FPG_PPC);
+    *shp = grid_dims(lo, hi, m, 0.0f, PN2_FPG_PPC);
   }
   __syncthreads();
-  const GridHdr h = sh;
+  const GridHdr h = *shp;
   auto cell_at = [&](float x, float y, float z) {
     const int ix = cell_coord(x, h.ox, h.inv, h.nx);
     const int iy = cell_coord(y, h.oy, h.inv, h.ny);
@@ -730,34 +748,50 @@ __global__ __launch_bounds__(kNNBlock) void fp_grid_fused_kernel(FpLayer p, floa
     return (iz * h.ny + iy) * h.nx + ix;
   };
 
-  // 2. counting sort: counts at s_off[1 + c], exclusive scan in place, then the scatter uses
-  // s_off[1 + c] as cell c's cursor, which leaves it at cell c's end = cell c+1's start
-  for (int i = t; i <= h.ncell; i += kNNBlock) s_off[i] = 0;
+  // 2. counting sort in one atomic pass: each point's count atomic (16-bit halves of 32-bit
+  // words; counts <= m < 2^16) returns its rank in its cell, kept with its cell in registers;
+  // an exclusive scan turns the counts into the cells' offsets; the scatter needs no cursor
+  for (int i = t; i < (h.ncell + 2) / 2; i += kNNBlock) s_cnt[i] = 0u;
   __syncthreads();
-  for (int k = t; k < m; k += kNNBlock)
-    atomicAdd(&s_off[1 + cell_at(K[3 * k + 0], K[3 * k + 1], K[3 * k + 2])], 1);
+  int kc[KPT], kr[KPT];
+#pragma unroll
+  for (int i = 0; i < KPT; ++i) {
+    const int k = t + i * kNNBlock;
+    kc[i] = 0;
+    kr[i] = 0;
+    if (k < m) {
+      const int c = cell_at(K[3 * k + 0], K[3 * k + 1], K[3 * k + 2]);
+      const int sh = 16 * (c & 1);
+      const uint32_t old = atomicAdd(&s_cnt[c >> 1], 1u << sh);
+      kc[i] = c;
+      kr[i] = (int)((old >> sh) & 0xFFFFu);
+    }
+  }
   __syncthreads();
   {
     const int per = (h.ncell + kNNBlock - 1) / kNNBlock;
     const int s0 = t * per, s1 = min(s0 + per, h.ncell);
     int sum = 0;
-    for (int i = s0; i < s1; ++i) sum += s_off[1 + i];
+    for (int i = s0; i < s1; ++i) sum += s_off[i];
     const int incl = wave_incl_scan(sum, lane);
     if (lane == kWave - 1) wsum[w] = incl;
     __syncthreads();
     int base = incl - sum;
     for (int i = 0; i < w; ++i) base += wsum[i];
     for (int i = s0; i < s1; ++i) {
-      const int c = s_off[1 + i];
-      s_off[1 + i] = base;
+      const int c = s_off[i];
+      s_off[i] = (uint16_t)base;
       base += c;
     }
+    if (t == 0) s_off[h.ncell] = (uint16_t)m;
   }
   __syncthreads();
-  for (int k = t; k < m; k += kNNBlock) {
-    const float x = K[3 * k + 0], y = K[3 * k + 1], z = K[3 * k + 2];
-    const int pos = atomicAdd(&s_off[1 + cell_at(x, y, z)], 1);
-    s_pts[pos] = make_float4(x, y, z, __int_as_float(k));
+#pragma unroll
+  for (int i = 0; i < KPT; ++i) {
+    const int k = t + i * kNNBlock;
+    if (k < m)
+      s_pts[s_off[kc[i]] + kr[i]] = make_float4(K[3 * k + 0], K[3 * k + 1], K[3 * k + 2],
+                                                __int_as_float(k));
   }
   __syncthreads();
 
@@ -778,13 +812,14 @@ __global__ __launch_bounds__(kNNBlock) void fp_grid_fused_kernel(FpLayer p, floa
       px = U[0]; py = U[1]; pz = U[2];
       u = jc;
     }
-    const Best3 res = grid_nn3_wave<kNNGroup>(h, s_pts, s_off, px, py, pz, q, valid);
+    const Best3 res = grid_nn3_wave<kNNGroup, uint16_t>(h, s_pts, s_off, px, py, pz, q, valid);
     if (valid && q == 0) {
       float w1, w2, w3;
       idw(res.d1, res.d2, res.d3, w1, w2, w3);
-      s_row[jl] = u;
-      s_idx[jl] = make_int4(res.i1, res.i2, res.i3, 0);
-      s_w[jl] = make_float4(w1, w2, w3, 0.0f);
+      s_idx[jl] = make_int4(res.i1, res.i2, res.i3, u);
+      s_wv[0][jl] = w1;
+      s_wv[1][jl] = w2;
+      s_wv[2][jl] = w3;
       if (dist) {
         float* D = dist + ((size_t)b * n + u) * 3;
         int32_t* I = idx + ((size_t)b * n + u) * 3;
@@ -795,7 +830,10 @@ __global__ __launch_bounds__(kNNBlock) void fp_grid_fused_kernel(FpLayer p, floa
   }
   __syncthreads();
   // 4. the rows
-  fp_write_rows<V2, V1, true, UN>(p, b, 0, j0, s_idx, s_w, s_row);
+  fp_write_rows<V2, V1, UN>(p, b, 0, j0, [&](int rl) {
+    const int4 I = s_idx[rl];
+    return FpRow{I, make_float4(s_wv[0][rl], s_wv[1][rl], s_wv[2][rl], 0.0f), I.w};
+  });
 }
 
 // Several FP layers in one launch (the FP layers that wait for the same sampler): logical
@@ -929,14 +967,18 @@ int fp_grid_launch(const float* xyz1, const float* xyz2, const void* ugrid, cons
   const dim3 grid(xcd_grid(f.blocks)), blk(kNNBlock);
   const size_t lds = fp_grid_lds(m);
   const int un = fp_unroll();
+#define PN2_FPG_K(V2, V1, U)                                                                   \
+  if (m <= 4 * kNNBlock) hipLaunchKernelGGL((fp_grid_fused_kernel<V2, V1, U, 4>), grid, blk, lds, stream, f.p, dist, idx); \
+  else hipLaunchKernelGGL((fp_grid_fused_kernel<V2, V1, U, kFpGridMaxKnown / kNNBlock>), grid, blk, lds, stream, f.p, dist, idx)
 #define PN2_FPG(V2, V1)                                                                        \
-  if (un == 1) hipLaunchKernelGGL((fp_grid_fused_kernel<V2, V1, 1>), grid, blk, lds, stream, f.p, dist, idx); \
-  else if (un == 4) hipLaunchKernelGGL((fp_grid_fused_kernel<V2, V1, 4>), grid, blk, lds, stream, f.p, dist, idx); \
-  else hipLaunchKernelGGL((fp_grid_fused_kernel<V2, V1, 2>), grid, blk, lds, stream, f.p, dist, idx)
-  if (f.v1) { PN2_FPG(4, 4); }
-  else if (f.v2) { PN2_FPG(4, 1); }
-  else { PN2_FPG(1, 1); }
+  if (un == 1) { PN2_FPG_K(V2, V1, 1); }                                                       \
+  else if (un == 4) { PN2_FPG_K(V2, V1, 4); }                                                  \
+  else { PN2_FPG_K(V2, V1, 2); }
+  if (f.v1) { PN2_FPG(4, 4) }
+  else if (f.v2) { PN2_FPG(4, 1) }
+  else { PN2_FPG(1, 1) }
 #undef PN2_FPG
+#undef PN2_FPG_K
   PN2_RETURN_LAUNCH();
 }
 
