@@ -13,14 +13,18 @@ T=$(ls $OUT/prof_cfg2/*/run_kernel_trace.csv 2>/dev/null | head -1)
 [ -n "$T" ] || T=$(find $OUT/prof_cfg2 -name "*kernel_trace.csv" | head -1)
 python3 tools/critical_path.py "$T" > $OUT/critical_path_cfg2.txt || exit 1
 python3 tools/lane_report.py "$T" > $OUT/lanes_cfg2.txt || exit 1
+# (gpurun returns at most 64 MiB: keep the stats, drop the traces)
+find $OUT -name "*kernel_trace.csv" -delete
 for cb in cfg2:16 cfg3:16 cfg5:8; do
   c=${cb%%:*}; b=${cb##*:}
   for C in FETCH_SIZE WRITE_SIZE; do
     timeout -s KILL 120 rocprofv3 --pmc $C --kernel-trace --output-format csv -d $OUT/pmc_${C}_$c -o run -- python3 bench.py --config $c --steps 5 --warmup 2 --no-cpu-baseline --e2e-steps 0 --latency-reps 0 --no-verify > $OUT/pmc_${C}_$c.log 2>&1 || { tail -5 $OUT/pmc_${C}_$c.log; exit 1; }
   done
   python3 tools/pmc_summary.py $OUT/pmc_FETCH_SIZE_$c $OUT/pmc_WRITE_SIZE_$c > $OUT/pmc_traffic_${c}_B$b.json || exit 1
+  rm -rf $OUT/pmc_FETCH_SIZE_$c $OUT/pmc_WRITE_SIZE_$c
 done
 timeout -k 10 200 python3 tools/stamp_fps_cull.py --json $OUT/sa1_cull_stamps.json > $OUT/stamps.log 2>&1 || { tail -20 $OUT/stamps.log; exit 1; }
 timeout -k 10 200 python3 tools/fps_stamp/lag_events.py > $OUT/lag.log 2>&1 || { tail -20 $OUT/lag.log; exit 1; }
 tail -1 $OUT/lag.log
+du -sh $OUT
 echo done
