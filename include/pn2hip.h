@@ -194,6 +194,17 @@ int pn2_ball_query_grid(const void* grid, const float* xyz2, int B, int N, int M
 int pn2_ball_group_xyz_grid(const void* grid, const float* xyz1, const float* xyz2, int B, int N,
                             int M, float radius, int nsample, int32_t* idx, int32_t* pts_cnt,
                             float* grouped_xyz, pn2_stream_t stream);
+/* pn2_ball_group_xyz_grid for nr radii (1 <= nr <= PN2_BQ_MAX_RADII) of the same queries in
+ * ONE launch (MSG's SA1: pointnet_util.py:162-203, the radius loop): the cells of the largest
+ * radius are walked once and every candidate is tested against each radius. Per radius r:
+ * radii[r], nsample[r], idx[r] (B,M,nsample[r]), pts_cnt[r] (B,M), grouped_xyz[r]
+ * (B,M,nsample[r],3) -- each exactly pn2_ball_group_xyz_grid's output for that radius. The
+ * pointer arrays are host memory. */
+#define PN2_BQ_MAX_RADII 3
+int pn2_ball_group_xyz_grid_radii(const void* grid, const float* xyz1, const float* xyz2, int B,
+                                  int N, int M, int nr, const float* radii, const int* nsample,
+                                  int32_t* const* idx, int32_t* const* pts_cnt,
+                                  float* const* grouped_xyz, pn2_stream_t stream);
 
 /* ---- k nearest neighbours ---------------------------------------------------------- *
  * pn2_select_top_k: select_top_k / SelectionSort (tf_grouping.py:22-31, tf_grouping_g.cu:

@@ -16,6 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PN2HIP_LIB") or os.path.join(_HERE, "libpn2hip.so")
 
 PN2_EINVAL = -22
+PN2_BQ_MAX_RADII = 3  # include/pn2hip.h
 PN2_EFAULT = -14
 PN2_FAULT_FPS_POLL = 1
 PN2_FPS_AUTO, PN2_FPS_BLOCKSCAN, PN2_FPS_HOTCULL_K128 = 0, 1, 6
@@ -92,6 +93,7 @@ SIGNATURES = {
     "pn2_grid_build": (_I, [_P, _I, _I, _F, _P, _S, _P]),
     "pn2_ball_query_grid": (_I, [_P, _P, _I, _I, _I, _F, _I, _P, _P, _P]),
     "pn2_ball_group_xyz_grid": (_I, [_P, _P, _P, _I, _I, _I, _F, _I, _P, _P, _P, _P]),
+    "pn2_ball_group_xyz_grid_radii": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P]),
     "pn2_three_nn_grid": (_I, [_P, _P, _P, _I, _I, _I, _P, _P, _P]),
     "pn2_fp_apply": (_I, [_P, _P, _P, _P, _I, _P, _I, _I, _I, _I, _P, _P]),
     "pn2_fp_grid_fused": (_I, [_P, _P, _P, _P, _I, _P, _I, _I, _I, _I, _P, _P, _P, _P]),

@@ -22,6 +22,8 @@
 // chosen for ~2 points per cell of the bounding box; it grows until the cells fit kGridCap.
 #include <math.h>
 
+#include <algorithm>
+
 #include "grid.h"
 
 namespace pn2 {
@@ -177,16 +179,28 @@ __global__ __launch_bounds__(kBuildBlock) void grid_build_kernel(const float* __
   }
 }
 
+// The radii of one launch (NR of them; MSG's SA1 serves its three from one walk): per radius
+// the hit threshold (pn2_ball_threshold), nsample and outputs.
+struct BqRadii {
+  float thresh[PN2_BQ_MAX_RADII];
+  int ns[PN2_BQ_MAX_RADII];
+  int32_t* idx[PN2_BQ_MAX_RADII];
+  int32_t* cnt[PN2_BQ_MAX_RADII];
+  float* gxyz[PN2_BQ_MAX_RADII];
+};
+
 // GROUP: also the grouped coordinates gxyz (B,M,ns,3) = xyz1[idx] - xyz2 (pn2_group_concat
 // with no points, pointnet_util.py:39-40): each lane writes the rows of the hits it ranks, so
 // the SA1 grouping of an xyz-only layer needs no launch of its own.
-template <int BLOCK, bool GROUP>
+// NR radii: the cells of the largest (`radius`) are walked once, every candidate's distance is
+// tested against each radius' threshold into that radius' bitmask, and each radius' rows are
+// written from its own bitmask -- the same outputs as NR single-radius launches.
+template <int BLOCK, bool GROUP, int NR>
 __global__ __launch_bounds__(BLOCK) void ball_query_grid_kernel(
     const char* __restrict__ grid, const float* __restrict__ xyz2, int N, int M, float radius,
-    float thresh, int ns, int qpb, int words, int gx, int nblk, int32_t* __restrict__ idx,
-    int32_t* __restrict__ pts_cnt, const float* __restrict__ xyz1, float* __restrict__ gxyz) {
+    int qpb, int words, int gx, int nblk, const BqRadii rd, const float* __restrict__ xyz1) {
   constexpr int NW = BLOCK / kWave;
-  extern __shared__ uint32_t bits[];  // NW x words
+  extern __shared__ uint32_t bits[];  // NW x NR x words
   // XCD-aware order (common.h): each XCD takes a contiguous range of (cloud, query chunk)
   // blocks, so a cloud's grid is fetched into one L2, not into all eight
   const int lb = xcd_block((int)blockIdx.x, nblk);
@@ -197,14 +211,21 @@ __global__ __launch_bounds__(BLOCK) void ball_query_grid_kernel(
   const GridHdr& h = g.h;
   const int* __restrict__ off = g.off;
   const float4* __restrict__ pts = g.pts;
-  uint32_t* mine = bits + (size_t)w * words;
+  uint32_t* mine = bits + (size_t)w * NR * words;  // radius r: mine + r * words
   const int wpl = (words + kWave - 1) / kWave;  // bitmask words per lane, in lane order
 
   const int q_end = min(M, (bx + 1) * qpb);
   for (int q = bx * qpb + w; q < q_end; q += NW) {
-    for (int i = lane; i < words; i += kWave) mine[i] = 0u;
+    for (int i = lane; i < NR * words; i += kWave) mine[i] = 0u;
     const float* Q = xyz2 + ((size_t)b * M + q) * 3;
     const float qx = Q[0], qy = Q[1], qz = Q[2];
+    auto hit = [&](const float4& p) {  // tf_grouping_g.cu:24-25, per radius
+      const float d = sqdist(qx, qy, qz, p.x, p.y, p.z);
+      const int k = __float_as_int(p.w);
+#pragma unroll
+      for (int r = 0; r < NR; ++r)
+        if (d < rd.thresh[r]) atomicOr(&mine[r * words + (k >> 5)], 1u << (k & 31));
+    };
     const float big = fmaxf(fmaxf(fmaxf(fabsf(qx), fabsf(qy)), fmaxf(fabsf(qz), radius)), 1.0f);
     const float rr = radius + big * 1e-5f;
     const int x0 = cell_coord(qx - rr, h.ox, h.inv, h.nx), x1 = cell_coord(qx + rr, h.ox, h.inv, h.nx);
@@ -215,13 +236,7 @@ __global__ __launch_bounds__(BLOCK) void ball_query_grid_kernel(
       for (int y = y0; y <= y1; ++y) {
         const int row = (z * h.ny + y) * h.nx;
         const int e = off[row + x1 + 1];  // cells x0..x1 of a row are contiguous
-        for (int i = off[row + x0] + lane; i < e; i += kWave) {
-          const float4 p = pts[i];
-          if (sqdist(qx, qy, qz, p.x, p.y, p.z) < thresh) {  // tf_grouping_g.cu:24-25
-            const int k = __float_as_int(p.w);
-            atomicOr(&mine[k >> 5], 1u << (k & 31));
-          }
-        }
+        for (int i = off[row + x0] + lane; i < e; i += kWave) hit(pts[i]);
       }
     }
 #else
@@ -250,13 +265,7 @@ __global__ __launch_bounds__(BLOCK) void ball_query_grid_kernel(
         for (int j = 0; j < nr; ++j) {
           const int bj = __builtin_amdgcn_readlane(beg, j);
           const int lj = __builtin_amdgcn_readlane(len, j);
-          for (int i = lane; i < lj; i += kWave) {
-            const float4 p = pts[bj + i];
-            if (sqdist(qx, qy, qz, p.x, p.y, p.z) < thresh) {  // tf_grouping_g.cu:24-25
-              const int k = __float_as_int(p.w);
-              atomicOr(&mine[k >> 5], 1u << (k & 31));
-            }
-          }
+          for (int i = lane; i < lj; i += kWave) hit(pts[bj + i]);
         }
         continue;
       }
@@ -273,58 +282,57 @@ __global__ __launch_bounds__(BLOCK) void ball_query_grid_kernel(
           const int bj = __builtin_amdgcn_readlane(beg, j);
           base = ej <= i ? bj - ej : base;
         }
-        if (i < total) {
-          const float4 p = pts[base + i];
-          if (sqdist(qx, qy, qz, p.x, p.y, p.z) < thresh) {  // tf_grouping_g.cu:24-25
-            const int k = __float_as_int(p.w);
-            atomicOr(&mine[k >> 5], 1u << (k & 31));
-          }
-        }
+        if (i < total) hit(pts[base + i]);
       }
     }
 #endif
-    // hits in index order: lane l owns bitmask words [l*wpl, (l+1)*wpl)
-    int pop = 0, myfirst = -1;
-    for (int j = 0; j < wpl; ++j) {
-      const int wi = lane * wpl + j;
-      if (wi < words) {
-        const uint32_t v = mine[wi];
-        if (myfirst < 0 && v) myfirst = 32 * wi + __builtin_ctz(v);
-        pop += __popc(v);
-      }
-    }
-    const int incl = wave_incl_scan(pop, lane);
-    const int total = __shfl(incl, kWave - 1, kWave);
-    const int cnt = min(total, ns);
-    int32_t* __restrict__ row = idx + ((size_t)b * M + q) * ns;
-    float* __restrict__ grow = GROUP ? gxyz + ((size_t)b * M + q) * ns * 3 : nullptr;
-    const float* __restrict__ X1 = GROUP ? xyz1 + (size_t)b * N * 3 : nullptr;
-    int rank = incl - pop;
-    for (int j = 0; j < wpl && rank < ns; ++j) {
-      const int wi = lane * wpl + j;
-      uint32_t v = wi < words ? mine[wi] : 0u;
-      while (v && rank < ns) {
-        const int k = 32 * wi + __builtin_ctz(v);
-        if constexpr (GROUP) {
-          grow[3 * rank + 0] = X1[3 * k + 0] - qx;  // pointnet_util.py:40
-          grow[3 * rank + 1] = X1[3 * k + 1] - qy;
-          grow[3 * rank + 2] = X1[3 * k + 2] - qz;
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      const uint32_t* mr = mine + r * words;
+      // hits in index order: lane l owns bitmask words [l*wpl, (l+1)*wpl)
+      int pop = 0, myfirst = -1;
+      for (int j = 0; j < wpl; ++j) {
+        const int wi = lane * wpl + j;
+        if (wi < words) {
+          const uint32_t v = mr[wi];
+          if (myfirst < 0 && v) myfirst = 32 * wi + __builtin_ctz(v);
+          pop += __popc(v);
         }
-        row[rank++] = k;
-        v &= v - 1u;
       }
-    }
-    const uint64_t has = __ballot(pop > 0);
-    const int first = has ? __shfl(myfirst, __ffsll((unsigned long long)has) - 1, kWave) : 0;
-    for (int p = cnt + lane; p < ns; p += kWave) {
-      row[p] = first;  // :26-29 (0 when no hit)
-      if constexpr (GROUP) {
-        grow[3 * p + 0] = X1[3 * first + 0] - qx;
-        grow[3 * p + 1] = X1[3 * first + 1] - qy;
-        grow[3 * p + 2] = X1[3 * first + 2] - qz;
+      const int incl = wave_incl_scan(pop, lane);
+      const int total = __shfl(incl, kWave - 1, kWave);
+      const int ns = rd.ns[r];
+      const int cnt = min(total, ns);
+      int32_t* __restrict__ row = rd.idx[r] + ((size_t)b * M + q) * ns;
+      float* __restrict__ grow = GROUP ? rd.gxyz[r] + ((size_t)b * M + q) * ns * 3 : nullptr;
+      const float* __restrict__ X1 = GROUP ? xyz1 + (size_t)b * N * 3 : nullptr;
+      int rank = incl - pop;
+      for (int j = 0; j < wpl && rank < ns; ++j) {
+        const int wi = lane * wpl + j;
+        uint32_t v = wi < words ? mr[wi] : 0u;
+        while (v && rank < ns) {
+          const int k = 32 * wi + __builtin_ctz(v);
+          if constexpr (GROUP) {
+            grow[3 * rank + 0] = X1[3 * k + 0] - qx;  // pointnet_util.py:40
+            grow[3 * rank + 1] = X1[3 * k + 1] - qy;
+            grow[3 * rank + 2] = X1[3 * k + 2] - qz;
+          }
+          row[rank++] = k;
+          v &= v - 1u;
+        }
       }
+      const uint64_t has = __ballot(pop > 0);
+      const int first = has ? __shfl(myfirst, __ffsll((unsigned long long)has) - 1, kWave) : 0;
+      for (int p = cnt + lane; p < ns; p += kWave) {
+        row[p] = first;  // :26-29 (0 when no hit)
+        if constexpr (GROUP) {
+          grow[3 * p + 0] = X1[3 * first + 0] - qx;
+          grow[3 * p + 1] = X1[3 * first + 1] - qy;
+          grow[3 * p + 2] = X1[3 * first + 2] - qz;
+        }
+      }
+      if (lane == 0) rd.cnt[r][(size_t)b * M + q] = cnt;
     }
-    if (lane == 0) pts_cnt[(size_t)b * M + q] = cnt;
   }
 }
 
@@ -361,13 +369,29 @@ int pn2_grid_build(const float* xyz, int B, int N, float cell_edge, void* grid,
 }
 
 namespace {
-int ball_query_grid(const void* grid, const float* xyz2, int B, int N, int M, float radius,
-                    int nsample, int32_t* idx, int32_t* pts_cnt, const float* xyz1, float* gxyz,
+// nr radii (1..PN2_BQ_MAX_RADII) in one launch; gxyz[r] all set (GROUP) or all NULL
+int ball_query_grid(const void* grid, const float* xyz2, int B, int N, int M, int nr,
+                    const float* radii, const int* nsample, int32_t* const* idx,
+                    int32_t* const* pts_cnt, const float* xyz1, float* const* gxyz,
                     hipStream_t stream) {
-  if (!(radius > 0.0f) || nsample <= 0 || B < 0 || N < 0 || M < 0) return PN2_EINVAL;
+  if (nr < 1 || nr > PN2_BQ_MAX_RADII || B < 0 || N < 0 || M < 0) return PN2_EINVAL;
+  for (int r = 0; r < nr; ++r)
+    if (!(radii[r] > 0.0f) || nsample[r] <= 0) return PN2_EINVAL;
   if ((long long)B * M == 0) return PN2_OK;
-  if (!grid || !xyz2 || !idx || !pts_cnt || B > 65535) return PN2_EINVAL;
-  if (gxyz && !xyz1) return PN2_EINVAL;
+  if (!grid || !xyz2 || B > 65535) return PN2_EINVAL;
+  const bool group = gxyz != nullptr;
+  if (group && !xyz1) return PN2_EINVAL;
+  pn2::BqRadii rd{};
+  float rmax = 0.0f;
+  for (int r = 0; r < nr; ++r) {
+    if (!idx[r] || !pts_cnt[r] || (group && !gxyz[r])) return PN2_EINVAL;
+    rd.thresh[r] = pn2_ball_threshold(radii[r]);
+    rd.ns[r] = nsample[r];
+    rd.idx[r] = idx[r];
+    rd.cnt[r] = pts_cnt[r];
+    rd.gxyz[r] = group ? gxyz[r] : nullptr;
+    rmax = std::max(rmax, radii[r]);
+  }
   const int words = (N + 31) / 32;
   if (words > pn2::kMaxBitWords) return PN2_EINVAL;
   constexpr int BLOCK = 256, NW = BLOCK / pn2::kWave;
@@ -376,35 +400,53 @@ int ball_query_grid(const void* grid, const float* xyz2, int B, int N, int M, fl
   long long qpb = (queries + 2047) / 2048;
   qpb = ((qpb + NW - 1) / NW) * NW;
   const unsigned gx = (unsigned)((M + qpb - 1) / qpb);
-  const size_t lds = (size_t)NW * (words > 0 ? words : 1) * 4;
+  const size_t lds = (size_t)NW * nr * (words > 0 ? words : 1) * 4;
+  if (lds > 160 * 1024) return PN2_EINVAL;
   const long long nblk = (long long)gx * B;
   if (nblk > INT32_MAX - pn2::kXcds) return PN2_EINVAL;
-  if (gxyz)
-    hipLaunchKernelGGL((pn2::ball_query_grid_kernel<BLOCK, true>), dim3(pn2::xcd_grid(nblk)),
-                       dim3(BLOCK), lds, stream, (const char*)grid, xyz2, N, M, radius,
-                       pn2_ball_threshold(radius), nsample, (int)qpb, words, (int)gx, (int)nblk,
-                       idx, pts_cnt, xyz1, gxyz);
-  else
-    hipLaunchKernelGGL((pn2::ball_query_grid_kernel<BLOCK, false>), dim3(pn2::xcd_grid(nblk)),
-                       dim3(BLOCK), lds, stream, (const char*)grid, xyz2, N, M, radius,
-                       pn2_ball_threshold(radius), nsample, (int)qpb, words, (int)gx, (int)nblk,
-                       idx, pts_cnt, nullptr, nullptr);
+  const dim3 grd(pn2::xcd_grid(nblk)), blk(BLOCK);
+  const char* g = (const char*)grid;
+#define PN2_BQG(GROUP, NR)                                                                     \
+  hipLaunchKernelGGL((pn2::ball_query_grid_kernel<BLOCK, GROUP, NR>), grd, blk, lds, stream, g, \
+                     xyz2, N, M, rmax, (int)qpb, words, (int)gx, (int)nblk, rd,               \
+                     GROUP ? xyz1 : nullptr)
+  if (group) {
+    if (nr == 1) PN2_BQG(true, 1);
+    else if (nr == 2) PN2_BQG(true, 2);
+    else PN2_BQG(true, 3);
+  } else {
+    if (nr == 1) PN2_BQG(false, 1);
+    else if (nr == 2) PN2_BQG(false, 2);
+    else PN2_BQG(false, 3);
+  }
+#undef PN2_BQG
   PN2_RETURN_LAUNCH();
 }
 }  // namespace
 
 int pn2_ball_query_grid(const void* grid, const float* xyz2, int B, int N, int M, float radius,
                         int nsample, int32_t* idx, int32_t* pts_cnt, pn2_stream_t stream) {
-  return ball_query_grid(grid, xyz2, B, N, M, radius, nsample, idx, pts_cnt, nullptr, nullptr,
-                         (hipStream_t)stream);
+  if (!idx || !pts_cnt) return PN2_EINVAL;
+  return ball_query_grid(grid, xyz2, B, N, M, 1, &radius, &nsample, &idx, &pts_cnt, nullptr,
+                         nullptr, (hipStream_t)stream);
 }
 
 int pn2_ball_group_xyz_grid(const void* grid, const float* xyz1, const float* xyz2, int B, int N,
                             int M, float radius, int nsample, int32_t* idx, int32_t* pts_cnt,
                             float* grouped_xyz, pn2_stream_t stream) {
-  if (!grouped_xyz) return PN2_EINVAL;
-  return ball_query_grid(grid, xyz2, B, N, M, radius, nsample, idx, pts_cnt, xyz1, grouped_xyz,
-                         (hipStream_t)stream);
+  if (!grouped_xyz || !idx || !pts_cnt) return PN2_EINVAL;
+  return ball_query_grid(grid, xyz2, B, N, M, 1, &radius, &nsample, &idx, &pts_cnt, xyz1,
+                         &grouped_xyz, (hipStream_t)stream);
+}
+
+int pn2_ball_group_xyz_grid_radii(const void* grid, const float* xyz1, const float* xyz2, int B,
+                                  int N, int M, int nr, const float* radii, const int* nsample,
+                                  int32_t* const* idx, int32_t* const* pts_cnt,
+                                  float* const* grouped_xyz, pn2_stream_t stream) {
+  if (!radii || !nsample || !idx || !pts_cnt || !grouped_xyz) return PN2_EINVAL;
+  if (nr < 1 || nr > PN2_BQ_MAX_RADII) return PN2_EINVAL;
+  return ball_query_grid(grid, xyz2, B, N, M, nr, radii, nsample, idx, pts_cnt, xyz1,
+                         grouped_xyz, (hipStream_t)stream);
 }
 
 }  // extern "C"

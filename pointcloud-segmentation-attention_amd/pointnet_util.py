@@ -25,9 +25,9 @@ reference's registered gradients.
 import torch
 
 from . import tf_grouping, tf_interpolate, tf_sampling, tf_util
-from ._lib import (POOL_MODES, PN2_FP_MAX_LAYERS, PN2_POOL_NONE, PN2_SA_MAX_LAYERS, PN2_USE_XYZ,
-                   PN2_XYZ_LAST, FpLayer, InvalidArgumentError, SaLayer, check, device_tensor, lib,
-                   ptr, stream_of)
+from ._lib import (POOL_MODES, PN2_BQ_MAX_RADII, PN2_FP_MAX_LAYERS, PN2_POOL_NONE,
+                   PN2_SA_MAX_LAYERS, PN2_USE_XYZ, PN2_XYZ_LAST, FpLayer, InvalidArgumentError,
+                   SaLayer, check, device_tensor, lib, ptr, stream_of)
 
 
 def _is_empty_points(points):
@@ -90,6 +90,40 @@ def ball_group_xyz(radius, nsample, xyz, new_xyz, grid):
                                         float(radius), ns, ptr(idx), ptr(cnt), ptr(grouped),
                                         stream_of(xyz)), "ball_group_xyz")
     return idx, cnt, grouped
+
+
+def ball_group_xyz_radii(radii, nsamples, xyz, new_xyz, grid):
+    """ball_group_xyz for several radii of the same queries (MSG's SA1 radius loop,
+    pointnet_util.py:162-203) in ONE kernel (pn2_ball_group_xyz_grid_radii: one walk over the
+    largest radius' cells). Returns [(idx, pts_cnt, grouped)] per radius, each bit-identical
+    to ball_group_xyz(radius, nsample, ...)."""
+    import ctypes
+    xyz = device_tensor(xyz, "xyz", torch.float32)
+    new_xyz = device_tensor(new_xyz, "new_xyz", torch.float32)
+    nr = len(radii)
+    if not 1 <= nr <= PN2_BQ_MAX_RADII or len(nsamples) != nr:
+        raise InvalidArgumentError(f"ball_group_xyz_radii: 1..{PN2_BQ_MAX_RADII} radii, one "
+                                   "nsample each")
+    if not grid.matches(xyz):
+        raise InvalidArgumentError("ball_group_xyz_radii: the grid was built over a different xyz")
+    B, N, M = int(xyz.shape[0]), int(xyz.shape[1]), int(new_xyz.shape[1])
+    if int(new_xyz.shape[0]) != B:
+        raise InvalidArgumentError("ball_group_xyz_radii: xyz and new_xyz need the same batch")
+    outs = []
+    for ns in nsamples:
+        ns = int(ns)
+        outs.append((torch.empty((B, M, ns), dtype=torch.int32, device=xyz.device),
+                     torch.empty((B, M), dtype=torch.int32, device=xyz.device),
+                     torch.empty((B, M, ns, 3), dtype=torch.float32, device=xyz.device)))
+    rad = (ctypes.c_float * nr)(*[float(r) for r in radii])
+    nsa = (ctypes.c_int * nr)(*[int(n) for n in nsamples])
+    ids = (ctypes.c_void_p * nr)(*[ptr(o[0]) for o in outs])
+    cnts = (ctypes.c_void_p * nr)(*[ptr(o[1]) for o in outs])
+    grps = (ctypes.c_void_p * nr)(*[ptr(o[2]) for o in outs])
+    check(lib().pn2_ball_group_xyz_grid_radii(ptr(grid.buf), ptr(xyz), ptr(new_xyz), B, N, M, nr,
+                                              rad, nsa, ids, cnts, grps, stream_of(xyz)),
+          "ball_group_xyz_radii")
+    return outs
 
 
 BALL_GROUP_MAX_POINTS = 1024  # pn2_ball_group_layers stages each cloud in LDS

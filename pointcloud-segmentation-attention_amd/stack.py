@@ -139,6 +139,9 @@ LANE_JOIN = os.environ.get("PN2_LANE_JOIN") == "1"
 SEG_MERGE = os.environ.get("PN2_SEG_MERGE") == "1"
 # lane-end events with timing (DIAGNOSTIC: bench.py --timeline sets it before the pipeline)
 TIMING_EVENTS = False
+# MSG_SA1_SPLIT (A/B, PN2_MSG_SA1_SPLIT=1): MSG SA1's radii as one grid query launch each
+# (round 3) instead of one launch for all three (pn2_ball_group_xyz_grid_radii)
+MSG_SA1_SPLIT = os.environ.get("PN2_MSG_SA1_SPLIT") == "1"
 # FP4_SPLIT (A/B, PN2_FP4_SPLIT=1): FP4 as the round-3 launches (grid build, three_nn over it,
 # then the interpolation: tasks nn4 and fp4) instead of one pn2_fp_grid_fused launch;
 # NN4_LANE (PN2_NN4_LANE=n): then the lane of nn4 (2: with the interpolation)
@@ -590,6 +593,16 @@ class Step:
                     v["bq"][(i, r)], v["gp"][(i, r)] = idx, new_points
             return f
 
+        def grp_radii():
+            # SA1's radii as ONE launch over the grid (pn2_ball_group_xyz_grid_radii: one walk
+            # over the largest radius' cells serves all three)
+            def f():
+                outs = pointnet_util.ball_group_xyz_radii(MSG_SA[0][1], MSG_SA[0][2], v["xyz"][0],
+                                                          v["xyz"][1], v["grid1"])
+                for r, (idx, _, gp) in enumerate(outs):
+                    v["bq"][(0, r)], v["gp"][(0, r)] = idx, gp
+            return f
+
         for i in range(len(MSG_SA)):
             # lane 0: SA1's sampler only; the later samplers run on lane 3 after it; radius 0's
             # grouping on lane 1, the other radii on lane 2
@@ -603,6 +616,9 @@ class Step:
             if i > 0 and MSG_SA[i - 1][0] <= pointnet_util.BALL_GROUP_MAX_POINTS \
                     and max(MSG_SA[i][2]) <= pointnet_util.BALL_GROUP_MAX_NSAMPLE:
                 tasks.append(Task(f"sa{i + 1}", 2, (f"fps{i + 1}",), grp_all(i)))
+                continue
+            if i == 0 and grid_level and not MSG_SA1_SPLIT:
+                tasks.append(Task("sa1", 1, ("fps1", "grid1"), grp_radii()))
                 continue
             for r in range(len(MSG_SA[i][1])):
                 # radius r on lane 1 + r when lane 3 is free (chain_lane 0), else radius 0 on

@@ -98,6 +98,16 @@ def test_grid_contract(pn2):
     assert lib.pn2_ball_query_grid(None, None, 1, 10, 10, 0.1, 0, None, None, None) == E
     assert lib.pn2_ball_query_grid(None, None, 1, 200000, 10, 0.1, 8, None, None, None) == E
     assert lib.pn2_three_nn_grid(None, None, None, 1, 10, 10, None, None, None) == E
+    # several radii in one launch: 1 <= nr <= 3, every array given
+    import ctypes
+    rad = (ctypes.c_float * 4)(0.1, 0.2, 0.4, 0.8)
+    nsa = (ctypes.c_int * 4)(8, 8, 8, 8)
+    ptrs = (ctypes.c_void_p * 4)()
+    assert lib.pn2_ball_group_xyz_grid_radii(None, None, None, 1, 10, 10, 0, rad, nsa, ptrs, ptrs, ptrs, None) == E
+    assert lib.pn2_ball_group_xyz_grid_radii(None, None, None, 1, 10, 10, 4, rad, nsa, ptrs, ptrs, ptrs, None) == E
+    assert lib.pn2_ball_group_xyz_grid_radii(None, None, None, 1, 10, 10, 2, None, nsa, ptrs, ptrs, ptrs, None) == E
+    assert lib.pn2_ball_group_xyz_grid_radii(None, None, None, 1, 10, 10, 2, rad, nsa, ptrs, ptrs, ptrs, None) == E
+    assert lib.pn2_ball_group_xyz_grid_radii(None, None, None, 0, 10, 10, 2, rad, nsa, ptrs, ptrs, ptrs, None) == 0
     assert lib.pn2_three_nn_grid(None, None, None, 0, 10, 10, None, None, None) == 0
     assert lib.pn2_fp_apply(None, None, None, None, 3, None, 4, 1, 4, 4, None, None) == E
     # pn2_fp_grid_fused: m in [1, 4096], dist and idx together, points1 with C1 > 0

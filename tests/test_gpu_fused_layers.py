@@ -153,3 +153,32 @@ def test_ball_group_xyz(env, kind, B, N, M, r, ns):
     assert np.array_equal(cnt.cpu().numpy(), rcnt)
     assert np.array_equal(idx.cpu().numpy(), ridx)
     assert np.array_equal(_bits(grouped.cpu().numpy()), _bits(rg))
+
+
+GROUP_RADII_CASES = [
+    ("scannet", 2, 16384, 512, (0.1, 0.2, 0.4), (16, 32, 128), 0.2),  # cfg5 SA1 (its grid)
+    ("scannet", 2, 8192, 1024, (0.4, 0.1), (8, 64), 0.1),             # unsorted, grid at r_min
+    ("grid", 2, 4096, 500, (1.0, 2.0, 1.5), (16, 8, 32), 1.0),        # lattice ties at radii
+    ("scannet", 1, 3000, 300, (0.3,), (40,), 0.5),                    # one radius
+]
+
+
+@pytest.mark.parametrize("kind,B,N,M,radii,nss,edge", GROUP_RADII_CASES)
+def test_ball_group_xyz_radii(env, kind, B, N, M, radii, nss, edge):
+    """pointnet_util.ball_group_xyz_radii (pn2_ball_group_xyz_grid_radii: one walk over the
+    largest radius' cells for all radii) == the oracle's ball_query + group_concat per radius,
+    bit for bit, and == ball_group_xyz radius by radius."""
+    pkg, O, torch, dev = env
+    x, _, q = _layer(pkg, O, kind, B, N, M, 0, 3)
+    xt, qt = torch.from_numpy(x).to(dev), torch.from_numpy(q).to(dev)
+    grid = pkg.tf_grouping.BallGrid(xt, edge)
+    outs = pkg.pointnet_util.ball_group_xyz_radii(radii, nss, xt, qt, grid)
+    for (idx, cnt, grouped), r, ns in zip(outs, radii, nss):
+        ridx, rcnt = O.ball_query(x, q, r, ns)
+        rg, _ = O.group_concat(x, None, q, ridx)
+        assert np.array_equal(cnt.cpu().numpy(), rcnt)
+        assert np.array_equal(idx.cpu().numpy(), ridx)
+        assert np.array_equal(_bits(grouped.cpu().numpy()), _bits(rg))
+        one = pkg.pointnet_util.ball_group_xyz(r, ns, xt, qt, grid)
+        assert torch.equal(one[0], idx) and torch.equal(one[1], cnt)
+        assert torch.equal(one[2].view(torch.int32), grouped.view(torch.int32))

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Micro-benchmark of the grid build and of cfg5's three SA1 grouped queries (B = 8 clouds of
 16,384 points, 512 centres, r = 0.1 / 0.2 / 0.4, ns = 16 / 32 / 128): one grid per radius
-(edge = radius) against ONE grid for all three radii (edge 0.1, 0.2, 0.4); every variant's
+(edge = radius) against ONE grid for all three radii (edge 0.1, 0.2, 0.4), and the three radii in one launch per grid; every variant's
 idx / grouped_xyz must equal the per-radius one bit for bit. HIP events, median of 20."""
 import importlib
 import json
@@ -52,6 +52,13 @@ def main():
             res[f"query r={r} on one grid edge {edge} (us)"] = t
             tot += t
         res[f"three queries on one grid edge {edge} (us)"] = tot
+        # all three radii in ONE launch (pn2_ball_group_xyz_grid_radii), bit for bit
+        outs = pu.ball_group_xyz_radii(radii, nss, x, q, g)
+        for (i, c, gx), (ri, rc, rg) in zip(outs, ref):
+            assert torch.equal(i, ri) and torch.equal(c, rc)
+            assert torch.equal(gx.view(torch.int32), rg.view(torch.int32))
+        res[f"three radii in one launch, grid edge {edge} (us)"] = timeit(
+            lambda: pu.ball_group_xyz_radii(radii, nss, x, q, g))
     print(json.dumps({k: round(v, 1) for k, v in res.items()}, indent=1))
 
 
