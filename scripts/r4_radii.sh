@@ -5,7 +5,7 @@ set -o pipefail
 export TMPDIR=/tmp
 OUT=gpurun_out/r4/radii
 mkdir -p $OUT
-timeout -k 10 600 python3 -u -m pytest -x -q --timeout 280 --timeout-method thread -m gpu tests/test_gpu_fused_layers.py tests/test_gpu_a_fullsize.py -k "radii or ball_group_xyz or cfg5 or msg or pipeline" > $OUT/pytest.log 2>&1 || { tail -30 $OUT/pytest.log; exit 1; }
+timeout -k 10 600 python3 -u -m pytest -x -q --timeout 280 --timeout-method thread -m gpu tests/test_gpu_fused_layers.py tests/test_gpu_a_fullsize.py -k "radii or ball_group_xyz or stack_full_size or pipeline" > $OUT/pytest.log 2>&1 || { tail -30 $OUT/pytest.log; exit 1; }
 tail -1 $OUT/pytest.log
 timeout -k 10 200 python3 tools/bench_msg_grid.py > $OUT/msg_grid.json 2> $OUT/msg_grid.err || { tail -20 $OUT/msg_grid.err; exit 1; }
 grep -i "three\|build" $OUT/msg_grid.json
