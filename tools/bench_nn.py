@@ -68,6 +68,17 @@ def main():
         None, k.data_ptr(), ug.buf.data_ptr(), None, 0, p2.data_ptr(), 128, B, n, m,
         out2.data_ptr(), dist.data_ptr(), idx.data_ptr(), st))
     assert torch.equal(out, out2) and torch.equal(idx, ref[1])
+    # cfg3's FP4: points1 = rgb + normals (C1 = 9, rows of 137 floats: not 16-B aligned)
+    p1 = torch.rand((B, n, 9), device=dev)
+    o3 = torch.empty((B, n, 137), device=dev)
+    o3b = torch.empty((B, n, 137), device=dev)
+    res["cfg3 fp4 apply only"] = timeit(lambda: L.pn2_fp_apply(
+        dist.data_ptr(), idx.data_ptr(), ug.buf.data_ptr(), p1.data_ptr(), 9, p2.data_ptr(), 128,
+        B, n, m, o3.data_ptr(), st))
+    res["cfg3 fp4 grid fused"] = timeit(lambda: L.pn2_fp_grid_fused(
+        None, k.data_ptr(), ug.buf.data_ptr(), p1.data_ptr(), 9, p2.data_ptr(), 128, B, n, m,
+        o3b.data_ptr(), None, None, st))
+    assert torch.equal(o3, o3b)
     res["build known grid"] = timeit(lambda: pkg.grid.PointGrid(k, 0.0))
     res["build cloud grid"] = timeit(lambda: pkg.grid.PointGrid(t1, 0.1))
     print(json.dumps({k_: round(v, 1) for k_, v in res.items()}, indent=1))

@@ -5,7 +5,7 @@ sys.path.insert(0, ROOT); sys.path.insert(0, os.path.join(ROOT, "tests"))
 import torch
 from conftest import PKG_NAME
 pkg = importlib.import_module(PKG_NAME)
-L = ctypes.CDLL(os.path.join(ROOT, "tools", "fps_stamp", "libpn2fpsstamp.so"))
+L = ctypes.CDLL(os.environ.get("PN2_STAMP_LIB") or os.path.join(ROOT, "tools", "fps_stamp", "libpn2fpsstamp.so"))
 L.pn2_fps_cull_stamp.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
 L.pn2_fps_cull_events.argtypes = [ctypes.c_void_p]
 dev = torch.device("cuda:0")

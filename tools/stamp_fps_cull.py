@@ -16,7 +16,7 @@ sys.path.insert(0, ROOT); sys.path.insert(0, os.path.join(ROOT, "tests"))
 import torch  # noqa: E402
 from conftest import PKG_NAME  # noqa: E402
 pkg = importlib.import_module(PKG_NAME)
-L = ctypes.CDLL(os.path.join(ROOT, "tools", "fps_stamp", "libpn2fpsstamp.so"))
+L = ctypes.CDLL(os.environ.get("PN2_STAMP_LIB") or os.path.join(ROOT, "tools", "fps_stamp", "libpn2fpsstamp.so"))
 for _f in (L.pn2_fps_cull_stamp, L.pn2_fps_cull_stamp_msg):
     _f.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                    ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
