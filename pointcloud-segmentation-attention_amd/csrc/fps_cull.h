@@ -25,10 +25,6 @@
 #pragma once
 #include "fps_kernels.h"
 
-#ifndef PN2_FPS_COLD_LAGPRIO
-#define PN2_FPS_COLD_LAGPRIO 0  // 1: lagging cold waves apply at a higher priority (A/B builds)
-#endif
-
 namespace pn2 {
 namespace {
 
@@ -824,15 +820,7 @@ __device__ __attribute__((always_inline)) inline void hotcull_body(
         stop = (sv & kEnd) != 0;  // set in the same word as the final count
         if (av - applied >= GRP || (stop && av > applied)) {
           const int a1 = min(av, applied + GRP);
-          if constexpr (PRIO > 1 && PN2_FPS_COLD_LAGPRIO) {
-            // (A/B) a wave with another group waiting after this one is behind: it outranks
-            // the cold waves that are keeping up (equal priorities go oldest wave first, so the
-            // last waves of the workgroup fell furthest behind: profiles/r4/final/lag.log)
-            if (av - a1 >= GRP) __builtin_amdgcn_s_setprio(PRIO - 1);
-            else __builtin_amdgcn_s_setprio(PRIO - 2);
-          } else if constexpr (PRIO > 0) {
-            __builtin_amdgcn_s_setprio(PRIO - 1);
-          }
+          if constexpr (PRIO > 0) __builtin_amdgcn_s_setprio(PRIO - 1);
           if constexpr (STAMP) tcnt0 = __builtin_amdgcn_s_memtime();
           const int ci = applied + lane / PPT;
           const bool valid = lane < GRP * PPT && ci < a1;
