@@ -177,6 +177,9 @@ PN2_DEV bool box_certifies(const GridHdr& h, float px, float py, float pz, int x
   return gap > 0.0f && d3 < gap * gap * 0.9999f;
 }
 
+#ifndef PN2_NN_FIRST
+#define PN2_NN_FIRST 1  // the walk's first pass: the cube of shells 0..PN2_NN_FIRST (A/B: 0)
+#endif
 #ifndef PN2_NN_ROWSPLIT
 #define PN2_NN_ROWSPLIT 0  // 1: the G lanes split a shell's rows (A/B builds)
 #endif
@@ -206,9 +209,12 @@ PN2_DEV Best3 grid_nn3(const GridHdr& h, const float4* __restrict__ pts,
   const int cy = cell_coord(py, h.oy, h.inv, h.ny);
   const int cz = cell_coord(pz, h.oz, h.inv, h.nz);
   Best3 res;
-  for (int s = 0;; ++s) {
+  // the first pass takes shells 0 and 1 together (the 3x3x3 block: nine full rows): the own
+  // cell alone (~2 points) almost never certifies, so its merge and test were wasted
+  for (int s = PN2_NN_FIRST;; ++s) {
     const int xl = cx - s, xh = cx + s, yl = cy - s, yh = cy + s, zl = cz - s, zh = cz + s;
     const int x0 = max(xl, 0), x1 = min(xh, h.nx - 1);
+    const bool block = s == PN2_NN_FIRST;  // every row of the cube, not just its shell
 #if PN2_NN_ROWSPLIT
     auto visit = [&](int lo, int hi) {  // sorted points [lo, hi), all of them by this lane
       int e = lo;
@@ -227,7 +233,7 @@ PN2_DEV Best3 grid_nn3(const GridHdr& h, const float4* __restrict__ pts,
     int z = zlo + q / ny, y = ylo + q % ny;  // row q, then every G-th
     for (; z <= zhi;) {
       const int row = (z * h.ny + y) * h.nx;
-      if (s == 0 || z == zl || z == zh || y == yl || y == yh) {
+      if (block || z == zl || z == zh || y == yl || y == yh) {
         visit(off[row + x0], off[row + x1 + 1]);  // a face row: all of x0..x1
       } else {
         if (xl >= 0) visit(off[row + xl], off[row + xl + 1]);
@@ -246,7 +252,7 @@ PN2_DEV Best3 grid_nn3(const GridHdr& h, const float4* __restrict__ pts,
     for (int z = max(zl, 0); z <= min(zh, h.nz - 1); ++z) {
       for (int y = max(yl, 0); y <= min(yh, h.ny - 1); ++y) {
         const int row = (z * h.ny + y) * h.nx;
-        if (s == 0 || z == zl || z == zh || y == yl || y == yh) {
+        if (block || z == zl || z == zh || y == yl || y == yh) {
           visit(off[row + x0], off[row + x1 + 1]);  // a face row: all of x0..x1
         } else {
           if (xl >= 0) visit(off[row + xl], off[row + xl + 1]);
