@@ -199,7 +199,8 @@ int pn2_ball_group_xyz_grid(const void* grid, const float* xyz1, const float* xy
  * radius are walked once and every candidate is tested against each radius. Per radius r:
  * radii[r], nsample[r], idx[r] (B,M,nsample[r]), pts_cnt[r] (B,M), grouped_xyz[r]
  * (B,M,nsample[r],3) -- each exactly pn2_ball_group_xyz_grid's output for that radius. The
- * pointer arrays are host memory. */
+ * pointer arrays are host memory. The nr bitmasks per wave must fit 64 KB of LDS:
+ * nr * ceil(N / 32) <= 4096 (PN2_EINVAL beyond: one launch per radius). */
 #define PN2_BQ_MAX_RADII 3
 int pn2_ball_group_xyz_grid_radii(const void* grid, const float* xyz1, const float* xyz2, int B,
                                   int N, int M, int nr, const float* radii, const int* nsample,

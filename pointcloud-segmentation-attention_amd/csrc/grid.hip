@@ -401,7 +401,7 @@ int ball_query_grid(const void* grid, const float* xyz2, int B, int N, int M, in
   qpb = ((qpb + NW - 1) / NW) * NW;
   const unsigned gx = (unsigned)((M + qpb - 1) / qpb);
   const size_t lds = (size_t)NW * nr * (words > 0 ? words : 1) * 4;
-  if (lds > 160 * 1024) return PN2_EINVAL;
+  if (lds > 64 * 1024) return PN2_EINVAL;  // (dynamic LDS; nr = 1 fits up to N = 131072)
   const long long nblk = (long long)gx * B;
   if (nblk > INT32_MAX - pn2::kXcds) return PN2_EINVAL;
   const dim3 grd(pn2::xcd_grid(nblk)), blk(BLOCK);

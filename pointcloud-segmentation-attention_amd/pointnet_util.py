@@ -109,6 +109,8 @@ def ball_group_xyz_radii(radii, nsamples, xyz, new_xyz, grid):
     B, N, M = int(xyz.shape[0]), int(xyz.shape[1]), int(new_xyz.shape[1])
     if int(new_xyz.shape[0]) != B:
         raise InvalidArgumentError("ball_group_xyz_radii: xyz and new_xyz need the same batch")
+    if nr * ((N + 31) // 32) > 4096:  # the bitmasks' LDS bound: one launch per radius
+        return [ball_group_xyz(r, ns, xyz, new_xyz, grid) for r, ns in zip(radii, nsamples)]
     outs = []
     for ns in nsamples:
         ns = int(ns)
