@@ -14,7 +14,11 @@ timeout -k 10 400 python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-basel
 timeout -k 10 400 python3 bench.py --steps 500 --no-cpu-baseline --e2e-steps 0 > $OUT/bench_cfg2_500.json 2> $OUT/bench_cfg2_500.err || { tail -20 $OUT/bench_cfg2_500.err; exit 1; }
 timeout -k 10 400 python3 bench.py --config cfg3 --no-cpu-baseline --e2e-steps 0 > $OUT/bench_cfg3.json 2> $OUT/bench_cfg3.err || { tail -20 $OUT/bench_cfg3.err; exit 1; }
 timeout -k 10 400 python3 bench.py --config cfg5 --no-cpu-baseline --e2e-steps 0 > $OUT/bench_cfg5.json 2> $OUT/bench_cfg5.err || { tail -20 $OUT/bench_cfg5.err; exit 1; }
-for c in drv_1 drv_2 cfg2_500 cfg3 cfg5; do
+# first use of a buffer set's graphs inside the timed window? (9 sets; warm-up 5 leaves 4 unused)
+timeout -k 10 400 python3 bench.py --gpus 1 --steps 20 --warmup 9 --no-cpu-baseline --e2e-steps 0 > $OUT/bench_drv_w9.json 2> $OUT/bench_drv_w9.err || { tail -20 $OUT/bench_drv_w9.err; exit 1; }
+timeout -k 10 400 python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --e2e-steps 0 > $OUT/bench_drv_w5.json 2> $OUT/bench_drv_w5.err || { tail -20 $OUT/bench_drv_w5.err; exit 1; }
+timeout -k 10 400 python3 bench.py --gpus 1 --steps 20 --warmup 18 --no-cpu-baseline --e2e-steps 0 > $OUT/bench_drv_w18.json 2> $OUT/bench_drv_w18.err || { tail -20 $OUT/bench_drv_w18.err; exit 1; }
+for c in drv_1 drv_2 cfg2_500 cfg3 cfg5 drv_w9 drv_w5 drv_w18; do
   python3 -c "import json; d=json.load(open('$OUT/bench_$c.json')); print('$c', round(d['value']), round(d['ms_per_step'],4), round(d['roofline']['avg_launch_ms'],4), d.get('verified'), d.get('fault_status'), round(d.get('latency_ms_per_batch', 0), 3), d['roofline'].get('traffic_source'))"
 done
 echo done
