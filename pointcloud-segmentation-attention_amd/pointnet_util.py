@@ -22,6 +22,8 @@ is required, the composition of differentiable ops (gather_point, group_point,
 three_interpolate) is used instead so that backward reaches xyz and points like the
 reference's registered gradients.
 """
+import ctypes
+
 import torch
 
 from . import tf_grouping, tf_interpolate, tf_sampling, tf_util
@@ -97,7 +99,6 @@ def ball_group_xyz_radii(radii, nsamples, xyz, new_xyz, grid):
     pointnet_util.py:162-203) in ONE kernel (pn2_ball_group_xyz_grid_radii: one walk over the
     largest radius' cells). Returns [(idx, pts_cnt, grouped)] per radius, each bit-identical
     to ball_group_xyz(radius, nsample, ...)."""
-    import ctypes
     xyz = device_tensor(xyz, "xyz", torch.float32)
     new_xyz = device_tensor(new_xyz, "new_xyz", torch.float32)
     nr = len(radii)
