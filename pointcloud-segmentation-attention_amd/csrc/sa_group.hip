@@ -49,6 +49,9 @@ constexpr int kSgMaxQpb = 64;   // queries per workgroup
 #ifndef PN2_SG_VEC  // the vector write phase (ball_group_layers_kernel, below); 0 = A/B off
 #define PN2_SG_VEC 1
 #endif
+#ifndef PN2_SG_PREFETCH  // the vector phase gathers the next chunk before storing this one
+#define PN2_SG_PREFETCH 1
+#endif
 constexpr int kSgVecFloats = 4096;  // the vector write phase's LDS staging chunk (16 KB)
 #ifndef PN2_SG_TILE_KB
 #define PN2_SG_TILE_KB 32
@@ -196,21 +199,31 @@ __global__ __launch_bounds__(kSgBlock) void ball_group_layers_kernel(SgArgs a) {
       const int RP = (((R + g.parts - 1) / g.parts) + 3) & ~3;
       const int rbeg = part * RP, rend = min(R, rbeg + RP);
       const float4* __restrict__ F4 = reinterpret_cast<const float4*>(F);
+      constexpr int UV = 4;
+      float4 v[UV];
+      int dst[UV];
+      // the gathers of chunk c0 (its rows' feature float4s) into v / dst, issued, not waited for
+      auto gather = [&](int c0, int f0) {
+        const int nf = min(CH, rend - c0) * C4;
+#pragma unroll
+        for (int u = 0; u < UV; ++u) {
+          const int f = min(f0 + u * kSgBlock, nf - 1);  // (a surplus lane reloads the last)
+          const int rr = (int)fdiv((uint32_t)f, g.div_c4);
+          const int cc = f - rr * C4;
+          v[u] = F4[(size_t)s_hit[c0 + rr] * C4 + cc];
+          dst[u] = rr * Cout + foff + 4 * cc;
+        }
+      };
+      // PN2_SG_PREFETCH: a chunk that one pass of UV float4s per thread covers has its
+      // successor's gathers issued before its own stores, so the gather round trip overlaps
+      // the store phase instead of following it
+      const bool one_pass = CH * C4 <= kSgBlock * UV;
+      if (PN2_SG_PREFETCH && one_pass && rbeg < rend) gather(rbeg, t);
       for (int c0 = rbeg; c0 < rend; c0 += CH) {
         const int nr = min(CH, rend - c0);
         const int nf = nr * C4;
-        constexpr int UV = 4;
         for (int f0 = t; f0 < nf; f0 += kSgBlock * UV) {
-          float4 v[UV];
-          int dst[UV];
-#pragma unroll
-          for (int u = 0; u < UV; ++u) {
-            const int f = min(f0 + u * kSgBlock, nf - 1);  // (a surplus lane reloads the last)
-            const int rr = (int)fdiv((uint32_t)f, g.div_c4);
-            const int cc = f - rr * C4;
-            v[u] = F4[(size_t)s_hit[c0 + rr] * C4 + cc];
-            dst[u] = rr * Cout + foff + 4 * cc;
-          }
+          if (!(PN2_SG_PREFETCH && one_pass)) gather(c0, f0);
 #pragma unroll
           for (int u = 0; u < UV; ++u) {
             if (f0 + u * kSgBlock < nf) {
@@ -232,6 +245,7 @@ __global__ __launch_bounds__(kSgBlock) void ball_group_layers_kernel(SgArgs a) {
           }
         }
         __syncthreads();
+        if (PN2_SG_PREFETCH && one_pass && c0 + CH < rend) gather(c0 + CH, t);
         float4* __restrict__ O4 = reinterpret_cast<float4*>(O + (size_t)c0 * Cout);
         const int n4 = (nr * Cout) >> 2;  // nr % 4 == 0 (R, RP and CH are multiples of 4)
         for (int k = t; k < n4; k += kSgBlock) O4[k] = s_out4[k];
