@@ -142,9 +142,6 @@ TIMING_EVENTS = False
 # MSG_SA1_SPLIT (A/B, PN2_MSG_SA1_SPLIT=1): MSG SA1's radii as one grid query launch each
 # (round 3) instead of one launch for all three (pn2_ball_group_xyz_grid_radii)
 MSG_SA1_SPLIT = os.environ.get("PN2_MSG_SA1_SPLIT") == "1"
-# CHAIN_PRIO (A/B, PN2_CHAIN_PRIO=1): the later samplers' own lane (the chain, 16 workgroups
-# on the step's latency path) at high stream priority, the SA1 sampler streams not
-CHAIN_PRIO = os.environ.get("PN2_CHAIN_PRIO") == "1"
 # FP4_SPLIT (A/B, PN2_FP4_SPLIT=1): FP4 as the round-3 launches (grid build, three_nn over it,
 # then the interpolation: tasks nn4 and fp4) instead of one pn2_fp_grid_fused launch;
 # NN4_LANE (PN2_NN4_LANE=n): then the lane of nn4 (2: with the interpolation)
@@ -214,10 +211,7 @@ def side_stream(dev, lane, part="side"):
     key = (str(dev), lane)
     if key not in _SIDE:
         masked = str(torch.device(dev)) in _CU_PART
-        # (a step's own sampler lane -- the chain -- has an int lane; Pipeline's extra SA1
-        # sampler streams are keyed ("sampler", i))
-        prio = -1 if (part == "sampler" and (str(torch.device(dev)) in _SAMPLER_PRIO
-                                             or (CHAIN_PRIO and isinstance(lane, int)))) else 0
+        prio = -1 if (part == "sampler" and str(torch.device(dev)) in _SAMPLER_PRIO) else 0
         _SIDE[key] = _masked_stream(dev, part) if masked else \
             torch.cuda.Stream(device=dev, priority=prio)
     return _SIDE[key]
