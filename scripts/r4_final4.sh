@@ -3,7 +3,7 @@
 # bound): the whole GPU suite, smoke, the driver's command twice, cfg3 and cfg5 once.
 set -o pipefail
 export TMPDIR=/tmp
-OUT=gpurun_out/r4/final4
+OUT=gpurun_out/r4/${FINAL_DIR:-final4}
 mkdir -p $OUT
 timeout -k 10 900 python3 -u -m pytest -x -q --timeout 280 --timeout-method thread -m gpu tests > $OUT/pytest_gpu.log 2>&1 || { tail -30 $OUT/pytest_gpu.log; exit 1; }
 tail -1 $OUT/pytest_gpu.log
