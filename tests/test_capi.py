@@ -108,6 +108,9 @@ def test_grid_contract(pn2):
     assert lib.pn2_ball_group_xyz_grid_radii(None, None, None, 1, 10, 10, 2, None, nsa, ptrs, ptrs, ptrs, None) == E
     assert lib.pn2_ball_group_xyz_grid_radii(None, None, None, 1, 10, 10, 2, rad, nsa, ptrs, ptrs, ptrs, None) == E
     assert lib.pn2_ball_group_xyz_grid_radii(None, None, None, 0, 10, 10, 2, rad, nsa, ptrs, ptrs, ptrs, None) == 0
+    # the bitmasks' LDS bound (nr * ceil(N / 32) <= 4096) is checked before any launch
+    fake = (ctypes.c_void_p * 4)(16, 16, 16, 16)
+    assert lib.pn2_ball_group_xyz_grid_radii(16, 16, 16, 1, 50000, 10, 3, rad, nsa, fake, fake, fake, None) == E
     assert lib.pn2_three_nn_grid(None, None, None, 0, 10, 10, None, None, None) == 0
     assert lib.pn2_fp_apply(None, None, None, None, 3, None, 4, 1, 4, 4, None, None) == E
     # pn2_fp_grid_fused: m in [1, 4096], dist and idx together, points1 with C1 > 0

@@ -160,6 +160,8 @@ GROUP_RADII_CASES = [
     ("scannet", 2, 8192, 1024, (0.4, 0.1), (8, 64), 0.1),             # unsorted, grid at r_min
     ("grid", 2, 4096, 500, (1.0, 2.0, 1.5), (16, 8, 32), 1.0),        # lattice ties at radii
     ("scannet", 1, 3000, 300, (0.3,), (40,), 0.5),                    # one radius
+    ("uniform", 1, 50000, 200, (0.03, 0.05, 0.08), (8, 16, 32), 0.05),  # beyond the LDS
+    # bound of one launch (3 x 1563 bitmask words): the wrapper's launch per radius
 ]
 
 
