@@ -375,6 +375,10 @@ def main():
     ap.add_argument("--hw-queues", type=int, default=None,
                     help="GPU_MAX_HW_QUEUES for this process (default: the environment's, else "
                          f"{DEFAULT_HW_QUEUES}; <= 32)")
+    ap.add_argument("--set-waits", choices=["host", "gpu"], default="host",
+                    help="before a buffer set is reused: the host waits for its previous step's "
+                         "lanes (host), or the step's sampler stream and lane 1 carry GPU wait "
+                         "packets on them and the host runs ahead (gpu; stack.GPU_SET_WAITS)")
     ap.add_argument("--alt-lanes", default=None,
                     help="comma list of side lanes whose work of every other buffer set runs on a "
                          "second stream (e.g. 2 = FP4's lane); default: the config's LAYOUTS entry")
@@ -493,6 +497,7 @@ def main():
         torch.cuda.synchronize()
         if pipelined:
             pkg.stack.TIMING_EVENTS = bool(args.timeline) and not model
+            pkg.stack.GPU_SET_WAITS = args.set_waits == "gpu"
             if not model and args.sampler_lanes > 1:
                 # CU-masked sampler and side streams (stack.set_cu_partition), before any
                 # stream of the pipeline exists
@@ -654,6 +659,7 @@ def main():
                        "lane0_priority": prio0,
                        "sampler_priority": args.sampler_priority,
                        "alt_lanes": list(alt_lanes),
+                       "set_waits": args.set_waits,
                        **({"DIAGNOSTIC_dup_tasks": sorted(pkg.stack.DUP_TASKS)}
                           if pkg.stack.DUP_TASKS else {}),
                        "streams": (("SA1 sampler + 3 side streams" if args.sampler_lanes <= 1 or args.model

@@ -139,6 +139,13 @@ LANE_JOIN = os.environ.get("PN2_LANE_JOIN") == "1"
 SEG_MERGE = os.environ.get("PN2_SEG_MERGE") == "1"
 # lane-end events with timing (DIAGNOSTIC: bench.py --timeline sets it before the pipeline)
 TIMING_EVENTS = False
+# GPU_SET_WAITS (bench.py --set-waits gpu, set before the pipeline is built): a buffer set's
+# next step waits for its previous step's lanes ON THE GPU -- its sampler stream and lane 1
+# (the grid build, the only other writer of a buffer another lane read) carry wait packets on
+# the set's lane-end events -- instead of the host blocking on those events before it
+# enqueues the step. The host then runs ahead, and a sampler starts when its set is free, not
+# after the host has woken up and enqueued the whole step.
+GPU_SET_WAITS = False
 # MSG_SA1_SPLIT (A/B, PN2_MSG_SA1_SPLIT=1): MSG SA1's radii as one grid query launch each
 # (round 3) instead of one launch for all three (pn2_ball_group_xyz_grid_radii)
 MSG_SA1_SPLIT = os.environ.get("PN2_MSG_SA1_SPLIT") == "1"
@@ -812,7 +819,7 @@ class Step:
     def segment_key(seg):
         return "+".join(t.name for t in seg)
 
-    def emit_plan(self, plan, graphs, main):
+    def emit_plan(self, plan, graphs, main, set_waits=False):
         """Record the step -- per launch segment (segments()): its cross-lane waits, its
         hipGraph (graphs[segment_key]) or direct sampler launch (the task's `chain` spec), and
         the release events other lanes wait for; lane 0 = `main`; then the lane join of run()
@@ -820,6 +827,13 @@ class Step:
         the whole step. The SA1 sampler is the plan's timed operation."""
         assert self.overlap and self.synced_inputs
         lane_of = {t.name: t.lane for t in self.tasks}
+        if set_waits:
+            # this set's previous step must be done with the buffers the step rewrites: the
+            # sampler's outputs (read by every lane) and the SA1 grid (read by FP4's lane); the
+            # other lanes' writes follow this step's sampler. (Never-recorded events: no-ops.)
+            for st in (main, self._stream(1, main)):
+                for lane in self.done_lanes():
+                    plan.wait(st, self.lane_done[lane])
         for seg in self.segments():
             lane = seg[0].lane
             st = self._stream(lane, main)
@@ -937,25 +951,25 @@ class GraphStep:
                       launch=lambda t: t.fn() if t.direct else self.graphs[t.name].replay())
         return self.outs
 
-    def plan_for(self, main):
+    def plan_for(self, main, set_waits=False):
         """The native plan of this step with `main` as lane 0, recorded at the first request
         (Pipeline records every (set, sampler stream) pair it will use up front, so no plan is
         built inside a timed region)."""
         if not hasattr(self, "plans"):
             self.plans = {}
-        p = self.plans.get(main.cuda_stream)
+        p = self.plans.get((main.cuda_stream, set_waits))
         if p is None:
             from .plan import Plan
             p = Plan()
-            self.step.emit_plan(p, self.graphs, main)
-            self.plans[main.cuda_stream] = p
+            self.step.emit_plan(p, self.graphs, main, set_waits)
+            self.plans[(main.cuda_stream, set_waits)] = p
         return p
 
-    def replay_plan(self, sampler_events=None):
+    def replay_plan(self, sampler_events=None, set_waits=False):
         """replay(join=False) through a native plan (one host call for the whole step) for the
         current stream as lane 0."""
         main = torch.cuda.current_stream(self.step.inp["xyz"].device)
-        self.plan_for(main).launch(sampler_events)
+        self.plan_for(main, set_waits).launch(sampler_events)
         self.step.ran = True
         return self.outs
 
@@ -1028,6 +1042,8 @@ class Pipeline:
         # (include/pn2plan.h), its side lanes as a few segment graphs, instead of the per-task
         # Python loop
         self.native_plan = native_plan and graphs and overlap and inp["xyz"].is_cuda
+        # set reuse ordered on the GPU (the plans built below carry the waits)
+        self.gpu_set_waits = GPU_SET_WAITS and self.native_plan
         # only: DIAGNOSTIC restriction of every step to its samplers or its side work
         if set_inputs is not None and len(set_inputs) != nsets:
             raise ValueError(f"set_inputs: {len(set_inputs)} input dicts for {nsets} sets")
@@ -1051,7 +1067,7 @@ class Pipeline:
             nl = len(self.lane0)
             for k in range(nsets * nl // math.gcd(nsets, nl)):
                 st = self.lane0[k % nl] or torch.cuda.current_stream(dev)
-                self.sets[k % nsets].plan_for(st)
+                self.sets[k % nsets].plan_for(st, self.gpu_set_waits)
 
     def run(self, sampler_events=None):
         st = self.lane0[self.k % len(self.lane0)]
@@ -1102,8 +1118,9 @@ class Pipeline:
         try:
             if isinstance(s, GraphStep):
                 if s.step.ran and s.step.overlap:
-                    for lane in s.step.done_lanes():  # this set's previous side work
-                        s.step.lane_done[lane].synchronize()
+                    if not self.gpu_set_waits:  # (else: wait packets in the plan)
+                        for lane in s.step.done_lanes():  # this set's previous side work
+                            s.step.lane_done[lane].synchronize()
                 else:
                     s.step.join()
                 t1 = time.perf_counter()
@@ -1116,7 +1133,7 @@ class Pipeline:
                     self._last_of_set[si] = len(tr) - 1
                 t0 = t1
                 if self.native_plan:
-                    return s.replay_plan(sampler_events)
+                    return s.replay_plan(sampler_events, self.gpu_set_waits)
                 return s.replay(sampler_events, join=False)
             s.join()
             return s.run(sampler_events, join=False)

@@ -127,18 +127,22 @@ def _poison_sampled(pipe, torch):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("lanes,native,layout,own,cus", [
-    (1, False, "a", False, 0), (1, True, "a", False, 0), (2, True, "a", False, 0),
-    (3, True, "b", False, 0), (3, True, "b", True, 0), (3, True, "b", True, 64)])
+@pytest.mark.parametrize("lanes,native,layout,own,cus,gpuwait", [
+    (1, False, "a", False, 0, False), (1, True, "a", False, 0, False),
+    (2, True, "a", False, 0, False), (3, True, "b", False, 0, False),
+    (3, True, "b", True, 0, False), (3, True, "b", True, 64, False),
+    (3, True, "b", True, 0, True), (1, True, "a", False, 0, True)])
 @pytest.mark.parametrize("config,B", CONFIGS)
-def test_pipeline_full_size(env, config, B, lanes, native, layout, own, cus):
+def test_pipeline_full_size(env, config, B, lanes, native, layout, own, cus, gpuwait):
     """What bench.py times: the software-pipelined hipGraph steps over 3 buffer sets, at the
     BASELINE batch, after several rotations, with one, two or three sampler streams
     (consecutive steps' samplers concurrent), enqueued by the Python task loop or by the native
     plan (include/pn2plan.h), side layouts a and b (stack.side_layout), the later samplers
     behind SA1 or on a stream of their own (chain_own). The sampled coordinates
     of every set are poisoned before the last three steps (a missing wait then shows), and the
-    last two steps' outputs (one per sampler stream) are compared with the oracle."""
+    last two steps' outputs (one per sampler stream) are compared with the oracle. gpuwait:
+    buffer-set reuse ordered by GPU wait packets (stack.GPU_SET_WAITS) while the host runs
+    ahead without blocking."""
     pkg, O, torch, dev = env
     # every set its own clouds (as bench.py runs it): a set that read another set's buffers
     # would give outputs that match no oracle run
@@ -149,8 +153,13 @@ def test_pipeline_full_size(env, config, B, lanes, native, layout, own, cus):
     saved = dict(pkg.stack._SIDE)
     if cus:
         pkg.stack._SIDE.clear()  # fresh (masked) streams for this pipeline
-    pipe = pkg.stack.Pipeline(inp, graphs=True, nsets=3, sampler_lanes=lanes, native_plan=native,
-                              layout=layout, chain_own=own, set_inputs=sets)
+    pkg.stack.GPU_SET_WAITS = gpuwait
+    try:
+        pipe = pkg.stack.Pipeline(inp, graphs=True, nsets=3, sampler_lanes=lanes,
+                                  native_plan=native, layout=layout, chain_own=own,
+                                  set_inputs=sets)
+    finally:
+        pkg.stack.GPU_SET_WAITS = False  # (the plans have their waits from here on)
     assert len(pipe.lane0) == lanes
     assert pipe.native_plan == native
     if native:  # every (set, sampler stream) plan exists before the first step
