@@ -353,9 +353,6 @@ def main():
                     help="with several sampler streams: the later samplers (SA2.. chain) on a "
                          "stream of their own or behind SA1 on its sampler stream (default: the "
                          "config's LAYOUTS entry)")
-    ap.add_argument("--cu-partition", type=int, default=None, metavar="CUS",
-                    help="run the samplers on CUS CUs and the side lanes on the others "
-                         "(CU-masked streams; default: the config's LAYOUTS entry, 0 = off)")
     ap.add_argument("--private-side", action="store_true",
                     help="every buffer set gets its own side streams (side work of consecutive "
                          "steps runs concurrently; needs 1 + 2 x sets + sampler lanes - 1 "
@@ -375,17 +372,9 @@ def main():
     ap.add_argument("--hw-queues", type=int, default=None,
                     help="GPU_MAX_HW_QUEUES for this process (default: the environment's, else "
                          f"{DEFAULT_HW_QUEUES}; <= 32)")
-    ap.add_argument("--set-waits", choices=["host", "gpu"], default="host",
-                    help="before a buffer set is reused: the host waits for its previous step's "
-                         "lanes (host), or the step's sampler stream and lane 1 carry GPU wait "
-                         "packets on them and the host runs ahead (gpu; stack.GPU_SET_WAITS)")
-    ap.add_argument("--alt-lanes", default=None,
-                    help="comma list of side lanes whose work of every other buffer set runs on a "
-                         "second stream (e.g. 2 = FP4's lane); default: the config's LAYOUTS entry")
-    ap.add_argument("--sampler-priority", choices=["default", "high"], default=None,
-                    help="stream priority of every sampler stream (lane 0, the extra sampler "
-                         "streams, the later samplers' own stream); default: the config's "
-                         "LAYOUTS entry")
+    ap.add_argument("--graph-launch", action="store_true",
+                    help="A/B: launch each side segment as its captured hipGraph instead of its "
+                         "kernels directly (pn2_plan_graph_direct; DESIGN.md §3.6d)")
     ap.add_argument("--lane0-priority", choices=["auto", "default", "high"], default="auto",
                     help="stream priority of lane 0 (the SA1 sampler chain); auto = default "
                          "for the geometric step, high for the whole model")
@@ -420,17 +409,12 @@ def main():
         args.sampler_lanes = 1 if args.model else lay["lanes"]
     if args.sets is None:
         args.sets = 3 if args.model else lay["sets"]
+    if args.sets < 2:
+        ap.error("--sets: a pipelined run needs at least 2 buffer sets")
     if args.side_layout is None:
         args.side_layout = lay["side"]
     if args.chain is None:
         args.chain = lay["chain"]
-    if args.cu_partition is None:
-        args.cu_partition = 0 if args.model else lay.get("cu", 0)
-    if args.sampler_priority is None:
-        args.sampler_priority = lay.get("prio", "default")
-    if args.alt_lanes is None:
-        args.alt_lanes = lay.get("alt", "")
-    alt_lanes = tuple(int(x) for x in args.alt_lanes.split(",") if x.strip())
     if args.hw_queues is None and not args.model and args.sampler_lanes == lay["lanes"]:
         args.hw_queues = lay["queues"]  # one queue per stream (the box's default is 4)
     if args.hw_queues is not None:
@@ -474,7 +458,7 @@ def main():
     def measure(model, steps, warmup):
         prio = args.lane0_priority
         if prio == "auto":
-            prio = "high" if (model or args.sampler_priority == "high") else "default"
+            prio = "high" if model else "default"
         lane0 = (torch.cuda.Stream(device=dev, priority=-1) if prio == "high"
                  else torch.cuda.current_stream(dev))
         with torch.cuda.stream(lane0):
@@ -490,19 +474,13 @@ def main():
         # every buffer set holds its own clouds (shard.set_ids): consecutive pipelined steps
         # sample different clouds, never one input replayed
         set_inputs = ([pkg.stack.make_inputs(args.config, pkg.shard.set_ids(rank, world, B, i),
-                                             dev, model=model) for i in range(max(2, args.sets))]
+                                             dev, model=model) for i in range(args.sets)]
                       if pipelined else None)
         inp = set_inputs[0] if pipelined else pkg.stack.make_inputs(args.config, ids, dev,
                                                                      model=model)
         torch.cuda.synchronize()
         if pipelined:
             pkg.stack.TIMING_EVENTS = bool(args.timeline) and not model
-            pkg.stack.GPU_SET_WAITS = args.set_waits == "gpu"
-            if not model and args.sampler_lanes > 1:
-                # CU-masked sampler and side streams (stack.set_cu_partition), before any
-                # stream of the pipeline exists
-                pkg.stack.set_cu_partition(dev, args.cu_partition)
-                pkg.stack.set_sampler_priority(dev, args.sampler_priority == "high")
             pipe = pkg.stack.Pipeline(inp, graphs=not args.eager, nsets=args.sets,
                                       sampler_lanes=1 if model else args.sampler_lanes,
                                       private_streams=model or args.private_side,
@@ -511,7 +489,7 @@ def main():
                                       chain_own=args.chain in ("own", "own2"),
                                       chain_streams=2 if args.chain == "own2" else 1,
                                       set_inputs=set_inputs,
-                                      alt_lanes=() if model else alt_lanes)
+                                      direct=not args.graph_launch)
         else:
             step = pkg.stack.Step(inp, overlap=overlap)
             graph = None if args.eager else pkg.stack.GraphStep(inp, overlap=overlap)
@@ -650,18 +628,12 @@ def main():
                        "parallelism": f"dp{world} (batch split)",
                        "launch": "eager" if args.eager else
                        ("samplers: direct launches; side lanes: hipGraph replay"
-                        + ("; one native plan call per step (include/pn2plan.h)"
+                        + ("; one native plan call per step (include/pn2plan.h), side "
+                           + ("segments as graph launches" if args.graph_launch else
+                              "kernels launched directly")
                            if pipelined and not args.no_native_plan else "")),
                        "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "0")),
-                       "cu_partition": (f"samplers on {args.cu_partition} CUs, side lanes on "
-                                        "the others" if args.cu_partition and not args.model
-                                        and args.sampler_lanes > 1 else "none"),
                        "lane0_priority": prio0,
-                       "sampler_priority": args.sampler_priority,
-                       "alt_lanes": list(alt_lanes),
-                       "set_waits": args.set_waits,
-                       **({"DIAGNOSTIC_dup_tasks": sorted(pkg.stack.DUP_TASKS)}
-                          if pkg.stack.DUP_TASKS else {}),
                        "streams": (("SA1 sampler + 3 side streams" if args.sampler_lanes <= 1 or args.model
                                     else f"{args.sampler_lanes} sampler streams (consecutive steps' "
                                     f"samplers concurrent; SA2.. samplers "

@@ -58,14 +58,16 @@ int pn2_plan_launch(pn2_plan* plan);
  * be NULL) */
 int pn2_plan_launch_timed(pn2_plan* plan, void* ev_start, void* ev_end);
 
-/* EXPERIMENTAL (measured as a loss, off by default; kept for A/B runs, bench.py
- * --cu-partition): a stream whose kernels run only on the CUs set in `mask` (bit i of word
- * i / 32 = CU i; hipExtStreamCreateWithCUMask), so the latency-bound samplers and the side
- * lanes can be given disjoint CUs (samplers 0.44 -> 0.41 ms, side lanes
- * slower by more). 0 and *stream, or the HIP error. Destroy with pn2_stream_destroy. No
- * product path calls these. */
-int pn2_stream_create_cu_mask(const uint32_t* mask, int words, pn2_stream_t* stream);
-int pn2_stream_destroy(pn2_stream_t stream);
+/* append: the nodes of the captured graph `graph` (hipGraph_t, not instantiated: torch
+ * CUDAGraph(keep_graph=True).raw_cuda_graph()) as direct kernel launches / memsets on
+ * `stream`, in dependency order -- what launching the graph would enqueue, without the graph
+ * launch's host cost (~24 vs ~5 us for a one-kernel graph, profiles/r5/start). Only a plain chain
+ * of kernel and memset nodes qualifies: anything else returns PN2_ENOTSUP and appends nothing
+ * (then use pn2_plan_graph). The graph's argument storage is borrowed: keep the graph alive and
+ * unchanged while the plan is launched. */
+int pn2_plan_graph_direct(pn2_plan* plan, void* graph, pn2_stream_t stream);
+
+#define PN2_ENOTSUP (-95) /* pn2_plan_graph_direct: not a plain chain of kernel / memset nodes */
 
 #ifdef __cplusplus
 }

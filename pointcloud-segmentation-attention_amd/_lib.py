@@ -19,8 +19,8 @@ PN2_EINVAL = -22
 PN2_BQ_MAX_RADII = 3  # include/pn2hip.h
 PN2_EFAULT = -14
 PN2_FAULT_FPS_POLL = 1
-PN2_FPS_AUTO, PN2_FPS_BLOCKSCAN, PN2_FPS_HOTCULL_K128 = 0, 1, 6
-PN2_FPS_HOTCULL_LEAN, PN2_FPS_HOTCULL_LDS = 7, 8
+PN2_ENOTSUP = -95  # include/pn2plan.h
+PN2_FPS_AUTO, PN2_FPS_BLOCKSCAN = 0, 1
 PN2_USE_XYZ = 1
 PN2_XYZ_LAST = 2
 POOL_MODES = {"max": 0, "avg": 1, "weighted_avg": 2, "max_and_avg": 3}
@@ -141,8 +141,7 @@ SIGNATURES = {
     "pn2_plan_size": (_I, [_P]),
     "pn2_plan_launch": (_I, [_P]),
     "pn2_plan_launch_timed": (_I, [_P, _P, _P]),
-    "pn2_stream_create_cu_mask": (_I, [_P, _I, _P]),
-    "pn2_stream_destroy": (_I, [_P]),
+    "pn2_plan_graph_direct": (_I, [_P, _P, _P]),
 }
 
 _lib = None

@@ -15,7 +15,7 @@
 
 namespace {
 
-enum OpKind { kGraph, kRecord, kWait, kFpsChain };
+enum OpKind { kGraph, kRecord, kWait, kFpsChain, kKernel, kMemset };
 
 struct Op {
   OpKind kind;
@@ -27,6 +27,10 @@ struct Op {
   int npoint[4];
   int32_t* idx[4];
   float* nx[4];
+  // kKernel / kMemset: a node of a captured graph, launched directly (pn2_plan_graph_direct);
+  // the argument arrays belong to the graph, which the caller keeps alive
+  hipKernelNodeParams kp;
+  hipMemsetParams mp;
 };
 
 }  // namespace
@@ -49,6 +53,17 @@ int run_op(const Op& o) {
     case kFpsChain:
       return pn2::fps_chain_launch(o.xyz, o.B, o.N, o.nstages, o.npoint, o.idx, o.nx, o.stream,
                                    false);
+    case kKernel:
+      return (int)hipLaunchKernel(o.kp.func, o.kp.gridDim, o.kp.blockDim, o.kp.kernelParams,
+                                  o.kp.sharedMemBytes, o.stream);
+    case kMemset:  // one row (pn2_plan_graph_direct accepts nothing else)
+      if (o.mp.elementSize == 4)
+        return (int)hipMemsetD32Async((hipDeviceptr_t)o.mp.dst, (int)o.mp.value, o.mp.width,
+                                      o.stream);
+      if (o.mp.elementSize == 2)
+        return (int)hipMemsetD16Async((hipDeviceptr_t)o.mp.dst, (unsigned short)o.mp.value,
+                                      o.mp.width, o.stream);
+      return (int)hipMemsetAsync(o.mp.dst, (int)o.mp.value, o.mp.width, o.stream);
   }
   return PN2_EINVAL;
 }
@@ -150,20 +165,74 @@ int pn2_plan_launch_timed(pn2_plan* plan, void* ev_start, void* ev_end) {
   return launch(plan, ev_start, ev_end);
 }
 
-// CU-partitioned streams (hipExtStreamCreateWithCUMask): `mask` holds one bit per CU (bit i of
-// word i / 32 = CU i). Returns 0 and the new stream, or the HIP error.
-int pn2_stream_create_cu_mask(const uint32_t* mask, int words, pn2_stream_t* stream) {
-  if (!mask || words <= 0 || !stream) return PN2_EINVAL;
-  hipStream_t s = nullptr;
-  const hipError_t e = hipExtStreamCreateWithCUMask(&s, (uint32_t)words, mask);
-  if (e != hipSuccess) return (int)e;
-  *stream = (pn2_stream_t)s;
+// The nodes of a captured graph as direct launches, in dependency order: a single-kernel graph
+// launch cost the host ~24 us per call against ~5 us for the kernel launch it wraps (rocprofv3
+// --hip-runtime-trace, profiles/r5/start), and the side lanes' segments are one or two
+// kernels each. Only a plain chain of kernel and memset nodes qualifies; anything else (a
+// fork, an event or copy node) returns PN2_ENOTSUP with nothing appended, and the caller
+// keeps the graph launch.
+int pn2_plan_graph_direct(pn2_plan* plan, void* graph, pn2_stream_t stream) {
+  if (!plan || !graph) return PN2_EINVAL;
+  hipGraph_t g = (hipGraph_t)graph;
+  size_t n = 0;
+  if (hipGraphGetNodes(g, nullptr, &n) != hipSuccess) return PN2_ENOTSUP;
+  if (n == 0) return PN2_OK;
+  std::vector<hipGraphNode_t> nodes(n);
+  if (hipGraphGetNodes(g, nodes.data(), &n) != hipSuccess) return PN2_ENOTSUP;
+  // the chain: each node has at most one dependency, and no two nodes share one
+  std::vector<int> prev(n, -1);
+  std::vector<int> nxt(n, -1);
+  for (size_t i = 0; i < n; ++i) {
+    size_t nd = 0;
+    if (hipGraphNodeGetDependencies(nodes[i], nullptr, &nd) != hipSuccess || nd > 1)
+      return PN2_ENOTSUP;
+    if (nd == 1) {
+      hipGraphNode_t d = nullptr;
+      if (hipGraphNodeGetDependencies(nodes[i], &d, &nd) != hipSuccess) return PN2_ENOTSUP;
+      int j = -1;
+      for (size_t k = 0; k < n; ++k)
+        if (nodes[k] == d) j = (int)k;
+      if (j < 0 || nxt[j] >= 0) return PN2_ENOTSUP;
+      nxt[j] = (int)i;
+      prev[i] = j;
+    }
+  }
+  int head = -1;
+  for (size_t i = 0; i < n; ++i) {
+    if (prev[i] < 0) {
+      if (head >= 0) return PN2_ENOTSUP;  // two roots
+      head = (int)i;
+    }
+  }
+  std::vector<Op> ops;
+  size_t seen = 0;
+  for (int i = head; i >= 0; i = nxt[i]) {
+    if (++seen > n) return PN2_ENOTSUP;
+    hipGraphNodeType t;
+    if (hipGraphNodeGetType(nodes[i], &t) != hipSuccess) return PN2_ENOTSUP;
+    Op o = blank(kKernel, (hipStream_t)stream, nullptr);
+    if (t == hipGraphNodeTypeKernel) {
+      if (hipGraphKernelNodeGetParams(nodes[i], &o.kp) != hipSuccess || o.kp.extra ||
+          !o.kp.func)
+        return PN2_ENOTSUP;
+    } else if (t == hipGraphNodeTypeMemset) {
+      o.kind = kMemset;
+      if (hipGraphMemsetNodeGetParams(nodes[i], &o.mp) != hipSuccess || o.mp.height > 1 ||
+          (o.mp.elementSize != 1 && o.mp.elementSize != 2 && o.mp.elementSize != 4))
+        return PN2_ENOTSUP;
+    } else if (t != hipGraphNodeTypeEmpty) {
+      return PN2_ENOTSUP;
+    } else {
+      continue;
+    }
+    ops.push_back(o);
+  }
+  if (seen != n) return PN2_ENOTSUP;  // (a cycle or an unreachable node)
+  for (const Op& o : ops) {
+    const int rc = append(plan, o);
+    if (rc != PN2_OK) return rc;
+  }
   return PN2_OK;
-}
-
-int pn2_stream_destroy(pn2_stream_t stream) {
-  const hipError_t e = hipStreamDestroy((hipStream_t)stream);
-  return e == hipSuccess ? PN2_OK : (int)e;
 }
 
 }  // extern "C"

@@ -1,9 +1,10 @@
 """Python owner of a native step plan (include/pn2plan.h, csrc/plan.hip).
 
 A plan records a step's stream operations once -- hipGraph launches of the captured side-lane
-tasks, the direct sampler launches, event records and cross-stream waits -- and enqueues all
-of them with ONE call into libpn2hip.so per step (stack.GraphStep.replay_plan). The handles
-it records are borrowed from torch (CUDAGraph.raw_cuda_graph_exec(), Event.cuda_event,
+tasks (or, when a task's graph is a plain chain of kernels, those kernels as direct launches),
+the direct sampler launches, event records and cross-stream waits -- and enqueues all of them
+with ONE call into libpn2hip.so per step (stack.GraphStep.replay_plan). The handles it
+records are borrowed from torch (CUDAGraph.raw_cuda_graph(_exec)(), Event.cuda_event,
 Stream.cuda_stream) and the sampler buffers from the step: the plan keeps references to those
 objects so they outlive it.
 """
@@ -11,7 +12,7 @@ import ctypes
 
 import torch
 
-from ._lib import InvalidArgumentError, check, lib
+from ._lib import PN2_ENOTSUP, InvalidArgumentError, check, lib
 
 
 def _event_handle(ev):
@@ -29,6 +30,7 @@ class Plan:
         if not self.h:
             raise MemoryError("pn2_plan_create")
         self._keep = []  # graphs, events, streams, tensors and ctypes arrays the plan points at
+        self.launches = {"direct": 0, "graph": 0}  # side segments by how they are enqueued
 
     def __del__(self):
         h, self.h = getattr(self, "h", None), None
@@ -43,6 +45,21 @@ class Plan:
         self._keep += [g, stream]
         check(self._lib.pn2_plan_graph(self.h, g.raw_cuda_graph_exec(), stream.cuda_stream),
               "pn2_plan_graph")
+        self.launches["graph"] += 1
+
+    def graph_direct(self, g, stream):
+        """The kernels of the captured torch CUDAGraph `g` (made with keep_graph=True) as direct
+        launches on `stream` (pn2_plan_graph_direct); a graph that is not a plain chain of
+        kernel / memset nodes is launched as a graph instead (pn2_plan_graph). Returns True
+        when the kernels went in directly."""
+        self._keep += [g, stream]
+        rc = self._lib.pn2_plan_graph_direct(self.h, g.raw_cuda_graph(), stream.cuda_stream)
+        if rc == PN2_ENOTSUP:
+            self.graph(g, stream)
+            return False
+        check(rc, "pn2_plan_graph_direct")
+        self.launches["direct"] += 1
+        return True
 
     def record(self, ev, stream):
         self._keep += [ev, stream]

@@ -130,97 +130,18 @@ def make_inputs(config, cloud_ids, device, seed=1234, model=False):
 
 
 _SIDE = {}
-# LANE_JOIN (A/B, PN2_LANE_JOIN=1): lanes 2.. hand their end to lane 1 with cross-queue waits
-# and one event marks a step's end; otherwise every lane records its own end event and the
-# host waits for all of them (no wait packets on the side queues)
-LANE_JOIN = os.environ.get("PN2_LANE_JOIN") == "1"
-# SEG_MERGE (A/B, PN2_SEG_MERGE=1): a lane's consecutive tasks share one launch segment even
-# when a later task waits for another producer (the segment then waits for all of them first)
-SEG_MERGE = os.environ.get("PN2_SEG_MERGE") == "1"
 # lane-end events with timing (DIAGNOSTIC: bench.py --timeline sets it before the pipeline)
 TIMING_EVENTS = False
-# GPU_SET_WAITS (bench.py --set-waits gpu, set before the pipeline is built): a buffer set's
-# next step waits for its previous step's lanes ON THE GPU -- its sampler stream and lane 1
-# (the grid build, the only other writer of a buffer another lane read) carry wait packets on
-# the set's lane-end events -- instead of the host blocking on those events before it
-# enqueues the step. The host then runs ahead, and a sampler starts when its set is free, not
-# after the host has woken up and enqueued the whole step.
-GPU_SET_WAITS = False
-# MSG_SA1_SPLIT (A/B, PN2_MSG_SA1_SPLIT=1): MSG SA1's radii as one grid query launch each
-# (round 3) instead of one launch for all three (pn2_ball_group_xyz_grid_radii)
-MSG_SA1_SPLIT = os.environ.get("PN2_MSG_SA1_SPLIT") == "1"
-# FP4_SPLIT (A/B, PN2_FP4_SPLIT=1): FP4 as the round-3 launches (grid build, three_nn over it,
-# then the interpolation: tasks nn4 and fp4) instead of one pn2_fp_grid_fused launch;
-# NN4_LANE (PN2_NN4_LANE=n): then the lane of nn4 (2: with the interpolation)
-FP4_SPLIT = os.environ.get("PN2_FP4_SPLIT") == "1"
-NN4_LANE = int(os.environ.get("PN2_NN4_LANE", "2"))
-# DIAGNOSTIC (PN2_DUP_TASKS=sa1,fp4,...): the named tasks run twice in their captured graph
-# (same inputs, same results), so a bench run prices one extra copy of each -- its marginal
-# cost in the pipelined step (scripts/r4_dup.sh). Never set by the product.
-DUP_TASKS = frozenset(t for t in os.environ.get("PN2_DUP_TASKS", "").split(",") if t)
-_CU_PART = {}  # device -> {"sampler": mask words, "side": mask words} (set_cu_partition)
 
 
-def set_cu_partition(dev, sampler_cus=64):
-    """Give the latency-bound samplers (SA1 streams and the later-sampler chain) and the side
-    lanes DISJOINT CUs: streams created from now on (side_stream, Pipeline's sampler streams)
-    are CU-masked (include/pn2plan.h pn2_stream_create_cu_mask). The sampler part is 8
-    consecutive CU bits out of every 32, so it spreads evenly over the XCDs whichever way the
-    bits map onto them; sampler_cus = 0 turns the partition off for new streams."""
-    key = str(torch.device(dev))
-    if not sampler_cus:
-        _CU_PART.pop(key, None)
-        return
-    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
-    per32 = max(1, min(31, round(32 * sampler_cus / ncu)))
-    words = (ncu + 31) // 32
-    samp = [0] * words
-    side = [0] * words
-    for i in range(ncu):
-        if i % 32 < per32:
-            samp[i // 32] |= 1 << (i % 32)
-        else:
-            side[i // 32] |= 1 << (i % 32)
-    _CU_PART[key] = {"sampler": samp, "side": side}
-
-
-def _masked_stream(dev, part):
-    import ctypes
-    from ._lib import check, lib
-    words = _CU_PART[str(torch.device(dev))][part]
-    arr = (ctypes.c_uint32 * len(words))(*words)
-    h = ctypes.c_void_p()
-    with torch.cuda.device(dev):
-        check(lib().pn2_stream_create_cu_mask(arr, len(words), ctypes.byref(h)), "cu mask stream")
-    return torch.cuda.ExternalStream(h.value, device=dev)
-
-
-_SAMPLER_PRIO = set()  # devices whose sampler streams are created with high priority
-
-
-def set_sampler_priority(dev, high=True):
-    """Streams created from now on for the samplers (Pipeline's extra sampler streams, the
-    later samplers' own lane) get high priority: when a CU drains, the dispatcher then
-    serves a waiting sampler workgroup (which needs a whole CU: 16 waves x 128 VGPRs, 150 KB
-    of LDS) before the side lanes' workgroups refill it."""
-    key = str(torch.device(dev))
-    if high:
-        _SAMPLER_PRIO.add(key)
-    else:
-        _SAMPLER_PRIO.discard(key)
-
-
-def side_stream(dev, lane, part="side"):
+def side_stream(dev, lane):
     """The process-wide side stream of `lane` on `dev`: every Step shares them, so the
     sampler chain (the current stream) and the side lanes stay on distinct hardware queues
     (HIP gives each new stream a new hardware queue up to GPU_MAX_HW_QUEUES, then shares the
     least-used ones): the first Step creates lanes 1-3 before any other stream exists."""
     key = (str(dev), lane)
     if key not in _SIDE:
-        masked = str(torch.device(dev)) in _CU_PART
-        prio = -1 if (part == "sampler" and str(torch.device(dev)) in _SAMPLER_PRIO) else 0
-        _SIDE[key] = _masked_stream(dev, part) if masked else \
-            torch.cuda.Stream(device=dev, priority=prio)
+        _SIDE[key] = torch.cuda.Stream(device=dev)
     return _SIDE[key]
 
 
@@ -280,7 +201,7 @@ class Step:
 
     SAMPLER = "fps1"
 
-    def __init__(self, inp, overlap=True, streams=None, chain_lane=3, layout="a", alt_lanes=()):
+    def __init__(self, inp, overlap=True, streams=None, chain_lane=3, layout="a"):
         # chain_lane: the lane of the later samplers (SA2..SA4 / MSG SA2); 0 = behind the SA1
         # sampler on its stream; -1 = a lane of their own after the side lanes (both: several
         # sampler streams, Pipeline); layout: side_layout()
@@ -296,26 +217,14 @@ class Step:
             self.tasks = self._tasks_ssg() if self.kind == "ssg" else self._tasks_msg()
         self.ran = False
         self.synced_inputs = False
-        if alt_lanes:
-            # this step's tasks of the side lanes in alt_lanes run on lanes of their own after
-            # every other lane (Pipeline gives them to every other buffer set: consecutive
-            # steps' work of a saturated lane then runs on two queues)
-            top = 1 + max(t.lane for t in self.tasks)
-            remap = {L: top + j for j, L in enumerate(sorted(alt_lanes))}
-            for t in self.tasks:
-                t.lane = remap.get(t.lane, t.lane)
         self.nlanes = 1 + max(t.lane for t in self.tasks)
         if self.overlap:
             dev = inp["xyz"].device
-            # the later samplers' own lane (chain "own") counts as a sampler under a CU
-            # partition (set_cu_partition)
-            samp = {t.lane for t in self.tasks if t.direct and t.lane > 0}
             if streams and len(streams) < self.nlanes:
                 raise ValueError(f"this step layout uses {self.nlanes} lanes, {len(streams)} "
                                  "streams given")
             self.streams = [None] + (list(streams[1:self.nlanes]) if streams else
-                                     [side_stream(dev, lane, "sampler" if lane in samp else "side")
-                                      for lane in range(1, self.nlanes)])
+                                     [side_stream(dev, lane) for lane in range(1, self.nlanes)])
             # HIP binds a stream to a hardware queue when the stream is first used: use the
             # lanes now, in order, so that they (not the warm-up or capture streams made later)
             # get the queues the current stream does not hold
@@ -420,20 +329,7 @@ class Step:
             tasks.append(Task("fps234", chain_lane, ("fps1",), lambda: [fps(i)() for i in (1, 2, 3)]))
             sampled = ("fps1", "fps234", "fps234", "fps234")
         tasks.append(Task("sa1", 1, (sampled[0],), sa(0)))
-        if FP4_SPLIT and big and tf_interpolate.use_grid(int(inp["xyz"].shape[1]), SSG_SA[0][0]):
-            # (A/B) FP4 as three launches: the known grid's build + the search (task nn4),
-            # then the interpolation (task fp4), two tasks of lane 2 (one launch segment)
-            def nn4():
-                v["nn"][3] = tf_interpolate.three_nn(v["xyz"][0], v["xyz"][1],
-                                                     unknown_grid=v["grid1"])
-
-            def fp4():
-                v["fp"][3] = pointnet_util.fp_apply(v["nn"][3], points[0], fp_feat[3],
-                                                    unknown_grid=v["grid1"])
-            tasks.append(Task("nn4", NN4_LANE, (sampled[0],) + grid_dep, nn4))
-            tasks.append(Task("fp4", 2, ("nn4",), fp4))
-        else:
-            tasks.append(Task("fp4", 2, (sampled[0],) + grid_dep, fp(0)))
+        tasks.append(Task("fp4", 2, (sampled[0],) + grid_dep, fp(0)))
         if npoints[0] <= pointnet_util.BALL_GROUP_MAX_POINTS and sampled[1:] == ("fps234",) * 3:
             # SA2..SA4 wait for the same sampler launch: their three ball queries and groupings
             # run as ONE kernel (pn2_ball_group_layers) instead of six launches on the lane
@@ -624,7 +520,7 @@ class Step:
                     and max(MSG_SA[i][2]) <= pointnet_util.BALL_GROUP_MAX_NSAMPLE:
                 tasks.append(Task(f"sa{i + 1}", 2, (f"fps{i + 1}",), grp_all(i)))
                 continue
-            if i == 0 and grid_level and not MSG_SA1_SPLIT:
+            if i == 0 and grid_level:
                 tasks.append(Task("sa1", 1, ("fps1", "grid1"), grp_radii()))
                 continue
             for r in range(len(MSG_SA[i][1])):
@@ -708,16 +604,13 @@ class Step:
             elif timed:
                 sampler_events[1].record(st)
         # every lane records its own end; the host (Pipeline) and join() wait for all of them
-        for lane in range(2, self.nlanes):
+        for lane in range(1, self.nlanes):
             self.lane_done[lane].record(self.streams[lane])
-            if LANE_JOIN:
-                self.streams[1].wait_event(self.lane_done[lane])
-        self.lane_done[1].record(self.streams[1])
         return self.join() if join else None
 
     def done_lanes(self):
         """The lanes whose end events mark the end of the step's side work."""
-        return [1] if LANE_JOIN else list(range(1, self.nlanes))
+        return list(range(1, self.nlanes))
 
     def _needed_waits(self, waits):
         """`waits` minus the events another waited task already implies (its own cross-lane
@@ -782,10 +675,10 @@ class Step:
                 continue
             cur = open_seg.get(lane)
             xd = {d for d in t.deps if lane_of[d] != lane}
-            # a task that would add a wait to the open segment starts its own (unless
-            # PN2_SEG_MERGE=1, the round-3 rule): otherwise the segment's earlier tasks would
-            # wait for it too (SA1's grouping behind the later samplers' chain)
-            if cur is not None and not SEG_MERGE and not xd <= seg_waits[lane]:
+            # a task that would add a wait to the open segment starts its own: otherwise the
+            # segment's earlier tasks would wait for it too (SA1's grouping behind the later
+            # samplers' chain; profiles/r4/ab4)
+            if cur is not None and not xd <= seg_waits[lane]:
                 del open_seg[lane]
                 cur = None
             if cur is None:
@@ -819,21 +712,15 @@ class Step:
     def segment_key(seg):
         return "+".join(t.name for t in seg)
 
-    def emit_plan(self, plan, graphs, main, set_waits=False):
+    def emit_plan(self, plan, graphs, main, direct=True):
         """Record the step -- per launch segment (segments()): its cross-lane waits, its
-        hipGraph (graphs[segment_key]) or direct sampler launch (the task's `chain` spec), and
-        the release events other lanes wait for; lane 0 = `main`; then the lane join of run()
-        -- into a native plan (plan.Plan over include/pn2plan.h), so one host call enqueues
-        the whole step. The SA1 sampler is the plan's timed operation."""
+        captured kernels (graphs[segment_key]: launched directly when direct=True and the graph
+        is a plain chain of kernels, else as a graph) or direct sampler launch (the task's
+        `chain` spec), and the release events other lanes wait for; lane 0 = `main`; then the
+        lane ends of run() -- into a native plan (plan.Plan over include/pn2plan.h), so one host
+        call enqueues the whole step. The SA1 sampler is the plan's timed operation."""
         assert self.overlap and self.synced_inputs
         lane_of = {t.name: t.lane for t in self.tasks}
-        if set_waits:
-            # this set's previous step must be done with the buffers the step rewrites: the
-            # sampler's outputs (read by every lane) and the SA1 grid (read by FP4's lane); the
-            # other lanes' writes follow this step's sampler. (Never-recorded events: no-ops.)
-            for st in (main, self._stream(1, main)):
-                for lane in self.done_lanes():
-                    plan.wait(st, self.lane_done[lane])
         for seg in self.segments():
             lane = seg[0].lane
             st = self._stream(lane, main)
@@ -848,6 +735,8 @@ class Step:
                 if seg[0].chain is None:
                     raise RuntimeError(f"task {seg[0].name}: a direct task needs its chain spec")
                 plan.fps_chain(*seg[0].chain, st)
+            elif direct:
+                plan.graph_direct(graphs[self.segment_key(seg)], st)
             else:
                 plan.graph(graphs[self.segment_key(seg)], st)
             if seg[0].name == self.SAMPLER:
@@ -855,11 +744,8 @@ class Step:
             for t in seg:
                 if any(t.name in u.deps and u.lane != lane for u in self.tasks):
                     plan.record(self.done[t.name], st)
-        for lane in range(2, self.nlanes):  # as run(): each lane records its own end
+        for lane in range(1, self.nlanes):  # as run(): each lane records its own end
             plan.record(self.lane_done[lane], self.streams[lane])
-            if LANE_JOIN:
-                plan.wait(self.streams[1], self.lane_done[lane])
-        plan.record(self.lane_done[1], self.streams[1])
 
     def join(self):
         """Make the current stream wait for every lane; returns the outputs (None before the
@@ -891,11 +777,11 @@ class GraphStep:
     eager step. Inputs stay resident, outputs are overwritten in place at every replay."""
 
     def __init__(self, inp, warmup=2, overlap=True, streams=None, chain_lane=3, segments=False,
-                 only=None, layout="a", alt_lanes=()):
+                 only=None, layout="a"):
         # segments: capture one graph per launch segment (Step.segments(), for a native plan:
         # replay_plan) instead of one per task (replay)
         self.step = Step(inp, overlap=overlap, streams=streams, chain_lane=chain_lane,
-                         layout=layout, alt_lanes=alt_lanes)
+                         layout=layout)
         self.segmented = segments and self.step.overlap
         dev = inp["xyz"].device
         warm = side_stream(dev, "warm")
@@ -916,7 +802,8 @@ class GraphStep:
         cap = side_stream(dev, "capture")
 
         def capture_tasks(ts, lane, key):
-            g = torch.cuda.CUDAGraph()
+            # keep_graph: the plan reads the captured nodes (pn2_plan_graph_direct)
+            g = torch.cuda.CUDAGraph(keep_graph=True)
             st = torch.cuda.current_stream(dev)
             cap.wait_stream(st)
             if lane not in pools:
@@ -924,8 +811,7 @@ class GraphStep:
             with torch.cuda.graph(g, pool=pools[lane], stream=cap):
                 for t in ts:
                     t.fn()
-                    if t.name in DUP_TASKS:
-                        t.fn()
+            g.instantiate()
             st.wait_stream(cap)
             self.graphs[key] = g
 
@@ -951,25 +837,26 @@ class GraphStep:
                       launch=lambda t: t.fn() if t.direct else self.graphs[t.name].replay())
         return self.outs
 
-    def plan_for(self, main, set_waits=False):
+    def plan_for(self, main, direct=True):
         """The native plan of this step with `main` as lane 0, recorded at the first request
         (Pipeline records every (set, sampler stream) pair it will use up front, so no plan is
-        built inside a timed region)."""
+        built inside a timed region). direct: the side segments' kernels launched directly
+        (pn2_plan_graph_direct) instead of as graph launches."""
         if not hasattr(self, "plans"):
             self.plans = {}
-        p = self.plans.get((main.cuda_stream, set_waits))
+        p = self.plans.get((main.cuda_stream, direct))
         if p is None:
             from .plan import Plan
             p = Plan()
-            self.step.emit_plan(p, self.graphs, main, set_waits)
-            self.plans[(main.cuda_stream, set_waits)] = p
+            self.step.emit_plan(p, self.graphs, main, direct)
+            self.plans[(main.cuda_stream, direct)] = p
         return p
 
-    def replay_plan(self, sampler_events=None, set_waits=False):
+    def replay_plan(self, sampler_events=None, direct=True):
         """replay(join=False) through a native plan (one host call for the whole step) for the
         current stream as lane 0."""
         main = torch.cuda.current_stream(self.step.inp["xyz"].device)
-        self.plan_for(main, set_waits).launch(sampler_events)
+        self.plan_for(main, direct).launch(sampler_events)
         self.step.ran = True
         return self.outs
 
@@ -999,7 +886,7 @@ class Pipeline:
 
     def __init__(self, inp, graphs=True, overlap=True, nsets=3, private_streams=False,
                  sampler_lanes=1, native_plan=True, only=None, layout="a", chain_own=False,
-                 set_inputs=None, chain_streams=1, alt_lanes=()):
+                 set_inputs=None, chain_streams=1, direct=True):
         # chain_streams (with chain_own): the later samplers of set i run on chain stream
         # i % chain_streams, so consecutive steps' chains can overlap (one shared chain stream
         # runs one chain per step back to back: its launch time bounds the step)
@@ -1028,35 +915,30 @@ class Pipeline:
         if multi:
             # queues go to streams in order of first use: the extra sampler streams now, then
             # each set's side lanes when its Step is built (Step.__init__ touches them in
-            # order), all before the sets' warm-up and capture streams. Under a CU partition
-            # (set_cu_partition) every sampler lane is a masked stream, the first one too.
+            # order), all before the sets' warm-up and capture streams
             cur = torch.cuda.current_stream(dev)
-            part = str(torch.device(dev)) in _CU_PART
-            if part:
-                self.lane0 = []
-            for i in range(0 if part else 1, sampler_lanes):
-                st = side_stream(dev, ("sampler", i), "sampler")
+            for i in range(1, sampler_lanes):
+                st = side_stream(dev, ("sampler", i))
                 st.wait_stream(cur)
                 self.lane0.append(st)
         # native_plan: a graph step is enqueued by ONE call into the C++ executor
         # (include/pn2plan.h), its side lanes as a few segment graphs, instead of the per-task
         # Python loop
         self.native_plan = native_plan and graphs and overlap and inp["xyz"].is_cuda
-        # set reuse ordered on the GPU (the plans built below carry the waits)
-        self.gpu_set_waits = GPU_SET_WAITS and self.native_plan
+        # direct: the plans launch the side segments' captured kernels directly
+        # (pn2_plan_graph_direct) instead of as one graph launch each
+        self.direct = direct
         # only: DIAGNOSTIC restriction of every step to its samplers or its side work
         if set_inputs is not None and len(set_inputs) != nsets:
             raise ValueError(f"set_inputs: {len(set_inputs)} input dicts for {nsets} sets")
         inps = list(set_inputs) if set_inputs is not None else [inp] * nsets
         cl = (lambda i: chain_lane - (i % max(1, chain_streams)) if chain_lane < 0
               else chain_lane)
-        # alt_lanes: side lanes whose work of every other buffer set runs on a second stream
-        al = (lambda i: tuple(alt_lanes) if i % 2 else ())
         mk = (lambda i: GraphStep(inps[i], overlap=overlap, streams=streams(i),
                                   chain_lane=cl(i), segments=self.native_plan, only=only,
-                                  layout=layout, alt_lanes=al(i))) \
+                                  layout=layout)) \
             if graphs else (lambda i: Step(inps[i], overlap=overlap, streams=streams(i),
-                                           chain_lane=cl(i), layout=layout, alt_lanes=al(i)))
+                                           chain_lane=cl(i), layout=layout))
         self.sets = [mk(i) for i in range(nsets)]
         self.inputs = inps
         self.k = 0
@@ -1067,7 +949,7 @@ class Pipeline:
             nl = len(self.lane0)
             for k in range(nsets * nl // math.gcd(nsets, nl)):
                 st = self.lane0[k % nl] or torch.cuda.current_stream(dev)
-                self.sets[k % nsets].plan_for(st, self.gpu_set_waits)
+                self.sets[k % nsets].plan_for(st, self.direct)
 
     def run(self, sampler_events=None):
         st = self.lane0[self.k % len(self.lane0)]
@@ -1118,9 +1000,8 @@ class Pipeline:
         try:
             if isinstance(s, GraphStep):
                 if s.step.ran and s.step.overlap:
-                    if not self.gpu_set_waits:  # (else: wait packets in the plan)
-                        for lane in s.step.done_lanes():  # this set's previous side work
-                            s.step.lane_done[lane].synchronize()
+                    for lane in s.step.done_lanes():  # this set's previous side work
+                        s.step.lane_done[lane].synchronize()
                 else:
                     s.step.join()
                 t1 = time.perf_counter()
@@ -1133,7 +1014,7 @@ class Pipeline:
                     self._last_of_set[si] = len(tr) - 1
                 t0 = t1
                 if self.native_plan:
-                    return s.replay_plan(sampler_events, self.gpu_set_waits)
+                    return s.replay_plan(sampler_events, self.direct)
                 return s.replay(sampler_events, join=False)
             s.join()
             return s.run(sampler_events, join=False)

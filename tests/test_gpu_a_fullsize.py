@@ -127,43 +127,39 @@ def _poison_sampled(pipe, torch):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("lanes,native,layout,own,cus,gpuwait", [
-    (1, False, "a", False, 0, False), (1, True, "a", False, 0, False),
-    (2, True, "a", False, 0, False), (3, True, "b", False, 0, False),
-    (3, True, "b", True, 0, False), (3, True, "b", True, 64, False),
-    (3, True, "b", True, 0, True), (1, True, "a", False, 0, True)])
+@pytest.mark.parametrize("lanes,native,layout,own,direct", [
+    (1, False, "a", False, True), (1, True, "a", False, True),
+    (2, True, "a", False, True), (3, True, "b", False, True),
+    (3, True, "b", True, True), (3, True, "b", True, False)])
 @pytest.mark.parametrize("config,B", CONFIGS)
-def test_pipeline_full_size(env, config, B, lanes, native, layout, own, cus, gpuwait):
+def test_pipeline_full_size(env, config, B, lanes, native, layout, own, direct):
     """What bench.py times: the software-pipelined hipGraph steps over 3 buffer sets, at the
     BASELINE batch, after several rotations, with one, two or three sampler streams
     (consecutive steps' samplers concurrent), enqueued by the Python task loop or by the native
-    plan (include/pn2plan.h), side layouts a and b (stack.side_layout), the later samplers
-    behind SA1 or on a stream of their own (chain_own). The sampled coordinates
-    of every set are poisoned before the last three steps (a missing wait then shows), and the
-    last two steps' outputs (one per sampler stream) are compared with the oracle. gpuwait:
-    buffer-set reuse ordered by GPU wait packets (stack.GPU_SET_WAITS) while the host runs
-    ahead without blocking."""
+    plan (include/pn2plan.h) -- its side segments' kernels launched directly
+    (pn2_plan_graph_direct) or as graph launches (direct=False) -- side layouts a and b
+    (stack.side_layout), the later samplers behind SA1 or on a stream of their own (chain_own).
+    The sampled coordinates of every set are poisoned before the last three steps (a missing
+    wait then shows), and the last two steps' outputs (one per sampler stream) are compared
+    with the oracle."""
     pkg, O, torch, dev = env
     # every set its own clouds (as bench.py runs it): a set that read another set's buffers
     # would give outputs that match no oracle run
     sets = [pkg.stack.make_inputs(config, list(range(100 + i * B, 100 + (i + 1) * B)), dev)
             for i in range(3)]
     inp = sets[0]
-    pkg.stack.set_cu_partition(dev, cus)  # CU-masked sampler / side streams (cus > 0)
-    saved = dict(pkg.stack._SIDE)
-    if cus:
-        pkg.stack._SIDE.clear()  # fresh (masked) streams for this pipeline
-    pkg.stack.GPU_SET_WAITS = gpuwait
-    try:
-        pipe = pkg.stack.Pipeline(inp, graphs=True, nsets=3, sampler_lanes=lanes,
-                                  native_plan=native, layout=layout, chain_own=own,
-                                  set_inputs=sets)
-    finally:
-        pkg.stack.GPU_SET_WAITS = False  # (the plans have their waits from here on)
+    pipe = pkg.stack.Pipeline(inp, graphs=True, nsets=3, sampler_lanes=lanes,
+                              native_plan=native, layout=layout, chain_own=own,
+                              set_inputs=sets, direct=direct)
     assert len(pipe.lane0) == lanes
     assert pipe.native_plan == native
     if native:  # every (set, sampler stream) plan exists before the first step
         assert all(getattr(s, "plans", None) for s in pipe.sets), "plans not built up front"
+        for s in pipe.sets:  # every side segment is a plain kernel chain: all go in directly
+            for p in s.plans.values():
+                want = "direct" if direct else "graph"
+                assert p.launches[want] > 0 and sum(p.launches.values()) == p.launches[want], \
+                    p.launches
     for _ in range(7):
         pipe.run()
     pipe.join()
@@ -172,10 +168,6 @@ def test_pipeline_full_size(env, config, B, lanes, native, layout, own, cus, gpu
         pipe.run()
     outs = pipe.join()
     assert pipe.check_faults() == 0
-    pkg.stack.set_cu_partition(dev, 0)
-    if cus:
-        pkg.stack._SIDE.clear()
-        pkg.stack._SIDE.update(saved)
     for back in (1, 2):
         s = pipe.sets[(pipe.k - back) % len(pipe.sets)]
         check_step(O, config, sets[(pipe.k - back) % 3], s.outs if back > 1 else outs,

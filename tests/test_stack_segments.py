@@ -62,21 +62,3 @@ def test_chain_own_lane_follows_the_side_lanes(config, layout, want, nth):
     assert chain and all(t.lane == want for t in chain)
     assert all(t.lane != want for t in step.tasks if not t.direct)
     assert max(t.lane for t in step.tasks) == want
-
-
-@pytest.mark.parametrize("config", ["cfg2", "cfg3", "cfg5"])
-@pytest.mark.parametrize("alt", [(2,), (1, 2)])
-def test_alt_lanes_move_a_lane_after_the_others(config, alt):
-    """Pipeline(alt_lanes=...) gives every other buffer set a Step whose tasks of those side
-    lanes run on lanes after all the others; the segments still respect every dependency."""
-    inp = pkg.stack.make_inputs(config, [0], "cpu")
-    base = pkg.stack.Step(inp, overlap=True, chain_lane=-1, layout="b")
-    step = pkg.stack.Step(inp, overlap=True, chain_lane=-1, layout="b", alt_lanes=alt)
-    base.overlap = step.overlap = True
-    top = 1 + max(t.lane for t in base.tasks)
-    want = {L: top + j for j, L in enumerate(sorted(alt))}
-    for a, b in zip(base.tasks, step.tasks):
-        assert a.name == b.name
-        assert b.lane == want.get(a.lane, a.lane)
-    names = [t.name for seg in step.segments() for t in seg]
-    assert sorted(names) == sorted(t.name for t in step.tasks)
