@@ -81,9 +81,6 @@ typedef void* pn2_stream_t; /* hipStream_t */
 /* pn2_fps_gather_sched schedules (all give identical outputs) */
 #define PN2_FPS_AUTO 0           /* the library's choice by N (what pn2_fps* run)            */
 #define PN2_FPS_BLOCKSCAN 1      /* one block-wide argmax per pick (the v9 register sampler) */
-#define PN2_FPS_HOTCULL_K128 6   /* culled hot-set sampler with 128 hot entries, N <= 8192  */
-#define PN2_FPS_HOTCULL_LEAN 7   /* culled hot-set sampler, cloud left in L2 (~57 KB LDS), N <= 8192 */
-#define PN2_FPS_HOTCULL_LDS 8    /* culled hot-set sampler with the cloud's LDS copy, N <= 8192 */
 
 /* flags of pn2_group_concat / pn2_sample_and_group */
 #define PN2_USE_XYZ 1  /* concat the centred xyz with the grouped features (use_xyz=True)      */
@@ -125,8 +122,8 @@ int pn2_fps_gather(const float* xyz, int B, int N, int npoint, int32_t* idx, flo
 int pn2_fps_max_points(void);
 /* pn2_fps_gather with an explicit sampler schedule, per call (no process-wide state; used by
  * the parity tests and A/B timing). PN2_FPS_AUTO = pn2_fps_gather; the other schedules exist
- * only where the culled hot-set sampler is the default (4096 < N <= 16384;
- * PN2_FPS_HOTCULL_K128 only up to N = 8192) and return PN2_EINVAL elsewhere. */
+ * only where the culled hot-set sampler is the default (4096 < N <= 16384) and return
+ * PN2_EINVAL elsewhere. */
 int pn2_fps_gather_sched(const float* xyz, int B, int N, int npoint, int32_t* idx,
                          float* new_xyz, int schedule, pn2_stream_t stream);
 /* The device fault word: 0, or the PN2_FAULT_* code a sampler launch stored (valid once that

@@ -111,9 +111,6 @@ __global__ void gather_point_grad_kernel(const float* __restrict__ out_g,
 }
 
 constexpr int kMaxRegPoints = 1024 * 16;
-#ifndef PN2_FPS_LEAN  // AUTO at the SA1 size runs the lean-LDS culled sampler (fps_cull.h)
-#define PN2_FPS_LEAN 0
-#endif
 
 // ---- device fault word ------------------------------------------------------------------
 // A kernel that finds a broken invariant (the culled sampler's cold waves waiting past their
@@ -160,10 +157,7 @@ int take_fault() {
 // fused kernel's SA1 loop ran ~4% behind the same loop in its own kernel, more than the
 // launch it saved -- profiles/r1/chain_split.log.)
 constexpr int kChainMax = 4;
-#ifndef PN2_CHAIN_BLOCK  // A/B: threads of the chain workgroup (its 1024-point stage: 1024 / BLOCK per lane)
-#define PN2_CHAIN_BLOCK 256
-#endif
-constexpr int kChainBlock = PN2_CHAIN_BLOCK;
+constexpr int kChainBlock = 256;  // 128 and 512 measured slower (profiles/r4/ab)
 constexpr int kChainNext = 1024;  // points per fused stage (LDS: input copy + 2 hand-over arrays)
 
 struct FpsChain {
@@ -175,24 +169,18 @@ struct FpsChain {
 
 // one stage (N <= kChainNext) for one cloud: the configuration fps_impl uses for this N
 PN2_DEV void chain_stage(const float* P, int N, int M, const float* CXYZ, int32_t* I, float* NX,
-                         float* SNEXT, uint2 (*red)[8], FpsSlot (*wslot)[8]) {
+                         float* SNEXT, uint2 (*red)[8]) {
   const bool w0 = threadIdx.x < kWave;
-  constexpr bool WC = PN2_FPS_WCOORD;  // winner coordinates carried (fps_kernels.h; <= 8 slots)
   if (N <= 64) { if (w0) fps_v9_body<64, 1, 1>(P, N, M, CXYZ, I, NX, SNEXT, red); }
   else if (N <= 128) { if (w0) fps_v9_body<64, 2, 2>(P, N, M, CXYZ, I, NX, SNEXT, red); }
-  else if (N <= 256) { if (w0) fps_v9_body<64, 4, 4, false, true, false, -1, WC>(P, N, M, CXYZ, I, NX, SNEXT, red, wslot); }
-  else if (N <= 512) { if (w0) fps_v9_body<64, 8, 4, false, true, false, -1, WC>(P, N, M, CXYZ, I, NX, SNEXT, red, wslot); }
-  else if constexpr (kChainBlock == 128)
-    fps_v9_body<128, 8, 4, false, true, false, -1, WC>(P, N, M, CXYZ, I, NX, SNEXT, red, wslot);
-  else if constexpr (kChainBlock == 512)
-    fps_v9_body<512, 2, 2, false, true, false, -1, WC>(P, N, M, CXYZ, I, NX, SNEXT, red, wslot);
-  else fps_v9_body<256, 4, 2, false, true, false, -1, WC>(P, N, M, CXYZ, I, NX, SNEXT, red, wslot);
+  else if (N <= 256) { if (w0) fps_v9_body<64, 4, 4, false, true>(P, N, M, CXYZ, I, NX, SNEXT, red); }
+  else if (N <= 512) { if (w0) fps_v9_body<64, 8, 4, false, true>(P, N, M, CXYZ, I, NX, SNEXT, red); }
+  else fps_v9_body<256, 4, 2, false, true>(P, N, M, CXYZ, I, NX, SNEXT, red);
 }
 
 __global__ __launch_bounds__(kChainBlock) void fps_chain_kernel(const float* __restrict__ xyz,
                                                                 FpsChain c) {
   __shared__ uint2 red[2][8];
-  __shared__ FpsSlot wslot[2][8];
   __shared__ float sxyz[3 * kChainNext];
   __shared__ float snew[2][3 * kChainNext];
   const int b = blockIdx.x;
@@ -203,7 +191,7 @@ __global__ __launch_bounds__(kChainBlock) void fps_chain_kernel(const float* __r
     const float* cxyz = i == 0 ? sxyz : snew[(i - 1) & 1];
     float* next = i + 1 < c.stages ? snew[i & 1] : nullptr;
     chain_stage(cxyz, c.n[i], c.m[i], cxyz, c.idx[i] + (size_t)b * c.m[i],
-                c.nx[i] + (size_t)b * c.m[i] * 3, next, red, wslot);
+                c.nx[i] + (size_t)b * c.m[i] * 3, next, red);
     __syncthreads();  // stage i's LDS output complete before stage i+1 reads it
   }
 }
@@ -211,15 +199,9 @@ __global__ __launch_bounds__(kChainBlock) void fps_chain_kernel(const float* __r
 int fps_impl(const float* xyz, int B, int N, int M, int32_t* idx, float* nx, void* ws,
              size_t ws_bytes, hipStream_t s, int sched = PN2_FPS_AUTO, bool take = true) {
   if (B < 0 || N < 0 || M <= 0 || (B > 0 && (!xyz || !idx))) return PN2_EINVAL;
-  // schedules other than AUTO exist only where the culled sampler runs (4096 < N <= 16384;
-  // the 128-entry variant up to 8192 points)
-  if (sched != PN2_FPS_AUTO && sched != PN2_FPS_BLOCKSCAN && sched != PN2_FPS_HOTCULL_K128 &&
-      sched != PN2_FPS_HOTCULL_LEAN && sched != PN2_FPS_HOTCULL_LDS)
-    return PN2_EINVAL;
+  // the block-scan schedule exists only where the culled sampler runs (4096 < N <= 16384)
+  if (sched != PN2_FPS_AUTO && sched != PN2_FPS_BLOCKSCAN) return PN2_EINVAL;
   if (sched != PN2_FPS_AUTO && (N <= 4096 || N > kMaxRegPoints)) return PN2_EINVAL;
-  if ((sched == PN2_FPS_HOTCULL_K128 || sched == PN2_FPS_HOTCULL_LEAN ||
-       sched == PN2_FPS_HOTCULL_LDS) && N > 8192)
-    return PN2_EINVAL;
   if (take && take_fault()) return PN2_EFAULT;
   if (B == 0) return PN2_OK;
   if (N == 0) {
@@ -238,17 +220,10 @@ int fps_impl(const float* xyz, int B, int N, int M, int32_t* idx, float* nx, voi
   else if (N <= 2048) launch_v9<256, 8, 2, true>(xyz, B, N, M, idx, nx, s);
   else if (N <= 4096) launch_v9<256, 16, 4, true>(xyz, B, N, M, idx, nx, s);
   else if (N <= 8192) {
-    // culled hot-set sampler (fps_cull.h; 0.40 vs 0.71 ms at B = 16); the v9
+    // culled hot-set sampler (fps_cull.h; 0.37 vs 0.71 ms at B = 16); the v9
     // block-scan sampler stays selectable for A/B timing and parity cross-checks
-    // (the lean-LDS form, PN2_FPS_HOTCULL_LEAN, leaves the cloud in L2 so the workgroup fits
-    // a CU that side-lane work partly occupies: fps_cull.h LEAN)
-    const bool lean = sched == PN2_FPS_HOTCULL_LEAN || (sched == PN2_FPS_AUTO && PN2_FPS_LEAN);
     if (sched == PN2_FPS_BLOCKSCAN)
-      launch_v9<256, 32, 4, true, false, PN2_SA1_PAD>(xyz, B, N, M, idx, nx, s);
-    else if (sched == PN2_FPS_HOTCULL_K128)
-      launch_hotcull<16, 9, 3, 2>(xyz, B, N, M, idx, nx, fault_word_dev(), s);
-    else if (lean)
-      launch_hotcull<16, 9, 3, 4, 8192, 1, true>(xyz, B, N, M, idx, nx, fault_word_dev(), s);
+      launch_v9<256, 32, 4, true, PN2_SA1_PAD>(xyz, B, N, M, idx, nx, s);
     else
       launch_hotcull<16, 9, 3, 4>(xyz, B, N, M, idx, nx, fault_word_dev(), s);
   }

@@ -949,29 +949,11 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
   hotcull_body<NW, PPT, NPTS, STAMP, PRIO, HQ, PPC, LEAN>(xyz, N, M, idx, new_xyz, fault);
 }
 
-// The lean-LDS form held to PN2_FPS_LEAN_WPE waves per SIMD's worth of VGPRs (16 waves need 4
-// per SIMD; 5 leaves each SIMD ~100 VGPRs for a side-lane wave beside the sampler)
-#ifndef PN2_FPS_LEAN_WPE
-#define PN2_FPS_LEAN_WPE 4
-#endif
-template <int NW, int PPT, int NPTS, int PRIO, int HQ>
-__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(PN2_FPS_LEAN_WPE)))
-void fps_hotcull_lean_kernel(const float* __restrict__ xyz, int N, int M,
-                             int32_t* __restrict__ idx, float* __restrict__ new_xyz,
-                             int* __restrict__ fault) {
-  hotcull_body<NW, PPT, NPTS, false, PRIO, HQ, 1, true>(xyz, N, M, idx, new_xyz, fault);
-}
-
-template <int NW, int PPT, int PRIO = 0, int HQ = 2, int NPTS = 8192, int PPC = 1,
-          bool LEAN = false>
+template <int NW, int PPT, int PRIO = 0, int HQ = 2, int NPTS = 8192, int PPC = 1>
 void launch_hotcull(const float* xyz, int B, int N, int M, int32_t* idx, float* nx, int* fault,
                     hipStream_t s) {
-  if constexpr (LEAN)
-    hipLaunchKernelGGL((fps_hotcull_lean_kernel<NW, PPT, NPTS, PRIO, HQ>), dim3(B), dim3(64 * NW),
-                       0, s, xyz, N, M, idx, nx, fault);
-  else
-    hipLaunchKernelGGL((fps_hotcull_kernel<NW, PPT, NPTS, false, PRIO, HQ, PPC>), dim3(B),
-                       dim3(64 * NW), 0, s, xyz, N, M, idx, nx, fault);
+  hipLaunchKernelGGL((fps_hotcull_kernel<NW, PPT, NPTS, false, PRIO, HQ, PPC>), dim3(B),
+                     dim3(64 * NW), 0, s, xyz, N, M, idx, nx, fault);
 }
 
 }  // namespace

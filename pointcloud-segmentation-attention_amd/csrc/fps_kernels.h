@@ -10,11 +10,6 @@ namespace {
 
 constexpr float kInitTemp = 1e38f;  // tf_sampling_g.cu:118
 
-// Wave issue priority (s_setprio) of the samplers' iteration loops; 0 = the hardware default.
-#ifndef PN2_FPS_PRIO
-#define PN2_FPS_PRIO 0
-#endif
-
 // Low word of the argmax key: larger = earlier in the reference's tie order.
 PN2_DEV uint32_t tie_low(int k) {
   const uint32_t tk = (((uint32_t)k & 511u) << 20) | ((uint32_t)k >> 9);
@@ -92,29 +87,13 @@ struct Lay9 {
 // LRES: every lane resolves its own winning slot with VALU selects right after the scan
 // (independent of, so interleaved with, the wave max), leaving one v_readlane after the ballot
 // instead of the scalar compare chain over the groups.
-// ATOM: the block step as ONE 64-bit LDS atomic max per wave -- key (wave max, tie_low(winner))
-// -- then a barrier and a broadcast read, instead of publish / barrier / DPP max / ballot over
-// the waves' entries. Three rotating slots: slot (j+1) % 3 is cleared by thread 0 before
-// iteration j's barrier, after every read of it (iteration j-2, before barrier j-1).
 // PAD >= 0: that many s_nop right before the iteration loop, shifting the loop's code address
-// by 4 * PAD bytes (code-placement experiments, profiles/r1/pad_fps.log; the product uses PAD = -1).
-// WC (with LRES, not ATOM): the winner's coordinates travel with its index instead of being
-// read back from CXYZ after the argmax: every lane selects its own candidate's coordinates
-// beside the wave max, the wave winner's come out of v_readlane, and with several waves they
-// ride in the LDS slot next to (max, index) -- one LDS round trip less on the pick's
-// dependency chain. The coordinates are the same floats (loaded from CXYZ at setup).
-#ifndef PN2_FPS_WCOORD  // measured: no gain standalone, the fused SA2-4 chain 126 -> 156 us: off
-#define PN2_FPS_WCOORD 0
-#endif
-struct FpsSlot {  // one wave's published winner (WC): max, index, coordinates
-  uint32_t km, k;
-  float x, y, z, pad0, pad1, pad2;
-};
-template <int BLOCK, int PPT, int G, bool STAMP = false, bool LRES = false, bool ATOM = false,
-          int PAD = -1, bool WC = false>
+// by 4 * PAD bytes (code placement, tools/place_sa1_loop.py; profiles/r1/pad_fps.log).
+// (Measured and removed: the block step as one 64-bit LDS atomic per wave, 794 vs 718 us at
+// SA1; the winner's coordinates carried through the block step, chain 126 -> 156 us.)
+template <int BLOCK, int PPT, int G, bool STAMP = false, bool LRES = false, int PAD = -1>
 PN2_DEV void fps_v9_body(const float* P, int N, int M, const float* CXYZ, int32_t* I, float* NX,
-                         float* SNEXT, uint2 (*red)[8], FpsSlot (*wslot)[8] = nullptr) {
-  static_assert(!WC || (LRES && !ATOM), "WC needs the lane resolve and the slot block step");
+                         float* SNEXT, uint2 (*red)[8]) {
   unsigned long long st_acc[6] = {0, 0, 0, 0, 0, 0}, st_prev = 0;
   using Lay = Lay9<BLOCK, PPT>;
   constexpr int NW = BLOCK / kWave;
@@ -168,15 +147,9 @@ PN2_DEV void fps_v9_body(const float* P, int N, int M, const float* CXYZ, int32_
     if (SNEXT) { SNEXT[0] = cx; SNEXT[1] = cy; SNEXT[2] = cz; }
   }
 
-  unsigned long long* aslot = reinterpret_cast<unsigned long long*>(&red[0][0]);
-  if constexpr (ATOM && NW > 1) {
-    if (t < 3) aslot[t] = 0ull;
-    __syncthreads();
-  }
   if constexpr (STAMP) {
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(st_prev)::"memory");
   }
-  if constexpr (PN2_FPS_PRIO > 0) __builtin_amdgcn_s_setprio(PN2_FPS_PRIO);
   if constexpr (PAD > 0) asm volatile(".rept %0\n\ts_nop 0\n\t.endr" ::"n"(PAD));
   for (int j = 1; j < M; ++j) {
     int dv[PPT];  // this iteration's squared distances as int bits
@@ -230,22 +203,6 @@ PN2_DEV void fps_v9_body(const float* P, int N, int M, const float* CXYZ, int32_
       ls = bg * G + r;
     }
     PN2_STAMP(0)
-    float wx = 0.0f, wy = 0.0f, wz = 0.0f;  // WC: this lane's candidate's coordinates
-    if constexpr (WC) {
-#pragma unroll
-      for (int q = 0; q < PPT; ++q) {
-        const bool sel = ls == q;
-        if constexpr (PK) {
-          wx = sel ? vx[q / 2][q % 2] : wx;
-          wy = sel ? vy[q / 2][q % 2] : wy;
-          wz = sel ? vz[q / 2][q % 2] : wz;
-        } else {
-          wx = sel ? px[q] : wx;
-          wy = sel ? py[q] : wy;
-          wz = sel ? pz[q] : wz;
-        }
-      }
-    }
     const uint32_t km = wave_max_u32(hi);
     PN2_STAMP(1)
     const uint64_t hold = __builtin_amdgcn_ballot_w64(hi == km);
@@ -269,40 +226,7 @@ PN2_DEV void fps_v9_body(const float* P, int N, int M, const float* CXYZ, int32_
     }
     int old = Lay::point(w * kWave + L, sq);
     PN2_STAMP(2)
-    if constexpr (WC) {
-      cx = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__float_as_int(wx), L));
-      cy = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__float_as_int(wy), L));
-      cz = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__float_as_int(wz), L));
-      if constexpr (NW > 1) {
-        if (lane == 0) {
-          FpsSlot sl;
-          sl.km = km;
-          sl.k = (uint32_t)old;
-          sl.x = cx; sl.y = cy; sl.z = cz;
-          sl.pad0 = sl.pad1 = sl.pad2 = 0.0f;
-          wslot[j & 1][w] = sl;
-        }
-        __syncthreads();
-        PN2_STAMP(3)
-        const FpsSlot r = (lane & 7) < NW ? wslot[j & 1][lane & 7] : FpsSlot{};
-        uint32_t bm = max_dpp_u32<kDppXor1>(r.km);
-        bm = max_dpp_u32<kDppXor2>(bm);
-        bm = max_dpp_u32<kDppHalfMirror>(bm);
-        const uint64_t wins = __builtin_amdgcn_ballot_w64(r.km == bm) & 0xFFull;
-        const int wi = (int)__builtin_amdgcn_readfirstlane((int)__builtin_ctzll(wins));
-        old = __builtin_amdgcn_readlane((int)r.k, wi);
-        cx = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__float_as_int(r.x), wi));
-        cy = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__float_as_int(r.y), wi));
-        cz = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__float_as_int(r.z), wi));
-      }
-    } else if constexpr (NW > 1 && ATOM) {
-      const int sl = j % 3;
-      if (lane == 0) atomicMax(&aslot[sl], ((unsigned long long)km << 32) | tie_low(old));
-      if (t == 0) aslot[sl == 2 ? 0 : sl + 1] = 0ull;
-      __syncthreads();
-      PN2_STAMP(3)
-      old = tie_decode((uint32_t)aslot[sl]);
-    } else if constexpr (NW > 1) {
+    if constexpr (NW > 1) {
       if (lane == 0) red[j & 1][w] = make_uint2(km, (uint32_t)old);
       __syncthreads();
       PN2_STAMP(3)
@@ -315,9 +239,7 @@ PN2_DEV void fps_v9_body(const float* P, int N, int M, const float* CXYZ, int32_
       old = __builtin_amdgcn_readlane((int)r.y, wi);
     }
     PN2_STAMP(4)
-    if constexpr (!WC) {
-      cx = CXYZ[3 * old + 0]; cy = CXYZ[3 * old + 1]; cz = CXYZ[3 * old + 2];
-    }
+    cx = CXYZ[3 * old + 0]; cy = CXYZ[3 * old + 1]; cz = CXYZ[3 * old + 2];
     if (t == 0) {
       I[j] = old;
       if (NX) { NX[3 * j + 0] = cx; NX[3 * j + 1] = cy; NX[3 * j + 2] = cz; }
@@ -332,14 +254,11 @@ PN2_DEV void fps_v9_body(const float* P, int N, int M, const float* CXYZ, int32_
 }
 
 template <int BLOCK, int PPT, int G, bool XYZ_LDS, bool STAMP = false, bool LRES = false,
-          bool ATOM = false, int PAD = -1>
+          int PAD = -1>
 __global__ __launch_bounds__(BLOCK) void fps_v9_kernel(const float* __restrict__ xyz, int N,
                                                        int M, int32_t* __restrict__ idx,
                                                        float* __restrict__ new_xyz) {
-  // (the per-lane select costs 3 VALU per slot: only for a few slots per lane)
-  constexpr bool WC = PN2_FPS_WCOORD && LRES && !ATOM && PPT <= 8;
   __shared__ uint2 red[2][8];
-  __shared__ FpsSlot wslot[WC ? 2 : 1][8];
   __shared__ float sxyz[XYZ_LDS ? 3 * BLOCK * PPT : 1];
   const int b = blockIdx.x;
   const float* __restrict__ P = xyz + (size_t)b * N * 3;
@@ -347,18 +266,18 @@ __global__ __launch_bounds__(BLOCK) void fps_v9_kernel(const float* __restrict__
     for (int e = threadIdx.x; e < 3 * N; e += BLOCK) sxyz[e] = P[e];
     __syncthreads();
   }
-  fps_v9_body<BLOCK, PPT, G, STAMP, LRES, ATOM, PAD, WC>(
+  fps_v9_body<BLOCK, PPT, G, STAMP, LRES, PAD>(
       P, N, M, XYZ_LDS ? sxyz : P, idx + (size_t)b * M,
-      new_xyz ? new_xyz + (size_t)b * M * 3 : nullptr, nullptr, red, WC ? wslot : nullptr);
+      new_xyz ? new_xyz + (size_t)b * M * 3 : nullptr, nullptr, red);
 }
 
-template <int BLOCK, int PPT, int G, bool LRES = false, bool ATOM = false, int PAD = -1>
+template <int BLOCK, int PPT, int G, bool LRES = false, int PAD = -1>
 void launch_v9(const float* xyz, int B, int N, int M, int32_t* idx, float* nx, hipStream_t s) {
   if constexpr (3 * BLOCK * PPT * 4 + 256 <= 160 * 1024)
-    hipLaunchKernelGGL((fps_v9_kernel<BLOCK, PPT, G, true, false, LRES, ATOM, PAD>), dim3(B),
+    hipLaunchKernelGGL((fps_v9_kernel<BLOCK, PPT, G, true, false, LRES, PAD>), dim3(B),
                        dim3(BLOCK), 0, s, xyz, N, M, idx, nx);
   else
-    hipLaunchKernelGGL((fps_v9_kernel<BLOCK, PPT, G, false, false, LRES, ATOM, PAD>), dim3(B),
+    hipLaunchKernelGGL((fps_v9_kernel<BLOCK, PPT, G, false, false, LRES, PAD>), dim3(B),
                        dim3(BLOCK), 0, s, xyz, N, M, idx, nx);
 }
 

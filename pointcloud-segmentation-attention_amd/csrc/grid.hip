@@ -30,14 +30,9 @@ namespace pn2 {
 namespace {
 
 constexpr int kBuildBlock = 1024;
-#ifndef PN2_GQ_FLAT
-#define PN2_GQ_FLAT 1
-#endif
 // rows of at least this many points on average are walked one by one (tools/bench_msg_grid.py:
 // the flattened walk won on short rows, lost at r = 0.4 on r-sized cells)
-#ifndef PN2_GQ_LONG_ROWS
-#define PN2_GQ_LONG_ROWS 24
-#endif
+constexpr int kGqLongRows = 24;
 constexpr int kMaxBitWords = 4096;  // bitmask words per wave (N <= 131072)
 // The cloud's points are read ONCE into registers (PPT per thread, every load issued before
 // the first is used): the bounding box, the count and the scatter all work from them. The
@@ -231,15 +226,6 @@ __global__ __launch_bounds__(BLOCK) void ball_query_grid_kernel(
     const int x0 = cell_coord(qx - rr, h.ox, h.inv, h.nx), x1 = cell_coord(qx + rr, h.ox, h.inv, h.nx);
     const int y0 = cell_coord(qy - rr, h.oy, h.inv, h.ny), y1 = cell_coord(qy + rr, h.oy, h.inv, h.ny);
     const int z0 = cell_coord(qz - rr, h.oz, h.inv, h.nz), z1 = cell_coord(qz + rr, h.oz, h.inv, h.nz);
-#if !PN2_GQ_FLAT  // A/B: one row at a time (two dependent offset loads per row)
-    for (int z = z0; z <= z1; ++z) {
-      for (int y = y0; y <= y1; ++y) {
-        const int row = (z * h.ny + y) * h.nx;
-        const int e = off[row + x1 + 1];  // cells x0..x1 of a row are contiguous
-        for (int i = off[row + x0] + lane; i < e; i += kWave) hit(pts[i]);
-      }
-    }
-#else
     // the cell range as rows (z, y) of contiguous cells x0..x1: the sorted-point ranges of up
     // to 64 rows are fetched at once (lane j: row r0 + j), then the wave walks the
     // concatenation of those ranges 64 points at a time -- one dependent memory trip per 64
@@ -260,7 +246,7 @@ __global__ __launch_bounds__(BLOCK) void ball_query_grid_kernel(
       const int total = __builtin_amdgcn_readlane(incl, kWave - 1);
       const int excl = incl - len;
       const int nr = min(kWave, nrows - r0);
-      if (total >= PN2_GQ_LONG_ROWS * nr) {
+      if (total >= kGqLongRows * nr) {
         // long rows (a large radius over small cells): row by row, offsets already in hand
         for (int j = 0; j < nr; ++j) {
           const int bj = __builtin_amdgcn_readlane(beg, j);
@@ -285,7 +271,6 @@ __global__ __launch_bounds__(BLOCK) void ball_query_grid_kernel(
         if (i < total) hit(pts[base + i]);
       }
     }
-#endif
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
       const uint32_t* mr = mine + r * words;

@@ -25,13 +25,9 @@ enum Layout : int {
 };
 
 constexpr int kBlock = 256;
-#ifndef PN2_GC_TILE  // A/B knobs (tools/bench_group.py): output floats per workgroup tile,
-#define PN2_GC_TILE 2048  // elements whose gathers a thread has in flight before its stores
-#endif
-#ifndef PN2_GC_U
-#define PN2_GC_U 4
-#endif
-constexpr int kTileElems = PN2_GC_TILE;  // output floats per workgroup tile
+// measured with tools/bench_group.py (profiles/r2/bench_group_r2.log)
+constexpr int kTileElems = 2048;  // output floats per workgroup tile
+constexpr int kGcU = 4;           // elements whose gathers a thread has in flight before its stores
 
 // Tile = `rows` consecutive output rows (rows*Cout <= max(kTileElems, Cout)).
 __global__ __launch_bounds__(kBlock) void group_concat_kernel(
@@ -42,7 +38,7 @@ __global__ __launch_bounds__(kBlock) void group_concat_kernel(
   // the tile's neighbour indices are staged in LDS first (one coalesced load per row), and a
   // thread then issues the gathers of kU elements before it stores any: one element at a time
   // made each element two dependent memory trips (idx, then the gather), latency-bound
-  constexpr int kU = PN2_GC_U;
+  constexpr int kU = kGcU;
   __shared__ int s_idx[kTileElems];
   // XCD-aware order (common.h): each XCD takes a contiguous range of tiles, so the rows of a
   // cloud's xyz / points are fetched into one L2, not into all eight

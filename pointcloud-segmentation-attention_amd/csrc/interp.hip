@@ -152,9 +152,6 @@ __global__ __launch_bounds__(kNNBlock) void three_nn_kernel(const float* __restr
 // xor exchanges, the (d, k)-lexicographic insert) into a copy that every lane of the quad
 // holds, and tests the certificate on it -- the same test for all four lanes, so the quad
 // leaves the walk together; the merged copy is the result.
-#ifndef PN2_NN_QUAD
-#define PN2_NN_QUAD 1  // 0: one lane per unknown (A/B builds, tools/bench_nn.py)
-#endif
 
 // squared-gap certificate: every point outside the cell box [xl..xh] x [yl..yh] x [zl..zh]
 // (faces on the grid boundary excepted: nothing lies beyond them) is farther from p than
@@ -177,21 +174,13 @@ PN2_DEV bool box_certifies(const GridHdr& h, float px, float py, float pz, int x
   return gap > 0.0f && d3 < gap * gap * 0.9999f;
 }
 
-#ifndef PN2_NN_FIRST
-#define PN2_NN_FIRST 1  // the walk's first pass: the cube of shells 0..PN2_NN_FIRST (A/B: 0)
-#endif
-#ifndef PN2_NN_ROWSPLIT
-#define PN2_NN_ROWSPLIT 0  // 1: the G lanes split a shell's rows (A/B builds)
-#endif
+constexpr int kNNFirst = 1;  // the walk's first pass: the cube of shells 0..kNNFirst
 
 // The three nearest known points of (px, py, pz) over a grid's sorted points (pts, off: in
 // LDS or global memory), lexicographic in (d, k): cubic shells of cells around the point's
 // cell until the certificate holds; G lanes (lane q of them) split each row's points and
-// merge their lists at the shell's end, so all G return the same result.
-// (A/B, PN2_NN_ROWSPLIT=1: the G lanes deal a shell's (z, y) rows round-robin, each walking
-// whole rows, so a lane loads a quarter of the rows' offsets -- measured slower, 33 -> 49 us
-// at FP4, tools/bench_nn.py, profiles/r4/rows: the lanes of a wave then run rows of different
-// lengths, and the wave runs the longest.)
+// merge their lists at the shell's end, so all G return the same result. (Measured slower and
+// removed: the G lanes dealing a shell's rows round-robin, 33 -> 49 us at FP4, profiles/r4/rows.)
 template <int G, typename Off>
 PN2_DEV Best3 grid_nn3(const GridHdr& h, const float4* __restrict__ pts,
                        const Off* __restrict__ off, float px, float py, float pz, int q) {
@@ -211,38 +200,10 @@ PN2_DEV Best3 grid_nn3(const GridHdr& h, const float4* __restrict__ pts,
   Best3 res;
   // the first pass takes shells 0 and 1 together (the 3x3x3 block: nine full rows): the own
   // cell alone (~2 points) almost never certifies, so its merge and test were wasted
-  for (int s = PN2_NN_FIRST;; ++s) {
+  for (int s = kNNFirst;; ++s) {
     const int xl = cx - s, xh = cx + s, yl = cy - s, yh = cy + s, zl = cz - s, zh = cz + s;
     const int x0 = max(xl, 0), x1 = min(xh, h.nx - 1);
-    const bool block = s == PN2_NN_FIRST;  // every row of the cube, not just its shell
-#if PN2_NN_ROWSPLIT
-    auto visit = [&](int lo, int hi) {  // sorted points [lo, hi), all of them by this lane
-      int e = lo;
-      for (; e + 1 < hi; e += 2) {
-        const float4 a = pts[e], b = pts[e + 1];
-        best3_insert_lex(best, sqdist(a.x, a.y, a.z, px, py, pz), __float_as_int(a.w));
-        best3_insert_lex(best, sqdist(b.x, b.y, b.z, px, py, pz), __float_as_int(b.w));
-      }
-      if (e < hi) {
-        const float4 a = pts[e];
-        best3_insert_lex(best, sqdist(a.x, a.y, a.z, px, py, pz), __float_as_int(a.w));
-      }
-    };
-    const int ylo = max(yl, 0), yhi = min(yh, h.ny - 1), zlo = max(zl, 0), zhi = min(zh, h.nz - 1);
-    const int ny = yhi - ylo + 1;
-    int z = zlo + q / ny, y = ylo + q % ny;  // row q, then every G-th
-    for (; z <= zhi;) {
-      const int row = (z * h.ny + y) * h.nx;
-      if (block || z == zl || z == zh || y == yl || y == yh) {
-        visit(off[row + x0], off[row + x1 + 1]);  // a face row: all of x0..x1
-      } else {
-        if (xl >= 0) visit(off[row + xl], off[row + xl + 1]);
-        if (xh < h.nx) visit(off[row + xh], off[row + xh + 1]);
-      }
-      y += G;
-      while (y > yhi) { y -= ny; ++z; }
-    }
-#else
+    const bool block = s == kNNFirst;  // every row of the cube, not just its shell
     auto visit = [&](int lo, int hi) {  // sorted points [lo, hi), this lane's share
       for (int e = lo + q; e < hi; e += G) {
         const float4 p = pts[e];
@@ -260,7 +221,6 @@ PN2_DEV Best3 grid_nn3(const GridHdr& h, const float4* __restrict__ pts,
         }
       }
     }
-#endif
     res = merged();
     if (xl <= 0 && yl <= 0 && zl <= 0 && xh >= h.nx - 1 && yh >= h.ny - 1 && zh >= h.nz - 1)
       break;  // every cell visited
@@ -269,77 +229,19 @@ PN2_DEV Best3 grid_nn3(const GridHdr& h, const float4* __restrict__ pts,
   return res;
 }
 
-#ifndef PN2_NN_MARGIN
-#define PN2_NN_MARGIN 0.0f  // > 0: the wave box with this margin, in cell edges (A/B builds)
-#endif
-
-// grid_nn3 for the unknowns of a whole wave (its G-lane groups; `valid`: this group has one),
-// in two passes:
-//   1. the wave's unknowns' bounding box, grown by PN2_NN_MARGIN cell edges, rounded out to
-//      cells: every group scans every known point of that cell box -- the same rows, the same
-//      trip counts and the same LDS addresses (broadcast) for the whole wave, no divergence;
-//   2. a group whose third-nearest distance the box does not certify (box_certifies: every
-//      point outside it is farther) walks the shells (grid_nn3) from scratch.
-// The unknowns of a wave are consecutive in the order of the SA1 grid, so its box is small:
-// at FP4 (ScanNet-like clouds, 16 unknowns a wave, the automatic edge) ~80 candidates per
-// unknown against ~69 for the walk, with none of the walk's per-row overhead or divergence,
-// and ~1 unknown in 10^4 falls back (tools/sim_nn_box.py). Exact either way: the result is
-// the (d, k)-lexicographic top 3 of a point set that provably contains it.
-// MEASURED SLOWER, so off by default (PN2_NN_MARGIN = 0: the shell walk alone): FP4 search
-// 34 -> 44 us standalone at margin 0.6 (43.5 / 45.6 at 0.45 / 0.8), 53 -> 160 us when the
-// unknowns come in input order (each wave's box is then the whole grid); the pipelined step
-// unchanged within noise (profiles/r4/box). The walk's cost is its ~17 inserts per lane, not
-// its row overhead or divergence, and the box scans as many candidates.
+// grid_nn3 for one G-lane group of a wave; a group without an unknown (valid = false) returns
+// an empty list. (A wave-box first pass -- every group scans its wave's bounding box, then
+// certifies -- was measured slower and removed: FP4 search 34 -> 44 us, profiles/r4/box.)
 template <int G, typename Off>
 PN2_DEV Best3 grid_nn3_wave(const GridHdr& h, const float4* __restrict__ pts,
                             const Off* __restrict__ off, float px, float py, float pz, int q,
                             bool valid) {
-  const float inf = __builtin_inff();
-  if constexpr (!(PN2_NN_MARGIN > 0.0f)) {
-    if (valid) return grid_nn3<G, Off>(h, pts, off, px, py, pz, q);
-    Best3 none;
-    best3_init(none);
-    return none;
-  }
-  // (every lane takes part in the reductions, before any divergence)
-  const float bx0 = wave_min_f(valid ? px : inf), bx1 = wave_max_f(valid ? px : -inf);
-  const float by0 = wave_min_f(valid ? py : inf), by1 = wave_max_f(valid ? py : -inf);
-  const float bz0 = wave_min_f(valid ? pz : inf), bz1 = wave_max_f(valid ? pz : -inf);
-  Best3 best;
-  best3_init(best);
-  if (!(bx0 <= bx1 && by0 <= by1 && bz0 <= bz1))
-    return valid ? grid_nn3<G, Off>(h, pts, off, px, py, pz, q) : best;  // (no valid lane)
-  const float mg = h.inv > 0.0f ? PN2_NN_MARGIN / h.inv : 0.0f;  // inv = 0: one cell
-  const int cx0 = cell_coord(bx0 - mg, h.ox, h.inv, h.nx), cx1 = cell_coord(bx1 + mg, h.ox, h.inv, h.nx);
-  const int cy0 = cell_coord(by0 - mg, h.oy, h.inv, h.ny), cy1 = cell_coord(by1 + mg, h.oy, h.inv, h.ny);
-  const int cz0 = cell_coord(bz0 - mg, h.oz, h.inv, h.nz), cz1 = cell_coord(bz1 + mg, h.oz, h.inv, h.nz);
-  for (int z = cz0; z <= cz1; ++z) {
-    for (int y = cy0; y <= cy1; ++y) {
-      const int row = (z * h.ny + y) * h.nx;
-      const int hi = off[row + cx1 + 1];
-      for (int e = off[row + cx0] + q; e < hi; e += G) {
-        const float4 p = pts[e];
-        best3_insert_lex(best, sqdist(p.x, p.y, p.z, px, py, pz), __float_as_int(p.w));
-      }
-    }
-  }
-  if constexpr (G == 4) {
-    best3_merge_xor(best, 1);
-    best3_merge_xor(best, 2);
-  }
-  if (!valid) return best;
-  const bool all = cx0 == 0 && cy0 == 0 && cz0 == 0 && cx1 == h.nx - 1 && cy1 == h.ny - 1 &&
-                   cz1 == h.nz - 1;
-  if (all || box_certifies(h, px, py, pz, cx0, cx1, cy0, cy1, cz0, cz1, best.d3)) return best;
-  return grid_nn3<G, Off>(h, pts, off, px, py, pz, q);
+  if (valid) return grid_nn3<G, Off>(h, pts, off, px, py, pz, q);
+  Best3 none;
+  best3_init(none);
+  return none;
 }
 
-#ifndef PN2_NN_ROWS
-#define PN2_NN_ROWS 1  // row blocks per workgroup (one staging of the known grid serves K)
-#endif
-#ifndef PN2_NN_LDS
-#define PN2_NN_LDS 1  // 0: the search reads the known grid from L2 (A/B builds)
-#endif
 
 // G lanes per unknown point (1, or 4 = a quad); BLOCK / G unknowns per row block, K row
 // blocks of one cloud per workgroup
@@ -674,13 +576,11 @@ __global__ __launch_bounds__(kNNBlock) void fp_fused_kernel(FpLayer p) {
 // A cloud's 128 workgroups each redo steps 1-2 over 12 KB of L2-resident points, which costs
 // less than the launch and the dependency they replace. Bit-identical to the three-launch path.
 constexpr int kFpGridMaxKnown = 4096;  // LDS: m float4 + (max(2m / ppc, 64) + 1) offsets
-#ifndef PN2_FPG_PPC
-#define PN2_FPG_PPC 2.0f  // the LDS grid's points per cell (grid_dims' automatic edge)
-#endif
+constexpr float kFpgPointsPerCell = 2.0f;  // the LDS grid's points per cell (profiles/r4/ppc)
 
 // dynamic LDS: the m sorted points, then the ncell + 1 cell offsets as uint16 (m <= 4096)
 inline size_t fp_grid_lds(int m) {
-  const size_t cells = (size_t)ceil((double)m * kAutoPointsPerCell / PN2_FPG_PPC);
+  const size_t cells = (size_t)ceil((double)m * kAutoPointsPerCell / kFpgPointsPerCell);
   return (size_t)m * 16 + ((std::max(cells, (size_t)kAutoMinCells) + 1) * 2 + 3) / 4 * 4;
 }
 
@@ -743,7 +643,7 @@ __global__ __launch_bounds__(kNNBlock) void fp_grid_fused_kernel(FpLayer p, floa
       for (int i = 1; i < NW; ++i) { lo[a] = fminf(lo[a], red[a][i]); hi[a] = fmaxf(hi[a], red[3 + a][i]); }
       if (!(hi[a] >= lo[a])) { lo[a] = 0.0f; hi[a] = 0.0f; }  // NaN-only axis
     }
-    *shp = grid_dims(lo, hi, m, 0.0f, PN2_FPG_PPC);
+    *shp = grid_dims(lo, hi, m, 0.0f, kFpgPointsPerCell);
   }
   __syncthreads();
   const GridHdr h = *shp;
@@ -876,18 +776,12 @@ int batch_chunk(int B, int n, int C, int rows) {
   return (int)(ch < B ? ch : B);
 }
 
-// Channel split of an FP layer over grid.z (A/B knobs, tools/bench_layers.py): split until
-// PN2_FP_MIN_BLOCKS workgroups, keeping >= PN2_FP_MIN_COLS vector columns per workgroup and
-// (search variant, which scans the m known points again per slice) m * slices <= the budget
-#ifndef PN2_FP_MIN_BLOCKS
-#define PN2_FP_MIN_BLOCKS 512
-#endif
-#ifndef PN2_FP_MIN_COLS
-#define PN2_FP_MIN_COLS 16
-#endif
-#ifndef PN2_FP_SCAN_BUDGET
-#define PN2_FP_SCAN_BUDGET 4096
-#endif
+// Channel split of an FP layer over grid.z (tools/bench_layers.py): split until kFpMinBlocks
+// workgroups, keeping >= kFpMinCols vector columns per workgroup and (search variant, which
+// scans the m known points again per slice) m * slices <= the budget
+constexpr int kFpMinBlocks = 512;
+constexpr int kFpMinCols = 16;
+constexpr int kFpScanBudget = 4096;
 
 // One layer's launch configuration: the FpLayer and its kernel variant (vector widths, PRE).
 struct FpPlan {
@@ -909,9 +803,9 @@ int fp_plan(const float* xyz1, const float* xyz2, const float* pdist, const int3
   // split the channels over grid.z until ~2 workgroups per CU, keeping >= 16 vector columns
   // per workgroup and (search variant) not re-running a long known-point scan too often
   int zsplit = 1;
-  while (split && (long long)row_blocks * B * zsplit < PN2_FP_MIN_BLOCKS &&
-         coutv / (zsplit * 2) >= PN2_FP_MIN_COLS &&
-         (pre || (long long)m * zsplit * 2 <= PN2_FP_SCAN_BUDGET))
+  while (split && (long long)row_blocks * B * zsplit < kFpMinBlocks &&
+         coutv / (zsplit * 2) >= kFpMinCols &&
+         (pre || (long long)m * zsplit * 2 <= kFpScanBudget))
     zsplit *= 2;
   const int cw = (coutv + zsplit - 1) / zsplit;
   if ((long long)kNNRows * cw * cw >= (1LL << 32)) return PN2_EINVAL;
@@ -925,31 +819,20 @@ int fp_plan(const float* xyz1, const float* xyz2, const float* pdist, const int3
   return PN2_OK;
 }
 
-int fp_unroll() {
-  static const int unroll = [] {  // (PN2_FP_UNROLL: A/B knob of tools/bench_fp.py)
-    const char* e = getenv("PN2_FP_UNROLL");
-    return e ? atoi(e) : 0;
-  }();
-  return unroll;
-}
-
 // the kernel variant of `f` over `blocks` logical blocks: K = fp_fused_kernel (arg FpLayer) or
-// fp_fused_layers_kernel (arg FpLayers)
+// fp_fused_layers_kernel (arg FpLayers); two elements' loads in flight per thread
+// (tools/bench_fp.py: 1 and 4 measured slower)
+constexpr int kFpUnroll = 2;
 #define PN2_FP_DISPATCH(KERNEL, f, arg, blocks, stream)                                        \
   do {                                                                                         \
     const dim3 grid__(xcd_grid(blocks));                                                       \
-    const int un__ = fp_unroll();                                                              \
-    if ((f).v1) { PN2_FP_PRE(KERNEL, 4, 4, f, arg, grid__, un__, stream); }                    \
-    else if ((f).v2) { PN2_FP_PRE(KERNEL, 4, 1, f, arg, grid__, un__, stream); }               \
-    else { PN2_FP_PRE(KERNEL, 1, 1, f, arg, grid__, un__, stream); }                           \
+    if ((f).v1) { PN2_FP_PRE(KERNEL, 4, 4, f, arg, grid__, stream); }                          \
+    else if ((f).v2) { PN2_FP_PRE(KERNEL, 4, 1, f, arg, grid__, stream); }                     \
+    else { PN2_FP_PRE(KERNEL, 1, 1, f, arg, grid__, stream); }                                 \
   } while (0)
-#define PN2_FP_PRE(KERNEL, V2, V1, f, arg, grid, un, stream)                                   \
-  if ((f).pre) PN2_FP_UN(KERNEL, V2, V1, true, arg, grid, un, stream);                         \
-  else PN2_FP_UN(KERNEL, V2, V1, false, arg, grid, un, stream)
-#define PN2_FP_UN(KERNEL, V2, V1, P, arg, grid, un, stream)                                    \
-  if (un == 1) hipLaunchKernelGGL((KERNEL<V2, V1, P, 1>), grid, dim3(kNNBlock), 0, stream, arg); \
-  else if (un == 4) hipLaunchKernelGGL((KERNEL<V2, V1, P, 4>), grid, dim3(kNNBlock), 0, stream, arg); \
-  else hipLaunchKernelGGL((KERNEL<V2, V1, P, 2>), grid, dim3(kNNBlock), 0, stream, arg)
+#define PN2_FP_PRE(KERNEL, V2, V1, f, arg, grid, stream)                                       \
+  if ((f).pre) hipLaunchKernelGGL((KERNEL<V2, V1, true, kFpUnroll>), grid, dim3(kNNBlock), 0, stream, arg); \
+  else hipLaunchKernelGGL((KERNEL<V2, V1, false, kFpUnroll>), grid, dim3(kNNBlock), 0, stream, arg)
 
 int fp_launch(const float* xyz1, const float* xyz2, const float* pdist, const int32_t* pidx,
               const void* ugrid, const float* points1, int C1, const float* points2, int C2,
@@ -972,14 +855,10 @@ int fp_grid_launch(const float* xyz1, const float* xyz2, const void* ugrid, cons
   if (rc != PN2_OK) return rc;
   const dim3 grid(xcd_grid(f.blocks)), blk(kNNBlock);
   const size_t lds = fp_grid_lds(m);
-  const int un = fp_unroll();
 #define PN2_FPG_K(V2, V1, U)                                                                   \
   if (m <= 4 * kNNBlock) hipLaunchKernelGGL((fp_grid_fused_kernel<V2, V1, U, 4>), grid, blk, lds, stream, f.p, dist, idx); \
   else hipLaunchKernelGGL((fp_grid_fused_kernel<V2, V1, U, kFpGridMaxKnown / kNNBlock>), grid, blk, lds, stream, f.p, dist, idx)
-#define PN2_FPG(V2, V1)                                                                        \
-  if (un == 1) { PN2_FPG_K(V2, V1, 1); }                                                       \
-  else if (un == 4) { PN2_FPG_K(V2, V1, 4); }                                                  \
-  else { PN2_FPG_K(V2, V1, 2); }
+#define PN2_FPG(V2, V1) PN2_FPG_K(V2, V1, kFpUnroll);
   if (f.v1) { PN2_FPG(4, 4) }
   else if (f.v2) { PN2_FPG(4, 1) }
   else { PN2_FPG(1, 1) }
@@ -1158,10 +1037,9 @@ int pn2_three_nn_grid(const void* known_grid, const void* unknown_grid, const fl
   // an automatic-edge known grid has at most max(m, kAutoMinCells) cells (grid.h); an
   // explicit-edge one may have up to kGridCap and is read from global memory
   const size_t lds = (size_t)m * 16 + (size_t)(std::max(m, pn2::kAutoMinCells) + 1) * 4;
-  constexpr int G = PN2_NN_QUAD ? 4 : 1;
-  constexpr int K = PN2_NN_ROWS;
+  constexpr int G = 4, K = 1;  // a quad per unknown, one row block per workgroup
   const dim3 grid(pn2::xcd_grid((long long)((n + BLOCK / G * K - 1) / (BLOCK / G * K)) * B));
-  if (PN2_NN_LDS && lds <= 64 * 1024)
+  if (lds <= 64 * 1024)
     hipLaunchKernelGGL((pn2::three_nn_grid_kernel<BLOCK, true, G, K>), grid, dim3(BLOCK), lds,
                        (hipStream_t)stream, known_grid, m, unknown_grid, xyz1, n, B, dist, idx);
   else

@@ -1153,14 +1153,7 @@ int launch_one(Params prm, long long nblocks, size_t lds, hipStream_t s) {
   // hold (a grid of exactly the co-resident slots with static tile ranges waited for the SA1
   // sampler's CUs in the whole-model pipeline).
   prm.tpw = 1;
-  static const int max_tpw = [] {  // tuning overrides (scripts/ab_tpw.sh)
-    const char* e = std::getenv("PN2_MLP_TPW");
-    return e ? std::atoi(e) : 8;
-  }();
-  static const int rounds = [] {
-    const char* e = std::getenv("PN2_MLP_ROUNDS");
-    return e ? std::atoi(e) : 4;
-  }();
+  constexpr int max_tpw = 8, rounds = 4;  // measured: scripts/ab_tpw.sh
   const long long slots = (long long)device_cus() * (lds * 2 <= kLdsLimit ? 2 : 1);
   while (slots > 0 && prm.tpw * 2 <= max_tpw && nblocks >= slots * rounds * prm.tpw * 2)
     prm.tpw *= 2;
@@ -1176,11 +1169,6 @@ int launch_one(Params prm, long long nblocks, size_t lds, hipStream_t s) {
 
 template <int SRC>
 int launch_rows_R(Params& prm, int R, long long nblocks, size_t lds, hipStream_t s) {
-  static const bool trace = std::getenv("PN2_MLP_TRACE") != nullptr;  // tuning diagnostics
-  if (trace)
-    std::fprintf(stderr, "pn2_mlp: src %d R %d wl %d blocks %lld lds %zu gpw %d passes %d "
-                 "attn %d nseg %d\n", SRC, R, prm.wfloats ? 1 : 0, nblocks, lds, prm.gpw,
-                 prm.passes, prm.attn, prm.att_nseg);
   if (nblocks <= 0) return PN2_OK;
   if (nblocks > 0x7fffffffLL) return PN2_EINVAL;
   if (prm.wfloats) {  // weights staged in LDS (small MLPs of the SA layers)
@@ -1236,11 +1224,7 @@ int choose_R_staged(Params& prm, int nl, const pn2_mlp_layer* layers, int cin0, 
   Params plain = prm;
   size_t lds_plain = 0;
   const int R_plain = choose_R(plain, nl, layers, cin0, false, tiles32, 1, &lds_plain);
-  static const bool off = [] {  // A/B override (scripts)
-    const char* e = std::getenv("PN2_MLP_STAGE_OUT");
-    return e && e[0] == '0';
-  }();
-  if (!off) {
+  {
     Params staged = prm;
     staged.stage_out = 1;
     size_t lds = 0;

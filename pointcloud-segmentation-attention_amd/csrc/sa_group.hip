@@ -31,31 +31,13 @@ constexpr int kSgMaxNs = 128;   // nsample
 constexpr int kSgUnroll = 4;    // 64-point steps per scan iteration
 constexpr int kSgHits = 2048;   // hit slots per workgroup: qpb * nsample
 constexpr int kSgMaxQpb = 64;   // queries per workgroup
-// A/B knobs (tools/bench_layers.py): output bytes per workgroup, query splitting
-// diagnostic builds only (results wrong): skip the scan (hits = the first ns points) or the
-// grouped-row writes, to split the kernel's time between its phases
-#ifndef PN2_SG_SKIP
-#define PN2_SG_SKIP 0
-#endif
-#ifndef PN2_SG_SPLIT_KB
-#define PN2_SG_SPLIT_KB 24
-#endif
-#ifndef PN2_SG_SPLIT_STAGE
-#define PN2_SG_SPLIT_STAGE 4096
-#endif
-#ifndef PN2_SG_U  // elements whose gathers are in flight per thread before its stores
-#define PN2_SG_U 4
-#endif
-#ifndef PN2_SG_VEC  // the vector write phase (ball_group_layers_kernel, below); 0 = A/B off
-#define PN2_SG_VEC 1
-#endif
-#ifndef PN2_SG_PREFETCH  // the vector phase gathers the next chunk before storing this one
-#define PN2_SG_PREFETCH 1
-#endif
+// measured on MI355X (tools/bench_layers.py, profiles/r3/sgs, r4/pf): output bytes per
+// workgroup, the split of a query of many channels, gathers in flight per thread
+constexpr int kSgTileKB = 32;      // output per workgroup over whole queries
+constexpr int kSgSplitKB = 24;     // a query above this is split over workgroups ...
+constexpr int kSgSplitStage = 4096;  // ... when its cloud stages in this many LDS bytes
+constexpr int kSgU = 4;            // elements whose gathers are in flight per thread
 constexpr int kSgVecFloats = 4096;  // the vector write phase's LDS staging chunk (16 KB)
-#ifndef PN2_SG_TILE_KB
-#define PN2_SG_TILE_KB 32
-#endif
 
 enum SgLayout : int {
   PN2_SG_POINTS_ONLY = 0,  // out = points[idx]                       (Cout = C)
@@ -74,7 +56,7 @@ struct SgLayer {
   float* out;
   int N, C, M, ns, Cout, layout, qpb, tiles;  // workgroups per cloud = tiles * parts
   int parts, chunk;  // a query split over `parts` workgroups of `chunk` elements each
-  int vec;           // the vector write phase applies (PN2_SG_VEC builds; host-checked)
+  int vec;           // the vector write phase applies (host-checked)
   float thresh;
   FastDiv div_cout, div_ns, div_c4;
 };
@@ -103,7 +85,7 @@ __global__ __launch_bounds__(kSgBlock) void ball_group_layers_kernel(SgArgs a) {
   __shared__ float sx[kSgCap], sy[kSgCap], sz[kSgCap];
   __shared__ int s_hit[kSgHits];          // the tile's rows: query qi's hits at qi*ns ..
   __shared__ float s_q[3 * kSgMaxQpb];    // the tile's query centres
-  __shared__ float4 s_out4[PN2_SG_VEC ? kSgVecFloats / 4 : 1];  // vector phase: chunk image
+  __shared__ float4 s_out4[kSgVecFloats / 4];  // vector phase: chunk image
   // logical blocks cloud-major: cloud b's blocks of every layer are one contiguous range, so
   // the XCD-aware order gives each XCD whole clouds (their rows in one L2) and every XCD the
   // same mix of layers
@@ -137,7 +119,6 @@ __global__ __launch_bounds__(kSgBlock) void ball_group_layers_kernel(SgArgs a) {
     const float qx = s_q[3 * qi + 0], qy = s_q[3 * qi + 1], qz = s_q[3 * qi + 2];
     int* hit = s_hit + qi * ns;
     int cnt = 0, first = 0;
-    if constexpr (PN2_SG_SKIP == 1) cnt = ns;
     for (int base = 0; base < N && cnt < ns; base += kWave * kSgUnroll) {
       bool h[kSgUnroll];
 #pragma unroll
@@ -179,8 +160,8 @@ __global__ __launch_bounds__(kSgBlock) void ball_group_layers_kernel(SgArgs a) {
   float* __restrict__ O = g.out + r_base * Cout;
   float* __restrict__ GX = g.grouped_xyz ? g.grouped_xyz + r_base * 3 : nullptr;
   const float* __restrict__ F = g.points ? g.points + (size_t)b * N * C : nullptr;
-  if constexpr (PN2_SG_VEC) {
-    if (g.vec) {
+  if (g.vec) {
+    {
       // ---- phase 2, vector form: the tile's rows go out in chunks of CH rows through LDS.
       // Feature columns are gathered as float4 (a points row is 16-B aligned: C % 4 == 0) and
       // the xyz columns computed from the LDS cloud copy, both into the chunk's row-major
@@ -214,16 +195,16 @@ __global__ __launch_bounds__(kSgBlock) void ball_group_layers_kernel(SgArgs a) {
           dst[u] = rr * Cout + foff + 4 * cc;
         }
       };
-      // PN2_SG_PREFETCH: a chunk that one pass of UV float4s per thread covers has its
+      // prefetch: a chunk that one pass of UV float4s per thread covers has its
       // successor's gathers issued before its own stores, so the gather round trip overlaps
       // the store phase instead of following it
       const bool one_pass = CH * C4 <= kSgBlock * UV;
-      if (PN2_SG_PREFETCH && one_pass && rbeg < rend) gather(rbeg, t);
+      if (one_pass && rbeg < rend) gather(rbeg, t);
       for (int c0 = rbeg; c0 < rend; c0 += CH) {
         const int nr = min(CH, rend - c0);
         const int nf = nr * C4;
         for (int f0 = t; f0 < nf; f0 += kSgBlock * UV) {
-          if (!(PN2_SG_PREFETCH && one_pass)) gather(c0, f0);
+          if (!one_pass) gather(c0, f0);
 #pragma unroll
           for (int u = 0; u < UV; ++u) {
             if (f0 + u * kSgBlock < nf) {
@@ -245,7 +226,7 @@ __global__ __launch_bounds__(kSgBlock) void ball_group_layers_kernel(SgArgs a) {
           }
         }
         __syncthreads();
-        if (PN2_SG_PREFETCH && one_pass && c0 + CH < rend) gather(c0 + CH, t);
+        if (one_pass && c0 + CH < rend) gather(c0 + CH, t);
         float4* __restrict__ O4 = reinterpret_cast<float4*>(O + (size_t)c0 * Cout);
         const int n4 = (nr * Cout) >> 2;  // nr % 4 == 0 (R, RP and CH are multiples of 4)
         for (int k = t; k < n4; k += kSgBlock) O4[k] = s_out4[k];
@@ -256,7 +237,7 @@ __global__ __launch_bounds__(kSgBlock) void ball_group_layers_kernel(SgArgs a) {
   }
   // this workgroup's elements of the tile: all, or part `part` of a split query
   const int e_beg = part * g.chunk;
-  const int E = PN2_SG_SKIP == 2 ? 0 : min(nq * ns * Cout, e_beg + g.chunk);
+  const int E = min(nq * ns * Cout, e_beg + g.chunk);
   auto value = [&](int e) -> float {
     const int r = (int)fdiv((uint32_t)e, g.div_cout);  // row of the tile
     const int c = e - r * Cout;
@@ -272,7 +253,7 @@ __global__ __launch_bounds__(kSgBlock) void ball_group_layers_kernel(SgArgs a) {
     }
     return F[(size_t)i * C + cp];
   };
-  constexpr int U = PN2_SG_U;
+  constexpr int U = kSgU;
   for (int e0 = e_beg + t; e0 < E; e0 += kSgBlock * U) {
     float v[U];
 #pragma unroll
@@ -288,7 +269,7 @@ __global__ __launch_bounds__(kSgBlock) void ball_group_layers_kernel(SgArgs a) {
   }
   // points-only rows carry no xyz channel: grouped_xyz (still an output of sample_and_group,
   // pointnet_util.py:58) gets its own pass over the tile, by the query's first part
-  if (GX && layout == PN2_SG_POINTS_ONLY && part == 0 && PN2_SG_SKIP != 2) {
+  if (GX && layout == PN2_SG_POINTS_ONLY && part == 0) {
     for (int e = t; e < nq * ns * 3; e += kSgBlock) {
       const int r = e / 3, cx = e - 3 * (e / 3);
       const int qi = (int)fdiv((uint32_t)r, g.div_ns);
@@ -336,18 +317,18 @@ int pn2_ball_group_layers(const pn2_sa_layer* layers, int nlayers, int B, pn2_st
     g.Cout = Cout; g.layout = layout;
     g.thresh = pn2_ball_threshold(s.radius);
     g.div_cout = pn2::make_fastdiv((uint32_t)Cout);
-    // work per workgroup: ~PN2_SG_TILE_KB of output over whole queries; a query of many
+    // work per workgroup: ~kSgTileKB of output over whole queries; a query of many
     // channels on a small cloud (cheap to stage and scan again) is split over several
-    // workgroups of ~PN2_SG_SPLIT_KB each, so the grid has enough waves to hide the gathers
+    // workgroups of ~kSgSplitKB each, so the grid has enough waves to hide the gathers
     const long long per_q = (long long)s.nsample * Cout * 4;
-    long long qpb = (PN2_SG_TILE_KB * 1024 + per_q / 2) / per_q;
+    long long qpb = (kSgTileKB * 1024 + per_q / 2) / per_q;
     if (qpb < 1) qpb = 1;
     if (qpb > pn2::kSgMaxQpb) qpb = pn2::kSgMaxQpb;
     if (qpb * s.nsample > pn2::kSgHits) qpb = pn2::kSgHits / s.nsample;
     long long parts = 1;
-    if (s.N * 12 <= PN2_SG_SPLIT_STAGE && per_q > PN2_SG_SPLIT_KB * 1024) {
+    if (s.N * 12 <= kSgSplitStage && per_q > kSgSplitKB * 1024) {
       qpb = 1;
-      parts = (per_q + PN2_SG_SPLIT_KB * 1024 - 1) / (PN2_SG_SPLIT_KB * 1024);
+      parts = (per_q + kSgSplitKB * 1024 - 1) / (kSgSplitKB * 1024);
     }
     const long long E = qpb * s.nsample * Cout;
     g.chunk = (int)(((E + parts - 1) / parts + 3) / 4 * 4);
@@ -357,11 +338,11 @@ int pn2_ball_group_layers(const pn2_sa_layer* layers, int nlayers, int B, pn2_st
     g.qpb = (int)qpb;
     g.div_ns = pn2::make_fastdiv((uint32_t)s.nsample);
     g.tiles = s.M > 0 ? (int)((s.M + qpb - 1) / qpb) : 0;
-    // the vector write phase (PN2_SG_VEC builds): float4 feature rows, whole queries per
+    // the vector write phase: float4 feature rows, whole queries per
     // workgroup, 16-B aligned buffers, ns % 4 == 0 (chunks start on 16-B boundaries), no
     // grouped_xyz output, at least 4 rows per LDS chunk
     g.div_c4 = pn2::make_fastdiv((uint32_t)(s.C / 4 > 0 ? s.C / 4 : 1));
-    g.vec = PN2_SG_VEC && layout != PN2_SG_XYZ_ONLY && s.C % 4 == 0 && s.nsample % 4 == 0 &&
+    g.vec = layout != PN2_SG_XYZ_ONLY && s.C % 4 == 0 && s.nsample % 4 == 0 &&
             !s.grouped_xyz && 4 * Cout <= pn2::kSgVecFloats &&
             (((uintptr_t)s.points | (uintptr_t)s.new_points) & 15) == 0;
     a.first[i] = (int)blocks;

@@ -239,9 +239,8 @@ def _cloud(pkg, kind, B, N, seed=0):
 
 
 # SA1-size clouds (4096 < N <= 8192) run the culled hot-set sampler by default; every schedule
-# pn2_fps_gather_sched offers there (PN2_FPS_AUTO, PN2_FPS_BLOCKSCAN = the v9 block scan,
-# PN2_FPS_HOTCULL_K128 = the culled sampler with 128 hot entries, PN2_FPS_HOTCULL_LEAN = its
-# lean-LDS form, PN2_FPS_HOTCULL_LDS = its LDS-copy form) must give the oracle's
+# pn2_fps_gather_sched offers there (PN2_FPS_AUTO, PN2_FPS_BLOCKSCAN = the v9 block scan)
+# must give the oracle's
 # indices: ScanNet crops with duplicates, uniform, the integer lattice (exact ties everywhere),
 # npoint beyond the distinct points, npoint > N, tiny npoint, odd N.
 SAMPLER_CASES = [
@@ -251,7 +250,7 @@ SAMPLER_CASES = [
     ("scannet", 3, 8192, 1), ("scannet", 2, 7777, 1500),
 ]
 # MSG SA1-size clouds (8192 < N <= 16384, cfg5): the culled sampler with its coordinates in L2
-# (AUTO) or the v9 512 x 32 block scan; the 128-entry schedule is rejected there
+# (AUTO) or the v9 512 x 32 block scan
 MSG_SAMPLER_CASES = [
     ("scannet", 8, 16384, 512), ("uniform", 2, 16384, 512), ("grid", 2, 16384, 1024),
     ("grid", 1, 16384, 4000), ("dup", 1, 12000, 40), ("fewuniq", 2, 16384, 600),
@@ -271,7 +270,7 @@ def _sched(pkg, torch, x, M, sched):
 
 
 @pytest.mark.parametrize("sched,kind,B,N,M",
-                         [(s,) + c for s in (0, 1, 6, 7, 8) for c in SAMPLER_CASES]
+                         [(s,) + c for s in (0, 1) for c in SAMPLER_CASES]
                          + [(s,) + c for s in (0, 1) for c in MSG_SAMPLER_CASES])
 def test_fps_sampler_schedules(env, sched, kind, B, N, M):
     pkg, O, torch, dev = env
@@ -287,14 +286,13 @@ def test_fps_sampler_schedules(env, sched, kind, B, N, M):
 
 def test_fps_schedule_rejections(env):
     """Schedules exist only where the culled sampler is the default: PN2_EINVAL elsewhere
-    (the 128-entry schedule at the MSG size, any non-AUTO schedule at small N, unknown ids),
-    never a silent fallback."""
+    (any non-AUTO schedule at small N, unknown ids -- among them the removed 128-entry and
+    lean schedules, 6-8), never a silent fallback."""
     pkg, O, torch, dev = env
     L = pkg._lib
     x = torch.from_numpy(_cloud(pkg, "scannet", 1, 16384)).to(dev)
-    assert _sched(pkg, torch, x, 64, L.PN2_FPS_HOTCULL_K128)[0] == L.PN2_EINVAL
-    assert _sched(pkg, torch, x, 64, L.PN2_FPS_HOTCULL_LEAN)[0] == L.PN2_EINVAL
-    assert _sched(pkg, torch, x, 64, L.PN2_FPS_HOTCULL_LDS)[0] == L.PN2_EINVAL
+    for gone in (6, 7, 8):
+        assert _sched(pkg, torch, x[:, :8192].contiguous(), 64, gone)[0] == L.PN2_EINVAL
     assert _sched(pkg, torch, x[:, :4096].contiguous(), 64, L.PN2_FPS_BLOCKSCAN)[0] == L.PN2_EINVAL
     assert _sched(pkg, torch, x, 64, 5)[0] == L.PN2_EINVAL
     assert _sched(pkg, torch, x, 64, L.PN2_FPS_AUTO)[0] == 0

@@ -2,10 +2,9 @@
 """Micro-benchmark of the fused FP interpolation + concat (pn2_fp_apply, fp_fused_kernel) at
 the FP4 sizes of cfg2 (C1 = 0) and cfg3 (C1 = 9 channels, scalar path) and an FP2-like size,
 with and without the unknown-grid row order. HIP events, median of 20; GB/s over the
-algorithmic bytes (output + points1 + dist/idx + points2 once). PN2_FP_UNROLL picks the
-elements in flight per thread (set before the library loads; tools only).
+algorithmic bytes (output + points1 + dist/idx + points2 once).
 
-    PN2_FP_UNROLL=1 python tools/bench_fp.py
+    python tools/bench_fp.py
 """
 import importlib
 import json
@@ -40,7 +39,7 @@ def main():
             ts.append(a.elapsed_time(b) * 1e3 / inner)
         return statistics.median(ts)
 
-    res = {"unroll": os.environ.get("PN2_FP_UNROLL", "default")}
+    res = {}
     B = 16
     for name, n, m, C1, C2 in (("fp4_cfg2", 8192, 1024, 0, 128), ("fp4_cfg3", 8192, 1024, 9, 128),
                                ("fp2", 1024, 256, 128, 256)):

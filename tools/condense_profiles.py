@@ -10,7 +10,7 @@ import json
 import os
 import sys
 
-KEEP_CFG = ("config", "clouds_per_gpu", "hw_queues", "streams", "launch", "cu_partition",
+KEEP_CFG = ("config", "clouds_per_gpu", "hw_queues", "streams", "launch",
             "lane0_priority")
 
 
