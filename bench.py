@@ -125,6 +125,77 @@ def cpu_baseline(config, B_per_step, seconds, threads):
                       "(the box allows its CPU share only)"}
 
 
+def cfg1_leg(dev, seconds=2.0):
+    """BASELINE.json configs[0] (BASELINE.md:61): B = 1, N = 1024 uniform points, ONE SA layer
+    (npoint 256, r 0.2, nsample 32, xyz only): farthest-point sampling + gather + ball query +
+    grouping. CPU: the C restatement (oracle/pn2_oracle.c, the reference's loops) on 1 thread,
+    repeated for ~`seconds`; GPU: pointnet_util.sample_and_group on this device (the same four
+    ops; HIP events, median of 50), both per layer call, and the outputs compared."""
+    import numpy as np
+    import torch
+    from oracle import oracle as O
+    pkg = importlib.import_module(PKG)
+    x = pkg.synth.batch([0], 1024, "uniform")[0]
+    O.set_threads(1)
+
+    def cpu_sa():
+        idx = O.fps(x, 256)
+        nx = O.gather_point(x, idx)
+        bidx, _ = O.ball_query(x, nx, 0.2, 32)
+        return nx, bidx, O.group_concat(x, None, nx, bidx)[0]
+    ref = cpu_sa()
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        cpu_sa()
+        n += 1
+    cpu_ms = (time.perf_counter() - t0) / n * 1e3
+    xt = torch.from_numpy(x).to(dev)
+    sg = pkg.pointnet_util.sample_and_group
+    for _ in range(5):
+        out = sg(256, 0.2, 32, xt, None)
+    ts = []
+    for _ in range(50):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        out = sg(256, 0.2, 32, xt, None)
+        b.record()
+        b.synchronize()
+        ts.append(a.elapsed_time(b))
+    ts.sort()
+    same = (np.array_equal(out[0].cpu().numpy(), ref[0]) and np.array_equal(out[2].cpu().numpy(), ref[1])
+            and np.array_equal(out[1].cpu().numpy().view(np.int32), ref[2].view(np.int32)))
+    return {"workload": "cfg1: B=1, N=1024 uniform, one SA layer (FPS 256 + gather + ball query "
+                        "r=0.2 ns=32 + grouping), BASELINE.json configs[0]",
+            "cpu_ms_per_call_1core": cpu_ms, "cpu_calls": n, "cpu_kind": "port",
+            "gpu_ms_per_call": ts[len(ts) // 2], "gpu_over_cpu": cpu_ms / ts[len(ts) // 2],
+            "gpu_note": "pointnet_util.sample_and_group on the MI355X, HIP events around one call "
+                        "(four launches), median of 50",
+            "outputs_equal": bool(same)}
+
+
+def copy_peak(dev, mib=1024, reps=5):
+    """A measured HBM figure beside the 8 TB/s nominal (BASELINE.md:75): a device-to-device copy
+    of `mib` MiB (hipMemcpyAsync through torch's copy_), read + write bytes per second, best of
+    `reps`."""
+    import torch
+    n = mib * 1024 * 1024 // 4
+    a = torch.empty(n, dtype=torch.float32, device=dev).fill_(1.0)
+    b = torch.empty_like(a)
+    b.copy_(a)
+    best = None
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        b.copy_(a)
+        e1.record()
+        e1.synchronize()
+        ms = e0.elapsed_time(e1)
+        best = ms if best is None else min(best, ms)
+    del a, b
+    return {"GBps": 2 * n * 4 / (best * 1e-3) / 1e9, "bytes": 2 * n * 4,
+            "method": f"device-to-device copy_ of {mib} MiB, read + write bytes, best of {reps}"}
+
+
 def pmc_traffic(config, B):
     """HBM bytes per launch of the SA1 sampler from the committed rocprofv3 --pmc summary
     (profiles/<round>/pmc_traffic_<config>_B<B>.json, written by tools/pmc_summary.py from
@@ -349,7 +420,7 @@ def main():
     ap.add_argument("--side-layout", choices=["a", "b", "c", "d"], default=None,
                     help="side-lane layout with several sampler streams (stack.side_layout; "
                          "default: the config's LAYOUTS entry)")
-    ap.add_argument("--chain", choices=["own", "own2", "behind"], default=None,
+    ap.add_argument("--chain", choices=["own", "own2", "own3", "behind"], default=None,
                     help="with several sampler streams: the later samplers (SA2.. chain) on a "
                          "stream of their own or behind SA1 on its sampler stream (default: the "
                          "config's LAYOUTS entry)")
@@ -486,8 +557,9 @@ def main():
                                       private_streams=model or args.private_side,
                                       native_plan=not args.no_native_plan,
                                       only=args.diag_only, layout=args.side_layout,
-                                      chain_own=args.chain in ("own", "own2"),
-                                      chain_streams=2 if args.chain == "own2" else 1,
+                                      chain_own=args.chain.startswith("own"),
+                                      chain_streams=int(args.chain[3:] or 1)
+                                      if args.chain.startswith("own") else 1,
                                       set_inputs=set_inputs,
                                       direct=not args.graph_launch)
         else:
@@ -637,9 +709,9 @@ def main():
                        "streams": (("SA1 sampler + 3 side streams" if args.sampler_lanes <= 1 or args.model
                                     else f"{args.sampler_lanes} sampler streams (consecutive steps' "
                                     f"samplers concurrent; SA2.. samplers "
-                                    + ({"own": "on their own stream", "own2": "on two streams of "
-                                        "their own, alternating by buffer set"}.get(args.chain,
-                                                                                 "behind SA1"))
+                                    + ("behind SA1" if args.chain == "behind" else
+                                       "on their own stream" if args.chain == "own" else
+                                       f"on {args.chain[3:]} streams of their own, by buffer set")
                                     + ") + side streams "
                                     f"(layout {args.side_layout})"
                                     + (" per buffer set" if args.private_side else ""))
@@ -671,11 +743,17 @@ def main():
             result["e2e"] = e2e
         if args.diag_only:
             result["diagnostic"] = f"only the {args.diag_only} of each step ran: not a benchmark result"
+        if world == 1 and not args.model:
+            try:  # (outside the timed region, after it)
+                result["roofline"]["hbm"]["copy_peak_measured"] = copy_peak(dev)
+            except Exception as e:  # a reported figure, never the product
+                log(f"copy peak failed: {e!r}")
         if world == 1 and not args.no_cpu_baseline and not args.model:
             try:
                 result["cpu_baseline"] = cpu_baseline(args.config, B, args.cpu_seconds,
                                                       args.cpu_threads or _cpu_share())
                 cb = result["cpu_baseline"]
+                cb["cfg1"] = cfg1_leg(dev)
                 # vs_baseline stays null (BASELINE.md publishes no number for this metric);
                 # the GPU/CPU ratios against the measured and extrapolated CPU rates:
                 cb["gpu_over_cpu"] = {"1core": value / cb["value_1core"],

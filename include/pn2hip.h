@@ -191,6 +191,16 @@ int pn2_ball_query_grid(const void* grid, const float* xyz2, int B, int N, int M
 int pn2_ball_group_xyz_grid(const void* grid, const float* xyz1, const float* xyz2, int B, int N,
                             int M, float radius, int nsample, int32_t* idx, int32_t* pts_cnt,
                             float* grouped_xyz, pn2_stream_t stream);
+/* pn2_ball_group_xyz_grid with features: ONE kernel for query_ball_point + group_point + the
+ * centring and concat of sample_and_group (tf_grouping_g.cu:3-57, pointnet_util.py:38-52; MSG
+ * order :186-191). new_points (B,M,nsample,3+C) = [xyz1[idx] - xyz2, points[idx]], or with
+ * flags & PN2_XYZ_LAST [points[idx], xyz1[idx] - xyz2]; flags must hold PN2_USE_XYZ when C > 0
+ * (C = 0: exactly pn2_ball_group_xyz_grid). idx / pts_cnt as pn2_ball_query_grid. Bit for bit
+ * pn2_ball_query_grid followed by pn2_group_concat. */
+int pn2_ball_group_grid(const void* grid, const float* xyz1, const float* points, int C,
+                        int flags, const float* xyz2, int B, int N, int M, float radius,
+                        int nsample, int32_t* idx, int32_t* pts_cnt, float* new_points,
+                        pn2_stream_t stream);
 /* pn2_ball_group_xyz_grid for nr radii (1 <= nr <= PN2_BQ_MAX_RADII) of the same queries in
  * ONE launch (MSG's SA1: pointnet_util.py:162-203, the radius loop): the cells of the largest
  * radius are walked once and every candidate is tested against each radius. Per radius r:

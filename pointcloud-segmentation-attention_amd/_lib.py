@@ -93,6 +93,7 @@ SIGNATURES = {
     "pn2_grid_build": (_I, [_P, _I, _I, _F, _P, _S, _P]),
     "pn2_ball_query_grid": (_I, [_P, _P, _I, _I, _I, _F, _I, _P, _P, _P]),
     "pn2_ball_group_xyz_grid": (_I, [_P, _P, _P, _I, _I, _I, _F, _I, _P, _P, _P, _P]),
+    "pn2_ball_group_grid": (_I, [_P, _P, _P, _I, _I, _P, _I, _I, _I, _F, _I, _P, _P, _P, _P]),
     "pn2_ball_group_xyz_grid_radii": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _P]),
     "pn2_three_nn_grid": (_I, [_P, _P, _P, _I, _I, _I, _P, _P, _P]),
     "pn2_fp_apply": (_I, [_P, _P, _P, _P, _I, _P, _I, _I, _I, _I, _P, _P]),

@@ -181,12 +181,19 @@ struct BqRadii {
   int ns[PN2_BQ_MAX_RADII];
   int32_t* idx[PN2_BQ_MAX_RADII];
   int32_t* cnt[PN2_BQ_MAX_RADII];
-  float* gxyz[PN2_BQ_MAX_RADII];
+  float* gout[PN2_BQ_MAX_RADII];  // GROUP: the grouped rows of radius r (B,M,ns,Cout)
+  const float* points;            // GROUP: the features (B,N,C), or null (C = 0)
+  int C, xoff, foff, cout;        // features, xyz / feature column offsets, row width
+  FastDiv div_cout;
+  int nsmax;                      // max ns[r]: each wave's hit list holds NR x nsmax
 };
 
-// GROUP: also the grouped coordinates gxyz (B,M,ns,3) = xyz1[idx] - xyz2 (pn2_group_concat
-// with no points, pointnet_util.py:39-40): each lane writes the rows of the hits it ranks, so
-// the SA1 grouping of an xyz-only layer needs no launch of its own.
+// GROUP: also the grouped rows (B,M,ns,Cout) of sample_and_group (pointnet_util.py:38-52, the
+// MSG order :186-191): the centred xyz1[idx] - xyz2 at columns xoff.. and, with features, the
+// points[idx] at foff.. (SSG [xyz, points], MSG [points, xyz]; C = 0: grouped_xyz alone), so an
+// SA layer's query + grouping is one launch. A wave first ranks its hits into an LDS list
+// (index order, padded with the first hit as the reference pads, tf_grouping_g.cu:26-29),
+// then writes the query's idx row and its ns x Cout floats as one coalesced range.
 // NR radii: the cells of the largest (`radius`) are walked once, every candidate's distance is
 // tested against each radius' threshold into that radius' bitmask, and each radius' rows are
 // written from its own bitmask -- the same outputs as NR single-radius launches.
@@ -195,7 +202,7 @@ __global__ __launch_bounds__(BLOCK) void ball_query_grid_kernel(
     const char* __restrict__ grid, const float* __restrict__ xyz2, int N, int M, float radius,
     int qpb, int words, int gx, int nblk, const BqRadii rd, const float* __restrict__ xyz1) {
   constexpr int NW = BLOCK / kWave;
-  extern __shared__ uint32_t bits[];  // NW x NR x words
+  extern __shared__ uint32_t bits[];  // NW x NR x words, then NW x NR x nsmax hit lists
   // XCD-aware order (common.h): each XCD takes a contiguous range of (cloud, query chunk)
   // blocks, so a cloud's grid is fetched into one L2, not into all eight
   const int lb = xcd_block((int)blockIdx.x, nblk);
@@ -207,6 +214,7 @@ __global__ __launch_bounds__(BLOCK) void ball_query_grid_kernel(
   const int* __restrict__ off = g.off;
   const float4* __restrict__ pts = g.pts;
   uint32_t* mine = bits + (size_t)w * NR * words;  // radius r: mine + r * words
+  int* hl = reinterpret_cast<int*>(bits + (size_t)NW * NR * words) + (size_t)w * NR * rd.nsmax;
   const int wpl = (words + kWave - 1) / kWave;  // bitmask words per lane, in lane order
 
   const int q_end = min(M, (bx + 1) * qpb);
@@ -289,31 +297,48 @@ __global__ __launch_bounds__(BLOCK) void ball_query_grid_kernel(
       const int ns = rd.ns[r];
       const int cnt = min(total, ns);
       int32_t* __restrict__ row = rd.idx[r] + ((size_t)b * M + q) * ns;
-      float* __restrict__ grow = GROUP ? rd.gxyz[r] + ((size_t)b * M + q) * ns * 3 : nullptr;
-      const float* __restrict__ X1 = GROUP ? xyz1 + (size_t)b * N * 3 : nullptr;
+      int* lst = hl + r * rd.nsmax;
       int rank = incl - pop;
       for (int j = 0; j < wpl && rank < ns; ++j) {
         const int wi = lane * wpl + j;
         uint32_t v = wi < words ? mr[wi] : 0u;
         while (v && rank < ns) {
-          const int k = 32 * wi + __builtin_ctz(v);
-          if constexpr (GROUP) {
-            grow[3 * rank + 0] = X1[3 * k + 0] - qx;  // pointnet_util.py:40
-            grow[3 * rank + 1] = X1[3 * k + 1] - qy;
-            grow[3 * rank + 2] = X1[3 * k + 2] - qz;
-          }
-          row[rank++] = k;
+          lst[rank++] = 32 * wi + __builtin_ctz(v);
           v &= v - 1u;
         }
       }
       const uint64_t has = __ballot(pop > 0);
       const int first = has ? __shfl(myfirst, __ffsll((unsigned long long)has) - 1, kWave) : 0;
-      for (int p = cnt + lane; p < ns; p += kWave) {
-        row[p] = first;  // :26-29 (0 when no hit)
-        if constexpr (GROUP) {
-          grow[3 * p + 0] = X1[3 * first + 0] - qx;
-          grow[3 * p + 1] = X1[3 * first + 1] - qy;
-          grow[3 * p + 2] = X1[3 * first + 2] - qz;
+      for (int p = cnt + lane; p < ns; p += kWave) lst[p] = first;  // :26-29 (0 when no hit)
+      // (one wave's DS operations execute in order: the reads below see every lane's writes)
+      for (int p = lane; p < ns; p += kWave) row[p] = lst[p];
+      if constexpr (GROUP) {
+        const int Cout = rd.cout, C = rd.C;
+        const float* __restrict__ X1 = xyz1 + (size_t)b * N * 3;
+        const float* __restrict__ F = C ? rd.points + (size_t)b * N * C : nullptr;
+        float* __restrict__ out = rd.gout[r] + ((size_t)b * M + q) * ns * Cout;
+        const int E = ns * Cout;
+        // four elements' gathers in flight per lane before any is stored
+        for (int e0 = lane; e0 < E; e0 += 4 * kWave) {
+          float v[4], sub[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int e = min(e0 + u * kWave, E - 1);
+            const int rr = (int)fdiv((uint32_t)e, rd.div_cout);
+            const int c = e - rr * Cout;
+            const int k = lst[rr];
+            const int cx = c - rd.xoff;
+            const bool isx = cx >= 0 && cx < 3;
+            const float* src = isx ? X1 + 3 * k + cx : F + (size_t)k * C + (c - rd.foff);
+            v[u] = *src;
+            // a feature column subtracts +0.0f: x - 0 == x, bit for bit (-0.0 included)
+            sub[u] = !isx ? 0.0f : cx == 0 ? qx : cx == 1 ? qy : qz;
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int e = e0 + u * kWave;
+            if (e < E) out[e] = v[u] - sub[u];  // pointnet_util.py:40
+          }
         }
       }
       if (lane == 0) rd.cnt[r][(size_t)b * M + q] = cnt;
@@ -354,29 +379,43 @@ int pn2_grid_build(const float* xyz, int B, int N, float cell_edge, void* grid,
 }
 
 namespace {
-// nr radii (1..PN2_BQ_MAX_RADII) in one launch; gxyz[r] all set (GROUP) or all NULL
+// nr radii (1..PN2_BQ_MAX_RADII) in one launch; gout[r] all set (GROUP) or all NULL; GROUP
+// rows: [xyz1[idx] - xyz2, points[idx]] (xyz_last: [points, xyz]) of C + 3 columns
 int ball_query_grid(const void* grid, const float* xyz2, int B, int N, int M, int nr,
                     const float* radii, const int* nsample, int32_t* const* idx,
-                    int32_t* const* pts_cnt, const float* xyz1, float* const* gxyz,
-                    hipStream_t stream) {
+                    int32_t* const* pts_cnt, const float* xyz1, float* const* gout,
+                    hipStream_t stream, const float* points = nullptr, int C = 0,
+                    bool xyz_last = false) {
   if (nr < 1 || nr > PN2_BQ_MAX_RADII || B < 0 || N < 0 || M < 0) return PN2_EINVAL;
   for (int r = 0; r < nr; ++r)
     if (!(radii[r] > 0.0f) || nsample[r] <= 0) return PN2_EINVAL;
   if ((long long)B * M == 0) return PN2_OK;
   if (!grid || !xyz2 || B > 65535) return PN2_EINVAL;
-  const bool group = gxyz != nullptr;
+  const bool group = gout != nullptr;
   if (group && !xyz1) return PN2_EINVAL;
+  if (C < 0 || (C > 0 && (!group || !points)) || C > 4096) return PN2_EINVAL;
   pn2::BqRadii rd{};
   float rmax = 0.0f;
+  int nsmax = 1;
   for (int r = 0; r < nr; ++r) {
-    if (!idx[r] || !pts_cnt[r] || (group && !gxyz[r])) return PN2_EINVAL;
+    if (!idx[r] || !pts_cnt[r] || (group && !gout[r])) return PN2_EINVAL;
     rd.thresh[r] = pn2_ball_threshold(radii[r]);
     rd.ns[r] = nsample[r];
     rd.idx[r] = idx[r];
     rd.cnt[r] = pts_cnt[r];
-    rd.gxyz[r] = group ? gxyz[r] : nullptr;
+    rd.gout[r] = group ? gout[r] : nullptr;
     rmax = std::max(rmax, radii[r]);
+    nsmax = std::max(nsmax, nsample[r]);
   }
+  rd.points = C ? points : nullptr;
+  rd.C = C;
+  rd.cout = C + 3;
+  rd.xoff = xyz_last ? C : 0;
+  rd.foff = xyz_last ? 0 : 3;
+  rd.div_cout = pn2::make_fastdiv((uint32_t)rd.cout);
+  rd.nsmax = nsmax;
+  // the 32-bit element arithmetic of a query's rows (fdiv: e * Cout < 2^32)
+  if ((long long)nsmax * rd.cout * rd.cout >= (1LL << 32)) return PN2_EINVAL;
   const int words = (N + 31) / 32;
   if (words > pn2::kMaxBitWords) return PN2_EINVAL;
   constexpr int BLOCK = 256, NW = BLOCK / pn2::kWave;
@@ -385,8 +424,8 @@ int ball_query_grid(const void* grid, const float* xyz2, int B, int N, int M, in
   long long qpb = (queries + 2047) / 2048;
   qpb = ((qpb + NW - 1) / NW) * NW;
   const unsigned gx = (unsigned)((M + qpb - 1) / qpb);
-  const size_t lds = (size_t)NW * nr * (words > 0 ? words : 1) * 4;
-  if (lds > 64 * 1024) return PN2_EINVAL;  // (dynamic LDS; nr = 1 fits up to N = 131072)
+  const size_t lds = (size_t)NW * nr * ((words > 0 ? words : 1) + nsmax) * 4;
+  if (lds > 64 * 1024) return PN2_EINVAL;  // (dynamic LDS; nr = 1 fits up to N ~ 130000)
   const long long nblk = (long long)gx * B;
   if (nblk > INT32_MAX - pn2::kXcds) return PN2_EINVAL;
   const dim3 grd(pn2::xcd_grid(nblk)), blk(BLOCK);
@@ -422,6 +461,16 @@ int pn2_ball_group_xyz_grid(const void* grid, const float* xyz1, const float* xy
   if (!grouped_xyz || !idx || !pts_cnt) return PN2_EINVAL;
   return ball_query_grid(grid, xyz2, B, N, M, 1, &radius, &nsample, &idx, &pts_cnt, xyz1,
                          &grouped_xyz, (hipStream_t)stream);
+}
+
+int pn2_ball_group_grid(const void* grid, const float* xyz1, const float* points, int C,
+                        int flags, const float* xyz2, int B, int N, int M, float radius,
+                        int nsample, int32_t* idx, int32_t* pts_cnt, float* new_points,
+                        pn2_stream_t stream) {
+  if (!new_points || !idx || !pts_cnt || C < 0 || (C > 0 && !points)) return PN2_EINVAL;
+  if (C > 0 && !(flags & PN2_USE_XYZ)) return PN2_EINVAL;  // (points only: pn2_group_point)
+  return ball_query_grid(grid, xyz2, B, N, M, 1, &radius, &nsample, &idx, &pts_cnt, xyz1,
+                         &new_points, (hipStream_t)stream, points, C, (flags & PN2_XYZ_LAST) != 0);
 }
 
 int pn2_ball_group_xyz_grid_radii(const void* grid, const float* xyz1, const float* xyz2, int B,

@@ -578,6 +578,24 @@ __global__ __launch_bounds__(kNNBlock) void fp_fused_kernel(FpLayer p) {
 constexpr int kFpGridMaxKnown = 4096;  // LDS: m float4 + (max(2m / ppc, 64) + 1) offsets
 constexpr float kFpgPointsPerCell = 2.0f;  // the LDS grid's points per cell (profiles/r4/ppc)
 
+// LDS per workgroup of the current device (cached per device id)
+size_t device_lds_per_block() {
+  static size_t cache[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 64 * 1024;
+  if (!cache[dev]) {
+    int v = 0, o = 0;  // the per-block limit, or the opt-in one where the device reports it
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) != hipSuccess)
+      v = 0;
+    if (hipDeviceGetAttribute(&o, hipDeviceAttributeSharedMemPerBlockOptin, dev) != hipSuccess)
+      o = 0;
+    v = std::max(v, o);
+    if (v <= 0) return 64 * 1024;
+    cache[dev] = (size_t)v;
+  }
+  return cache[dev];
+}
+
 // dynamic LDS: the m sorted points, then the ncell + 1 cell offsets as uint16 (m <= 4096)
 inline size_t fp_grid_lds(int m) {
   const size_t cells = (size_t)ceil((double)m * kAutoPointsPerCell / kFpgPointsPerCell);
@@ -855,6 +873,10 @@ int fp_grid_launch(const float* xyz1, const float* xyz2, const void* ugrid, cons
   if (rc != PN2_OK) return rc;
   const dim3 grid(xcd_grid(f.blocks)), blk(kNNBlock);
   const size_t lds = fp_grid_lds(m);
+  // the known grid must fit this device's LDS per workgroup (160 KB on gfx950; m = 4096 needs
+  // ~74 KB): a smaller part reports PN2_EINVAL, and fp_interpolate then takes the three-launch
+  // path (grid build + three_nn_grid + fp_apply)
+  if (lds + 2048 > device_lds_per_block()) return PN2_EINVAL;
 #define PN2_FPG_K(V2, V1, U)                                                                   \
   if (m <= 4 * kNNBlock) hipLaunchKernelGGL((fp_grid_fused_kernel<V2, V1, U, 4>), grid, blk, lds, stream, f.p, dist, idx); \
   else hipLaunchKernelGGL((fp_grid_fused_kernel<V2, V1, U, kFpGridMaxKnown / kNNBlock>), grid, blk, lds, stream, f.p, dist, idx)

@@ -85,7 +85,10 @@ __global__ __launch_bounds__(kSgBlock) void ball_group_layers_kernel(SgArgs a) {
   __shared__ float sx[kSgCap], sy[kSgCap], sz[kSgCap];
   __shared__ int s_hit[kSgHits];          // the tile's rows: query qi's hits at qi*ns ..
   __shared__ float s_q[3 * kSgMaxQpb];    // the tile's query centres
-  __shared__ float4 s_out4[kSgVecFloats / 4];  // vector phase: chunk image
+  // vector phase: the chunk image, dynamic LDS sized by the host -- 16 KB when some layer of
+  // the launch has the vector phase, none otherwise (the scalar-only launches keep their
+  // occupancy)
+  extern __shared__ float4 s_out4[];
   // logical blocks cloud-major: cloud b's blocks of every layer are one contiguous range, so
   // the XCD-aware order gives each XCD whole clouds (their rows in one L2) and every XCD the
   // same mix of layers
@@ -352,8 +355,11 @@ int pn2_ball_group_layers(const pn2_sa_layer* layers, int nlayers, int B, pn2_st
   a.first[nlayers] = (int)blocks;
   a.B = B;
   if (blocks * B == 0) return PN2_OK;
+  bool vec = false;
+  for (int i = 0; i < nlayers; ++i) vec = vec || a.l[i].vec;
+  const size_t lds = vec ? (size_t)pn2::kSgVecFloats * 4 : 0;
   hipLaunchKernelGGL(pn2::ball_group_layers_kernel, dim3(pn2::xcd_grid(blocks * B)),
-                     dim3(pn2::kSgBlock), 0, (hipStream_t)stream, a);
+                     dim3(pn2::kSgBlock), lds, (hipStream_t)stream, a);
   PN2_RETURN_LAUNCH();
 }
 

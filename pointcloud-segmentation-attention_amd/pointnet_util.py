@@ -27,7 +27,7 @@ import ctypes
 import torch
 
 from . import tf_grouping, tf_interpolate, tf_sampling, tf_util
-from ._lib import (POOL_MODES, PN2_BQ_MAX_RADII, PN2_FP_MAX_LAYERS, PN2_POOL_NONE,
+from ._lib import (POOL_MODES, PN2_BQ_MAX_RADII, PN2_EINVAL, PN2_FP_MAX_LAYERS, PN2_POOL_NONE,
                    PN2_SA_MAX_LAYERS, PN2_USE_XYZ, PN2_XYZ_LAST, FpLayer, InvalidArgumentError,
                    SaLayer, check, device_tensor, lib, ptr, stream_of)
 
@@ -94,6 +94,32 @@ def ball_group_xyz(radius, nsample, xyz, new_xyz, grid):
     return idx, cnt, grouped
 
 
+def ball_group(radius, nsample, xyz, points, new_xyz, grid, xyz_last=False):
+    """query_ball_point over `grid` (a tf_grouping.BallGrid built over xyz) and the grouping +
+    centring + concat of sample_and_group (pointnet_util.py:38-52; xyz_last: the MSG order
+    :186-191) in ONE kernel (pn2_ball_group_grid). points None: ball_group_xyz. Returns (idx,
+    pts_cnt, new_points), bit-identical to query_ball_point + group_concat."""
+    if points is None:
+        return ball_group_xyz(radius, nsample, xyz, new_xyz, grid)
+    xyz = device_tensor(xyz, "xyz", torch.float32)
+    points = device_tensor(points, "points", torch.float32)
+    new_xyz = device_tensor(new_xyz, "new_xyz", torch.float32)
+    if not grid.matches(xyz):
+        raise InvalidArgumentError("ball_group: the grid was built over a different xyz")
+    B, N, M, ns = int(xyz.shape[0]), int(xyz.shape[1]), int(new_xyz.shape[1]), int(nsample)
+    if int(new_xyz.shape[0]) != B or tuple(points.shape[:2]) != (B, N):
+        raise InvalidArgumentError("ball_group: xyz (B,N,3), points (B,N,C), new_xyz (B,M,3)")
+    C = int(points.shape[2])
+    idx = torch.empty((B, M, ns), dtype=torch.int32, device=xyz.device)
+    cnt = torch.empty((B, M), dtype=torch.int32, device=xyz.device)
+    new_points = torch.empty((B, M, ns, C + 3), dtype=torch.float32, device=xyz.device)
+    flags = PN2_USE_XYZ | (PN2_XYZ_LAST if xyz_last else 0)
+    check(lib().pn2_ball_group_grid(ptr(grid.buf), ptr(xyz), ptr(points), C, flags,
+                                    ptr(new_xyz), B, N, M, float(radius), ns, ptr(idx),
+                                    ptr(cnt), ptr(new_points), stream_of(xyz)), "ball_group")
+    return idx, cnt, new_points
+
+
 def ball_group_xyz_radii(radii, nsamples, xyz, new_xyz, grid):
     """ball_group_xyz for several radii of the same queries (MSG's SA1 radius loop,
     pointnet_util.py:162-203) in ONE kernel (pn2_ball_group_xyz_grid_radii: one walk over the
@@ -110,7 +136,8 @@ def ball_group_xyz_radii(radii, nsamples, xyz, new_xyz, grid):
     B, N, M = int(xyz.shape[0]), int(xyz.shape[1]), int(new_xyz.shape[1])
     if int(new_xyz.shape[0]) != B:
         raise InvalidArgumentError("ball_group_xyz_radii: xyz and new_xyz need the same batch")
-    if nr * ((N + 31) // 32) > 4096:  # the bitmasks' LDS bound: one launch per radius
+    if nr * ((N + 31) // 32 + max(int(n) for n in nsamples)) > 4096:
+        # the bitmasks' and hit lists' LDS bound: one launch per radius
         return [ball_group_xyz(r, ns, xyz, new_xyz, grid) for r, ns in zip(radii, nsamples)]
     outs = []
     for ns in nsamples:
@@ -292,11 +319,17 @@ def fp_interpolate(xyz1, xyz2, points1, points2, known_grid=None, unknown_grid=N
         if return_nn:
             nn = (torch.empty((B, n, 3), dtype=torch.float32, device=xyz1.device),
                   torch.empty((B, n, 3), dtype=torch.int32, device=xyz1.device))
-        check(lib().pn2_fp_grid_fused(ptr(xyz1), ptr(xyz2),
-                                      None if unknown_grid is None else ptr(unknown_grid.buf),
-                                      ptr(points1), C1, ptr(points2), C2, B, n, m, ptr(out),
-                                      ptr(nn[0]) if nn else None, ptr(nn[1]) if nn else None,
-                                      stream_of(xyz1)), "fp_interpolate")
+        rc = lib().pn2_fp_grid_fused(ptr(xyz1), ptr(xyz2),
+                                     None if unknown_grid is None else ptr(unknown_grid.buf),
+                                     ptr(points1), C1, ptr(points2), C2, B, n, m, ptr(out),
+                                     ptr(nn[0]) if nn else None, ptr(nn[1]) if nn else None,
+                                     stream_of(xyz1))
+        if rc == PN2_EINVAL and B > 0 and n > 0:
+            # (the arguments are valid: the known grid does not fit this device's LDS)
+            nn = tf_interpolate.three_nn(xyz1, xyz2, None, unknown_grid)
+            out = fp_apply(nn, points1, points2, unknown_grid)
+        else:
+            check(rc, "fp_interpolate")
     elif known_grid is not None or tf_interpolate.use_grid(n, m):
         nn = tf_interpolate.three_nn(xyz1, xyz2, known_grid, unknown_grid)
         out = fp_apply(nn, points1, points2, unknown_grid)

@@ -273,10 +273,11 @@ class Step:
             def f():
                 _, radius, nsample, _ = SSG_SA[i]
                 xyz, new_xyz = v["xyz"][i], v["xyz"][i + 1]
-                if i == 0 and points[0] is None and v.get("grid1") is not None:
-                    # xyz-only SA1 (cfg2): query and grouping in one kernel
-                    idx, _, new_points = pointnet_util.ball_group_xyz(radius, nsample, xyz,
-                                                                      new_xyz, v["grid1"])
+                if i == 0 and v.get("grid1") is not None:
+                    # SA1 (cfg2 xyz only, cfg3 with rgb + normals): query and grouping in one
+                    # kernel over the grid
+                    idx, _, new_points = pointnet_util.ball_group(radius, nsample, xyz,
+                                                                  points[0], new_xyz, v["grid1"])
                 else:
                     idx, _ = tf_grouping.query_ball_point(radius, nsample, xyz, new_xyz,
                                                           grid=v.get("grid1") if i == 0 else None)

@@ -184,3 +184,57 @@ def test_ball_group_xyz_radii(env, kind, B, N, M, radii, nss, edge):
         one = pkg.pointnet_util.ball_group_xyz(r, ns, xt, qt, grid)
         assert torch.equal(one[0], idx) and torch.equal(one[1], cnt)
         assert torch.equal(one[2].view(torch.int32), grouped.view(torch.int32))
+
+
+GROUP_FEAT_CASES = [
+    # kind, B, N, M, C, r, ns, xyz_last
+    ("scannet", 2, 8192, 1024, 6, 0.1, 32, False),   # cfg3 SA1: rgb + normals
+    ("scannet", 2, 8192, 1024, 6, 0.1, 32, True),    # the MSG order
+    ("grid", 2, 4096, 500, 9, 1.0, 16, False),       # lattice ties at the radius
+    ("uniform", 1, 3000, 300, 64, 0.3, 40, True),    # wide rows, queries short of ns
+    ("scannet", 1, 16384, 512, 1, 0.4, 128, False),  # ns 128, one channel
+    ("uniform", 1, 5, 7, 3, 0.5, 8, False),          # tiny cloud
+]
+
+
+@pytest.mark.parametrize("kind,B,N,M,C,r,ns,xyz_last", GROUP_FEAT_CASES)
+def test_ball_group_features(env, kind, B, N, M, C, r, ns, xyz_last):
+    """pointnet_util.ball_group (pn2_ball_group_grid: grid query + grouping with features in
+    one kernel) == the oracle's ball_query + group_concat ([xyz - new_xyz, points], or the MSG
+    order), bit for bit, including a query with no hit; C = 0 is ball_group_xyz."""
+    pkg, O, torch, dev = env
+    x, p, q = _layer(pkg, O, kind, B, N, M, C, 5)
+    xt, pt, qt = (torch.from_numpy(a).to(dev) for a in (x, p, q))
+    grid = pkg.tf_grouping.BallGrid(xt, r)
+    idx, cnt, new_points = pkg.pointnet_util.ball_group(r, ns, xt, pt, qt, grid,
+                                                        xyz_last=xyz_last)
+    ridx, rcnt = O.ball_query(x, q, r, ns)
+    rnp, _ = O.group_concat(x, p, q, ridx, use_xyz=True, xyz_last=xyz_last)
+    assert np.array_equal(cnt.cpu().numpy(), rcnt)
+    assert np.array_equal(idx.cpu().numpy(), ridx)
+    assert np.array_equal(_bits(new_points.cpu().numpy()), _bits(rnp))
+    i0, c0, g0 = pkg.pointnet_util.ball_group(r, ns, xt, None, qt, grid)
+    rg, _ = O.group_concat(x, None, q, ridx)
+    assert torch.equal(i0, idx) and np.array_equal(_bits(g0.cpu().numpy()), _bits(rg))
+
+
+def test_ball_group_rejects(env):
+    """PN2_EINVAL (InvalidArgumentError) for features without use_xyz, a negative C, or
+    features with no pointer -- never a silent fallback."""
+    pkg, O, torch, dev = env
+    L = pkg._lib
+    x, p, q = _layer(pkg, O, "uniform", 1, 100, 10, 4, 1)
+    xt, pt, qt = (torch.from_numpy(a).to(dev) for a in (x, p, q))
+    grid = pkg.tf_grouping.BallGrid(xt, 0.2)
+    idx = torch.empty((1, 10, 8), dtype=torch.int32, device=dev)
+    cnt = torch.empty((1, 10), dtype=torch.int32, device=dev)
+    out = torch.empty((1, 10, 8, 7), device=dev)
+    st = torch.cuda.current_stream().cuda_stream
+    lib = L.lib()
+    args = lambda C, flags, pts: (grid.buf.data_ptr(), xt.data_ptr(), pts, C, flags,  # noqa: E731
+                                  qt.data_ptr(), 1, 100, 10, 0.2, 8, idx.data_ptr(),
+                                  cnt.data_ptr(), out.data_ptr(), st)
+    assert lib.pn2_ball_group_grid(*args(4, 0, pt.data_ptr())) == L.PN2_EINVAL
+    assert lib.pn2_ball_group_grid(*args(-1, L.PN2_USE_XYZ, pt.data_ptr())) == L.PN2_EINVAL
+    assert lib.pn2_ball_group_grid(*args(4, L.PN2_USE_XYZ, None)) == L.PN2_EINVAL
+    assert lib.pn2_ball_group_grid(*args(4, L.PN2_USE_XYZ, pt.data_ptr())) == 0
