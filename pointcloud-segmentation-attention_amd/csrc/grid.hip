@@ -197,7 +197,7 @@ struct BqRadii {
 // NR radii: the cells of the largest (`radius`) are walked once, every candidate's distance is
 // tested against each radius' threshold into that radius' bitmask, and each radius' rows are
 // written from its own bitmask -- the same outputs as NR single-radius launches.
-template <int BLOCK, bool GROUP, int NR>
+template <int BLOCK, bool GROUP, int NR, bool FEAT = false>
 __global__ __launch_bounds__(BLOCK) void ball_query_grid_kernel(
     const char* __restrict__ grid, const float* __restrict__ xyz2, int N, int M, float radius,
     int qpb, int words, int gx, int nblk, const BqRadii rd, const float* __restrict__ xyz1) {
@@ -214,6 +214,7 @@ __global__ __launch_bounds__(BLOCK) void ball_query_grid_kernel(
   const int* __restrict__ off = g.off;
   const float4* __restrict__ pts = g.pts;
   uint32_t* mine = bits + (size_t)w * NR * words;  // radius r: mine + r * words
+  // FEAT: each wave's hit lists (NR x nsmax) after the bitmasks
   int* hl = reinterpret_cast<int*>(bits + (size_t)NW * NR * words) + (size_t)w * NR * rd.nsmax;
   const int wpl = (words + kWave - 1) / kWave;  // bitmask words per lane, in lane order
 
@@ -297,47 +298,79 @@ __global__ __launch_bounds__(BLOCK) void ball_query_grid_kernel(
       const int ns = rd.ns[r];
       const int cnt = min(total, ns);
       int32_t* __restrict__ row = rd.idx[r] + ((size_t)b * M + q) * ns;
-      int* lst = hl + r * rd.nsmax;
-      int rank = incl - pop;
-      for (int j = 0; j < wpl && rank < ns; ++j) {
-        const int wi = lane * wpl + j;
-        uint32_t v = wi < words ? mr[wi] : 0u;
-        while (v && rank < ns) {
-          lst[rank++] = 32 * wi + __builtin_ctz(v);
-          v &= v - 1u;
-        }
-      }
-      const uint64_t has = __ballot(pop > 0);
-      const int first = has ? __shfl(myfirst, __ffsll((unsigned long long)has) - 1, kWave) : 0;
-      for (int p = cnt + lane; p < ns; p += kWave) lst[p] = first;  // :26-29 (0 when no hit)
-      // (one wave's DS operations execute in order: the reads below see every lane's writes)
-      for (int p = lane; p < ns; p += kWave) row[p] = lst[p];
-      if constexpr (GROUP) {
-        const int Cout = rd.cout, C = rd.C;
-        const float* __restrict__ X1 = xyz1 + (size_t)b * N * 3;
-        const float* __restrict__ F = C ? rd.points + (size_t)b * N * C : nullptr;
-        float* __restrict__ out = rd.gout[r] + ((size_t)b * M + q) * ns * Cout;
-        const int E = ns * Cout;
-        // four elements' gathers in flight per lane before any is stored
-        for (int e0 = lane; e0 < E; e0 += 4 * kWave) {
-          float v[4], sub[4];
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const int e = min(e0 + u * kWave, E - 1);
-            const int rr = (int)fdiv((uint32_t)e, rd.div_cout);
-            const int c = e - rr * Cout;
-            const int k = lst[rr];
-            const int cx = c - rd.xoff;
-            const bool isx = cx >= 0 && cx < 3;
-            const float* src = isx ? X1 + 3 * k + cx : F + (size_t)k * C + (c - rd.foff);
-            v[u] = *src;
-            // a feature column subtracts +0.0f: x - 0 == x, bit for bit (-0.0 included)
-            sub[u] = !isx ? 0.0f : cx == 0 ? qx : cx == 1 ? qy : qz;
+      if constexpr (!FEAT) {
+        // no features: each lane writes the rows of the hits it ranks (measured faster than
+        // the hit list for 3-float rows: 22.1 vs 23.8 us at cfg2's SA1, profiles/r5/grp)
+        float* __restrict__ grow = GROUP ? rd.gout[r] + ((size_t)b * M + q) * ns * 3 : nullptr;
+        const float* __restrict__ X1 = GROUP ? xyz1 + (size_t)b * N * 3 : nullptr;
+        int rank = incl - pop;
+        for (int j = 0; j < wpl && rank < ns; ++j) {
+          const int wi = lane * wpl + j;
+          uint32_t v = wi < words ? mr[wi] : 0u;
+          while (v && rank < ns) {
+            const int k = 32 * wi + __builtin_ctz(v);
+            if constexpr (GROUP) {
+              grow[3 * rank + 0] = X1[3 * k + 0] - qx;  // pointnet_util.py:40
+              grow[3 * rank + 1] = X1[3 * k + 1] - qy;
+              grow[3 * rank + 2] = X1[3 * k + 2] - qz;
+            }
+            row[rank++] = k;
+            v &= v - 1u;
           }
+        }
+        const uint64_t has = __ballot(pop > 0);
+        const int first = has ? __shfl(myfirst, __ffsll((unsigned long long)has) - 1, kWave) : 0;
+        for (int p = cnt + lane; p < ns; p += kWave) {
+          row[p] = first;  // :26-29 (0 when no hit)
+          if constexpr (GROUP) {
+            grow[3 * p + 0] = X1[3 * first + 0] - qx;
+            grow[3 * p + 1] = X1[3 * first + 1] - qy;
+            grow[3 * p + 2] = X1[3 * first + 2] - qz;
+          }
+        }
+      } else {
+        int* lst = hl + r * rd.nsmax;
+        int rank = incl - pop;
+        for (int j = 0; j < wpl && rank < ns; ++j) {
+          const int wi = lane * wpl + j;
+          uint32_t v = wi < words ? mr[wi] : 0u;
+          while (v && rank < ns) {
+            lst[rank++] = 32 * wi + __builtin_ctz(v);
+            v &= v - 1u;
+          }
+        }
+        const uint64_t has = __ballot(pop > 0);
+        const int first = has ? __shfl(myfirst, __ffsll((unsigned long long)has) - 1, kWave) : 0;
+        for (int p = cnt + lane; p < ns; p += kWave) lst[p] = first;  // :26-29 (0 when no hit)
+        // (one wave's DS operations execute in order: the reads below see every lane's writes)
+        for (int p = lane; p < ns; p += kWave) row[p] = lst[p];
+        {
+          const int Cout = rd.cout, C = rd.C;
+          const float* __restrict__ X1 = xyz1 + (size_t)b * N * 3;
+          const float* __restrict__ F = C ? rd.points + (size_t)b * N * C : nullptr;
+          float* __restrict__ out = rd.gout[r] + ((size_t)b * M + q) * ns * Cout;
+          const int E = ns * Cout;
+          // four elements' gathers in flight per lane before any is stored
+          for (int e0 = lane; e0 < E; e0 += 4 * kWave) {
+            float v[4], sub[4];
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const int e = e0 + u * kWave;
-            if (e < E) out[e] = v[u] - sub[u];  // pointnet_util.py:40
+            for (int u = 0; u < 4; ++u) {
+              const int e = min(e0 + u * kWave, E - 1);
+              const int rr = (int)fdiv((uint32_t)e, rd.div_cout);
+              const int c = e - rr * Cout;
+              const int k = lst[rr];
+              const int cx = c - rd.xoff;
+              const bool isx = cx >= 0 && cx < 3;
+              const float* src = isx ? X1 + 3 * k + cx : F + (size_t)k * C + (c - rd.foff);
+              v[u] = *src;
+              // a feature column subtracts +0.0f: x - 0 == x, bit for bit (-0.0 included)
+              sub[u] = !isx ? 0.0f : cx == 0 ? qx : cx == 1 ? qy : qz;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              const int e = e0 + u * kWave;
+              if (e < E) out[e] = v[u] - sub[u];  // pointnet_util.py:40
+            }
           }
         }
       }
@@ -424,7 +457,7 @@ int ball_query_grid(const void* grid, const float* xyz2, int B, int N, int M, in
   long long qpb = (queries + 2047) / 2048;
   qpb = ((qpb + NW - 1) / NW) * NW;
   const unsigned gx = (unsigned)((M + qpb - 1) / qpb);
-  const size_t lds = (size_t)NW * nr * ((words > 0 ? words : 1) + nsmax) * 4;
+  const size_t lds = (size_t)NW * nr * ((words > 0 ? words : 1) + (C > 0 ? nsmax : 0)) * 4;
   if (lds > 64 * 1024) return PN2_EINVAL;  // (dynamic LDS; nr = 1 fits up to N ~ 130000)
   const long long nblk = (long long)gx * B;
   if (nblk > INT32_MAX - pn2::kXcds) return PN2_EINVAL;
@@ -434,7 +467,11 @@ int ball_query_grid(const void* grid, const float* xyz2, int B, int N, int M, in
   hipLaunchKernelGGL((pn2::ball_query_grid_kernel<BLOCK, GROUP, NR>), grd, blk, lds, stream, g, \
                      xyz2, N, M, rmax, (int)qpb, words, (int)gx, (int)nblk, rd,               \
                      GROUP ? xyz1 : nullptr)
-  if (group) {
+  if (C > 0) {  // features: the hit-list output phase (one radius per launch)
+    if (nr != 1) return PN2_EINVAL;
+    hipLaunchKernelGGL((pn2::ball_query_grid_kernel<BLOCK, true, 1, true>), grd, blk, lds, stream,
+                       g, xyz2, N, M, rmax, (int)qpb, words, (int)gx, (int)nblk, rd, xyz1);
+  } else if (group) {
     if (nr == 1) PN2_BQG(true, 1);
     else if (nr == 2) PN2_BQG(true, 2);
     else PN2_BQG(true, 3);
