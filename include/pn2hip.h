@@ -356,6 +356,19 @@ int pn2_fp_grid_fused(const float* xyz1, const float* xyz2, const void* unknown_
  * out[4h:4h+4] = aᵀ V_h. C must be a multiple of 4. */
 int pn2_attn_reduce(const float* Q, const float* K, const float* V, int B, int M, int ns,
                     int C, float* out, pn2_stream_t stream);
+/* Several attention reductions of one nsample in ONE launch (the SSG stack's four SA layers,
+ * attention_layer.py:35-42 per layer): per layer exactly pn2_attn_reduce(Q, K, V, B, M, ns,
+ * C, out). nsample in {8, 16, 32, 64, 128}, the same for every layer, else PN2_EINVAL. */
+#define PN2_ATTN_MAX_LAYERS 4
+typedef struct pn2_attn_layer {
+  const float* Q;
+  const float* K;
+  const float* V;
+  int M, ns, C;
+  float* out;
+} pn2_attn_layer;
+int pn2_attn_reduce_layers(const pn2_attn_layer* layers, int nlayers, int B,
+                           pn2_stream_t stream);
 /* Backward of pn2_attn_reduce (TF autodiff of attention_layer.py:35-42): grad_Q (B,M,C),
  * grad_K / grad_V (B,M,ns,C) from grad_out (B,M,C). Every element written (no accumulation);
  * 16-byte aligned buffers, C % 4 == 0. */

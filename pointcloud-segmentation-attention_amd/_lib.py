@@ -68,6 +68,16 @@ class FpLayer(ctypes.Structure):
 
 PN2_FP_MAX_LAYERS = 4
 
+
+class AttnLayer(ctypes.Structure):
+    """struct pn2_attn_layer (include/pn2hip.h)."""
+    _fields_ = [("Q", ctypes.c_void_p), ("K", ctypes.c_void_p), ("V", ctypes.c_void_p),
+                ("M", ctypes.c_int), ("ns", ctypes.c_int), ("C", ctypes.c_int),
+                ("out", ctypes.c_void_p)]
+
+
+PN2_ATTN_MAX_LAYERS = 4
+
 # name -> (restype, argtypes); mirrors include/pn2hip.h and include/pn2plan.h (tests/test_capi.py checks the header)
 SIGNATURES = {
     "pn2_version": (ctypes.c_char_p, []),
@@ -114,6 +124,7 @@ SIGNATURES = {
     "pn2_fp_fused_layers": (_I, [_P, _I, _I, _P]),
     "pn2_fp_fused": (_I, [_P, _P, _P, _I, _P, _I, _I, _I, _I, _P, _P]),
     "pn2_attn_reduce": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P]),
+    "pn2_attn_reduce_layers": (_I, [_P, _I, _I, _P]),
     "pn2_attn_reduce_grad": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P]),
     "pn2_group_pool": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _P]),
     "pn2_mlp_packed_size": (_S, [_I, _I]),

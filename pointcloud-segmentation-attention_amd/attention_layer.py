@@ -6,10 +6,13 @@ AttentionLayer mirrors the reference layer (:10-45): its Dense query/key/value p
 reduction is the kernel. The reference instantiates it with key_dim = output_dim = 4 and
 num_heads = C/4 (:256-258, :313-315); that is the configuration the kernel implements.
 """
+import ctypes
+
 import torch
 
 from . import pointnet_util, tf_grouping, tf_sampling, tf_util
-from ._lib import InvalidArgumentError, check, device_tensor, lib, ptr, stream_of
+from ._lib import (PN2_ATTN_MAX_LAYERS, AttnLayer, InvalidArgumentError, check, device_tensor,
+                   lib, ptr, stream_of)
 from ._torch_ops import call
 
 
@@ -31,6 +34,37 @@ def attention_reduce(Q, K, V):
     return call("attn_reduce", device_tensor(Q, "Q", torch.float32),
                              device_tensor(K, "K", torch.float32),
                              device_tensor(V, "V", torch.float32))
+
+
+def attention_reduce_layers(qkvs):
+    """attention_reduce of several layers that share nsample (the SSG stack's four SA layers)
+    in ONE launch (pn2_attn_reduce_layers): qkvs = [(Q, K, V)], returns [out] per layer,
+    each exactly attention_reduce(Q, K, V). Inference only (no autograd)."""
+    if not 1 <= len(qkvs) <= PN2_ATTN_MAX_LAYERS:
+        raise InvalidArgumentError(f"attention_reduce_layers: 1..{PN2_ATTN_MAX_LAYERS} layers")
+    arr = (AttnLayer * len(qkvs))()
+    outs, keep, B, ns = [], [], None, None
+    for i, (Q, K, V) in enumerate(qkvs):
+        if Q.dim() == 4 and Q.shape[2] == 1:
+            Q = Q.squeeze(2)
+        Q = device_tensor(Q, "Q", torch.float32)
+        K = device_tensor(K, "K", torch.float32)
+        V = device_tensor(V, "V", torch.float32)
+        if Q.dim() != 3 or K.dim() != 4 or tuple(V.shape) != tuple(K.shape):
+            raise InvalidArgumentError("attention_reduce_layers expects Q (B,M,C), K and V "
+                                       "(B,M,ns,C)")
+        b, M, n, C = (int(s) for s in K.shape)
+        if tuple(Q.shape) != (b, M, C) or C % 4 != 0 or (B is not None and (b, n) != (B, ns)):
+            raise InvalidArgumentError("attention_reduce_layers: Q (B,M,C), C % 4 == 0, one B "
+                                       "and one nsample for all layers")
+        B, ns = b, n
+        out = torch.empty((B, M, C), dtype=torch.float32, device=Q.device)
+        arr[i] = AttnLayer(Q.data_ptr(), K.data_ptr(), V.data_ptr(), M, n, C, out.data_ptr())
+        outs.append(out)
+        keep += [Q, K, V]
+    check(lib().pn2_attn_reduce_layers(ctypes.addressof(arr), len(qkvs), B,
+                                       stream_of(outs[0])), "attention_reduce_layers")
+    return outs
 
 
 def attention_reduce_grad(Q, K, V, grad_out):

@@ -71,14 +71,23 @@ struct AttnLayer {
 
 // NS = nsample (power of two). LPH lanes per head, KPL pseudo-keys per lane, HPW heads per
 // wave task; a wave keeps TIF tasks in flight (their K / V loads issued before any reduction).
+// Several layers of the same nsample in one launch (the SSG stack's four attention
+// reductions): one task space, layer li's tasks at [first[li], first[li + 1]).
+constexpr int kAttnMaxLayers = PN2_ATTN_MAX_LAYERS;
+struct AttnLayers {
+  AttnLayer l[kAttnMaxLayers];
+  long long first[kAttnMaxLayers + 1];
+  int nlayers;
+};
+
 template <int NS, int TIF>
-__global__ __launch_bounds__(kBlock) void attn_reduce_kernel(AttnLayer L) {
+__global__ __launch_bounds__(kBlock) void attn_reduce_kernel(AttnLayers A) {
   constexpr int LPH = NS < kWave ? NS : kWave;
   constexpr int KPL = NS / LPH;
   constexpr int HPW = kWave / LPH;  // heads per wave step
   const int lane = lane_id();
   const int hl = lane / LPH, sl = lane % LPH;
-  const long long tasks = (long long)L.G * L.steps;
+  const long long tasks = A.first[A.nlayers];
   const long long nwaves = (long long)gridDim.x * kWavesPerBlock;
   for (long long t0 = (long long)blockIdx.x * kWavesPerBlock + threadIdx.x / kWave; t0 < tasks;
        t0 += nwaves * TIF) {
@@ -90,7 +99,10 @@ __global__ __launch_bounds__(kBlock) void attn_reduce_kernel(AttnLayer L) {
       long long task = t0 + i * nwaves;
       ok[i] = task < tasks;
       task = ok[i] ? task : t0;
-      const uint32_t lt = (uint32_t)task;
+      int li = 0;  // (wave-uniform)
+      while (li + 1 < A.nlayers && task >= A.first[li + 1]) ++li;
+      const AttnLayer& L = A.l[li];
+      const uint32_t lt = (uint32_t)(task - A.first[li]);
       const uint32_t g = fdiv(lt, L.div_steps);
       const int step = (int)(lt - g * (uint32_t)L.steps);
       const int H = L.C / 4;
@@ -293,19 +305,26 @@ unsigned grid_for(long long waves) {
   return (unsigned)(blocks > 0 ? blocks : 1);
 }
 
+// every layer of A shares nsample NS; fills each layer's task stepping and A.first
 template <int NS>
-void launch_attn(AttnLayer& L, hipStream_t s) {
+void launch_attn(AttnLayers& A, hipStream_t s) {
   constexpr int LPH = NS < kWave ? NS : kWave;
   constexpr int HPW = kWave / LPH;
-  L.steps = (L.C / 4 + HPW - 1) / HPW;
-  L.div_steps = make_fastdiv((uint32_t)L.steps);
+  long long tasks = 0;
+  for (int i = 0; i < A.nlayers; ++i) {
+    AttnLayer& L = A.l[i];
+    L.steps = (L.C / 4 + HPW - 1) / HPW;
+    L.div_steps = make_fastdiv((uint32_t)L.steps);
+    A.first[i] = tasks;
+    tasks += (long long)L.G * L.steps;
+  }
+  A.first[A.nlayers] = tasks;
   constexpr int TIF = 2;
-  const long long tasks = (long long)L.G * L.steps;
   hipLaunchKernelGGL((attn_reduce_kernel<NS, TIF>), dim3(grid_for((tasks + TIF - 1) / TIF)),
-                     dim3(kBlock), 0, s, L);
+                     dim3(kBlock), 0, s, A);
 }
 
-int attn_launch(AttnLayer& a, int ns, hipStream_t s) {
+int attn_launch(AttnLayers& a, int ns, hipStream_t s) {
   if (ns == 8) launch_attn<8>(a, s);
   else if (ns == 16) launch_attn<16>(a, s);
   else if (ns == 32) launch_attn<32>(a, s);
@@ -313,6 +332,12 @@ int attn_launch(AttnLayer& a, int ns, hipStream_t s) {
   else if (ns == 128) launch_attn<128>(a, s);
   else return PN2_EINVAL;
   return PN2_OK;
+}
+
+// a layer's FastDiv task arithmetic stays exact (worst case HPW = 1)
+bool attn_small_tasks(long long G, int C) {
+  const long long steps_max = (long long)C / 4;
+  return G * steps_max * steps_max < (1LL << 32);
 }
 
 }  // namespace
@@ -328,13 +353,38 @@ int pn2_attn_reduce(const float* Q, const float* K, const float* V, int B, int M
   if (!Q || !K || !V || !out || G > INT32_MAX) return PN2_EINVAL;
   if ((((uintptr_t)Q | (uintptr_t)K | (uintptr_t)V | (uintptr_t)out) & 15) != 0) return PN2_EINVAL;
   hipStream_t s = (hipStream_t)stream;
-  const long long steps_max = (long long)C / 4;  // worst case HPW = 1
-  const bool small_tasks = G * steps_max * steps_max < (1LL << 32);  // FastDiv exactness
-  pn2::AttnLayer a{Q, K, V, out, (int)G, C, 0, {}};
-  if (!small_tasks || pn2::attn_launch(a, ns, s) != PN2_OK)
+  pn2::AttnLayers a{};
+  a.l[0] = pn2::AttnLayer{Q, K, V, out, (int)G, C, 0, {}};
+  a.nlayers = 1;
+  if (!pn2::attn_small_tasks(G, C) || pn2::attn_launch(a, ns, s) != PN2_OK)
     hipLaunchKernelGGL(pn2::attn_reduce_generic_kernel,
                        dim3(pn2::grid_for(G * (C / 4))), dim3(pn2::kBlock), 0, s, Q, K, V,
                        (int)G, ns, C, out);
+  PN2_RETURN_LAUNCH();
+}
+
+int pn2_attn_reduce_layers(const pn2_attn_layer* layers, int nlayers, int B,
+                           pn2_stream_t stream) {
+  if (!layers || nlayers < 1 || nlayers > PN2_ATTN_MAX_LAYERS || B < 0) return PN2_EINVAL;
+  hipStream_t s = (hipStream_t)stream;
+  pn2::AttnLayers a{};
+  int ns = 0;
+  for (int i = 0; i < nlayers; ++i) {
+    const pn2_attn_layer& l = layers[i];
+    if (l.M < 0 || l.ns <= 0 || l.C < 0 || (l.C % 4) != 0) return PN2_EINVAL;
+    if (ns && l.ns != ns) return PN2_EINVAL;  // one nsample per launch
+    ns = l.ns;
+    const long long G = (long long)B * l.M;
+    if (G == 0 || l.C == 0) continue;
+    if (!l.Q || !l.K || !l.V || !l.out || G > INT32_MAX) return PN2_EINVAL;
+    if ((((uintptr_t)l.Q | (uintptr_t)l.K | (uintptr_t)l.V | (uintptr_t)l.out) & 15) != 0)
+      return PN2_EINVAL;
+    if (!pn2::attn_small_tasks(G, l.C)) return PN2_EINVAL;
+    a.l[a.nlayers++] = pn2::AttnLayer{l.Q, l.K, l.V, l.out, (int)G, l.C, 0, {}};
+  }
+  if (a.nlayers == 0) return PN2_OK;
+  const int rc = pn2::attn_launch(a, ns, s);
+  if (rc != PN2_OK) return rc;  // (an nsample the layers kernel has no instance for)
   PN2_RETURN_LAUNCH();
 }
 

@@ -123,12 +123,14 @@ __global__ __launch_bounds__(kBuildBlock) void grid_build_kernel(const float* __
     const int iz = cell_coord(z, h.oz, h.inv, h.nz);
     return (iz * h.ny + iy) * h.nx + ix;
   };
-  int rc[R];
+  // (with the points in registers the count's atomic returns each point's rank in its cell,
+  // kept beside its cell: the scatter then needs no second atomic pass)
+  int rc[R], rk[R];
   if constexpr (PPT > 0) {
 #pragma unroll
     for (int i = 0; i < PPT; ++i) {
       rc[i] = cell_at(rx[i], ry[i], rz[i]);
-      if (t + i * kBuildBlock < N) atomicAdd(&cnt[rc[i]], 1u);
+      rk[i] = t + i * kBuildBlock < N ? (int)atomicAdd(&cnt[rc[i]], 1u) : 0;
     }
   } else {
     for (int k = t; k < N; k += kBuildBlock)
@@ -160,10 +162,7 @@ __global__ __launch_bounds__(kBuildBlock) void grid_build_kernel(const float* __
 #pragma unroll
     for (int i = 0; i < PPT; ++i) {
       const int k = t + i * kBuildBlock;
-      if (k < N) {
-        const int pos = (int)atomicAdd(&cnt[rc[i]], 1u);
-        pts[pos] = make_float4(rx[i], ry[i], rz[i], __int_as_float(k));
-      }
+      if (k < N) pts[(int)cnt[rc[i]] + rk[i]] = make_float4(rx[i], ry[i], rz[i], __int_as_float(k));
     }
   } else {
     for (int k = t; k < N; k += kBuildBlock) {

@@ -83,10 +83,10 @@ PN2_DEV void best3_merge_xor(Best3& b, int mask) {
 // points of one cloud. Every thread of the block must call it (tiles are staged with
 // barriers). On return every lane of the quad holds the quad's result.
 PN2_DEV void scan_known(const float* __restrict__ K, int m, float x1, float y1, float z1,
-                        float4* sk, Best3& best) {
+                        float4* sk, Best3& best, int tile = kNNTile) {
   const int q = threadIdx.x & (kNNGroup - 1);
-  for (int t0 = 0; t0 < m; t0 += kNNTile) {
-    const int cnt = min(kNNTile, m - t0);
+  for (int t0 = 0; t0 < m; t0 += tile) {
+    const int cnt = min(tile, m - t0);
     __syncthreads();  // previous tile fully consumed
     for (int e = threadIdx.x; e < cnt; e += kNNBlock) {
       const float* p = K + 3 * (size_t)(t0 + e);
@@ -175,6 +175,9 @@ PN2_DEV bool box_certifies(const GridHdr& h, float px, float py, float pz, int x
 }
 
 constexpr int kNNFirst = 1;  // the walk's first pass: the cube of shells 0..kNNFirst
+#ifndef PN2_NN_PF
+#define PN2_NN_PF 0
+#endif
 
 // The three nearest known points of (px, py, pz) over a grid's sorted points (pts, off: in
 // LDS or global memory), lexicographic in (d, k): cubic shells of cells around the point's
@@ -210,6 +213,37 @@ PN2_DEV Best3 grid_nn3(const GridHdr& h, const float4* __restrict__ pts,
         best3_insert_lex(best, sqdist(p.x, p.y, p.z, px, py, pz), __float_as_int(p.w));
       }
     };
+#if PN2_NN_PF
+    if (block) {
+      // the cube, one z slab (<= 3 rows) at a time: the slab's row offsets, then every row's
+      // first point of this lane, are loaded together -- two dependent LDS round trips per
+      // slab instead of two per row and one per point; a row's further points follow
+      const int ylo = max(yl, 0), yhi = min(yh, h.ny - 1);
+      for (int z = max(zl, 0); z <= min(zh, h.nz - 1); ++z) {
+        int lo[3], hi[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          const int y = ylo + i;
+          const int row = (z * h.ny + min(y, yhi)) * h.nx;
+          lo[i] = off[row + x0];
+          hi[i] = y <= yhi ? (int)off[row + x1 + 1] : lo[i];
+        }
+        float4 p[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          const int e = lo[i] + q;
+          p[i] = pts[e < hi[i] ? e : 0];
+        }
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+          if (lo[i] + q < hi[i])
+            best3_insert_lex(best, sqdist(p[i].x, p[i].y, p[i].z, px, py, pz),
+                             __float_as_int(p[i].w));
+#pragma unroll
+        for (int i = 0; i < 3; ++i) visit(lo[i] + G, hi[i]);
+      }
+    } else
+#endif
     for (int z = max(zl, 0); z <= min(zh, h.nz - 1); ++z) {
       for (int y = max(yl, 0); y <= min(yh, h.ny - 1); ++y) {
         const int row = (z * h.ny + y) * h.nx;
@@ -499,9 +533,10 @@ PN2_DEV void fp_write_rows(const FpLayer& p, int b, int zb, int j0, RowFn row) {
   }
 }
 
+// sk: the known-point tile (dynamic LDS of `tile` float4, sized by the launch to its largest m
+// up to kNNTile: a 32 KB static tile held FP1-3's workgroups to 4 per CU for m <= 256)
 template <int V2, int V1, bool PRE, int UN>
-PN2_DEV void fp_fused_body(const FpLayer& p, int Lg) {
-  __shared__ float4 sk[PRE ? 1 : kNNTile];
+PN2_DEV void fp_fused_body(const FpLayer& p, int Lg, float4* sk, int tile) {
   __shared__ int4 s_idx[kNNRows];
   __shared__ float4 s_w[kNNRows];
   __shared__ int s_row[PRE ? kNNRows : 1];
@@ -534,7 +569,7 @@ PN2_DEV void fp_fused_body(const FpLayer& p, int Lg) {
     const float* U = xyz1 + ((size_t)b * n + (valid ? j : 0)) * 3;
     Best3 best;
     best3_init(best);
-    scan_known(xyz2 + (size_t)b * m * 3, m, U[0], U[1], U[2], sk, best);
+    scan_known(xyz2 + (size_t)b * m * 3, m, U[0], U[1], U[2], sk, best, tile);
     if ((threadIdx.x & (kNNGroup - 1)) == 0) {
       float w1, w2, w3;
       idw(best.d1, best.d2, best.d3, w1, w2, w3);
@@ -556,11 +591,12 @@ PN2_DEV void fp_fused_body(const FpLayer& p, int Lg) {
 // order, so their neighbours' feature rows are shared through the caches. Logical blocks are
 // XCD-aware: the blocks of a cloud share one L2, which then holds its points2 rows once.
 template <int V2, int V1, bool PRE, int UN>
-__global__ __launch_bounds__(kNNBlock) void fp_fused_kernel(FpLayer p) {
+__global__ __launch_bounds__(kNNBlock) void fp_fused_kernel(FpLayer p, int tile) {
+  extern __shared__ float4 sk[];
   const int total = (p.n + kNNRows - 1) / kNNRows * p.B * p.Z;
   const int Lg = xcd_block(blockIdx.x, total);
   if (Lg >= total) return;
-  fp_fused_body<V2, V1, PRE, UN>(p, Lg);
+  fp_fused_body<V2, V1, PRE, UN>(p, Lg, sk, tile);
 }
 
 // pointnet_fp_module geometry over a grid of the KNOWN points that every workgroup builds in
@@ -605,8 +641,12 @@ inline size_t fp_grid_lds(int m) {
 // KPT: known points per thread (m <= KPT * kNNBlock), kept in registers between the count
 // and the scatter. LDS at FP4 (m = 1024, B = 16): 16 KB points + 2 KB offsets + 1.75 KB, so
 // 8 workgroups fit a CU (the LDS bound; their 32 waves are the wave bound).
+#ifndef PN2_FPG_WPE
+#define PN2_FPG_WPE 1
+#endif
 template <int V2, int V1, int UN, int KPT>
-__global__ __launch_bounds__(kNNBlock) void fp_grid_fused_kernel(FpLayer p, float* __restrict__ dist,
+__global__ __launch_bounds__(kNNBlock) __attribute__((amdgpu_waves_per_eu(PN2_FPG_WPE)))
+void fp_grid_fused_kernel(FpLayer p, float* __restrict__ dist,
                                                               int32_t* __restrict__ idx) {
   constexpr int NW = kNNBlock / kWave;
   extern __shared__ float4 s_pts[];  // m known points sorted by cell, then ncell + 1 offsets
@@ -769,7 +809,8 @@ struct FpLayers {
   int nlayers, B;
 };
 template <int V2, int V1, bool PRE, int UN>
-__global__ __launch_bounds__(kNNBlock) void fp_fused_layers_kernel(FpLayers a) {
+__global__ __launch_bounds__(kNNBlock) void fp_fused_layers_kernel(FpLayers a, int tile) {
+  extern __shared__ float4 sk[];
   // cloud-major: cloud b's blocks of every layer are contiguous (each XCD gets whole clouds
   // and the same mix of layers); first[] = each layer's first block within a cloud
   const int per_cloud_all = a.first[a.nlayers];
@@ -781,7 +822,7 @@ __global__ __launch_bounds__(kNNBlock) void fp_fused_layers_kernel(FpLayers a) {
   int li = 0;
   while (li + 1 < a.nlayers && lc >= a.first[li + 1]) ++li;
   const int per_cloud = a.first[li + 1] - a.first[li];
-  fp_fused_body<V2, V1, PRE, UN>(a.l[li], b * per_cloud + (lc - a.first[li]));
+  fp_fused_body<V2, V1, PRE, UN>(a.l[li], b * per_cloud + (lc - a.first[li]), sk, tile);
 }
 
 // Largest batch chunk whose 32-bit row arithmetic stays exact (rows*n < 2^32, see FastDiv).
@@ -841,16 +882,19 @@ int fp_plan(const float* xyz1, const float* xyz2, const float* pdist, const int3
 // fp_fused_layers_kernel (arg FpLayers); two elements' loads in flight per thread
 // (tools/bench_fp.py: 1 and 4 measured slower)
 constexpr int kFpUnroll = 2;
-#define PN2_FP_DISPATCH(KERNEL, f, arg, blocks, stream)                                        \
+// MAXM: the largest m of the launch; the search variant stages the known points in an LDS
+// tile of min(MAXM, kNNTile) float4
+#define PN2_FP_DISPATCH(KERNEL, f, arg, blocks, MAXM, stream)                                  \
   do {                                                                                         \
     const dim3 grid__(xcd_grid(blocks));                                                       \
-    if ((f).v1) { PN2_FP_PRE(KERNEL, 4, 4, f, arg, grid__, stream); }                          \
-    else if ((f).v2) { PN2_FP_PRE(KERNEL, 4, 1, f, arg, grid__, stream); }                     \
-    else { PN2_FP_PRE(KERNEL, 1, 1, f, arg, grid__, stream); }                                 \
+    const int tile__ = std::max(1, std::min((int)(MAXM), kNNTile));                            \
+    if ((f).v1) { PN2_FP_PRE(KERNEL, 4, 4, f, arg, grid__, tile__, stream); }                  \
+    else if ((f).v2) { PN2_FP_PRE(KERNEL, 4, 1, f, arg, grid__, tile__, stream); }             \
+    else { PN2_FP_PRE(KERNEL, 1, 1, f, arg, grid__, tile__, stream); }                         \
   } while (0)
-#define PN2_FP_PRE(KERNEL, V2, V1, f, arg, grid, stream)                                       \
-  if ((f).pre) hipLaunchKernelGGL((KERNEL<V2, V1, true, kFpUnroll>), grid, dim3(kNNBlock), 0, stream, arg); \
-  else hipLaunchKernelGGL((KERNEL<V2, V1, false, kFpUnroll>), grid, dim3(kNNBlock), 0, stream, arg)
+#define PN2_FP_PRE(KERNEL, V2, V1, f, arg, grid, tile, stream)                                 \
+  if ((f).pre) hipLaunchKernelGGL((KERNEL<V2, V1, true, kFpUnroll>), grid, dim3(kNNBlock), 0, stream, arg, tile); \
+  else hipLaunchKernelGGL((KERNEL<V2, V1, false, kFpUnroll>), grid, dim3(kNNBlock), (size_t)(tile) * sizeof(float4), stream, arg, tile)
 
 int fp_launch(const float* xyz1, const float* xyz2, const float* pdist, const int32_t* pidx,
               const void* ugrid, const float* points1, int C1, const float* points2, int C2,
@@ -858,7 +902,7 @@ int fp_launch(const float* xyz1, const float* xyz2, const float* pdist, const in
   FpPlan f;
   const int rc = fp_plan(xyz1, xyz2, pdist, pidx, ugrid, points1, C1, points2, C2, B, n, m, out, f);
   if (rc != PN2_OK) return rc;
-  PN2_FP_DISPATCH(fp_fused_kernel, f, f.p, f.blocks, stream);
+  PN2_FP_DISPATCH(fp_fused_kernel, f, f.p, f.blocks, m, stream);
   PN2_RETURN_LAUNCH();
 }
 
@@ -895,7 +939,7 @@ int fp_layers_launch(const pn2_fp_layer* layers, int nlayers, int B, hipStream_t
   FpLayers a{};
   FpPlan f0{};
   long long blocks = 0;
-  int nl = 0;
+  int nl = 0, maxm = 0;
   for (int i = 0; i < nlayers; ++i) {
     const pn2_fp_layer& s = layers[i];
     if (s.n < 0 || s.m < 0 || s.C1 < 0 || s.C2 < 0) return PN2_EINVAL;
@@ -910,12 +954,13 @@ int fp_layers_launch(const pn2_fp_layer* layers, int nlayers, int B, hipStream_t
     if (nl == 0) f0 = f;
     if (f.v2 != f0.v2 || f.v1 != f0.v1) {
       // another kernel variant: this layer runs as its own launch
-      PN2_FP_DISPATCH(fp_fused_kernel, f, f.p, f.blocks, stream);
+      PN2_FP_DISPATCH(fp_fused_kernel, f, f.p, f.blocks, s.m, stream);
       const hipError_t e = hipGetLastError();
       if (e != hipSuccess) return (int)e;
       continue;
     }
     a.l[nl] = f.p;
+    maxm = std::max(maxm, s.m);
     a.first[nl] = (int)blocks;
     blocks += f.blocks / B;  // per cloud
     ++nl;
@@ -924,7 +969,7 @@ int fp_layers_launch(const pn2_fp_layer* layers, int nlayers, int B, hipStream_t
   a.first[nl] = (int)blocks;
   a.nlayers = nl;
   a.B = B;
-  PN2_FP_DISPATCH(fp_fused_layers_kernel, f0, a, blocks * B, stream);
+  PN2_FP_DISPATCH(fp_fused_layers_kernel, f0, a, blocks * B, maxm, stream);
   PN2_RETURN_LAUNCH();
 }
 

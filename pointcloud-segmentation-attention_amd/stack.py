@@ -362,8 +362,12 @@ class Step:
             tasks.append(Task("fp2", lane["fp123"], (sampled[2],), fp(2)))
             tasks.append(Task("fp1", lane["fp123"], (sampled[3],), fp(3)))
         if attn_lane is not None:
-            for i in range(4):
-                tasks.append(Task(f"att{i + 1}", attn_lane, (), att(i)))
+            # the four reductions as ONE launch (pn2_attn_reduce_layers): they read only their
+            # resident inputs and share nsample
+            def att_all():
+                for i, o in enumerate(attention_layer.attention_reduce_layers(inp["attn"])):
+                    v["att"][i] = o
+            tasks.append(Task("att", attn_lane, (), att_all))
         return tasks
 
     def _tasks_ssg_model(self):

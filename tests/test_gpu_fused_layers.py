@@ -238,3 +238,42 @@ def test_ball_group_rejects(env):
     assert lib.pn2_ball_group_grid(*args(-1, L.PN2_USE_XYZ, pt.data_ptr())) == L.PN2_EINVAL
     assert lib.pn2_ball_group_grid(*args(4, L.PN2_USE_XYZ, None)) == L.PN2_EINVAL
     assert lib.pn2_ball_group_grid(*args(4, L.PN2_USE_XYZ, pt.data_ptr())) == 0
+
+
+@pytest.mark.parametrize("shapes", [
+    # the SSG stack's four attention SA layers at cfg3 (ns 32, C = 64 .. 512), B = 2
+    [(1024, 32, 64), (256, 32, 128), (64, 32, 256), (16, 32, 512)],
+    [(100, 8, 4), (7, 8, 12)],          # few heads, odd group counts
+    [(33, 128, 32)],                    # one layer, ns 128
+])
+def test_attention_reduce_layers(env, shapes):
+    """attention_layer.attention_reduce_layers (pn2_attn_reduce_layers: several layers' attention
+    reductions in one launch) == attention_reduce per layer, bit for bit (the same kernel body),
+    and within 1e-5 of the oracle's restatement of attention_layer.py:35-42."""
+    pkg, O, torch, dev = env
+    B = 2
+    qkvs = []
+    for i, (M, ns, C) in enumerate(shapes):
+        g = torch.Generator(device=dev)
+        g.manual_seed(100 + i)
+        qkvs.append((torch.rand((B, M, C), generator=g, device=dev) * 2 - 1,
+                     torch.rand((B, M, ns, C), generator=g, device=dev) * 2 - 1,
+                     torch.rand((B, M, ns, C), generator=g, device=dev) * 2 - 1))
+    outs = pkg.attention_layer.attention_reduce_layers(qkvs)
+    for (Q, K, V), o in zip(qkvs, outs):
+        ref = pkg.attention_layer.attention_reduce(Q, K, V)
+        assert torch.equal(o.view(torch.int32), ref.view(torch.int32))
+        np.testing.assert_allclose(o.cpu().numpy(), O.attn_reduce(Q.cpu().numpy(), K.cpu().numpy(),
+                                                                  V.cpu().numpy()),
+                                   rtol=1e-5, atol=1e-5)
+
+
+def test_attention_reduce_layers_rejects(env):
+    """Layers of different nsample in one launch: PN2_EINVAL, never a silent fallback."""
+    pkg, O, torch, dev = env
+    a = (torch.zeros((1, 4, 8), device=dev), torch.zeros((1, 4, 8, 8), device=dev),
+         torch.zeros((1, 4, 8, 8), device=dev))
+    b = (torch.zeros((1, 4, 8), device=dev), torch.zeros((1, 4, 16, 8), device=dev),
+         torch.zeros((1, 4, 16, 8), device=dev))
+    with pytest.raises(pkg._lib.InvalidArgumentError):
+        pkg.attention_layer.attention_reduce_layers([a, b])

@@ -81,7 +81,7 @@ def main():
     assert torch.equal(o3, o3b)
     res["build known grid"] = timeit(lambda: pkg.grid.PointGrid(k, 0.0))
     res["build cloud grid"] = timeit(lambda: pkg.grid.PointGrid(t1, 0.1))
-    print(json.dumps({k_: round(v, 1) for k_, v in res.items()}, indent=1))
+    print(json.dumps({k_: round(v, 1) for k_, v in res.items()}))
 
 
 if __name__ == "__main__":

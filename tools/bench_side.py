@@ -30,7 +30,8 @@ def task_bytes(S, config, B):
             grp = n_in * (3 + c_in) * 4 + M * 12 + M * ns * 4 + M * 4 + M * ns * (3 + c_in) * 4
             out[f"sa{i + 1}"] = grp
             if attn:
-                out[f"att{i + 1}"] = M * c_out * 4 + 2 * M * ns * c_out * 4 + M * c_out * 4
+                out["att"] = out.get("att", 0) + M * c_out * 4 + 2 * M * ns * c_out * 4 \
+                    + M * c_out * 4
             levels.append(M)
             chans.append(c_out)
             n_in, c_in = M, c_out
