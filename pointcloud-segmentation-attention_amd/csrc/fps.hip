@@ -168,25 +168,18 @@ struct FpsChain {
 };
 
 // one stage (N <= kChainNext) for one cloud: the configuration fps_impl uses for this N
+// (Measured and not kept, profiles/r5/chain: the 1,024-point stage on ONE wave, 16 points a
+// lane and no barrier -- 126.5 -> 129 us for the chain, 140 us with each lane's candidate
+// coordinates read speculatively; a single wave issues the pick's ~110 dependent VALU ops at
+// ~8 cycles each, which costs what the 4-wave form's barrier and cross-wave step cost.)
 PN2_DEV void chain_stage(const float* P, int N, int M, const float* CXYZ, int32_t* I, float* NX,
-                         float* SNEXT, uint2 (*red)[8], float* scratch, int32_t* SI) {
+                         float* SNEXT, uint2 (*red)[8]) {
   const bool w0 = threadIdx.x < kWave;
   if (N <= 64) { if (w0) fps_v9_body<64, 1, 1>(P, N, M, CXYZ, I, NX, SNEXT, red); }
   else if (N <= 128) { if (w0) fps_v9_body<64, 2, 2>(P, N, M, CXYZ, I, NX, SNEXT, red); }
   else if (N <= 256) { if (w0) fps_v9_body<64, 4, 4, false, true>(P, N, M, CXYZ, I, NX, SNEXT, red); }
   else if (N <= 512) { if (w0) fps_v9_body<64, 8, 4, false, true>(P, N, M, CXYZ, I, NX, SNEXT, red); }
-#ifndef PN2_CHAIN_W1
-#define PN2_CHAIN_W1 0
-#endif
-#if PN2_CHAIN_W1 == 1
-  else { if (w0) fps_v9_body<64, 16, 4, false, true>(P, N, M, CXYZ, I, NX, SNEXT, red); }
-#elif PN2_CHAIN_W1 == 2
-  else { if (w0) fps_wave_body<16, false>(CXYZ, N, M, I, NX, SNEXT ? SNEXT : scratch, SI); }
-#elif PN2_CHAIN_W1 == 3
-  else { if (w0) fps_wave_body<16, true>(CXYZ, N, M, I, NX, SNEXT ? SNEXT : scratch, SI); }
-#else
   else fps_v9_body<256, 4, 2, false, true>(P, N, M, CXYZ, I, NX, SNEXT, red);
-#endif
 }
 
 __global__ __launch_bounds__(kChainBlock) void fps_chain_kernel(const float* __restrict__ xyz,
@@ -194,7 +187,6 @@ __global__ __launch_bounds__(kChainBlock) void fps_chain_kernel(const float* __r
   __shared__ uint2 red[2][8];
   __shared__ float sxyz[3 * kChainNext];
   __shared__ float snew[2][3 * kChainNext];
-  __shared__ int32_t sidx[kChainNext];  // the one-wave stage's picks (fps_wave_body)
   const int b = blockIdx.x;
   const float* __restrict__ P = xyz + (size_t)b * c.n[0] * 3;
   for (int e = threadIdx.x; e < 3 * c.n[0]; e += kChainBlock) sxyz[e] = P[e];
@@ -203,7 +195,7 @@ __global__ __launch_bounds__(kChainBlock) void fps_chain_kernel(const float* __r
     const float* cxyz = i == 0 ? sxyz : snew[(i - 1) & 1];
     float* next = i + 1 < c.stages ? snew[i & 1] : nullptr;
     chain_stage(cxyz, c.n[i], c.m[i], cxyz, c.idx[i] + (size_t)b * c.m[i],
-                c.nx[i] + (size_t)b * c.m[i] * 3, next, red, snew[i & 1], sidx);
+                c.nx[i] + (size_t)b * c.m[i] * 3, next, red);
     __syncthreads();  // stage i's LDS output complete before stage i+1 reads it
   }
 }

@@ -253,121 +253,6 @@ PN2_DEV void fps_v9_body(const float* P, int N, int M, const float* CXYZ, int32_
   }
 }
 
-// One wave samples M of N <= 64 * PPT points held in LDS (CXYZ), the chain's 1,024-point
-// stage (fps_chain_kernel). The v9 layout, scan and lane resolve of fps_v9_body with BLOCK = 64
-// -- no barrier and no cross-wave step: the 4-wave form spent ~1,000 cycles a pick, most of it
-// in the publish / barrier / second reduction / coordinate read after it. Per pick: the packed
-// distance update of the lane's PPT points, the grouped max and lane resolve, ONE wave max,
-// and the winner's coordinates:
-//   SPEC  every lane reads its own candidate's coordinates from LDS right after the lane
-//         resolve, while the wave max runs; the winner's come out of v_readlane;
-//   else  read from LDS at the winner's index after the wave max.
-// The picks go to LDS (SI: indices, SNEXT: coordinates = the next stage's input) and leave for
-// global memory in one coalesced pass after the loop.
-template <int PPT, bool SPEC>
-PN2_DEV void fps_wave_body(const float* CXYZ, int N, int M, int32_t* I, float* NX, float* SNEXT,
-                           int32_t* SI) {
-  using Lay = Lay9<64, PPT>;
-  constexpr int G = 4, NG = PPT / G, NP = PPT / 2;
-  static_assert(PPT % G == 0, "slot groups of 4");
-  const int lane = threadIdx.x & (kWave - 1);
-  using f2 = float __attribute__((ext_vector_type(2)));
-  f2 vx[NP], vy[NP], vz[NP];
-  int tb[PPT];
-  {
-    float lx[PPT], ly[PPT], lz[PPT];
-#pragma unroll
-    for (int s = 0; s < PPT; ++s) {
-      const int k = Lay::point(lane, s);
-      const int kk = k < N ? k : 0;
-      lx[s] = CXYZ[3 * kk + 0];
-      ly[s] = CXYZ[3 * kk + 1];
-      lz[s] = CXYZ[3 * kk + 2];
-    }
-#pragma unroll
-    for (int s = 0; s < PPT; ++s) {
-      const bool in = Lay::point(lane, s) < N;
-      vx[s / 2][s % 2] = in ? lx[s] : 0.0f;
-      vy[s / 2][s % 2] = in ? ly[s] : 0.0f;
-      vz[s / 2][s % 2] = in ? lz[s] : 0.0f;
-      tb[s] = in ? __float_as_int(kInitTemp) : -1;
-    }
-  }
-  float cx = CXYZ[0], cy = CXYZ[1], cz = CXYZ[2];
-  if (lane == 0) {
-    SI[0] = 0;
-    SNEXT[0] = cx; SNEXT[1] = cy; SNEXT[2] = cz;
-  }
-  for (int j = 1; j < M; ++j) {
-    int dv[PPT];
-    {
-      const f2 c2x = {cx, cx}, c2y = {cy, cy}, c2z = {cz, cz};
-#pragma unroll
-      for (int h = 0; h < NP; ++h) {  // same rounding sequence as sqdist(), two points per op
-        const f2 dx = vx[h] - c2x, dy = vy[h] - c2y, dz = vz[h] - c2z;
-        const f2 d = (dx * dx + dy * dy) + dz * dz;
-        dv[2 * h] = __float_as_int(d.x);
-        dv[2 * h + 1] = __float_as_int(d.y);
-      }
-    }
-    int bd = -1, bg = 0;
-#pragma unroll
-    for (int g = 0; g < NG; ++g) {
-      int v[G];
-#pragma unroll
-      for (int q = 0; q < G; ++q) {
-        v[q] = min(dv[g * G + q], tb[g * G + q]);
-        tb[g * G + q] = v[q];
-      }
-      const int m = max(max(max(max(v[0], v[1]), v[2]), v[3]), bd);
-      bg = m > bd ? g : bg;
-      bd = m;
-    }
-    // the lane's first slot holding bd (lane resolve)
-    int a[G - 1];
-#pragma unroll
-    for (int q = 0; q + 1 < G; ++q) a[q] = tb[q];
-#pragma unroll
-    for (int g = 1; g < NG; ++g) {
-      const bool sel = bg == g;
-#pragma unroll
-      for (int q = 0; q + 1 < G; ++q) a[q] = sel ? tb[g * G + q] : a[q];
-    }
-    int r = G - 1;
-#pragma unroll
-    for (int q = G - 2; q >= 0; --q) r = a[q] == bd ? q : r;
-    const int ls = bg * G + r;
-    float sx = 0.0f, sy = 0.0f, sz = 0.0f;
-    if constexpr (SPEC) {  // this lane's candidate (a padding-only lane reads point 0)
-      const int kl = bd >= 0 ? Lay::point(lane, ls) : 0;
-      sx = CXYZ[3 * kl + 0];
-      sy = CXYZ[3 * kl + 1];
-      sz = CXYZ[3 * kl + 2];
-    }
-    const uint32_t hi = (uint32_t)(bd + 1);  // 0 for lanes with padding only
-    const uint32_t km = wave_max_u32(hi);
-    const uint64_t hold = __builtin_amdgcn_ballot_w64(hi == km);
-    const int L = (int)__builtin_amdgcn_readfirstlane((int)__builtin_ctzll(hold));
-    const int sq = __builtin_amdgcn_readlane(ls, L);
-    const int old = Lay::point(L, sq);
-    if constexpr (SPEC) {
-      cx = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__float_as_int(sx), L));
-      cy = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__float_as_int(sy), L));
-      cz = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__float_as_int(sz), L));
-    } else {
-      cx = CXYZ[3 * old + 0]; cy = CXYZ[3 * old + 1]; cz = CXYZ[3 * old + 2];
-    }
-    if (lane == 0) {
-      SI[j] = old;
-      SNEXT[3 * j + 0] = cx; SNEXT[3 * j + 1] = cy; SNEXT[3 * j + 2] = cz;
-    }
-  }
-  // (the wave's own LDS writes are in order: its reads below see them)
-  for (int e = lane; e < M; e += kWave) I[e] = SI[e];
-  if (NX)
-    for (int e = lane; e < 3 * M; e += kWave) NX[e] = SNEXT[e];
-}
-
 template <int BLOCK, int PPT, int G, bool XYZ_LDS, bool STAMP = false, bool LRES = false,
           int PAD = -1>
 __global__ __launch_bounds__(BLOCK) void fps_v9_kernel(const float* __restrict__ xyz, int N,

@@ -175,9 +175,9 @@ PN2_DEV bool box_certifies(const GridHdr& h, float px, float py, float pz, int x
 }
 
 constexpr int kNNFirst = 1;  // the walk's first pass: the cube of shells 0..kNNFirst
-#ifndef PN2_NN_PF
-#define PN2_NN_PF 0
-#endif
+// (Measured and not kept, profiles/r5/round2: the cube's rows a z slab at a time with the
+// slab's offsets and first points loaded together -- FP4 42.5 -> 44.3 us; the walk is not
+// bound by its dependent LDS round trips.)
 
 // The three nearest known points of (px, py, pz) over a grid's sorted points (pts, off: in
 // LDS or global memory), lexicographic in (d, k): cubic shells of cells around the point's
@@ -213,37 +213,6 @@ PN2_DEV Best3 grid_nn3(const GridHdr& h, const float4* __restrict__ pts,
         best3_insert_lex(best, sqdist(p.x, p.y, p.z, px, py, pz), __float_as_int(p.w));
       }
     };
-#if PN2_NN_PF
-    if (block) {
-      // the cube, one z slab (<= 3 rows) at a time: the slab's row offsets, then every row's
-      // first point of this lane, are loaded together -- two dependent LDS round trips per
-      // slab instead of two per row and one per point; a row's further points follow
-      const int ylo = max(yl, 0), yhi = min(yh, h.ny - 1);
-      for (int z = max(zl, 0); z <= min(zh, h.nz - 1); ++z) {
-        int lo[3], hi[3];
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-          const int y = ylo + i;
-          const int row = (z * h.ny + min(y, yhi)) * h.nx;
-          lo[i] = off[row + x0];
-          hi[i] = y <= yhi ? (int)off[row + x1 + 1] : lo[i];
-        }
-        float4 p[3];
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-          const int e = lo[i] + q;
-          p[i] = pts[e < hi[i] ? e : 0];
-        }
-#pragma unroll
-        for (int i = 0; i < 3; ++i)
-          if (lo[i] + q < hi[i])
-            best3_insert_lex(best, sqdist(p[i].x, p[i].y, p[i].z, px, py, pz),
-                             __float_as_int(p[i].w));
-#pragma unroll
-        for (int i = 0; i < 3; ++i) visit(lo[i] + G, hi[i]);
-      }
-    } else
-#endif
     for (int z = max(zl, 0); z <= min(zh, h.nz - 1); ++z) {
       for (int y = max(yl, 0); y <= min(yh, h.ny - 1); ++y) {
         const int row = (z * h.ny + y) * h.nx;
@@ -641,12 +610,8 @@ inline size_t fp_grid_lds(int m) {
 // KPT: known points per thread (m <= KPT * kNNBlock), kept in registers between the count
 // and the scatter. LDS at FP4 (m = 1024, B = 16): 16 KB points + 2 KB offsets + 1.75 KB, so
 // 8 workgroups fit a CU (the LDS bound; their 32 waves are the wave bound).
-#ifndef PN2_FPG_WPE
-#define PN2_FPG_WPE 1
-#endif
 template <int V2, int V1, int UN, int KPT>
-__global__ __launch_bounds__(kNNBlock) __attribute__((amdgpu_waves_per_eu(PN2_FPG_WPE)))
-void fp_grid_fused_kernel(FpLayer p, float* __restrict__ dist,
+__global__ __launch_bounds__(kNNBlock) void fp_grid_fused_kernel(FpLayer p, float* __restrict__ dist,
                                                               int32_t* __restrict__ idx) {
   constexpr int NW = kNNBlock / kWave;
   extern __shared__ float4 s_pts[];  // m known points sorted by cell, then ncell + 1 offsets
