@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
 """Condense an A/B sweep directory under profiles/: every bench.py JSON line in it (recursively)
 becomes one row of <dir>/summary.jsonl (file name, value, ms_per_step, the SA1 sampler's launch
-time, the layout fields of `config`, e2e value), and the raw .json / .err files are removed.
-Other files (logs, csv) stay.
+time, the layout fields of `config`, e2e value); every other JSON object (tools/bench_*.py
+results) one row {"file", "data"} of <dir>/tools.jsonl; the raw .json / .err files are
+removed. Other files (logs, csv, txt) stay.
 
     python tools/condense_profiles.py profiles/r3/plan profiles/r3/layouts ...
 """
@@ -15,22 +16,27 @@ KEEP_CFG = ("config", "clouds_per_gpu", "hw_queues", "streams", "launch",
 
 
 def condense(d):
-    rows, drop = [], []
+    rows, other, drop = [], [], []
     for root, _, files in os.walk(d):
         for f in sorted(files):
             p = os.path.join(root, f)
             if f.endswith(".err"):
                 drop.append(p)
                 continue
-            if not f.endswith(".json") or f == "summary.jsonl":
+            if not f.endswith(".json"):
                 continue
             try:
                 with open(p) as fh:
-                    txt = fh.read().strip().splitlines()
-                obj = json.loads([ln for ln in txt if ln.startswith("{")][-1])
+                    raw = fh.read().strip()
+                try:
+                    obj = json.loads(raw)  # (an indented tool result)
+                except ValueError:
+                    obj = json.loads([ln for ln in raw.splitlines() if ln.startswith("{")][-1])
             except (ValueError, IndexError):
                 continue
-            if "value" not in obj:
+            if not isinstance(obj, dict) or "value" not in obj or "metric" not in obj:
+                other.append({"file": os.path.relpath(p, d), "data": obj})
+                drop.append(p)
                 continue
             cfg = obj.get("config") or {}
             rows.append({"file": os.path.relpath(p, d), "value": obj.get("value"),
@@ -40,11 +46,13 @@ def condense(d):
                          "diagnostic": obj.get("diagnostic"),
                          "config": {k: cfg[k] for k in KEEP_CFG if k in cfg}})
             drop.append(p)
-    if not rows:
+    if not rows and not other:
         return 0
-    with open(os.path.join(d, "summary.jsonl"), "a") as fh:
-        for r in rows:
-            fh.write(json.dumps(r) + "\n")
+    for name, lst in (("summary.jsonl", rows), ("tools.jsonl", other)):
+        if lst:
+            with open(os.path.join(d, name), "a") as fh:
+                for r in lst:
+                    fh.write(json.dumps(r) + "\n")
     for p in drop:
         os.remove(p)
     for root, dirs, files in os.walk(d, topdown=False):
