@@ -446,6 +446,11 @@ def main():
     ap.add_argument("--graph-launch", action="store_true",
                     help="A/B: launch each side segment as its captured hipGraph instead of its "
                          "kernels directly (pn2_plan_graph_direct; DESIGN.md §3.6d)")
+    ap.add_argument("--fp4-known-grid", choices=["lane", "sampler", "off"], default=None,
+                    help="A/B: FP4's known-point grid built by a launch on FP4's lane, "
+                         "by the SA1 sampler after its last pick (pn2_fps_chain_grid), or by "
+                         "each FP4 workgroup in LDS (off); default: per config "
+                         "(stack.FP4_KNOWN_GRID_BY_CONFIG)")
     ap.add_argument("--lane0-priority", choices=["auto", "default", "high"], default="auto",
                     help="stream priority of lane 0 (the SA1 sampler chain); auto = default "
                          "for the geometric step, high for the whole model")
@@ -552,6 +557,7 @@ def main():
         torch.cuda.synchronize()
         if pipelined:
             pkg.stack.TIMING_EVENTS = bool(args.timeline) and not model
+            pkg.stack.FP4_KNOWN_GRID = args.fp4_known_grid
             pipe = pkg.stack.Pipeline(inp, graphs=not args.eager, nsets=args.sets,
                                       sampler_lanes=1 if model else args.sampler_lanes,
                                       private_streams=model or args.private_side,
@@ -705,6 +711,9 @@ def main():
                               "kernels launched directly")
                            if pipelined and not args.no_native_plan else "")),
                        "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "0")),
+                       "fp4_known_grid": None if args.model or args.config == "cfg5"
+                       else (pkg.stack.FP4_KNOWN_GRID
+                             or pkg.stack.FP4_KNOWN_GRID_BY_CONFIG.get(args.config, "off")),
                        "lane0_priority": prio0,
                        "streams": (("SA1 sampler + 3 side streams" if args.sampler_lanes <= 1 or args.model
                                     else f"{args.sampler_lanes} sampler streams (consecutive steps' "

@@ -143,6 +143,15 @@ int pn2_fps_ws(const float* xyz, int B, int N, int npoint, int32_t* idx, float* 
  * the ordinary sampler, then every remaining stage fused in one launch. */
 int pn2_fps_chain(const float* xyz, int B, int N, int nstages, const int* npoint,
                   int32_t* const* idx, float* const* new_xyz, pn2_stream_t stream);
+/* pn2_fps_chain plus the automatic-edge grid of stage 0's picks (the known points of the last
+ * FP layer, pointnet2_sem_seg*.py:55 / pointnet_util.py:218): grid0 (pn2_grid_size(B,
+ * npoint[0]) bytes, 16-byte aligned) gets exactly what pn2_grid_build(new_xyz[0], B,
+ * npoint[0], 0, grid0) writes, up to the order of the points inside a cell. The culled
+ * sampler builds it in its own workgroups after the last pick (npoint[0] <= 4096; otherwise
+ * one pn2_grid_build launch follows on `stream`). new_xyz[0] must not be NULL. */
+int pn2_fps_chain_grid(const float* xyz, int B, int N, int nstages, const int* npoint,
+                       int32_t* const* idx, float* const* new_xyz, void* grid0,
+                       size_t grid0_bytes, pn2_stream_t stream);
 /* out (B,M,3) = inp[b, idx[b,j], :]; inp must have 3 channels (tf_sampling.cpp:131). */
 int pn2_gather_point(const float* inp, const int32_t* idx, int B, int N, int M, float* out,
                      pn2_stream_t stream);
@@ -346,6 +355,15 @@ int pn2_fp_apply(const float* dist, const int32_t* idx, const void* unknown_grid
 int pn2_fp_grid_fused(const float* xyz1, const float* xyz2, const void* unknown_grid,
                       const float* points1, int C1, const float* points2, int C2, int B, int n,
                       int m, float* out, float* dist, int32_t* idx, pn2_stream_t stream);
+/* pn2_fp_grid_fused from a grid of the known points built before (known_grid =
+ * pn2_grid_build(xyz2, B, m, 0, ...) or pn2_fps_chain_grid's grid0): each workgroup copies
+ * its cloud's grid into LDS instead of sorting xyz2 itself. The same output, bit for bit. A
+ * grid with more than max(m, 64) cells (an explicit edge) is not staged: the workgroups then
+ * build their own from xyz2, which is therefore always required. */
+int pn2_fp_grid_fused_known(const void* known_grid, const float* xyz1, const float* xyz2,
+                            const void* unknown_grid, const float* points1, int C1,
+                            const float* points2, int C2, int B, int n, int m, float* out,
+                            float* dist, int32_t* idx, pn2_stream_t stream);
 
 /* ---------------------------------------------------------------- attention / pooling --- */
 

@@ -42,6 +42,10 @@ int pn2_plan_wait(pn2_plan* plan, pn2_stream_t stream, void* event);
 int pn2_plan_fps_chain(pn2_plan* plan, const float* xyz, int B, int N, int nstages,
                        const int* npoint, int32_t* const* idx, float* const* new_xyz,
                        pn2_stream_t stream);
+/* append: pn2_fps_chain_grid (the same, plus stage 0's picks' grid into grid0) */
+int pn2_plan_fps_chain_grid(pn2_plan* plan, const float* xyz, int B, int N, int nstages,
+                            const int* npoint, int32_t* const* idx, float* const* new_xyz,
+                            void* grid0, size_t grid0_bytes, pn2_stream_t stream);
 /* mark the operation appended last as the timed one: pn2_plan_launch_timed brackets it with
  * its two events (recorded on that operation's stream) */
 int pn2_plan_mark_timed(pn2_plan* plan);

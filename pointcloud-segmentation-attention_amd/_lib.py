@@ -91,6 +91,7 @@ SIGNATURES = {
     "pn2_prob_sample": (_I, [_P, _P, _I, _I, _I, _P, _S, _P, _P]),
     "pn2_fps_workspace_size": (_S, [_I, _I]),
     "pn2_fps_chain": (_I, [_P, _I, _I, _I, _P, _P, _P, _P]),
+    "pn2_fps_chain_grid": (_I, [_P, _I, _I, _I, _P, _P, _P, _P, _S, _P]),
     "pn2_fps_ws": (_I, [_P, _I, _I, _I, _P, _P, _P, _S, _P]),
     "pn2_gather_point": (_I, [_P, _P, _I, _I, _I, _P, _P]),
     "pn2_gather_point_grad": (_I, [_P, _P, _I, _I, _I, _P, _P]),
@@ -108,6 +109,8 @@ SIGNATURES = {
     "pn2_three_nn_grid": (_I, [_P, _P, _P, _I, _I, _I, _P, _P, _P]),
     "pn2_fp_apply": (_I, [_P, _P, _P, _P, _I, _P, _I, _I, _I, _I, _P, _P]),
     "pn2_fp_grid_fused": (_I, [_P, _P, _P, _P, _I, _P, _I, _I, _I, _I, _P, _P, _P, _P]),
+    "pn2_fp_grid_fused_known": (_I, [_P, _P, _P, _P, _P, _I, _P, _I, _I, _I, _I, _P, _P, _P,
+                                     _P]),
     "pn2_group_point": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _P]),
     "pn2_group_point_grad": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _P]),
     "pn2_group_concat": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P, _P, _P]),
@@ -149,6 +152,7 @@ SIGNATURES = {
     "pn2_plan_record": (_I, [_P, _P, _P]),
     "pn2_plan_wait": (_I, [_P, _P, _P]),
     "pn2_plan_fps_chain": (_I, [_P, _P, _I, _I, _I, _P, _P, _P, _P]),
+    "pn2_plan_fps_chain_grid": (_I, [_P, _P, _I, _I, _I, _P, _P, _P, _P, _S, _P]),
     "pn2_plan_mark_timed": (_I, [_P]),
     "pn2_plan_size": (_I, [_P]),
     "pn2_plan_launch": (_I, [_P]),

@@ -163,7 +163,8 @@ int fps_chain_check(const float* xyz, int B, int N, int nstages, const int* npoi
 // pn2_fps_chain without the stored-fault report (the plan executor takes the fault word once,
 // before it enqueues anything, so a plan never stops part-way through a step)
 int fps_chain_launch(const float* xyz, int B, int N, int nstages, const int* npoint,
-                     int32_t* const* idx, float* const* new_xyz, hipStream_t s, bool take);
+                     int32_t* const* idx, float* const* new_xyz, hipStream_t s, bool take,
+                     void* grid0 = nullptr, size_t grid0_bytes = 0);
 // a fault stored by an earlier sampler launch, cleared (0: none)
 int fps_take_fault();
 

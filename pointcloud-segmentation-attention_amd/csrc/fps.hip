@@ -111,6 +111,7 @@ __global__ void gather_point_grad_kernel(const float* __restrict__ out_g,
 }
 
 constexpr int kMaxRegPoints = 1024 * 16;
+constexpr int kCullGridMax = 4096;  // picks whose grid the culled sampler builds itself
 
 // ---- device fault word ------------------------------------------------------------------
 // A kernel that finds a broken invariant (the culled sampler's cold waves waiting past their
@@ -200,9 +201,15 @@ __global__ __launch_bounds__(kChainBlock) void fps_chain_kernel(const float* __r
   }
 }
 
+// kgrid (optional, pn2_grid_size(B, M) bytes): also the picks' automatic-edge grid, exactly
+// pn2_grid_build(nx, B, M, 0, kgrid): built inside the culled sampler's workgroups (N <= 8192,
+// M <= 4096), else by a pn2_grid_build launch after the sampler
 int fps_impl(const float* xyz, int B, int N, int M, int32_t* idx, float* nx, void* ws,
-             size_t ws_bytes, hipStream_t s, int sched = PN2_FPS_AUTO, bool take = true) {
+             size_t ws_bytes, hipStream_t s, int sched = PN2_FPS_AUTO, bool take = true,
+             char* kgrid = nullptr, size_t kgrid_bytes = 0) {
   if (B < 0 || N < 0 || M <= 0 || (B > 0 && (!xyz || !idx))) return PN2_EINVAL;
+  if (kgrid && (!nx || kgrid_bytes < pn2_grid_size(B, M) || ((uintptr_t)kgrid & 15)))
+    return PN2_EINVAL;
   // the block-scan schedule exists only where the culled sampler runs (4096 < N <= 16384)
   if (sched != PN2_FPS_AUTO && sched != PN2_FPS_BLOCKSCAN) return PN2_EINVAL;
   if (sched != PN2_FPS_AUTO && (N <= 4096 || N > kMaxRegPoints)) return PN2_EINVAL;
@@ -226,22 +233,36 @@ int fps_impl(const float* xyz, int B, int N, int M, int32_t* idx, float* nx, voi
   else if (N <= 8192) {
     // culled hot-set sampler (fps_cull.h; 0.37 vs 0.71 ms at B = 16); the v9
     // block-scan sampler stays selectable for A/B timing and parity cross-checks
-    if (sched == PN2_FPS_BLOCKSCAN)
+    if (sched == PN2_FPS_BLOCKSCAN) {
       launch_v9<256, 32, 4, true, PN2_SA1_PAD>(xyz, B, N, M, idx, nx, s);
-    else
-      launch_hotcull<16, 9, 3, 4>(xyz, B, N, M, idx, nx, fault_word_dev(), s);
+    } else {
+      if (kgrid && M <= kCullGridMax) {
+        launch_hotcull_grid<16, 9, 3, 4>(xyz, B, N, M, idx, nx, fault_word_dev(), s, kgrid);
+        kgrid = nullptr;  // (built)
+      } else {
+        launch_hotcull<16, 9, 3, 4>(xyz, B, N, M, idx, nx, fault_word_dev(), s);
+      }
+    }
   }
   else if (N <= kMaxRegPoints) {
     // MSG SA1 size (cfg5, 16384 -> 512): the culled sampler with coordinates read from L2 and
     // two points per lane per cell (135 cells of 128 points), the cold points' z in LDS: 0.33
     // vs 0.59 ms for v9 512 x 32 at B = 8 (tools/fps_hot_check.py --msg,
     // profiles/r2/fps_msg_ab.log), index-exact; 12 or 8 waves spill more (0.49, 0.66 ms)
-    if (sched == PN2_FPS_BLOCKSCAN) launch_v9<512, 32, 4>(xyz, B, N, M, idx, nx, s);
-    else launch_hotcull<16, 9, 3, 4, 16384, 2>(xyz, B, N, M, idx, nx, fault_word_dev(), s);
+    if (sched == PN2_FPS_BLOCKSCAN) {
+      launch_v9<512, 32, 4>(xyz, B, N, M, idx, nx, s);
+    } else {
+      launch_hotcull<16, 9, 3, 4, 16384, 2>(xyz, B, N, M, idx, nx, fault_word_dev(), s);
+    }
   }
   else {
     if (!ws || ws_bytes < (size_t)B * N * sizeof(float)) return PN2_EINVAL;
     hipLaunchKernelGGL(fps_ws_kernel, dim3(B), dim3(1024), 0, s, xyz, N, M, (float*)ws, idx, nx);
+  }
+  if (kgrid) {  // not built inside the sampler: the grid build launch
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return (int)e;
+    return pn2_grid_build(nx, B, M, 0.0f, kgrid, kgrid_bytes, s);
   }
   PN2_RETURN_LAUNCH();
 }
@@ -265,15 +286,19 @@ int fps_chain_check(const float* xyz, int B, int N, int nstages, const int* npoi
 int fps_take_fault() { return take_fault(); }
 
 int fps_chain_launch(const float* xyz, int B, int N, int nstages, const int* npoint,
-                     int32_t* const* idx, float* const* new_xyz, hipStream_t s, bool take) {
+                     int32_t* const* idx, float* const* new_xyz, hipStream_t s, bool take,
+                     void* grid0, size_t grid0_bytes) {
   const int rc0 = fps_chain_check(xyz, B, N, nstages, npoint, idx, new_xyz);
   if (rc0 != PN2_OK || B == 0) return rc0;
+  if (grid0 && (grid0_bytes < pn2_grid_size(B, npoint[0]) || ((uintptr_t)grid0 & 15)))
+    return PN2_EINVAL;
   int first = 0;  // first stage of the fused tail
-  if (N > kChainNext) {  // the big first stage as its own sampler launch
+  if (N > kChainNext) {  // the big first stage as its own sampler launch (+ its picks' grid)
     const int rc = fps_impl(xyz, B, N, npoint[0], idx[0], new_xyz[0], nullptr, 0, s,
-                            PN2_FPS_AUTO, take);
+                            PN2_FPS_AUTO, take, (char*)grid0, grid0_bytes);
     if (rc != PN2_OK) return rc;
     if (nstages == 1) return PN2_OK;
+    grid0 = nullptr;
     xyz = new_xyz[0];
     N = npoint[0];
     first = 1;
@@ -290,6 +315,11 @@ int fps_chain_launch(const float* xyz, int B, int N, int nstages, const int* npo
     if (on) n = c.m[i];
   }
   hipLaunchKernelGGL(fps_chain_kernel, dim3(B), dim3(kChainBlock), 0, s, xyz, c);
+  if (grid0) {  // stage 0 ran inside the chain kernel: its picks' grid as a launch after it
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return (int)e;
+    return pn2_grid_build(new_xyz[0], B, npoint[0], 0.0f, grid0, grid0_bytes, s);
+  }
   PN2_RETURN_LAUNCH();
 }
 }  // namespace pn2
@@ -313,7 +343,15 @@ int pn2_fps_gather_sched(const float* xyz, int B, int N, int npoint, int32_t* id
 int pn2_fps_chain(const float* xyz, int B, int N, int nstages, const int* npoint,
                   int32_t* const* idx, float* const* new_xyz, pn2_stream_t stream) {
   return pn2::fps_chain_launch(xyz, B, N, nstages, npoint, idx, new_xyz, (hipStream_t)stream,
-                               true);
+                               true, nullptr, 0);
+}
+
+int pn2_fps_chain_grid(const float* xyz, int B, int N, int nstages, const int* npoint,
+                       int32_t* const* idx, float* const* new_xyz, void* grid0,
+                       size_t grid0_bytes, pn2_stream_t stream) {
+  if (!grid0) return PN2_EINVAL;
+  return pn2::fps_chain_launch(xyz, B, N, nstages, npoint, idx, new_xyz, (hipStream_t)stream,
+                               true, grid0, grid0_bytes);
 }
 
 size_t pn2_fps_workspace_size(int B, int N) {

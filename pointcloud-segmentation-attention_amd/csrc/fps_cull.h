@@ -24,6 +24,7 @@
 // ~34 refreshes for 1,023 picks at K = 128; 25 measured at K = 256, ~93 % of (cell, centre) pairs skipped).
 #pragma once
 #include "fps_kernels.h"
+#include "grid.h"
 
 namespace pn2 {
 namespace {
@@ -246,11 +247,13 @@ PN2_DEV void hot_update(int (&hv)[2 * HP], const hf2 (&hx)[HP], const hf2 (&hy)[
 // LDS once the sort is done. ~53 KB of LDS instead of ~155 KB: with fewer VGPRs too
 // (fps_hotcull_lean_kernel), a CU that side-lane workgroups partly occupy can still take a
 // sampler workgroup (the 155 KB / 128-VGPR workgroup waits for a CU to drain completely).
+// KG: also the picks' automatic-edge grid into kgrid (pn2_fps_chain_grid), built by the
+// workgroup after its last pick (a separate instantiation: the product sampler keeps its code)
 template <int NW, int PPT, int NPTS, bool STAMP = false, int PRIO = 0, int HQ = 2, int PPC = 1,
-          bool LEAN = false>
+          bool LEAN = false, bool KG = false>
 __device__ __attribute__((always_inline)) inline void hotcull_body(
     const float* __restrict__ xyz, int N, int M, int32_t* __restrict__ idx,
-    float* __restrict__ new_xyz, int* __restrict__ fault) {
+    float* __restrict__ new_xyz, int* __restrict__ fault, char* __restrict__ kgrid = nullptr) {
   constexpr int BLOCK = 64 * NW;
   constexpr int NCW = NW - 1;  // cold waves
   constexpr int NCELL = NCW * PPT;
@@ -327,6 +330,10 @@ __device__ __attribute__((always_inline)) inline void hotcull_body(
   const float* __restrict__ X = XYZ_LDS ? (const float*)sxyz : P;  // coordinates
   for (int e = t; e < NBK; e += BLOCK) shist[e] = 0u;
   if (t < NW * 4) swcnt[t / 4][t % 4] = 0u;
+  // KG: the grid's address waits in LDS until the epilogue (a pointer kept in registers
+  // through the pick loop made the allocator spill inside it)
+  __shared__ char* s_kgrid;
+  if (KG && t == 0) s_kgrid = NX && M <= NBK ? kgrid + (size_t)b * grid_stride(M) : nullptr;
   __syncthreads();
   {
     float mx[3] = {-INFINITY, -INFINITY, -INFINITY}, mn[3] = {-INFINITY, -INFINITY, -INFINITY};
@@ -917,6 +924,13 @@ __device__ __attribute__((always_inline)) inline void hotcull_body(
       if (round_end(std::true_type{}, round)) break;
     }
   }
+  if constexpr (KG) {  // the picks' grid, from the new_xyz rows this workgroup just wrote
+    __syncthreads();
+    if (char* const G = s_kgrid) {  // (thread id from the wave index and mbcnt: threadIdx.x
+      __shared__ GridHdr sgh;        // kept live through the loop cost registers as well)
+      block_grid_build<BLOCK>(NX, M, G, shist, sbox, swmax, &sgh, w * kWave + (int)__lane_id());
+    }
+  }
   if constexpr (STAMP) {
     if (lane == 0 && b < 16) {
 #pragma unroll
@@ -949,11 +963,31 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_kernel(const float* __res
   hotcull_body<NW, PPT, NPTS, STAMP, PRIO, HQ, PPC, LEAN>(xyz, N, M, idx, new_xyz, fault);
 }
 
+template <int NW, int PPT, int NPTS, int PRIO, int HQ>
+__global__ __launch_bounds__(64 * NW) void fps_hotcull_grid_kernel(const float* __restrict__ xyz,
+                                                                int N, int M,
+                                                                int32_t* __restrict__ idx,
+                                                                float* __restrict__ new_xyz,
+                                                                int* __restrict__ fault,
+                                                                char* __restrict__ kgrid) {
+  hotcull_body<NW, PPT, NPTS, false, PRIO, HQ, 1, false, true>(xyz, N, M, idx, new_xyz, fault,
+                                                               kgrid);
+}
+
 template <int NW, int PPT, int PRIO = 0, int HQ = 2, int NPTS = 8192, int PPC = 1>
 void launch_hotcull(const float* xyz, int B, int N, int M, int32_t* idx, float* nx, int* fault,
                     hipStream_t s) {
   hipLaunchKernelGGL((fps_hotcull_kernel<NW, PPT, NPTS, false, PRIO, HQ, PPC>), dim3(B),
                      dim3(64 * NW), 0, s, xyz, N, M, idx, nx, fault);
+}
+
+// the same launch plus the picks' grid (one point per lane per cell only; kgrid non-null,
+// nx non-null, M <= 4096: checked by the caller)
+template <int NW, int PPT, int PRIO = 0, int HQ = 2, int NPTS = 8192>
+void launch_hotcull_grid(const float* xyz, int B, int N, int M, int32_t* idx, float* nx,
+                         int* fault, hipStream_t s, char* kgrid) {
+  hipLaunchKernelGGL((fps_hotcull_grid_kernel<NW, PPT, NPTS, PRIO, HQ>), dim3(B), dim3(64 * NW),
+                     0, s, xyz, N, M, idx, nx, fault, kgrid);
 }
 
 }  // namespace

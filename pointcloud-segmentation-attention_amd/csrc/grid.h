@@ -112,4 +112,85 @@ PN2_DEV GridHdr grid_dims(const float lo[3], const float hi[3], int N, float edg
   return h;
 }
 
+// The automatic-edge grid of M points P (xyz AoS, global memory, written by this workgroup
+// before a barrier), built by a whole workgroup of BLOCK threads into the grid G of one cloud
+// (grid_stride(M) bytes, pn2_grid_build's layout and header: the same cells as
+// pn2_grid_build(P, ..., cell_edge = 0)). The order inside a cell is the order of the atomics
+// -- the searches that read a grid do not depend on it. LDS: scnt >= max(M, kAutoMinCells)
+// words, red [BLOCK / 64][8] floats, wsum [BLOCK / 64] ints, one header. Every thread calls
+// it, t = its thread index.
+template <int BLOCK>
+PN2_DEV void block_grid_build(const float* __restrict__ P, int M, char* __restrict__ G,
+                              uint32_t* scnt, float (*red)[8], int* wsum, GridHdr* shh, int t) {
+  constexpr int NW = BLOCK / kWave;
+  const int lane = t & (kWave - 1), w = t / kWave;
+  int* __restrict__ off = (int*)(G + sizeof(GridHdr));
+  float4* __restrict__ pts = (float4*)(G + kGridOffBytes);
+  float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+  for (int k = t; k < M; k += BLOCK) {
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      const float v = P[3 * k + a];
+      mn[a] = fminf(mn[a], v);
+      mx[a] = fmaxf(mx[a], v);
+    }
+  }
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    mn[a] = wave_min_f(mn[a]);
+    mx[a] = wave_max_f(mx[a]);
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int a = 0; a < 3; ++a) { red[w][a] = mn[a]; red[w][4 + a] = mx[a]; }
+  }
+  __syncthreads();
+  if (t == 0) {
+    float lo[3], hi[3];
+    for (int a = 0; a < 3; ++a) {
+      lo[a] = red[0][a];
+      hi[a] = red[0][4 + a];
+      for (int i = 1; i < NW; ++i) { lo[a] = fminf(lo[a], red[i][a]); hi[a] = fmaxf(hi[a], red[i][4 + a]); }
+      if (!(hi[a] >= lo[a])) { lo[a] = 0.0f; hi[a] = 0.0f; }  // NaN-only axis
+    }
+    *shh = grid_dims(lo, hi, M, 0.0f);
+    *(GridHdr*)G = *shh;
+  }
+  __syncthreads();
+  const GridHdr h = *shh;
+  for (int c = t; c < h.ncell; c += BLOCK) scnt[c] = 0u;
+  __syncthreads();
+  auto cell_at = [&](int k) {
+    const int ix = cell_coord(P[3 * k + 0], h.ox, h.inv, h.nx);
+    const int iy = cell_coord(P[3 * k + 1], h.oy, h.inv, h.ny);
+    const int iz = cell_coord(P[3 * k + 2], h.oz, h.inv, h.nz);
+    return (iz * h.ny + iy) * h.nx + ix;
+  };
+  for (int k = t; k < M; k += BLOCK) atomicAdd(&scnt[cell_at(k)], 1u);
+  __syncthreads();
+  {  // exclusive scan of the counts: a contiguous run of cells per thread
+    const int per = (h.ncell + BLOCK - 1) / BLOCK;
+    const int s0 = min(t * per, h.ncell), s1 = min(s0 + per, h.ncell);
+    int sum = 0;
+    for (int c = s0; c < s1; ++c) sum += (int)scnt[c];
+    const int incl = wave_incl_scan(sum, lane);
+    if (lane == kWave - 1) wsum[w] = incl;
+    __syncthreads();
+    int base = incl - sum;
+    for (int i = 0; i < w; ++i) base += wsum[i];
+    for (int c = s0; c < s1; ++c) {
+      const int n = (int)scnt[c];
+      scnt[c] = (uint32_t)base;
+      off[c] = base;
+      base += n;
+    }
+    if (t == 0) off[h.ncell] = M;
+  }
+  __syncthreads();
+  for (int k = t; k < M; k += BLOCK) {
+    const int pos = (int)atomicAdd(&scnt[cell_at(k)], 1u);
+    pts[pos] = make_float4(P[3 * k + 0], P[3 * k + 1], P[3 * k + 2], __int_as_float(k));
+  }
+}
+
 }  // namespace pn2

@@ -388,7 +388,7 @@ struct FpRow {
 // The output rows j0 .. j0 + 63 of cloud b, column slice zb, from the rows' three neighbours
 // and IDW weights (row(rl) -> FpRow for the workgroup's row rl): interpolated columns
 // ((p1*w1)+(p2*w2))+(p3*w3), then the points1 concat.
-template <int V2, int V1, int UN, typename RowFn>
+template <int V2, int V1, int UN, int FB = kNNBlock, typename RowFn>
 PN2_DEV void fp_write_rows(const FpLayer& p, int b, int zb, int j0, RowFn row) {
   const float* __restrict__ points1 = p.points1;
   const float* __restrict__ points2 = p.points2;
@@ -403,7 +403,7 @@ PN2_DEV void fp_write_rows(const FpLayer& p, int b, int zb, int j0, RowFn row) {
   if (ce <= cb) return;
   // element e -> (row e / cw, column cb + e % cw); the last channel slice can be narrower
   // than cw (coutv % zsplit != 0), its surplus columns are skipped
-  const int nrows = min(kNNRows, n - j0);
+  const int nrows = min(FB / kNNGroup, n - j0);
   const int elems = nrows * cw;
   using V2T = typename std::conditional<V2 == 4, float4, float>::type;
   using V1T = typename std::conditional<V1 == 4, float4, float>::type;
@@ -414,7 +414,7 @@ PN2_DEV void fp_write_rows(const FpLayer& p, int b, int zb, int j0, RowFn row) {
   // combined, so a thread waits for one memory round trip per U elements (one per element
   // made this loop latency-bound: 34 dependent trips per thread at Cout = 137).
   constexpr int U = UN;
-  for (int e0 = threadIdx.x; e0 < elems; e0 += kNNBlock * U) {
+  for (int e0 = threadIdx.x; e0 < elems; e0 += FB * U) {
     V2T a[U], bb[U], cc[U];
     V1T q[U];  // (both branches set every array: arrays set on one branch went to scratch)
     float4 W[U];
@@ -422,7 +422,7 @@ PN2_DEV void fp_write_rows(const FpLayer& p, int b, int zb, int j0, RowFn row) {
     size_t o[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int e = e0 + u * kNNBlock;
+      const int e = e0 + u * FB;
       const int rl = (int)fdiv((uint32_t)(e < elems ? e : e0), div_cw);
       int c = cb + ((e < elems ? e : e0) - rl * cw);
       ok[u] = e < elems && c < ce;
@@ -582,6 +582,12 @@ __global__ __launch_bounds__(kNNBlock) void fp_fused_kernel(FpLayer p, int tile)
 // less than the launch and the dependency they replace. Bit-identical to the three-launch path.
 constexpr int kFpGridMaxKnown = 4096;  // LDS: m float4 + (max(2m / ppc, 64) + 1) offsets
 constexpr float kFpgPointsPerCell = 2.0f;  // the LDS grid's points per cell (profiles/r4/ppc)
+// threads per workgroup (a quad per unknown: FB / 4 unknowns). The known grid is built (or
+// staged) once per workgroup, but fewer, bigger workgroups were slower at FP4: 512 / 1024
+// threads 49.0 / 55.8 us against 46.9 (profiles/r5/fb), and so were 2 / 4 row blocks per
+// 256-thread workgroup (54.9 / 80.9 us, profiles/r5/rpw): the search and the writes need
+// the workgroups' parallelism more than the build needs amortising
+constexpr int kFpgBlock = 256;
 
 // LDS per workgroup of the current device (cached per device id)
 size_t device_lds_per_block() {
@@ -610,119 +616,140 @@ inline size_t fp_grid_lds(int m) {
 // KPT: known points per thread (m <= KPT * kNNBlock), kept in registers between the count
 // and the scatter. LDS at FP4 (m = 1024, B = 16): 16 KB points + 2 KB offsets + 1.75 KB, so
 // 8 workgroups fit a CU (the LDS bound; their 32 waves are the wave bound).
-template <int V2, int V1, int UN, int KPT>
-__global__ __launch_bounds__(kNNBlock) void fp_grid_fused_kernel(FpLayer p, float* __restrict__ dist,
-                                                              int32_t* __restrict__ idx) {
-  constexpr int NW = kNNBlock / kWave;
+// kgrid (pn2_fp_grid_fused_known): a grid of the known points built before (the SA1 sampler
+// builds it, fps.hip): a workgroup copies its cloud's header, offsets and points into LDS
+// instead of steps 1-2 -- a third of the kernel's time at FP4 (profiles/r5/ab). A grid with
+// more cells than the LDS holds (an explicit edge) falls back to the build.
+template <int V2, int V1, int UN, int KPT, int FB>
+__global__ __launch_bounds__(FB) void fp_grid_fused_kernel(FpLayer p, float* __restrict__ dist,
+                                                        int32_t* __restrict__ idx,
+                                                        const char* __restrict__ kgrid) {
+  constexpr int NW = FB / kWave;
+  constexpr int FR = FB / kNNGroup;  // unknowns per workgroup
   extern __shared__ float4 s_pts[];  // m known points sorted by cell, then ncell + 1 offsets
-  __shared__ int4 s_idx[kNNRows];     // the row's three neighbours and its output row
-  __shared__ float s_wv[3][kNNRows];  // the row's IDW weights; before the search: the build's
+  __shared__ int4 s_idx[FR];     // the row's three neighbours and its output row
+  __shared__ float s_wv[3][FR];  // the row's IDW weights; before the search: the build's
                                       // scratch (bbox partials, scan partials, header)
   float(*red)[NW] = reinterpret_cast<float(*)[NW]>(&s_wv[0][0]);  // [6][NW] <= 64 floats
   int* wsum = reinterpret_cast<int*>(&s_wv[1][0]);
   GridHdr* shp = reinterpret_cast<GridHdr*>(&s_wv[2][0]);
-  static_assert(6 * NW <= kNNRows && sizeof(GridHdr) <= kNNRows * 4, "build scratch fits");
+  static_assert(6 * NW <= FR && sizeof(GridHdr) <= FR * 4, "build scratch fits");
   const int n = p.n, m = p.m;
-  const int R = (n + kNNRows - 1) / kNNRows;
+  const int R = (n + FR - 1) / FR;
   const int total = R * p.B;
   const int Lg = xcd_block(blockIdx.x, total);
   if (Lg >= total) return;
   const int b = Lg / R;
-  const int j0 = (Lg - b * R) * kNNRows;
+  const int j0 = (Lg - b * R) * FR;
   const int t = threadIdx.x, lane = t & (kWave - 1), w = t / kWave;
-  const float* __restrict__ K = p.xyz2 + (size_t)b * m * 3;
   uint16_t* s_off = reinterpret_cast<uint16_t*>(s_pts + m);
   uint32_t* s_cnt = reinterpret_cast<uint32_t*>(s_pts + m);  // the offsets as counter pairs
-
-  // 1. bounding box -> header
-  float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+  GridHdr h;
+  bool built = false;
+  if (kgrid) {  // the prebuilt grid, when its offsets fit the LDS's max(m, 64) + 1
+    const char* G = kgrid + (size_t)b * grid_stride(m);
+    h = *reinterpret_cast<const GridHdr*>(G);
+    if (h.ncell >= 1 && h.ncell <= max(m, kAutoMinCells)) {
+      const int* goff = reinterpret_cast<const int*>(G + sizeof(GridHdr));
+      const float4* gpts = reinterpret_cast<const float4*>(G + kGridOffBytes);
+      for (int i = t; i < m; i += FB) s_pts[i] = gpts[i];
+      for (int i = t; i <= h.ncell; i += FB) s_off[i] = (uint16_t)goff[i];
+      __syncthreads();
+      built = true;
+    }
+  }
+  if (!built) {
+    const float* __restrict__ K = p.xyz2 + (size_t)b * m * 3;
+    // 1. bounding box -> header
+    float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
 #pragma unroll
-  for (int i = 0; i < KPT; ++i) {
-    const int k = t + i * kNNBlock;
-    if (k < m) {
+    for (int i = 0; i < KPT; ++i) {
+      const int k = t + i * FB;
+      if (k < m) {
 #pragma unroll
-      for (int a = 0; a < 3; ++a) {
-        const float v = K[3 * k + a];
-        mn[a] = fminf(mn[a], v);
-        mx[a] = fmaxf(mx[a], v);
+        for (int a = 0; a < 3; ++a) {
+          const float v = K[3 * k + a];
+          mn[a] = fminf(mn[a], v);
+          mx[a] = fmaxf(mx[a], v);
+        }
       }
     }
-  }
 #pragma unroll
-  for (int a = 0; a < 3; ++a) {
-    mn[a] = wave_min_f(mn[a]);
-    mx[a] = wave_max_f(mx[a]);
-  }
-  if (lane == 0) {
-#pragma unroll
-    for (int a = 0; a < 3; ++a) { red[a][w] = mn[a]; red[3 + a][w] = mx[a]; }
-  }
-  __syncthreads();
-  if (t == 0) {
-    float lo[3], hi[3];
     for (int a = 0; a < 3; ++a) {
-      lo[a] = red[a][0];
-      hi[a] = red[3 + a][0];
-      for (int i = 1; i < NW; ++i) { lo[a] = fminf(lo[a], red[a][i]); hi[a] = fmaxf(hi[a], red[3 + a][i]); }
-      if (!(hi[a] >= lo[a])) { lo[a] = 0.0f; hi[a] = 0.0f; }  // NaN-only axis
+      mn[a] = wave_min_f(mn[a]);
+      mx[a] = wave_max_f(mx[a]);
     }
-    *shp = grid_dims(lo, hi, m, 0.0f, kFpgPointsPerCell);
-  }
-  __syncthreads();
-  const GridHdr h = *shp;
-  auto cell_at = [&](float x, float y, float z) {
-    const int ix = cell_coord(x, h.ox, h.inv, h.nx);
-    const int iy = cell_coord(y, h.oy, h.inv, h.ny);
-    const int iz = cell_coord(z, h.oz, h.inv, h.nz);
-    return (iz * h.ny + iy) * h.nx + ix;
-  };
-
-  // 2. counting sort in one atomic pass: each point's count atomic (16-bit halves of 32-bit
-  // words; counts <= m < 2^16) returns its rank in its cell, kept with its cell in registers;
-  // an exclusive scan turns the counts into the cells' offsets; the scatter needs no cursor
-  for (int i = t; i < (h.ncell + 2) / 2; i += kNNBlock) s_cnt[i] = 0u;
-  __syncthreads();
-  int kc[KPT], kr[KPT];
+    if (lane == 0) {
 #pragma unroll
-  for (int i = 0; i < KPT; ++i) {
-    const int k = t + i * kNNBlock;
-    kc[i] = 0;
-    kr[i] = 0;
-    if (k < m) {
-      const int c = cell_at(K[3 * k + 0], K[3 * k + 1], K[3 * k + 2]);
-      const int sh = 16 * (c & 1);
-      const uint32_t old = atomicAdd(&s_cnt[c >> 1], 1u << sh);
-      kc[i] = c;
-      kr[i] = (int)((old >> sh) & 0xFFFFu);
+      for (int a = 0; a < 3; ++a) { red[a][w] = mn[a]; red[3 + a][w] = mx[a]; }
     }
-  }
-  __syncthreads();
-  {
-    const int per = (h.ncell + kNNBlock - 1) / kNNBlock;
-    const int s0 = t * per, s1 = min(s0 + per, h.ncell);
-    int sum = 0;
-    for (int i = s0; i < s1; ++i) sum += s_off[i];
-    const int incl = wave_incl_scan(sum, lane);
-    if (lane == kWave - 1) wsum[w] = incl;
     __syncthreads();
-    int base = incl - sum;
-    for (int i = 0; i < w; ++i) base += wsum[i];
-    for (int i = s0; i < s1; ++i) {
-      const int c = s_off[i];
-      s_off[i] = (uint16_t)base;
-      base += c;
+    if (t == 0) {
+      float lo[3], hi[3];
+      for (int a = 0; a < 3; ++a) {
+        lo[a] = red[a][0];
+        hi[a] = red[3 + a][0];
+        for (int i = 1; i < NW; ++i) { lo[a] = fminf(lo[a], red[a][i]); hi[a] = fmaxf(hi[a], red[3 + a][i]); }
+        if (!(hi[a] >= lo[a])) { lo[a] = 0.0f; hi[a] = 0.0f; }  // NaN-only axis
+      }
+      *shp = grid_dims(lo, hi, m, 0.0f, kFpgPointsPerCell);
     }
-    if (t == 0) s_off[h.ncell] = (uint16_t)m;
-  }
-  __syncthreads();
+    __syncthreads();
+    h = *shp;
+    auto cell_at = [&](float x, float y, float z) {
+      const int ix = cell_coord(x, h.ox, h.inv, h.nx);
+      const int iy = cell_coord(y, h.oy, h.inv, h.ny);
+      const int iz = cell_coord(z, h.oz, h.inv, h.nz);
+      return (iz * h.ny + iy) * h.nx + ix;
+    };
+
+    // 2. counting sort in one atomic pass: each point's count atomic (16-bit halves of 32-bit
+    // words; counts <= m < 2^16) returns its rank in its cell, kept with its cell in registers;
+    // an exclusive scan turns the counts into the cells' offsets; the scatter needs no cursor
+    for (int i = t; i < (h.ncell + 2) / 2; i += FB) s_cnt[i] = 0u;
+    __syncthreads();
+    int kc[KPT], kr[KPT];
 #pragma unroll
-  for (int i = 0; i < KPT; ++i) {
-    const int k = t + i * kNNBlock;
-    if (k < m)
-      s_pts[s_off[kc[i]] + kr[i]] = make_float4(K[3 * k + 0], K[3 * k + 1], K[3 * k + 2],
-                                                __int_as_float(k));
+    for (int i = 0; i < KPT; ++i) {
+      const int k = t + i * FB;
+      kc[i] = 0;
+      kr[i] = 0;
+      if (k < m) {
+        const int c = cell_at(K[3 * k + 0], K[3 * k + 1], K[3 * k + 2]);
+        const int sh = 16 * (c & 1);
+        const uint32_t old = atomicAdd(&s_cnt[c >> 1], 1u << sh);
+        kc[i] = c;
+        kr[i] = (int)((old >> sh) & 0xFFFFu);
+      }
+    }
+    __syncthreads();
+    {
+      const int per = (h.ncell + FB - 1) / FB;
+      const int s0 = t * per, s1 = min(s0 + per, h.ncell);
+      int sum = 0;
+      for (int i = s0; i < s1; ++i) sum += s_off[i];
+      const int incl = wave_incl_scan(sum, lane);
+      if (lane == kWave - 1) wsum[w] = incl;
+      __syncthreads();
+      int base = incl - sum;
+      for (int i = 0; i < w; ++i) base += wsum[i];
+      for (int i = s0; i < s1; ++i) {
+        const int c = s_off[i];
+        s_off[i] = (uint16_t)base;
+        base += c;
+      }
+      if (t == 0) s_off[h.ncell] = (uint16_t)m;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < KPT; ++i) {
+      const int k = t + i * FB;
+      if (k < m)
+        s_pts[s_off[kc[i]] + kr[i]] = make_float4(K[3 * k + 0], K[3 * k + 1], K[3 * k + 2],
+                                                  __int_as_float(k));
+    }
+    __syncthreads();
   }
-  __syncthreads();
 
   // 3. the search, a quad per unknown (the quad's lanes share j)
   const int jl = t / kNNGroup, q = t & (kNNGroup - 1);
@@ -759,7 +786,7 @@ __global__ __launch_bounds__(kNNBlock) void fp_grid_fused_kernel(FpLayer p, floa
   }
   __syncthreads();
   // 4. the rows
-  fp_write_rows<V2, V1, UN>(p, b, 0, j0, [&](int rl) {
+  fp_write_rows<V2, V1, UN, FB>(p, b, 0, j0, [&](int rl) {
     const int4 I = s_idx[rl];
     return FpRow{I, make_float4(s_wv[0][rl], s_wv[1][rl], s_wv[2][rl], 0.0f), I.w};
   });
@@ -875,20 +902,25 @@ int fp_launch(const float* xyz1, const float* xyz2, const float* pdist, const in
 // workgroup searches its rows once)
 int fp_grid_launch(const float* xyz1, const float* xyz2, const void* ugrid, const float* points1,
                    int C1, const float* points2, int C2, int B, int n, int m, float* out,
-                   float* dist, int32_t* idx, hipStream_t stream) {
+                   float* dist, int32_t* idx, const void* kgrid, hipStream_t stream) {
   FpPlan f;
   const int rc = fp_plan(xyz1, xyz2, nullptr, nullptr, ugrid, points1, C1, points2, C2, B, n, m,
                          out, f, /*split=*/false);
   if (rc != PN2_OK) return rc;
-  const dim3 grid(xcd_grid(f.blocks)), blk(kNNBlock);
+  const dim3 grid(xcd_grid((long long)((n + kFpgBlock / kNNGroup - 1) / (kFpgBlock / kNNGroup)) *
+                           B)),
+      blk(kFpgBlock);
   const size_t lds = fp_grid_lds(m);
   // the known grid must fit this device's LDS per workgroup (160 KB on gfx950; m = 4096 needs
   // ~74 KB): a smaller part reports PN2_EINVAL, and fp_interpolate then takes the three-launch
   // path (grid build + three_nn_grid + fp_apply)
-  if (lds + 2048 > device_lds_per_block()) return PN2_EINVAL;
+  constexpr int FR = kFpgBlock / kNNGroup;
+  if (lds + 28 * FR + 64 > device_lds_per_block()) return PN2_EINVAL;  // (+ s_idx, s_wv, hdr)
+  if ((long long)FR * f.p.cw * f.p.cw >= (1LL << 32)) return PN2_EINVAL;
+  const char* kg = (const char*)kgrid;
 #define PN2_FPG_K(V2, V1, U)                                                                   \
-  if (m <= 4 * kNNBlock) hipLaunchKernelGGL((fp_grid_fused_kernel<V2, V1, U, 4>), grid, blk, lds, stream, f.p, dist, idx); \
-  else hipLaunchKernelGGL((fp_grid_fused_kernel<V2, V1, U, kFpGridMaxKnown / kNNBlock>), grid, blk, lds, stream, f.p, dist, idx)
+  if (m <= 4 * kFpgBlock) hipLaunchKernelGGL((fp_grid_fused_kernel<V2, V1, U, 4, kFpgBlock>), grid, blk, lds, stream, f.p, dist, idx, kg); \
+  else hipLaunchKernelGGL((fp_grid_fused_kernel<V2, V1, U, (kFpGridMaxKnown + kFpgBlock - 1) / kFpgBlock, kFpgBlock>), grid, blk, lds, stream, f.p, dist, idx, kg)
 #define PN2_FPG(V2, V1) PN2_FPG_K(V2, V1, kFpUnroll);
   if (f.v1) { PN2_FPG(4, 4) }
   else if (f.v2) { PN2_FPG(4, 1) }
@@ -1056,7 +1088,24 @@ int pn2_fp_grid_fused(const float* xyz1, const float* xyz2, const void* unknown_
   if (!xyz2 || (!xyz1 && !unknown_grid) || !out || (C2 > 0 && !points2))
     return PN2_EINVAL;
   return pn2::fp_grid_launch(xyz1, xyz2, unknown_grid, points1, C1, points2, C2, B, n, m, out,
-                             dist, idx, (hipStream_t)stream);
+                             dist, idx, nullptr, (hipStream_t)stream);
+}
+
+int pn2_fp_grid_fused_known(const void* known_grid, const float* xyz1, const float* xyz2,
+                            const void* unknown_grid, const float* points1, int C1,
+                            const float* points2, int C2, int B, int n, int m, float* out,
+                            float* dist, int32_t* idx, pn2_stream_t stream) {
+  if (!known_grid || ((uintptr_t)known_grid & 15)) return PN2_EINVAL;
+  if (B < 0 || n < 0 || m < 1 || m > pn2::kFpGridMaxKnown || C1 < 0 || C2 < 0 || B > 65535)
+    return PN2_EINVAL;
+  if (!points1 && C1 != 0) return PN2_EINVAL;
+  if ((dist == nullptr) != (idx == nullptr)) return PN2_EINVAL;
+  if ((long long)B * n == 0) return PN2_OK;
+  if (C1 + C2 == 0) return dist ? PN2_EINVAL : PN2_OK;
+  if (!xyz2 || (!xyz1 && !unknown_grid) || !out || (C2 > 0 && !points2))
+    return PN2_EINVAL;
+  return pn2::fp_grid_launch(xyz1, xyz2, unknown_grid, points1, C1, points2, C2, B, n, m, out,
+                             dist, idx, known_grid, (hipStream_t)stream);
 }
 
 int pn2_three_nn_grid(const void* known_grid, const void* unknown_grid, const float* xyz1,

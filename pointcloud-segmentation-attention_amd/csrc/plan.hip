@@ -27,6 +27,8 @@ struct Op {
   int npoint[4];
   int32_t* idx[4];
   float* nx[4];
+  void* grid0;  // stage 0's picks' grid (pn2_fps_chain_grid) or NULL
+  size_t grid0_bytes;
   // kKernel / kMemset: a node of a captured graph, launched directly (pn2_plan_graph_direct);
   // the argument arrays belong to the graph, which the caller keeps alive
   hipKernelNodeParams kp;
@@ -52,7 +54,7 @@ int run_op(const Op& o) {
       return (int)hipStreamWaitEvent(o.stream, (hipEvent_t)o.handle, 0);
     case kFpsChain:
       return pn2::fps_chain_launch(o.xyz, o.B, o.N, o.nstages, o.npoint, o.idx, o.nx, o.stream,
-                                   false);
+                                   false, o.grid0, o.grid0_bytes);
     case kKernel:
       return (int)hipLaunchKernel(o.kp.func, o.kp.gridDim, o.kp.blockDim, o.kp.kernelParams,
                                   o.kp.sharedMemBytes, o.stream);
@@ -136,8 +138,18 @@ int pn2_plan_wait(pn2_plan* plan, pn2_stream_t stream, void* event) {
 int pn2_plan_fps_chain(pn2_plan* plan, const float* xyz, int B, int N, int nstages,
                        const int* npoint, int32_t* const* idx, float* const* new_xyz,
                        pn2_stream_t stream) {
+  return pn2_plan_fps_chain_grid(plan, xyz, B, N, nstages, npoint, idx, new_xyz, nullptr, 0,
+                                 stream);
+}
+
+int pn2_plan_fps_chain_grid(pn2_plan* plan, const float* xyz, int B, int N, int nstages,
+                            const int* npoint, int32_t* const* idx, float* const* new_xyz,
+                            void* grid0, size_t grid0_bytes, pn2_stream_t stream) {
   const int rc = pn2::fps_chain_check(xyz, B, N, nstages, npoint, idx, new_xyz);
   if (rc != PN2_OK) return rc;
+  if (grid0 && (!new_xyz[0] || grid0_bytes < pn2_grid_size(B, npoint[0]) ||
+                ((uintptr_t)grid0 & 15)))
+    return PN2_EINVAL;
   Op o = blank(kFpsChain, (hipStream_t)stream, nullptr);
   o.xyz = xyz;
   o.B = B;
@@ -148,6 +160,8 @@ int pn2_plan_fps_chain(pn2_plan* plan, const float* xyz, int B, int N, int nstag
     o.idx[i] = idx[i];
     o.nx[i] = new_xyz[i];
   }
+  o.grid0 = grid0;
+  o.grid0_bytes = grid0_bytes;
   return append(plan, o);
 }
 

@@ -12,6 +12,7 @@ import ctypes
 
 import torch
 
+from . import tf_sampling
 from ._lib import PN2_ENOTSUP, InvalidArgumentError, check, lib
 
 
@@ -71,8 +72,9 @@ class Plan:
         check(self._lib.pn2_plan_wait(self.h, stream.cuda_stream, _event_handle(ev)),
               "pn2_plan_wait")
 
-    def fps_chain(self, npoints, xyz, outs, stream):
-        """pn2_fps_chain(npoints) of `xyz` into the fixed buffers `outs` [(idx, new_xyz)]."""
+    def fps_chain(self, npoints, xyz, outs, stream, grid0=None):
+        """pn2_fps_chain(npoints) of `xyz` into the fixed buffers `outs` [(idx, new_xyz)];
+        with grid0 (tf_sampling.farthest_point_sample_chain's) pn2_fps_chain_grid."""
         npoints = [int(m) for m in npoints]
         if (xyz.dim() != 3 or xyz.shape[2] != 3 or xyz.dtype != torch.float32
                 or not xyz.is_contiguous() or len(outs) != len(npoints)):
@@ -89,7 +91,14 @@ class Plan:
         arr_i = (ctypes.c_int * k)(*npoints)
         arr_idx = (ctypes.c_void_p * k)(*[o[0].data_ptr() for o in outs])
         arr_nx = (ctypes.c_void_p * k)(*[o[1].data_ptr() for o in outs])
-        self._keep += [xyz, outs, stream, arr_i, arr_idx, arr_nx]
+        self._keep += [xyz, outs, stream, arr_i, arr_idx, arr_nx, grid0]
+        if grid0 is not None:
+            tf_sampling.check_grid0(grid0, outs[0][1])
+            check(self._lib.pn2_plan_fps_chain_grid(
+                self.h, xyz.data_ptr(), B, N, k, ctypes.addressof(arr_i),
+                ctypes.addressof(arr_idx), ctypes.addressof(arr_nx), grid0.buf.data_ptr(),
+                grid0.nbytes, stream.cuda_stream), "pn2_plan_fps_chain_grid")
+            return
         check(self._lib.pn2_plan_fps_chain(self.h, xyz.data_ptr(), B, N, k,
                                            ctypes.addressof(arr_i), ctypes.addressof(arr_idx),
                                            ctypes.addressof(arr_nx), stream.cuda_stream),

@@ -310,7 +310,29 @@ def fp_interpolate(xyz1, xyz2, points1, points2, known_grid=None, unknown_grid=N
     else:
         C1 = 0
     nn = None
-    if known_grid is None and tf_interpolate.use_grid(n, m) and m <= FP_GRID_MAX_KNOWN \
+    if known_grid is not None and known_grid.cell_edge <= 0 and m <= FP_GRID_MAX_KNOWN \
+            and C1 + C2 > 0 and tf_interpolate.use_grid(n, m):
+        # one launch over the known points' prebuilt grid (pn2_fp_grid_fused_known: the SA1
+        # sampler built it, pn2_fps_chain_grid), staged into each workgroup's LDS
+        if not known_grid.matches(xyz2) or (unknown_grid is not None
+                                            and not unknown_grid.matches(xyz1)):
+            raise InvalidArgumentError("fp_interpolate: a grid was built over other points")
+        out = torch.empty((B, n, C2 + C1), dtype=torch.float32, device=xyz1.device)
+        if return_nn:
+            nn = (torch.empty((B, n, 3), dtype=torch.float32, device=xyz1.device),
+                  torch.empty((B, n, 3), dtype=torch.int32, device=xyz1.device))
+        rc = lib().pn2_fp_grid_fused_known(
+            ptr(known_grid.buf), ptr(xyz1), ptr(xyz2),
+            None if unknown_grid is None else ptr(unknown_grid.buf),
+            ptr(points1), C1, ptr(points2), C2, B, n, m, ptr(out),
+            ptr(nn[0]) if nn else None, ptr(nn[1]) if nn else None, stream_of(xyz1))
+        if rc == PN2_EINVAL and B > 0 and n > 0:
+            # (the arguments are valid: the known grid does not fit this device's LDS)
+            nn = tf_interpolate.three_nn(xyz1, xyz2, known_grid, unknown_grid)
+            out = fp_apply(nn, points1, points2, unknown_grid)
+        else:
+            check(rc, "fp_interpolate")
+    elif known_grid is None and tf_interpolate.use_grid(n, m) and m <= FP_GRID_MAX_KNOWN \
             and C1 + C2 > 0:
         # one launch: each workgroup grids the known points in LDS, searches, writes its rows
         if unknown_grid is not None and not unknown_grid.matches(xyz1):

@@ -27,8 +27,8 @@ import time
 
 import torch
 
-from . import attention_layer, pointnet_util, synth, tf_grouping, tf_interpolate, tf_sampling, \
-    tf_util
+from . import attention_layer, grid, pointnet_util, synth, tf_grouping, tf_interpolate, \
+    tf_sampling, tf_util
 
 SSG_SA = ((1024, 0.1, 32, 64), (256, 0.2, 32, 128), (64, 0.4, 32, 256), (16, 0.8, 32, 512))
 SSG_FP_OUT = (256, 256, 128, 128)
@@ -40,6 +40,16 @@ SSG_FP_MLP = ((256, 256), (256, 256), (256, 128), (128, 128, 128))
 NUM_CLASSES = 21  # ScanNet (pointnet2_sem_seg_attention.py:17)
 # cell edge of the one grid that serves all of MSG SA1's radii (tools/bench_msg_grid.py)
 MSG_GRID_EDGE = 0.2  # 105 us for the three radii vs 110 at 0.1, 122 at 0.4 (profiles/r4/ab2)
+
+# FP4's known points (SA1's picks) gridded once per cloud instead of inside each of FP4's
+# workgroups (pn2_fp_grid_fused_known): "lane" = a grid build launch before FP4 on its lane,
+# "sampler" = by the SA1 sampler's own workgroups after the last pick (pn2_fps_chain_grid),
+# "off" = each FP4 workgroup sorts them in LDS (pn2_fp_grid_fused). None = per config
+# (FP4_KNOWN_GRID_BY_CONFIG, else "off"): the 500-step A/B (profiles/r5/kgrid2) gave cfg3
+# 60.6-60.8k with "lane" against 57.6-57.7k "off" (58.8k "sampler"), cfg2 87.2-87.4k "lane",
+# 87.9-88.4k "sampler", 88.5k "off". bench.py --fp4-known-grid overrides it.
+FP4_KNOWN_GRID = None
+FP4_KNOWN_GRID_BY_CONFIG = {"cfg3": "lane"}
 
 NSIDE = 4  # side streams of the whole-model step (the geometric steps use 3)
 MAX_LANES = 8  # lanes of any step layout (0 = the sampler stream)
@@ -297,8 +307,11 @@ class Step:
         def fp(i):
             def f():
                 k = 3 - i  # the FP layer whose coarse level (i+1) just became available
+                if i == 0 and v.get("kgrid") is not None and v["kgrid_mode"] == "lane":
+                    v["kgrid"].rebuild()
                 v["fp"][k], v["nn"][k] = pointnet_util.fp_interpolate(
                     v["xyz"][i], v["xyz"][i + 1], points[i], fp_feat[k],
+                    known_grid=v.get("kgrid") if i == 0 else None,
                     unknown_grid=v.get("grid1") if i == 0 else None, return_nn=True)
             return f
 
@@ -313,13 +326,23 @@ class Step:
                           for m in npoints]
             for i, (_, nx) in enumerate(v["chain"]):
                 v["xyz"][i + 1] = nx
+            # FP4's known points (SA1's picks) gridded by the SA1 sampler's own workgroups
+            # after the last pick (pn2_fps_chain_grid), not by each FP4 workgroup again
+            kgrid = None
+            mode = FP4_KNOWN_GRID or FP4_KNOWN_GRID_BY_CONFIG.get(inp["config"], "off")
+            v["kgrid_mode"] = mode
+            if mode != "off" and big and xyz.is_cuda and tf_interpolate.use_grid(
+                    int(xyz.shape[1]), npoints[0]) and npoints[0] <= pointnet_util.FP_GRID_MAX_KNOWN:
+                v["kgrid"] = grid.PointGrid(v["chain"][0][1], build=False)
+                if mode == "sampler":
+                    kgrid = v["kgrid"]
 
             # lane 0: SA1's sampler alone (bench.py times it); lane 4: SA2..SA4's samplers
             # fused in one launch, so the next step's SA1 sampler follows this one directly.
             # Both are direct launches into fixed buffers.
             tasks.append(Task("fps1", 0, (), lambda: tf_sampling.farthest_point_sample_chain(
-                npoints[:1], xyz, out=v["chain"][:1]), direct=True,
-                chain=(npoints[:1], xyz, v["chain"][:1])))
+                npoints[:1], xyz, out=v["chain"][:1], grid0=kgrid), direct=True,
+                chain=(npoints[:1], xyz, v["chain"][:1], kgrid)))
             tasks.append(Task("fps234", chain_lane, ("fps1",), lambda: tf_sampling.farthest_point_sample_chain(
                 npoints[1:], v["xyz"][1], out=v["chain"][1:]), direct=True,
                 chain=(npoints[1:], v["xyz"][1], v["chain"][1:])))
@@ -739,7 +762,8 @@ class Step:
             if seg[0].direct:
                 if seg[0].chain is None:
                     raise RuntimeError(f"task {seg[0].name}: a direct task needs its chain spec")
-                plan.fps_chain(*seg[0].chain, st)
+                c = seg[0].chain
+                plan.fps_chain(c[0], c[1], c[2], st, c[3] if len(c) > 3 else None)
             elif direct:
                 plan.graph_direct(graphs[self.segment_key(seg)], st)
             else:

@@ -64,12 +64,15 @@ def chain_supported(N, npoints):
             and all(0 < m <= CHAIN_MAX_FEED for m in npoints[:-1]) and npoints[-1] > 0)
 
 
-def farthest_point_sample_chain(npoints, inp, out=None):
+def farthest_point_sample_chain(npoints, inp, out=None, grid0=None):
     """The samplers of consecutive SA layers (pn2_fps_chain: a big first stage, then the rest
     fused in one launch): stage i samples
     npoints[i] points of stage i-1's new_xyz (stage 0 of inp (B,N,3)). Returns
     [(idx_i, new_xyz_i)], each exactly farthest_point_sample_and_gather(npoints[i], input_i).
-    `out` optionally supplies those tensors (written in place, e.g. a step's fixed buffers)."""
+    `out` optionally supplies those tensors (written in place, e.g. a step's fixed buffers).
+    grid0: a grid.PointGrid(out[0][1], build=False) (automatic edge) that the launch fills
+    with stage 0's picks (pn2_fps_chain_grid: the culled sampler grids them itself), so the
+    FP layer that interpolates onto the input cloud need not sort them again."""
     if inp.dim() != 3 or inp.shape[2] != 3:  # tf_sampling.cpp:105
         raise InvalidArgumentError("FarthestPointSample expects (batch_size,num_points,3) inp shape")
     npoints = [int(m) for m in npoints]
@@ -97,10 +100,25 @@ def farthest_point_sample_chain(npoints, inp, out=None):
     arr_i = (ctypes.c_int * k)(*npoints)
     arr_idx = (ctypes.c_void_p * k)(*[o[0].data_ptr() for o in outs])
     arr_nx = (ctypes.c_void_p * k)(*[o[1].data_ptr() for o in outs])
+    if grid0 is not None:
+        check_grid0(grid0, outs[0][1])
+        check(lib().pn2_fps_chain_grid(ptr(inp), B, N, k, ctypes.addressof(arr_i),
+                                       ctypes.addressof(arr_idx), ctypes.addressof(arr_nx),
+                                       ptr(grid0.buf), grid0.nbytes, stream_of(inp)),
+              "FarthestPointSample")
+        return outs
     check(lib().pn2_fps_chain(ptr(inp), B, N, k, ctypes.addressof(arr_i),
                               ctypes.addressof(arr_idx), ctypes.addressof(arr_nx),
                               stream_of(inp)), "FarthestPointSample")
     return outs
+
+
+def check_grid0(grid0, new_xyz0):
+    """grid0 must be an automatic-edge PointGrid allocated over stage 0's new_xyz tensor."""
+    if (grid0.cell_edge > 0 or grid0.xyz.data_ptr() != new_xyz0.data_ptr()
+            or not grid0.matches(new_xyz0)):
+        raise InvalidArgumentError("farthest_point_sample_chain: grid0 must be "
+                                   "PointGrid(out[0][1], build=False) (automatic edge)")
 
 
 def _check_gather(inp, idx, name="GatherPoint"):

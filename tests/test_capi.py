@@ -120,6 +120,20 @@ def test_grid_contract(pn2):
     assert lib.pn2_fp_grid_fused(None, None, None, None, 0, None, 4, 1, 10, 10, None, 1, None, None) == E
     assert lib.pn2_fp_grid_fused(None, None, None, None, 0, None, 4, 1, 10, 10, None, None, None, None) == E
     assert lib.pn2_fp_grid_fused(None, None, None, None, 0, None, 4, 0, 10, 10, None, None, None, None) == 0
+    # pn2_fp_grid_fused_known: a known grid is required (16-byte aligned), then the same checks
+    assert lib.pn2_fp_grid_fused_known(None, None, None, None, None, 0, None, 4, 0, 10, 10, None, None, None, None) == E
+    assert lib.pn2_fp_grid_fused_known(8, None, None, None, None, 0, None, 4, 0, 10, 10, None, None, None, None) == E
+    assert lib.pn2_fp_grid_fused_known(16, None, None, None, None, 0, None, 4, 1, 10, 4097, None, None, None, None) == E
+    assert lib.pn2_fp_grid_fused_known(16, None, None, None, None, 0, None, 4, 1, 10, 10, None, None, None, None) == E
+    assert lib.pn2_fp_grid_fused_known(16, None, None, None, None, 0, None, 4, 0, 10, 10, None, None, None, None) == 0
+    # pn2_fps_chain_grid: grid0 required, sized for stage 0 and aligned (checked before any launch)
+    npt = (ctypes.c_int * 1)(256)
+    bufs1 = (ctypes.c_void_p * 1)(16)
+    assert lib.pn2_fps_chain_grid(8, 2, 4096, 1, ctypes.addressof(npt), ctypes.addressof(bufs1),
+                                  ctypes.addressof(bufs1), None, 0, None) == E
+    assert lib.pn2_fps_chain_grid(8, 2, 4096, 1, ctypes.addressof(npt), ctypes.addressof(bufs1),
+                                  ctypes.addressof(bufs1), 4096, lib.pn2_grid_size(2, 256) - 1,
+                                  None) == E
 
 
 def test_fps_workspace_contract(pn2):
@@ -256,10 +270,21 @@ def test_plan_records_and_checks_without_launching(pn2):
                                       ctypes.addressof(bufs), None) == E
         assert lib.pn2_plan_fps_chain(p, None, 2, 4096, 2, ctypes.addressof(npoint),
                                       ctypes.addressof(bufs), ctypes.addressof(bufs), None) == E
+        # pn2_plan_fps_chain_grid: grid0 smaller than pn2_grid_size(B, npoint[0]) or not
+        # 16-byte aligned
+        need = lib.pn2_grid_size(2, 256)
+        for g, nb in ((4096, need - 1), (4104, need)):
+            assert lib.pn2_plan_fps_chain_grid(p, 8, 2, 4096, 2, ctypes.addressof(npoint),
+                                               ctypes.addressof(bufs), ctypes.addressof(bufs),
+                                               g, nb, None) == E
         assert lib.pn2_plan_size(p) == 0                   # nothing appended on error
         assert lib.pn2_plan_fps_chain(p, 8, 2, 4096, 2, ctypes.addressof(npoint),
                                       ctypes.addressof(bufs), ctypes.addressof(bufs), None) == 0
         assert lib.pn2_plan_size(p) == 1
+        assert lib.pn2_plan_fps_chain_grid(p, 8, 2, 4096, 2, ctypes.addressof(npoint),
+                                           ctypes.addressof(bufs), ctypes.addressof(bufs),
+                                           4096, need, None) == 0
+        assert lib.pn2_plan_size(p) == 2
         assert lib.pn2_plan_mark_timed(p) == 0
     finally:
         lib.pn2_plan_destroy(p)

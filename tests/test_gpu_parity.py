@@ -764,3 +764,94 @@ def test_fps_chain(env, kind, B, N, npoints):
         assert torch.equal(idx, ridx) and torch.equal(nx, rnx)
         assert np.array_equal(idx.cpu().numpy(), O.fps(cur_np, m))
         cur, cur_np = nx, nx.cpu().numpy()
+
+
+def _grid_parts(buf, B, N):
+    """(header words, offsets, per-cell sorted point rows) of every cloud of a grid buffer
+    (csrc/grid.h layout): the order of the points inside a cell is not part of the contract."""
+    import numpy as np_
+    kcap = 32768
+    off_bytes = ((32 + (kcap + 1) * 4) + 15) & ~15
+    stride = off_bytes + N * 16
+    raw = buf.cpu().numpy()
+    out = []
+    for b in range(B):
+        g = raw[b * stride:(b + 1) * stride]
+        hdr = g[:32].view(np_.uint32)
+        ncell = int(g[28:32].view(np_.int32)[0])
+        off = g[32:32 + (ncell + 1) * 4].view(np_.int32).copy()
+        pts = g[off_bytes:off_bytes + N * 16].view(np_.uint32).reshape(N, 4)
+        cells = [sorted(map(tuple, pts[off[c]:off[c + 1]])) for c in range(ncell)]
+        out.append((hdr.copy(), off, cells))
+    return out
+
+
+@pytest.mark.parametrize("kind,B,N,npoints", [
+    ("scannet", 3, 8192, [1024, 256, 64, 16]),  # culled sampler: grid built in its epilogue
+    ("scannet", 1, 8192, [4096]),               # the epilogue's bound (M = 4096)
+    ("dup", 1, 8192, [1024]),                    # one repeated point: a single cell
+    ("uniform", 2, 3000, [700, 128, 32]),        # block-scan sampler + a grid build launch
+    ("uniform", 2, 900, [300, 40]),              # stage 0 inside the chain kernel
+    ("uniform", 2, 16384, [512])])               # MSG-size sampler + a grid build launch
+def test_fps_chain_grid(env, kind, B, N, npoints):
+    """pn2_fps_chain_grid: the chain's picks exactly as pn2_fps_chain, and grid0 = the
+    automatic-edge pn2_grid_build over stage 0's new_xyz (same header and cell offsets, same
+    points per cell); FP4 over it (pn2_fp_grid_fused_known, also through the native plan)
+    equals the fused scan bit for bit, and an explicit-edge known grid falls back to the
+    in-workgroup build with the same result."""
+    pkg, O, torch, dev = env
+    x = _cloud(pkg, kind, B, N)
+    xt = torch.from_numpy(x).to(dev)
+    ref = pkg.tf_sampling.farthest_point_sample_chain(npoints, xt)
+    outs = [(torch.empty_like(i), torch.empty_like(n)) for i, n in ref]
+    g0 = pkg.grid.PointGrid(outs[0][1], build=False)
+    g0.buf.fill_(0xA5)
+    pkg.tf_sampling.farthest_point_sample_chain(npoints, xt, out=outs, grid0=g0)
+    for (i, n), (ri, rn) in zip(outs, ref):
+        assert torch.equal(i, ri) and torch.equal(n, rn)
+    built = pkg.grid.PointGrid(ref[0][1])
+    for (h, o, c), (rh, ro, rc) in zip(_grid_parts(g0.buf, B, npoints[0]),
+                                       _grid_parts(built.buf, B, npoints[0])):
+        assert np.array_equal(h, rh) and np.array_equal(o, ro) and c == rc
+    # the same launch recorded in a native plan
+    outs2 = [(torch.empty_like(i), torch.empty_like(n)) for i, n in ref]
+    g2 = pkg.grid.PointGrid(outs2[0][1], build=False)
+    plan = pkg.plan.Plan()
+    st = torch.cuda.current_stream()
+    plan.fps_chain(npoints, xt, outs2, st, g2)
+    plan.launch()
+    torch.cuda.synchronize()
+    assert torch.equal(g2.buf, g0.buf) or all(
+        np.array_equal(a[1], b[1]) and a[2] == b[2]
+        for a, b in zip(_grid_parts(g2.buf, B, npoints[0]), _grid_parts(g0.buf, B, npoints[0])))
+    for (i, n), (ri, rn) in zip(outs2, ref):
+        assert torch.equal(i, ri) and torch.equal(n, rn)
+    # FP4 over the prebuilt grid
+    m = npoints[0]
+    if m < 3:
+        return
+    x2 = ref[0][1]
+    C1, C2 = 9, 64
+    p1 = torch.from_numpy(pkg.synth.features_uniform(1, (B, N, C1))).to(dev)
+    p2 = torch.from_numpy(pkg.synth.features_uniform(2, (B, m, C2))).to(dev)
+    L = pkg.lib()
+    fused = torch.empty((B, N, C1 + C2), device=dev)
+    assert L.pn2_fp_fused(xt.data_ptr(), x2.data_ptr(), p1.data_ptr(), C1, p2.data_ptr(), C2,
+                          B, N, m, fused.data_ptr(), st.cuda_stream) == 0
+    rd, ri = O.three_nn(x, x2.cpu().numpy())
+    ug = pkg.grid.PointGrid(xt, 0.1)
+    for kg in (g0, pkg.grid.PointGrid(x2, 0.02)):
+        for u in (None, ug):
+            out = torch.full((B, N, C1 + C2), float("nan"), device=dev)
+            d = torch.empty((B, N, 3), device=dev)
+            i = torch.empty((B, N, 3), dtype=torch.int32, device=dev)
+            assert L.pn2_fp_grid_fused_known(
+                kg.buf.data_ptr(), xt.data_ptr(), x2.data_ptr(),
+                None if u is None else u.buf.data_ptr(), p1.data_ptr(), C1, p2.data_ptr(), C2,
+                B, N, m, out.data_ptr(), d.data_ptr(), i.data_ptr(), st.cuda_stream) == 0
+            assert torch.equal(out, fused)
+            assert np.array_equal(i.cpu().numpy(), ri)
+            assert np.array_equal(_bits(d.cpu().numpy()), _bits(rd))
+    if pkg.tf_interpolate.use_grid(N, m):
+        a = pkg.pointnet_util.fp_interpolate(xt, x2, p1, p2, known_grid=g0, unknown_grid=ug)
+        assert torch.equal(a, fused)

@@ -67,10 +67,13 @@ def main():
     ap.add_argument("--reps", type=int, default=15)
     ap.add_argument("--inner", type=int, default=10)
     ap.add_argument("--json", default=None)
+    ap.add_argument("--fp4-known-grid", choices=["lane", "sampler", "off"], default=None,
+                    help="stack.FP4_KNOWN_GRID (A/B)")
     args = ap.parse_args()
     import torch
     pkg = importlib.import_module("pointcloud-segmentation-attention_amd")
     S = pkg.stack
+    S.FP4_KNOWN_GRID = args.fp4_known_grid
     dev = torch.device("cuda:0")
     B = 8 if args.config == "cfg5" else 16
     inp = S.make_inputs(args.config, list(range(B)), dev)
