@@ -22,6 +22,19 @@ namespace {
 
 constexpr int kBlock = 256;
 constexpr int kWavesPerBlock = kBlock / kWave;
+// tasks in flight per wave; blocks per CU before the grid strides (8 x 4 waves = a full CU);
+// K / V loaded non-temporal (streamed once). The four SSG layers in one launch, no data reused
+// from the last-level cache (tools/bench_attn.py `layers4`, profiles/r5/attn*): 117 us with
+// 16 blocks per CU and plain loads, 107 non-temporal, 99.7 non-temporal at 8 blocks per CU
+// (5.2 TB/s); 4 tasks in flight or 1, and 4 or 32 blocks per CU, were slower
+constexpr int kAttnTif = 2;
+constexpr int kAttnBlocksPerCu = 8;
+// K / V are streamed once: non-temporal loads (no reuse in the caches)
+PN2_DEV float4 ld_stream(const float* p) {
+  using v4 = float __attribute__((ext_vector_type(4)));
+  const v4 r = __builtin_nontemporal_load(reinterpret_cast<const v4*>(p));
+  return make_float4(r.x, r.y, r.z, r.w);
+}
 
 PN2_DEV float dot4(float4 q, float4 k) {  // (1x4)·(4x1) of tf.matmul, summed left to right
   float s = q.x * k.x;
@@ -115,8 +128,8 @@ __global__ __launch_bounds__(kBlock) void attn_reduce_kernel(AttnLayers A) {
 #pragma unroll
       for (int kk = 0; kk < KPL; ++kk) {
         const int s = sl + kk * LPH;
-        k[i][kk] = *reinterpret_cast<const float4*>(Kh + 4 * s);
-        v[i][kk] = *reinterpret_cast<const float4*>(Vh + 4 * s);
+        k[i][kk] = ld_stream(Kh + 4 * s);
+        v[i][kk] = ld_stream(Vh + 4 * s);
       }
       op[i] = L.out + (size_t)g * L.C + 4 * h;
     }
@@ -299,9 +312,9 @@ __global__ __launch_bounds__(kBlock) void group_pool_kernel(const float* __restr
   }
 }
 
-unsigned grid_for(long long waves) {
+unsigned grid_for(long long waves, int per_cu = 16) {
   long long blocks = (waves + kWavesPerBlock - 1) / kWavesPerBlock;
-  if (blocks > 256 * 16) blocks = 256 * 16;  // grid-stride beyond ~16 blocks per CU
+  if (blocks > 256LL * per_cu) blocks = 256LL * per_cu;  // grid-stride beyond
   return (unsigned)(blocks > 0 ? blocks : 1);
 }
 
@@ -319,8 +332,9 @@ void launch_attn(AttnLayers& A, hipStream_t s) {
     tasks += (long long)L.G * L.steps;
   }
   A.first[A.nlayers] = tasks;
-  constexpr int TIF = 2;
-  hipLaunchKernelGGL((attn_reduce_kernel<NS, TIF>), dim3(grid_for((tasks + TIF - 1) / TIF)),
+  constexpr int TIF = kAttnTif;
+  hipLaunchKernelGGL((attn_reduce_kernel<NS, TIF>),
+                     dim3(grid_for((tasks + TIF - 1) / TIF, kAttnBlocksPerCu)),
                      dim3(kBlock), 0, s, A);
 }
 

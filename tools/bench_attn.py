@@ -46,6 +46,22 @@ def main():
         us = timeit(run)
         nbytes = (Q.numel() + K.numel() + V.numel() + out.numel()) * 4
         res[name] = {"us": round(us, 1), "GBps": round(nbytes / us / 1e3, 0)}
+    # the four layers in one launch (pn2_attn_reduce_layers, what the cfg3 step runs)
+    import ctypes
+    bufs, tot = [], 0
+    arr = (pkg._lib.AttnLayer * 4)()
+    for i, (M, C) in enumerate(((1024, 64), (256, 128), (64, 256), (16, 512))):
+        Q = torch.rand((B, M, C), device=dev) - 0.5
+        K = torch.rand((B, M, ns, C), device=dev) - 0.5
+        V = torch.rand((B, M, ns, C), device=dev) - 0.5
+        out = torch.empty((B, M, C), device=dev)
+        bufs += [Q, K, V, out]
+        arr[i] = pkg._lib.AttnLayer(Q.data_ptr(), K.data_ptr(), V.data_ptr(), M, ns, C,
+                                    out.data_ptr())
+        tot += (Q.numel() + K.numel() + V.numel() + out.numel()) * 4
+    us = timeit(lambda: L.pn2_attn_reduce_layers(ctypes.addressof(arr), 4, B, st))
+    res["layers4"] = {"us": round(us, 1), "GBps": round(tot / us / 1e3, 0)}
+    res["lib"] = os.path.basename(os.environ.get("PN2HIP_LIB") or "libpn2hip.so")
     print(json.dumps(res), flush=True)
 
 
