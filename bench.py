@@ -568,9 +568,12 @@ def main():
                                       if args.chain.startswith("own") else 1,
                                       set_inputs=set_inputs,
                                       direct=not args.graph_launch)
+            # every buffer set's step once, before the warm-up (Pipeline.prime)
+            primed = pipe.prime()
         else:
             step = pkg.stack.Step(inp, overlap=overlap)
             graph = None if args.eager else pkg.stack.GraphStep(inp, overlap=overlap)
+            primed = 0
 
         def run_step(events=None):
             if pipelined:
@@ -612,7 +615,7 @@ def main():
             if getattr(pipe, "trace", None) is not None:
                 with open(args.timeline, "w") as fh:
                     json.dump({"elapsed_ms": elapsed * 1e3, "steps": pipe.finish_trace()}, fh)
-        post = {}
+        post = {"primed_steps": primed}
         # the sampler fault word (include/pn2hip.h pn2_fault_status) after the timed steps:
         # a fault raises here, so a fast but wrong line is never printed
         post["fault_status"] = pipe.check_faults() if pipelined else \
@@ -740,6 +743,10 @@ def main():
                          "achieved_GBps": step_bytes * world / (elapsed / args.steps) / 1e9,
                          "frac": step_bytes * world / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBPS},
             "checksum": float(sums.sum().item()),
+            "primed_steps": post.get("primed_steps"),
+            "primed_note": "before the warm-up steps, every buffer set's step ran once and was "
+                           "waited for (stack.Pipeline.prime): each set's first plan launch is "
+                           "then outside the timed region",
             "verified": post.get("verified"),
             "verify": post.get("verify"),
             "fault_status": post.get("fault_status"),
