@@ -588,6 +588,17 @@ constexpr float kFpgPointsPerCell = 2.0f;  // the LDS grid's points per cell (pr
 // 256-thread workgroup (54.9 / 80.9 us, profiles/r5/rpw): the search and the writes need
 // the workgroups' parallelism more than the build needs amortising
 constexpr int kFpgBlock = 256;
+// DIAGNOSTIC build flag (tools/stamp_fp4.py): s_memtime at the phase boundaries of the first
+// 4096 workgroups, read back with pn2_fpg_stamps()
+#ifndef PN2_FPG_STAMP
+#define PN2_FPG_STAMP 0
+#endif
+#if PN2_FPG_STAMP
+__device__ unsigned long long g_fpg_stamp[4096 * 8];
+#define PN2_FPG_T(K) if (t == 0 && Lg < 4096) g_fpg_stamp[Lg * 8 + (K)] = __builtin_amdgcn_s_memtime();
+#else
+#define PN2_FPG_T(K)
+#endif
 
 // LDS per workgroup of the current device (cached per device id)
 size_t device_lds_per_block() {
@@ -644,6 +655,7 @@ __global__ __launch_bounds__(FB) void fp_grid_fused_kernel(FpLayer p, float* __r
   const int t = threadIdx.x, lane = t & (kWave - 1), w = t / kWave;
   uint16_t* s_off = reinterpret_cast<uint16_t*>(s_pts + m);
   uint32_t* s_cnt = reinterpret_cast<uint32_t*>(s_pts + m);  // the offsets as counter pairs
+  PN2_FPG_T(0)
   GridHdr h;
   bool built = false;
   if (kgrid) {  // the prebuilt grid, when its offsets fit the LDS's max(m, 64) + 1
@@ -696,6 +708,7 @@ __global__ __launch_bounds__(FB) void fp_grid_fused_kernel(FpLayer p, float* __r
     }
     __syncthreads();
     h = *shp;
+    PN2_FPG_T(1)
     auto cell_at = [&](float x, float y, float z) {
       const int ix = cell_coord(x, h.ox, h.inv, h.nx);
       const int iy = cell_coord(y, h.oy, h.inv, h.ny);
@@ -751,6 +764,7 @@ __global__ __launch_bounds__(FB) void fp_grid_fused_kernel(FpLayer p, float* __r
     __syncthreads();
   }
 
+  PN2_FPG_T(2)
   // 3. the search, a quad per unknown (the quad's lanes share j)
   const int jl = t / kNNGroup, q = t & (kNNGroup - 1);
   const int j = j0 + jl;
@@ -785,11 +799,13 @@ __global__ __launch_bounds__(FB) void fp_grid_fused_kernel(FpLayer p, float* __r
     }
   }
   __syncthreads();
+  PN2_FPG_T(3)
   // 4. the rows
   fp_write_rows<V2, V1, UN, FB>(p, b, 0, j0, [&](int rl) {
     const int4 I = s_idx[rl];
     return FpRow{I, make_float4(s_wv[0][rl], s_wv[1][rl], s_wv[2][rl], 0.0f), I.w};
   });
+  PN2_FPG_T(4)
 }
 
 // Several FP layers in one launch (the FP layers that wait for the same sampler): logical
@@ -1090,6 +1106,14 @@ int pn2_fp_grid_fused(const float* xyz1, const float* xyz2, const void* unknown_
   return pn2::fp_grid_launch(xyz1, xyz2, unknown_grid, points1, C1, points2, C2, B, n, m, out,
                              dist, idx, nullptr, (hipStream_t)stream);
 }
+
+#if PN2_FPG_STAMP
+int pn2_fpg_stamps(unsigned long long* host_out) {  // 4096 x 8 u64 (DIAGNOSTIC builds only)
+  return (int)hipMemcpyFromSymbol(host_out, HIP_SYMBOL(pn2::g_fpg_stamp),
+                                  sizeof(unsigned long long) * 4096 * 8, 0,
+                                  hipMemcpyDeviceToHost);
+}
+#endif
 
 int pn2_fp_grid_fused_known(const void* known_grid, const float* xyz1, const float* xyz2,
                             const void* unknown_grid, const float* points1, int C1,
