@@ -49,16 +49,30 @@ PN2_DEV int cell_coord(float v, float o, float inv, int n) {
 
 constexpr float kAutoPointsPerCell = 2.0f;
 
-PN2_DEV float wave_min_f(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, kWave));
+// min / max over the wave (every lane gets it): DPP within rows of 16, then the gfx950
+// permlane swaps across rows -- no LDS crossbar round trip per step (ds_bpermute shuffles)
+template <bool MAX>
+PN2_DEV float wave_minmax_f(float v) {
+  auto op = [](float a, float b) { return MAX ? fmaxf(a, b) : fminf(a, b); };
+#define PN2_MM_DPP(C) v = op(v, __int_as_float(__builtin_amdgcn_update_dpp( \
+                             __float_as_int(v), __float_as_int(v), C, 0xF, 0xF, false)))
+  PN2_MM_DPP(kDppXor1);
+  PN2_MM_DPP(kDppXor2);
+  PN2_MM_DPP(kDppHalfMirror);
+  PN2_MM_DPP(kDppMirror);
+#undef PN2_MM_DPP
+  {
+    auto x = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = op(__uint_as_float(x[0]), __uint_as_float(x[1]));
+  }
+  {
+    auto x = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = op(__uint_as_float(x[0]), __uint_as_float(x[1]));
+  }
   return v;
 }
-PN2_DEV float wave_max_f(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, kWave));
-  return v;
-}
+PN2_DEV float wave_min_f(float v) { return wave_minmax_f<false>(v); }
+PN2_DEV float wave_max_f(float v) { return wave_minmax_f<true>(v); }
 PN2_DEV int wave_incl_scan(int v, int lane) {
 #pragma unroll
   for (int o = 1; o < kWave; o <<= 1) {
