@@ -406,7 +406,8 @@ PN2_DEV void fp_write_rows(const FpLayer& p, int b, int zb, int j0, RowFn row) {
   const int nrows = min(FB / kNNGroup, n - j0);
   const int elems = nrows * cw;
   using V2T = typename std::conditional<V2 == 4, float4, float>::type;
-  using V1T = typename std::conditional<V1 == 4, float4, float>::type;
+  using V1T = typename std::conditional<
+      V1 == 4, float4, typename std::conditional<V1 == 2, float2, float>::type>::type;
   const V2T* P2 = reinterpret_cast<const V2T*>(points2 + (size_t)b * m * C2);
   const float* P1 = points1 + (size_t)b * n * C1;
   float* O = out + (size_t)b * n * Cout;
@@ -489,6 +490,9 @@ PN2_DEV void fp_write_rows(const FpLayer& p, int b, int zb, int j0, RowFn row) {
         v.w = (a[u].w * W[u].x + bb[u].w * W[u].y) + cc[u].w * W[u].z;
         if (V1 == 4 || (o[u] & 3) == 0) {  // 16 B aligned (always when C1 % 4 == 0)
           *reinterpret_cast<float4*>(O + o[u]) = v;
+        } else if (V1 == 2) {  // an even row width (C1 % 2 == 0): 8 B aligned, two float2
+          *reinterpret_cast<float2*>(O + o[u]) = make_float2(v.x, v.y);
+          *reinterpret_cast<float2*>(O + o[u] + 2) = make_float2(v.z, v.w);
         } else {  // a row of odd width C2 + C1 starts off 16 B: four dword stores
           O[o[u]] = v.x;
           O[o[u] + 1] = v.y;
@@ -899,8 +903,13 @@ int fp_plan(const float* xyz1, const float* xyz2, const float* pdist, const int3
   // interpolated columns of 4 floats when C2 % 4 == 0 (16 B aligned loads and, on rows that
   // start 16 B aligned, stores); concat columns of 4 when C1 % 4 == 0 as well
   const bool v2 = C2 % 4 == 0 && ((((uintptr_t)points2 | (uintptr_t)out) & 15) == 0);
-  const bool v1 = v2 && C1 % 4 == 0 && (((uintptr_t)points1 & 15) == 0);
-  const int coutv = C2 / (v2 ? 4 : 1) + C1 / (v1 ? 4 : 1);
+  // concat columns of 4 floats when C1 % 4 == 0 (16 B aligned), of 2 when C1 is even
+  // (cfg3's C1 = 6: rows of C2 + 6 floats start 8 B aligned; float2 loads and stores instead
+  // of dwords), else 1
+  const int v1 = !v2 ? 1
+                 : C1 % 4 == 0 && (((uintptr_t)points1 & 15) == 0) ? 4
+                 : C1 % 2 == 0 && (((uintptr_t)points1 & 7) == 0) ? 2 : 1;
+  const int coutv = C2 / (v2 ? 4 : 1) + C1 / v1;
   const int row_blocks = (n + kNNRows - 1) / kNNRows;
   // split the channels over grid.z until ~2 workgroups per CU, keeping >= 16 vector columns
   // per workgroup and (search variant) not re-running a long known-point scan too often
@@ -931,7 +940,8 @@ constexpr int kFpUnroll = 2;
   do {                                                                                         \
     const dim3 grid__(xcd_grid(blocks));                                                       \
     const int tile__ = std::max(1, std::min((int)(MAXM), kNNTile));                            \
-    if ((f).v1) { PN2_FP_PRE(KERNEL, 4, 4, f, arg, grid__, tile__, stream); }                  \
+    if ((f).v1 == 4) { PN2_FP_PRE(KERNEL, 4, 4, f, arg, grid__, tile__, stream); }             \
+    else if ((f).v1 == 2) { PN2_FP_PRE(KERNEL, 4, 2, f, arg, grid__, tile__, stream); }        \
     else if ((f).v2) { PN2_FP_PRE(KERNEL, 4, 1, f, arg, grid__, tile__, stream); }             \
     else { PN2_FP_PRE(KERNEL, 1, 1, f, arg, grid__, tile__, stream); }                         \
   } while (0)
@@ -973,7 +983,8 @@ int fp_grid_launch(const float* xyz1, const float* xyz2, const void* ugrid, cons
   if (m <= 4 * kFpgBlock) hipLaunchKernelGGL((fp_grid_fused_kernel<V2, V1, U, 4, kFpgBlock>), grid, blk, lds, stream, f.p, dist, idx, kg); \
   else hipLaunchKernelGGL((fp_grid_fused_kernel<V2, V1, U, (kFpGridMaxKnown + kFpgBlock - 1) / kFpgBlock, kFpgBlock>), grid, blk, lds, stream, f.p, dist, idx, kg)
 #define PN2_FPG(V2, V1) PN2_FPG_K(V2, V1, kFpUnroll);
-  if (f.v1) { PN2_FPG(4, 4) }
+  if (f.v1 == 4) { PN2_FPG(4, 4) }
+  else if (f.v1 == 2) { PN2_FPG(4, 2) }
   else if (f.v2) { PN2_FPG(4, 1) }
   else { PN2_FPG(1, 1) }
 #undef PN2_FPG

@@ -395,7 +395,7 @@ FP_GRID_CASES = NN_GRID_CASES + [("scannet", 1, 8192, 4096)]  # m at the LDS bou
 
 
 @pytest.mark.parametrize("kind,B,n,m", FP_GRID_CASES)
-@pytest.mark.parametrize("C1,C2", [(0, 128), (9, 64), (8, 70)])
+@pytest.mark.parametrize("C1,C2", [(0, 128), (9, 64), (8, 70), (6, 128)])
 def test_fp_grid_fused(env, kind, B, n, m, C1, C2):
     """pn2_fp_grid_fused (each workgroup grids the known points in its own LDS, searches and
     writes its rows) = the oracle's three_nn (dist / idx bit-exact) and the fused scan's rows
@@ -435,6 +435,12 @@ def test_fp_grid_fused(env, kind, B, n, m, C1, C2):
         assert np.array_equal(_bits(d.cpu().numpy()), _bits(rd))
         if m >= 3:
             assert torch.equal(out, ref)
+            # the interpolated columns against the oracle too (not only the other HIP kernel),
+            # the concat columns as a copy
+            oref = O.fp_fused(x1, x2, p1.cpu().numpy() if C1 else None, p2.cpu().numpy())
+            np.testing.assert_allclose(out.cpu().numpy(), oref, **TOL)
+            if C1:
+                assert np.array_equal(_bits(out[..., C2:].cpu().numpy()), _bits(p1.cpu().numpy()))
         # without the neighbour outputs, through the op wrapper
         a = pkg.pointnet_util.fp_interpolate(t1, t2, p1 if C1 else None, p2, unknown_grid=u)
         if m >= 3 and pkg.tf_interpolate.use_grid(n, m):
@@ -469,7 +475,9 @@ def test_three_interpolate_and_idw(env, C):
                                        # evenly over the workgroups' channel slices
                                        # (__graft_entry__.smoke's FP layer: 2048 <- 256, 9 + 64)
                                        (2048, 256, 9, 64), (2048, 256, 9, 67), (1024, 128, 5, 60),
-                                       (4096, 512, 9, 64), (8192, 1024, 9, 70), (512, 64, 12, 52)])
+                                       (4096, 512, 9, 64), (8192, 1024, 9, 70), (512, 64, 12, 52),
+                                       # even C1 not a multiple of 4: float2 concat columns
+                                       (1024, 256, 6, 64), (512, 64, 2, 52), (256, 64, 10, 128)])
 def test_fp_fused(env, n, m, C1, C2):
     pkg, O, torch, dev = env
     x1 = _cloud(pkg, "scannet", 2, n, seed=11)
