@@ -93,14 +93,15 @@ PN2_DEV GridHdr grid_dims(const float lo[3], const float hi[3], int N, float edg
   // (then also at most max(N, 64) cells, which bounds the grid's size for LDS staging);
   // grown by 1.25x until the cells fit kGridCap;
   // degenerate extents (inf / NaN coordinates) fall back to one cell (inv = 0)
+  // (the automatic edge's cube root in fp32: any edge gives exact search results, and the
+  // double-precision cbrt held the building workgroup at its barrier)
   float c = edge;
   if (!(c > 0.0f)) {
     const float ext = fmaxf(fmaxf(hi[0] - lo[0], hi[1] - lo[1]), hi[2] - lo[2]);
-    const double cells = fmax((double)N / ppc, 1.0);
-    double e = cbrt((double)(hi[0] - lo[0]) * (hi[1] - lo[1]) * (hi[2] - lo[2]) / cells);
-    if (!(e > 0.0)) e = (double)ext / cbrt(cells);
-    c = (float)e;
-    if (!(c > 0.0f)) c = 1.0f;  // all points identical: any edge gives one cell
+    const float cells = fmaxf((float)N / ppc, 1.0f);
+    c = cbrtf((hi[0] - lo[0]) * (hi[1] - lo[1]) * (hi[2] - lo[2]) / cells);
+    if (!(c > 0.0f)) c = ext / cbrtf(cells);
+    if (!(c > 0.0f) || !(c < INFINITY)) c = 1.0f;  // all points identical: one cell
   }
   int n[3] = {1, 1, 1};
   bool ok = false;

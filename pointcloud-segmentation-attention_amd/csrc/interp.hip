@@ -604,41 +604,6 @@ __device__ unsigned long long g_fpg_stamp[4096 * 8];
 #define PN2_FPG_T(K)
 #endif
 
-// The header of the FP4 kernel's own LDS grid: grid_dims' automatic edge computed in fp32
-// (one thread; the double-precision cube root and cell products of grid_dims held the
-// workgroup at its second barrier). Any cell layout gives the same search results; the
-// bound that matters -- at most max(2m / ppc, 64) cells, what the LDS is sized for -- is kept.
-PN2_DEV GridHdr grid_dims_f32(const float lo[3], const float hi[3], int N, float ppc) {
-  const float cap = fmaxf(ceilf((float)N * kAutoPointsPerCell / ppc), (float)kAutoMinCells);
-  const float ext = fmaxf(fmaxf(hi[0] - lo[0], hi[1] - lo[1]), hi[2] - lo[2]);
-  const float cells0 = fmaxf((float)N / ppc, 1.0f);
-  float c = cbrtf((hi[0] - lo[0]) * (hi[1] - lo[1]) * (hi[2] - lo[2]) / cells0);
-  if (!(c > 0.0f)) c = ext / cbrtf(cells0);
-  if (!(c > 0.0f) || !(c < INFINITY)) c = 1.0f;  // all points identical: one cell
-  int n[3] = {1, 1, 1};
-  bool ok = false;
-  for (int it = 0; it < 400 && !ok; ++it) {
-    float d[3], cells = 1.0f;
-    for (int a = 0; a < 3; ++a) {
-      d[a] = floorf((hi[a] - lo[a]) / c) + 1.0f;
-      cells *= d[a];
-    }
-    if (cells <= cap) {
-      for (int a = 0; a < 3; ++a) n[a] = (int)d[a];
-      ok = true;
-    } else {
-      c *= 1.25f;
-    }
-  }
-  GridHdr h;
-  if (!ok) { n[0] = n[1] = n[2] = 1; c = INFINITY; }
-  h.ox = lo[0]; h.oy = lo[1]; h.oz = lo[2];
-  h.inv = ok ? 1.0f / c : 0.0f;
-  h.nx = n[0]; h.ny = n[1]; h.nz = n[2];
-  h.ncell = n[0] * n[1] * n[2];
-  return h;
-}
-
 // LDS per workgroup of the current device (cached per device id)
 size_t device_lds_per_block() {
   static size_t cache[64] = {0};
@@ -743,7 +708,7 @@ __global__ __launch_bounds__(FB) void fp_grid_fused_kernel(FpLayer p, float* __r
         for (int i = 1; i < NW; ++i) { lo[a] = fminf(lo[a], red[a][i]); hi[a] = fmaxf(hi[a], red[3 + a][i]); }
         if (!(hi[a] >= lo[a])) { lo[a] = 0.0f; hi[a] = 0.0f; }  // NaN-only axis
       }
-      *shp = grid_dims_f32(lo, hi, m, kFpgPointsPerCell);
+      *shp = grid_dims(lo, hi, m, 0.0f, kFpgPointsPerCell);
     }
     __syncthreads();
     h = *shp;
