@@ -588,8 +588,8 @@ constexpr int kFpGridMaxKnown = 4096;  // LDS: m float4 + (max(2m / ppc, 64) + 1
 constexpr float kFpgPointsPerCell = 2.0f;  // the LDS grid's points per cell (profiles/r4/ppc)
 // threads per workgroup (a quad per unknown: FB / 4 unknowns). The known grid is built (or
 // staged) once per workgroup, but fewer, bigger workgroups were slower at FP4: 512 / 1024
-// threads 49.0 / 55.8 us against 46.9 (profiles/r5/fb), and so were 2 / 4 row blocks per
-// 256-thread workgroup (54.9 / 80.9 us, profiles/r5/rpw): the search and the writes need
+// threads 49.0 / 55.8 us against 46.9 (profiles/r5/ab_misc fb/), and so were 2 / 4 row blocks per
+// 256-thread workgroup (54.9 / 80.9 us, profiles/r5/ab_misc rpw/): the search and the writes need
 // the workgroups' parallelism more than the build needs amortising
 constexpr int kFpgBlock = 256;
 // DIAGNOSTIC build flag (tools/stamp_fp4.py): s_memtime at the phase boundaries of the first
