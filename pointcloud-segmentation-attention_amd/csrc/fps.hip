@@ -168,13 +168,442 @@ struct FpsChain {
   float* nx[kChainMax];
 };
 
-// one stage (N <= kChainNext) for one cloud: the configuration fps_impl uses for this N
+// ---- hot-set schedule of one fused chain stage (N <= kChainNext, the whole workgroup) -----
+// The culled sampler's certificate (fps_cull.h, HOT SET) without its cells, with the roles
+// split by wave. Waves 1-3 (the cold waves) hold the cloud's points, PPT per thread, in the
+// reference's tie order (k mod 512, k div 512) (tf_sampling_g.cu:146-163); wave 0 (the hot
+// wave, alone on its SIMD) holds no points. A round:
+//   1. the cold waves' running mins are exact; the block max Mx and tau = Mx * frac (the
+//      smallest fraction whose count of points above it fits K = 64; the last round's
+//      fraction first) choose the hot set, which the cold waves stage, in tie order;
+//   2. wave 0 takes one hot point per lane and picks from them alone while its best value is
+//      > tau: every other point is <= tau and running mins only decrease, so that best IS the
+//      reference's next centre. Per pick: a wave max, one ballot, four readlanes and one LDS
+//      write of the centre -- no barrier, no LDS read;
+//   3. meanwhile the cold waves apply every published centre to their points (they poll the
+//      pick list), so their mins are exact again when the round ends.
+// A cloud of at most 64 points is all hot (wave 0 alone, tau = -1). If no fraction fits (ties
+// crowd the top) or the max is negative, one exact block argmax (fps_v9's rule: the lowest
+// position holding the max, position 0 when every value is below 0) picks the centre. The
+// outputs (idx, new_xyz, the next stage's LDS copy) are written from the pick list after the
+// stage. Same picks as fps_v9_body bit for bit: the same fp32 distance, the same int-bit
+// running mins and tie order.
+constexpr int kHotFracs = 12;  // kCullFrac (fps_cull.h): the thresholds
+constexpr int kHotK = kWave;  // hot points: one per lane of wave 0
+constexpr int kHotCold = kChainBlock / kWave - 1;  // cold waves
+constexpr int kHotPollLimit = 1 << 22;
+#ifndef PN2_HOT_EXACT
+#define PN2_HOT_EXACT 16
+#endif
+#ifndef PN2_HOT_EXACT2
+#define PN2_HOT_EXACT2 6
+#endif
+constexpr int kHotExact = PN2_HOT_EXACT;  // picks of the 1,024-point stage made one at a time
+constexpr int kHotExact2 = PN2_HOT_EXACT2;  // ... of the smaller ones  // a cold wave's polls per round (never reached: bound)
+struct HotLds {
+  float4 pc[kChainNext];          // picks by number: x, y, z, bits(index); w = -1 until written
+  float4 hk[2][kHotCold][kHotK];  // hot staging for two thresholds, per cold wave: x, y, z, bits(index)
+  int hv[2][kHotCold][kHotK];     // hot staging: running min (int bits)
+  int wmax[2][kHotCold];          // per cold wave: its max (double-buffered by try)
+  int cnt[2][2][kHotCold];        // [try parity][threshold][cold wave]: points above it
+  uint2 red[2][kHotCold];         // exact argmax by pick parity: (max + 1, index) per cold wave
+  int pub[2];                     // by round parity: picks published | kHotEnd when the round ends
+};
+constexpr int kHotEnd = 1 << 30;
+
+// DIAGNOSTIC build flag (tools/stamp_chain.py): per round of cloud 0's stages, s_memtime at
+// the round's start (after the block max), when the hot set fits, the hot wave's end and the
+// first cold wave's end, plus the picks made and the tries; read back with pn2_hot_stamps()
+#ifndef PN2_HOT_STAMP
+#define PN2_HOT_STAMP 0
+#endif
+#if PN2_HOT_STAMP
+__device__ unsigned long long g_hot_ev[3 * 64 * 8];
+#define PN2_HOTEV(R, F, V)                                                            \
+  if (blockIdx.x == 0 && lane == 0 && (R) < 64)                                      \
+    g_hot_ev[((N > 512 ? 0 : (N > 64 ? 1 : 2)) * 64 + (R)) * 8 + (F)] = (unsigned long long)(V);
+#else
+#define PN2_HOTEV(R, F, V)
+#endif
+
+// tie position p -> point index: p = k below 512 points, else p = 2 (k mod 512) + k div 512
+PN2_DEV int hot_point(int p, bool wide) { return wide ? (p >> 1) + ((p & 1) << 9) : p; }
+
+// wave 0's picks from its hot points (value hv, point hk, coordinates hx/hy/hz; empty lanes
+// hold INT_MIN) while the best is > tau and j < M; each pick is published at once: the
+// winning lane writes its centre to pc[j], then the count to *pub (fps_cull.h hot_publish;
+// DS operations of one wave execute in order, so a cold wave that reads the count reads the
+// centre). Returns the picks made so far.
+using hf4 = float __attribute__((ext_vector_type(4)));
+// the publishing of a pick by its lane L (fps_cull.h hot_publish, with the centre as ONE
+// 16-byte write): the entry e = (x, y, z, bits(k)) to the pick list at va_c, then the count
+// n to va_n; every lane gets the centre
+PN2_DEV void hot_publish4(int L, int va_c, int va_n, int vcnt, hf4 e, float& cx, float& cy,
+                          float& cz) {
+  uint64_t sv;
+  asm volatile(
+      "s_mov_b64 %[sv], exec\n\t"
+      "s_lshl_b64 exec, 1, %[L]\n\t"
+      "ds_write_b128 %[a], %[e]\n\t"
+      "ds_write_b32 %[c], %[n]\n\t"
+      "v_readlane_b32 %[cx], %[x], %[L]\n\t"
+      "v_readlane_b32 %[cy], %[y], %[L]\n\t"
+      "v_readlane_b32 %[cz], %[z], %[L]\n\t"
+      "s_mov_b64 exec, %[sv]"
+      : [sv] "=&s"(sv), [cx] "=&s"(cx), [cy] "=&s"(cy), [cz] "=&s"(cz)
+      : [L] "s"(L), [a] "v"(va_c), [c] "v"(va_n), [e] "v"(e), [x] "v"(e.x), [y] "v"(e.y),
+        [z] "v"(e.z), [n] "v"(vcnt)
+      : "memory", "scc");
+}
+
+// wave 0's picks from its hot entries (e = x, y, z, bits(point index), value hv; empty lanes
+// hold INT_MIN) while the best is > tau and j < M; each pick is published at once (the count
+// after the centre: DS operations of one wave execute in order, so a cold wave that reads the
+// count reads the centre). CHECKED: the count is tested per pick (fewer than 64 picks left,
+// or tau < 0); otherwise the loop cannot outrun the hot set: a picked entry drops to 0 <= tau.
+// Returns the picks made so far.
+template <bool CHECKED>
+PN2_DEV int hot_picks(hf4 e, int hv, int tau, int j, int M, int* pub, HotLds& S) {
+  j = __builtin_amdgcn_readfirstlane(j);  // (a scalar loop count: no exec-mask bookkeeping)
+  // publishing addresses and the count in VGPRs, advanced by one VALU add per pick
+  int va_c, va_n, vcnt;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(va_c)
+               : "s"((uint32_t)(uintptr_t)(__attribute__((address_space(3))) float4*)&S.pc[j]));
+  asm volatile("v_mov_b32 %0, %1" : "=v"(va_n)
+               : "s"((uint32_t)(uintptr_t)(__attribute__((address_space(3))) int*)pub));
+  asm volatile("v_mov_b32 %0, %1" : "=v"(vcnt) : "s"(j + 1));
+  int n = 0;
+  // (one exit, at the bottom: the loop carries no break flags)
+  int km = __builtin_amdgcn_readlane(wave_max_i32_l63(hv), kWave - 1);
+  while (km > tau) {  // else the certificate fails: the round ends
+    const int L = (int)__builtin_ctzll(__builtin_amdgcn_ballot_w64(hv == km));
+    float cx, cy, cz;
+    hot_publish4(L, va_c, va_n, vcnt, e, cx, cy, cz);
+    __builtin_amdgcn_sched_barrier(0);
+    ++n;
+    hv = min(hv, __float_as_int(sqdist(e.x, e.y, e.z, cx, cy, cz)));
+    va_c += 16;
+    vcnt += 1;
+    km = __builtin_amdgcn_readlane(wave_max_i32_l63(hv), kWave - 1);
+    if constexpr (CHECKED) km = j + n >= M ? tau : km;
+  }
+  return j + n;
+}
+
+template <int PPT>
+PN2_DEV void fps_hot_body(const float* CXYZ, int N, int M, int32_t* I, float* NX, float* SNEXT,
+                          HotLds& S) {
+  const int t = threadIdx.x, lane = t & (kWave - 1), w = t / kWave;
+  const bool wide = N > 512;
+  const float c0x = CXYZ[0], c0y = CXYZ[1], c0z = CXYZ[2];
+  if (t == 0) S.pc[0] = make_float4(c0x, c0y, c0z, __int_as_float(0));
+  int j = 1;  // picks made (uniform)
+  PN2_HOTEV(63, 0, __builtin_amdgcn_s_memtime())
+  if (N <= kHotK) {
+    // all hot: wave 0 alone, point k on lane k
+    if (w == 0) {
+      const bool in = lane < N;
+      const float hx = in ? CXYZ[3 * lane + 0] : 0.0f, hy = in ? CXYZ[3 * lane + 1] : 0.0f,
+                  hz = in ? CXYZ[3 * lane + 2] : 0.0f;
+      int hv = in ? min(__float_as_int(kInitTemp), __float_as_int(sqdist(hx, hy, hz, c0x, c0y, c0z)))
+                  : (-2147483647 - 1);
+      while (j < M) {
+        j = hot_picks<true>(hf4{hx, hy, hz, __int_as_float(lane)}, hv, -1, j, M, &S.pub[0], S);
+        if (j >= M) break;
+        // every value < 0 (padding / negative NaN bits): fps_v9 picks point 0; refresh the
+        // lanes' values from the centres published since (cheap: this path is degenerate)
+        hv = in ? __float_as_int(kInitTemp) : (-2147483647 - 1);
+        if (lane == 0) S.pc[j] = make_float4(c0x, c0y, c0z, __int_as_float(0));
+        ++j;
+        for (int p = 0; p < j && in; ++p) {
+          const float4 c = S.pc[p];
+          hv = min(hv, __float_as_int(sqdist(hx, hy, hz, c.x, c.y, c.z)));
+        }
+      }
+    }
+  } else {
+    // cold waves: tie positions p = u * PPT + s, u = t - 64
+    const int u = t - kWave;
+    using f2 = float __attribute__((ext_vector_type(2)));
+    constexpr bool PK = PPT % 2 == 0;
+    constexpr int NP = PK ? PPT / 2 : 1;
+    float px[PPT], py[PPT], pz[PPT];
+    int tb[PPT], pk[PPT];
+    f2 vx[NP], vy[NP], vz[NP];
+    if (w > 0) {
+#pragma unroll
+      for (int s = 0; s < PPT; ++s) {
+        const int pp = u * PPT + s;
+        const int k = hot_point(pp, wide);
+        const bool in = pp < kChainNext && k < N;
+        const int kk = in ? k : 0;
+        pk[s] = k;
+        px[s] = in ? CXYZ[3 * kk + 0] : 0.0f;
+        py[s] = in ? CXYZ[3 * kk + 1] : 0.0f;
+        pz[s] = in ? CXYZ[3 * kk + 2] : 0.0f;
+        tb[s] = in ? __float_as_int(kInitTemp) : -1;  // padding never wins
+        if constexpr (PK) { vx[s / 2][s % 2] = px[s]; vy[s / 2][s % 2] = py[s]; vz[s / 2][s % 2] = pz[s]; }
+      }
+    }
+    auto apply = [&](float cx, float cy, float cz) {
+      if constexpr (PK) {
+        const f2 c2x = {cx, cx}, c2y = {cy, cy}, c2z = {cz, cz};
+#pragma unroll
+        for (int h = 0; h < NP; ++h) {
+          const f2 dx = vx[h] - c2x, dy = vy[h] - c2y, dz = vz[h] - c2z;
+          const f2 d = (dx * dx + dy * dy) + dz * dz;
+          tb[2 * h] = min(tb[2 * h], __float_as_int(d.x));
+          tb[2 * h + 1] = min(tb[2 * h + 1], __float_as_int(d.y));
+        }
+      } else {
+#pragma unroll
+        for (int s = 0; s < PPT; ++s)
+          tb[s] = min(tb[s], __float_as_int(sqdist(px[s], py[s], pz[s], cx, cy, cz)));
+      }
+    };
+    if (w > 0) apply(c0x, c0y, c0z);
+    int r = 1;       // cold waves: picks applied
+    int fi = 0;      // threshold fraction (kept from round to round)
+    int round = 0;
+    int tries = 0;   // parity of the count buffers
+    // one exact block argmax over the cold waves (fps_v9's order), every thread: pick j
+    auto exact_pick = [&]() {
+      if (w > 0) {
+        int bd = -1, bs = 0;
+#pragma unroll
+        for (int s = 0; s < PPT; ++s) {
+          bs = tb[s] > bd ? s : bs;
+          bd = max(bd, tb[s]);
+        }
+        const uint32_t hi = (uint32_t)(bd + 1);
+        const uint32_t km = wave_max_u32(hi);
+        const int L = (int)__builtin_amdgcn_readfirstlane(
+            (int)__builtin_ctzll(__builtin_amdgcn_ballot_w64(hi == km)));
+        const int sq = __builtin_amdgcn_readlane(bs, L);
+        if (lane == 0)
+          S.red[j & 1][w - 1] = make_uint2(km, (uint32_t)hot_point((u - lane + L) * PPT + sq, wide));
+      }
+      __syncthreads();
+      uint2 best = S.red[j & 1][0];
+#pragma unroll
+      for (int i = 1; i < kHotCold; ++i) {
+        const uint2 q = S.red[j & 1][i];
+        best = q.x > best.x ? q : best;  // ties: the lowest wave
+      }
+      const int old = __builtin_amdgcn_readfirstlane((int)best.y);
+      const float cx = CXYZ[3 * old + 0], cy = CXYZ[3 * old + 1], cz = CXYZ[3 * old + 2];
+      if (t == 0) S.pc[j] = make_float4(cx, cy, cz, __int_as_float(old));
+      if (w > 0) apply(cx, cy, cz);
+      ++j;
+      r = j;
+    };
+    // the first picks one at a time: the first rounds certify only 1-4 picks each
+    // (tools/stamp_chain.py), less than a round costs
+    const int e0 = min(M, PPT >= 6 ? kHotExact : kHotExact2);
+    while (j < e0) exact_pick();
+    PN2_HOTEV(63, 2, __builtin_amdgcn_s_memtime())
+    // the thresholds' fractions, lane f holding fraction f (read with one readlane per round)
+    const float fracv = kCullFrac[lane < kHotFracs ? lane : kHotFracs - 1];
+    int tref = -1;  // the last round's tau: every value is <= it now (-1: none)
+    while (j < M) {
+      // this round's publishing word reset (its last readers, two rounds ago, are past the
+      // barriers since)
+      if (t == 0) S.pub[(round + 1) & 1] = j;
+      // 1. the reference value for the thresholds: the last round's tau (an upper bound of
+      // the block max, no barrier needed), else the block max itself
+      int ref = tref;
+      bool exact_ref = ref < 0;
+      if (exact_ref) {
+        if (w > 0) {
+          int lm = tb[0];
+#pragma unroll
+          for (int s = 1; s < PPT; ++s) lm = max(lm, tb[s]);
+          lm = wave_max_i32(lm);
+          if (lane == 0) S.wmax[tries & 1][w - 1] = lm;
+        }
+        __syncthreads();
+        ref = S.wmax[tries & 1][0];
+#pragma unroll
+        for (int i = 1; i < kHotCold; ++i) ref = max(ref, S.wmax[tries & 1][i]);
+        ref = __builtin_amdgcn_readfirstlane(ref);
+      }
+      PN2_HOTEV(round, 0, __builtin_amdgcn_s_memtime())
+      const int tries0 = tries;
+      (void)tries0;
+      // 2. the hot set: counted and staged for two thresholds at once (fractions fi, fi + 1
+      // of the reference), the lower one taken when it fits; both too large: two fractions
+      // up; a bound as the reference and nothing fits: again with the block max (each pass
+      // also publishes the cold waves' maxima)
+      int tau = 0, sel = 0, c[kHotCold] = {0, 0, 0};
+      bool fits = false;
+      while (ref >= 0) {
+        const int fa = fi, fb = min(fi + 1, kHotFracs - 1);
+        const float rf = __int_as_float(ref);
+        const int ta = __builtin_amdgcn_readfirstlane(
+            __float_as_int(rf * __int_as_float(__builtin_amdgcn_readlane(__float_as_int(fracv), fa))));
+        const int tbb = __builtin_amdgcn_readfirstlane(
+            __float_as_int(rf * __int_as_float(__builtin_amdgcn_readlane(__float_as_int(fracv), fb))));
+        if (w > 0) {
+          int pa = 0, pb = 0, ca = 0, cb = 0, lm = tb[0];
+#pragma unroll
+          for (int s = 0; s < PPT; ++s) {
+            const uint64_t ba = __builtin_amdgcn_ballot_w64(tb[s] > ta);
+            const uint64_t bb = __builtin_amdgcn_ballot_w64(tb[s] > tbb);
+            pa += (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(ba >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ba, 0u));
+            pb += (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bb, 0u));
+            ca += __builtin_popcountll(ba);
+            cb += __builtin_popcountll(bb);
+            lm = max(lm, tb[s]);
+          }
+#pragma unroll
+          for (int s = 0; s < PPT; ++s) {
+            const float4 en = make_float4(px[s], py[s], pz[s], __int_as_float(pk[s]));
+            if (tb[s] > ta) {
+              if (pa < kHotK) { S.hk[0][w - 1][pa] = en; S.hv[0][w - 1][pa] = tb[s]; }
+              ++pa;
+            }
+            if (tb[s] > tbb) {
+              if (pb < kHotK) { S.hk[1][w - 1][pb] = en; S.hv[1][w - 1][pb] = tb[s]; }
+              ++pb;
+            }
+          }
+          if (!exact_ref) lm = wave_max_i32(lm);
+          if (lane == 0) {
+            S.cnt[tries & 1][0][w - 1] = ca;
+            S.cnt[tries & 1][1][w - 1] = cb;
+            if (!exact_ref) S.wmax[tries & 1][w - 1] = lm;
+          }
+        }
+        __syncthreads();
+        int ca[kHotCold], cb[kHotCold], tota = 0, totb = 0;
+#pragma unroll
+        for (int i = 0; i < kHotCold; ++i) {
+          ca[i] = __builtin_amdgcn_readfirstlane(S.cnt[tries & 1][0][i]);
+          cb[i] = __builtin_amdgcn_readfirstlane(S.cnt[tries & 1][1][i]);
+          tota += ca[i];
+          totb += cb[i];
+        }
+        const int tr = tries++;
+        if (tota >= 1 && tota <= kHotK) {
+          fits = true;
+          tau = ta;
+          sel = 0;
+#pragma unroll
+          for (int i = 0; i < kHotCold; ++i) c[i] = ca[i];
+          if (2 * tota < kHotK && fi > 0) --fi;  // a small set: a lower fraction next round
+          break;
+        }
+        if (totb >= 1 && totb <= kHotK) {
+          fits = true;
+          tau = tbb;
+          sel = 1;
+#pragma unroll
+          for (int i = 0; i < kHotCold; ++i) c[i] = cb[i];
+          fi = fb;
+          break;
+        }
+        if (!exact_ref) {  // the bound did not serve: the block max, same fractions
+          int m = S.wmax[tr & 1][0];
+#pragma unroll
+          for (int i = 1; i < kHotCold; ++i) m = max(m, S.wmax[tr & 1][i]);
+          ref = __builtin_amdgcn_readfirstlane(m);
+          exact_ref = true;
+          if (tota > kHotK) fi = min(fb + 1, kHotFracs - 1);
+          continue;
+        }
+        if (totb == 0 || fb == kHotFracs - 1) break;  // (no higher fraction fits either)
+        fi = min(fb + 1, kHotFracs - 1);
+      }
+      tref = fits ? tau : -1;
+      if (!fits) {  // ties crowd the top, or only negative values are left
+        exact_pick();
+        continue;
+      }
+      PN2_HOTEV(round, 1, __builtin_amdgcn_s_memtime())
+      PN2_HOTEV(round, 4, tries - tries0)
+      ++round;
+      int* const pub = &S.pub[round & 1];
+      if (w == 0) {
+        // 2. the picks: lane l takes hot entry l (the cold waves' stagings in wave order)
+        const int i1 = lane - c[0], i2 = i1 - c[1];
+        const int src = lane < c[0] ? 0 : (i1 < c[1] ? 1 : 2);
+        const int off = src == 0 ? lane : (src == 1 ? i1 : i2);
+        const bool in = lane < c[0] + c[1] + c[2];
+        const hf4 e = *reinterpret_cast<const hf4*>(&S.hk[sel][src][in ? off : 0]);
+        const int hv = in ? S.hv[sel][src][off] : (-2147483647 - 1);
+        j = M - j >= kHotK ? hot_picks<false>(e, hv, tau, j, M, pub, S)
+                           : hot_picks<true>(e, hv, tau, j, M, pub, S);
+        PN2_HOTEV(round - 1, 2, __builtin_amdgcn_s_memtime())
+        PN2_HOTEV(round - 1, 3, j)
+        if (lane == 0) {
+          asm volatile("" ::: "memory");
+          __hip_atomic_store(pub, j | kHotEnd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+      } else {
+        // 3. the cold waves apply the centres as wave 0 publishes them, up to 64 per poll: the
+        // count and the next 64 entries are read in ONE round trip, the count first (DS
+        // operations execute in order, so every entry below the count read is the centre)
+        using f4 = float __attribute__((ext_vector_type(4)));
+        const uint32_t a_pub = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) int*)pub;
+        for (int it = 0; it < kHotPollLimit; ++it) {
+          int sv;
+          f4 cv;
+          const uint32_t a_pc = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float4*)&S.pc[min(r + lane, kChainNext - 1)];
+          asm volatile("ds_read_b32 %0, %2\n\tds_read_b128 %1, %3\n\ts_waitcnt lgkmcnt(0)"
+                       : "=v"(sv), "=v"(cv) : "v"(a_pub), "v"(a_pc) : "memory");
+          sv = __builtin_amdgcn_readfirstlane(sv);
+          const int av = sv & (kHotEnd - 1);
+          if (av > r) {
+            const int n = min(av - r, kWave);
+            for (int i = 0; i < n; ++i) {
+              const float cx = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__float_as_int(cv.x), i));
+              const float cy = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__float_as_int(cv.y), i));
+              const float cz = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__float_as_int(cv.z), i));
+              apply(cx, cy, cz);
+            }
+            r += n;
+            continue;
+          }
+          if (sv & kHotEnd) break;  // av is final and applied
+        }
+        if (w == 1) { PN2_HOTEV(round - 1, 5, __builtin_amdgcn_s_memtime()) }
+        j = r;
+      }
+    }
+  }
+  __syncthreads();
+  PN2_HOTEV(63, 1, __builtin_amdgcn_s_memtime())
+  // the outputs from the pick list
+  for (int i = t; i < M; i += kChainBlock) {
+    const float4 c = S.pc[i];
+    I[i] = __float_as_int(c.w);
+    if (NX) { NX[3 * i + 0] = c.x; NX[3 * i + 1] = c.y; NX[3 * i + 2] = c.z; }
+    if (SNEXT) { SNEXT[3 * i + 0] = c.x; SNEXT[3 * i + 1] = c.y; SNEXT[3 * i + 2] = c.z; }
+  }
+}
+
+// one stage (N <= kChainNext) for one cloud, every thread of the workgroup: the hot-set
+// schedule (cold points per thread: 2 up to 384 points, 3 up to 512, 6 up to 1,024).
 // (Measured and not kept, profiles/r5/chain: the 1,024-point stage on ONE wave, 16 points a
 // lane and no barrier -- 126.5 -> 129 us for the chain, 140 us with each lane's candidate
 // coordinates read speculatively; a single wave issues the pick's ~110 dependent VALU ops at
 // ~8 cycles each, which costs what the 4-wave form's barrier and cross-wave step cost.)
+#ifndef PN2_CHAIN_HOT
+#define PN2_CHAIN_HOT 1
+#endif
 PN2_DEV void chain_stage(const float* P, int N, int M, const float* CXYZ, int32_t* I, float* NX,
-                         float* SNEXT, uint2 (*red)[8]) {
+                         float* SNEXT, uint2 (*red)[8], HotLds& hot) {
+#if PN2_CHAIN_HOT
+  // (the pick list holds kChainNext: a larger last stage takes the v9 bodies below)
+  if (M <= kChainNext) {
+    if (N <= 384) fps_hot_body<2>(CXYZ, N, M, I, NX, SNEXT, hot);
+    else if (N <= 512) fps_hot_body<3>(CXYZ, N, M, I, NX, SNEXT, hot);
+    else fps_hot_body<6>(CXYZ, N, M, I, NX, SNEXT, hot);
+    return;
+  }
+#else
+  (void)hot;
+#endif
   const bool w0 = threadIdx.x < kWave;
   if (N <= 64) { if (w0) fps_v9_body<64, 1, 1>(P, N, M, CXYZ, I, NX, SNEXT, red); }
   else if (N <= 128) { if (w0) fps_v9_body<64, 2, 2>(P, N, M, CXYZ, I, NX, SNEXT, red); }
@@ -188,6 +617,7 @@ __global__ __launch_bounds__(kChainBlock) void fps_chain_kernel(const float* __r
   __shared__ uint2 red[2][8];
   __shared__ float sxyz[3 * kChainNext];
   __shared__ float snew[2][3 * kChainNext];
+  __shared__ HotLds hot;
   const int b = blockIdx.x;
   const float* __restrict__ P = xyz + (size_t)b * c.n[0] * 3;
   for (int e = threadIdx.x; e < 3 * c.n[0]; e += kChainBlock) sxyz[e] = P[e];
@@ -196,7 +626,7 @@ __global__ __launch_bounds__(kChainBlock) void fps_chain_kernel(const float* __r
     const float* cxyz = i == 0 ? sxyz : snew[(i - 1) & 1];
     float* next = i + 1 < c.stages ? snew[i & 1] : nullptr;
     chain_stage(cxyz, c.n[i], c.m[i], cxyz, c.idx[i] + (size_t)b * c.m[i],
-                c.nx[i] + (size_t)b * c.m[i] * 3, next, red);
+                c.nx[i] + (size_t)b * c.m[i] * 3, next, red, hot);
     __syncthreads();  // stage i's LDS output complete before stage i+1 reads it
   }
 }
@@ -327,6 +757,14 @@ int fps_chain_launch(const float* xyz, int B, int N, int nstages, const int* npo
 extern "C" {
 
 int pn2_fps_max_points(void) { return pn2::kMaxRegPoints; }
+
+#if PN2_HOT_STAMP
+int pn2_hot_stamps(unsigned long long* host_out) {  // 3 x 64 x 8 u64 (DIAGNOSTIC builds only)
+  return (int)hipMemcpyFromSymbol(host_out, HIP_SYMBOL(pn2::g_hot_ev),
+                                  sizeof(unsigned long long) * 3 * 64 * 8, 0,
+                                  hipMemcpyDeviceToHost);
+}
+#endif
 
 int pn2_fault_status(int clear) {
   if (!pn2::g_fault_host) return 0;
