@@ -235,35 +235,13 @@ PN2_DEV int hot_point(int p, bool wide) { return wide ? (p >> 1) + ((p & 1) << 9
 // DS operations of one wave execute in order, so a cold wave that reads the count reads the
 // centre). Returns the picks made so far.
 using hf4 = float __attribute__((ext_vector_type(4)));
-// the publishing of a pick by its lane L (fps_cull.h hot_publish, with the centre as ONE
-// 16-byte write): the entry e = (x, y, z, bits(k)) to the pick list at va_c, then the count
-// n to va_n; every lane gets the centre
-PN2_DEV void hot_publish4(int L, int va_c, int va_n, int vcnt, hf4 e, float& cx, float& cy,
-                          float& cz) {
-  uint64_t sv;
-  asm volatile(
-      "s_mov_b64 %[sv], exec\n\t"
-      "s_lshl_b64 exec, 1, %[L]\n\t"
-      "ds_write_b128 %[a], %[e]\n\t"
-      "ds_write_b32 %[c], %[n]\n\t"
-      "v_readlane_b32 %[cx], %[x], %[L]\n\t"
-      "v_readlane_b32 %[cy], %[y], %[L]\n\t"
-      "v_readlane_b32 %[cz], %[z], %[L]\n\t"
-      "s_mov_b64 exec, %[sv]"
-      : [sv] "=&s"(sv), [cx] "=&s"(cx), [cy] "=&s"(cy), [cz] "=&s"(cz)
-      : [L] "s"(L), [a] "v"(va_c), [c] "v"(va_n), [e] "v"(e), [x] "v"(e.x), [y] "v"(e.y),
-        [z] "v"(e.z), [n] "v"(vcnt)
-      : "memory", "scc");
-}
 
 // wave 0's picks from its hot entries (e = x, y, z, bits(point index), value hv; empty lanes
 // hold INT_MIN) while the best is > tau and j < M; each pick is published at once (the count
-// after the centre: DS operations of one wave execute in order, so a cold wave that reads the
-// count reads the centre). CHECKED: the count is tested per pick (fewer than 64 picks left,
-// or tau < 0); otherwise the loop cannot outrun the hot set: a picked entry drops to 0 <= tau.
-// Returns the picks made so far.
-template <bool CHECKED>
-PN2_DEV int hot_picks(hf4 e, int hv, int tau, int j, int M, int* pub, HotLds& S) {
+// after the centre; a cold wave reads the count, waits for it, then the centres). At most lim picks (a picked entry drops to 0 <= tau, so a round
+// cannot outrun its hot set -- except through NaN distances, which the bound covers; the all-hot
+// path, tau = -1, needs it to stop at M). Returns the picks made so far.
+PN2_DEV int hot_picks(hf4 e, int hv, int tau, int j, int lim, int* pub, HotLds& S) {
   j = __builtin_amdgcn_readfirstlane(j);  // (a scalar loop count: no exec-mask bookkeeping)
   // publishing addresses and the count in VGPRs, advanced by one VALU add per pick
   int va_c, va_n, vcnt;
@@ -278,14 +256,17 @@ PN2_DEV int hot_picks(hf4 e, int hv, int tau, int j, int M, int* pub, HotLds& S)
   while (km > tau) {  // else the certificate fails: the round ends
     const int L = (int)__builtin_ctzll(__builtin_amdgcn_ballot_w64(hv == km));
     float cx, cy, cz;
-    hot_publish4(L, va_c, va_n, vcnt, e, cx, cy, cz);
+    // (the centre as four 4-byte writes, fps_cull.h hot_publish: measured, a 16-byte write
+    // followed by the count's 4-byte write let a poller read the count with the centre not yet
+    // all there -- tools/pipe_stress.py, 9 mismatching tensors in 40 rotations)
+    hot_publish(L, va_c, va_n, vcnt, e.x, e.y, e.z, __float_as_int(e.w), cx, cy, cz);
     __builtin_amdgcn_sched_barrier(0);
     ++n;
     hv = min(hv, __float_as_int(sqdist(e.x, e.y, e.z, cx, cy, cz)));
     va_c += 16;
     vcnt += 1;
     km = __builtin_amdgcn_readlane(wave_max_i32_l63(hv), kWave - 1);
-    if constexpr (CHECKED) km = j + n >= M ? tau : km;
+    km = n >= lim ? tau : km;
   }
   return j + n;
 }
@@ -308,7 +289,7 @@ PN2_DEV void fps_hot_body(const float* CXYZ, int N, int M, int32_t* I, float* NX
       int hv = in ? min(__float_as_int(kInitTemp), __float_as_int(sqdist(hx, hy, hz, c0x, c0y, c0z)))
                   : (-2147483647 - 1);
       while (j < M) {
-        j = hot_picks<true>(hf4{hx, hy, hz, __int_as_float(lane)}, hv, -1, j, M, &S.pub[0], S);
+        j = hot_picks(hf4{hx, hy, hz, __int_as_float(lane)}, hv, -1, j, M - j, &S.pub[0], S);
         if (j >= M) break;
         // every value < 0 (padding / negative NaN bits): fps_v9 picks point 0; refresh the
         // lanes' values from the centres published since (cheap: this path is degenerate)
@@ -531,8 +512,7 @@ PN2_DEV void fps_hot_body(const float* CXYZ, int N, int M, int32_t* I, float* NX
         const bool in = lane < c[0] + c[1] + c[2];
         const hf4 e = *reinterpret_cast<const hf4*>(&S.hk[sel][src][in ? off : 0]);
         const int hv = in ? S.hv[sel][src][off] : (-2147483647 - 1);
-        j = M - j >= kHotK ? hot_picks<false>(e, hv, tau, j, M, pub, S)
-                           : hot_picks<true>(e, hv, tau, j, M, pub, S);
+        j = hot_picks(e, hv, tau, j, min(M - j, kHotK), pub, S);
         PN2_HOTEV(round - 1, 2, __builtin_amdgcn_s_memtime())
         PN2_HOTEV(round - 1, 3, j)
         if (lane == 0) {
@@ -540,21 +520,14 @@ PN2_DEV void fps_hot_body(const float* CXYZ, int N, int M, int32_t* I, float* NX
           __hip_atomic_store(pub, j | kHotEnd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
       } else {
-        // 3. the cold waves apply the centres as wave 0 publishes them, up to 64 per poll: the
-        // count and the next 64 entries are read in ONE round trip, the count first (DS
-        // operations execute in order, so every entry below the count read is the centre)
-        using f4 = float __attribute__((ext_vector_type(4)));
-        const uint32_t a_pub = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) int*)pub;
+        // 3. the cold waves apply the centres as wave 0 publishes them, up to 64 per LDS read
         for (int it = 0; it < kHotPollLimit; ++it) {
-          int sv;
-          f4 cv;
-          const uint32_t a_pc = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) float4*)&S.pc[min(r + lane, kChainNext - 1)];
-          asm volatile("ds_read_b32 %0, %2\n\tds_read_b128 %1, %3\n\ts_waitcnt lgkmcnt(0)"
-                       : "=v"(sv), "=v"(cv) : "v"(a_pub), "v"(a_pc) : "memory");
-          sv = __builtin_amdgcn_readfirstlane(sv);
+          const int sv = __builtin_amdgcn_readfirstlane(
+              __hip_atomic_load(pub, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
           const int av = sv & (kHotEnd - 1);
           if (av > r) {
             const int n = min(av - r, kWave);
+            const float4 cv = S.pc[r + min(lane, n - 1)];
             for (int i = 0; i < n; ++i) {
               const float cx = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__float_as_int(cv.x), i));
               const float cy = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__float_as_int(cv.y), i));

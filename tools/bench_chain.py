@@ -8,6 +8,8 @@ import torch
 pkg = importlib.import_module("pointcloud-segmentation-attention_amd")
 dev = torch.device("cuda:0")
 B, N, npts = 16, 8192, [1024, 256, 64, 16]
+if "--msg" in sys.argv:  # cfg5's MSG samplers: B = 8, 16384 -> 512 -> 128
+    B, N, npts = 8, 16384, [512, 128]
 x = torch.from_numpy(pkg.synth.batch(range(B), N, "scannet")[0]).to(dev)
 ts = pkg.tf_sampling
 
@@ -27,15 +29,15 @@ def timeit(fn, reps=20):
 
 
 res = {"chain_us": timeit(lambda: ts.farthest_point_sample_chain(npts, x))}
-for k in (1, 2, 3):  # the chain cut after k stages
+for k in range(1, len(npts)):  # the chain cut after k stages
     res[f"chain{k}_us"] = timeit(lambda k=k: ts.farthest_point_sample_chain(npts[:k], x))
 ins = [x]
 for m in npts:
     ins.append(ts.farthest_point_sample_and_gather(m, ins[-1])[1])
 for i, m in enumerate(npts):
     res[f"stage{i + 1}_us"] = timeit(lambda i=i, m=m: ts.farthest_point_sample_and_gather(m, ins[i]))
-res["stages_sum_us"] = sum(res[f"stage{i + 1}_us"] for i in range(4))
-# what the pipelined step launches on its chain lane: SA2..SA4's samplers fused (fps234)
+res["stages_sum_us"] = sum(res[f"stage{i + 1}_us"] for i in range(len(npts)))
+# what the pipelined step launches on its chain lane: the later samplers fused (fps234)
 res["tail_234_us"] = timeit(lambda: ts.farthest_point_sample_chain(npts[1:], ins[1]))
 # index-exact against the stage-by-stage samplers
 for (i_, x_), m, src in zip(ts.farthest_point_sample_chain(npts[1:], ins[1]), npts[1:], ins[1:]):
