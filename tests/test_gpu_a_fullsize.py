@@ -182,6 +182,43 @@ def test_pipeline_full_size(env, config, B, lanes, native, layout, own, direct):
 
 
 @pytest.mark.timeout(300)
+def test_pipeline_rotations_equal_eager(env):
+    """Concurrency: the cfg2 pipeline (3 sampler streams, layout b, native plan, direct
+    launches) for 12 rotations over 3 sets of distinct clouds, the sampled coordinates poisoned
+    before every other rotation; every set's outputs and index intermediates after every
+    rotation equal the same clouds' eager step bit for bit. (A race inside the sampler chain's
+    publishing -- a 16-byte centre write -- showed here once in ~40 rotations:
+    profiles/r5/chain_hot/pipe_stress_b128_publish.json; tools/pipe_stress.py runs longer.)"""
+    pkg, O, torch, dev = env
+    S = pkg.stack
+    B = 16
+    sets = [S.make_inputs("cfg2", list(range(100 + i * B, 100 + (i + 1) * B)), dev)
+            for i in range(3)]
+    refs = []
+    for inp in sets:
+        st = S.Step(inp)
+        outs = st()
+        torch.cuda.synchronize()
+        refs.append(([o.clone() for o in outs], {k: v.clone() for k, v in st.intermediates().items()}))
+    pipe = S.Pipeline(sets[0], graphs=True, nsets=3, sampler_lanes=3, native_plan=True,
+                      layout="b", chain_own=False, set_inputs=sets, direct=True)
+    for rot in range(12):
+        if rot % 2 == 1:
+            _poison_sampled(pipe, torch)
+        for _ in range(3):
+            pipe.run()
+        pipe.join()
+        for si, (_, souts, sinter) in enumerate(pipe.outputs_by_set()):
+            ro, ri = refs[si]
+            for i, (g, r) in enumerate(zip(souts, ro)):
+                assert torch.equal(g, r) or torch.equal(g.view(torch.int32), r.view(torch.int32)), \
+                    (rot, si, i)
+            for name, t in sinter.items():
+                assert torch.equal(t, ri[name]), (rot, si, name)
+    assert pipe.check_faults() == 0
+
+
+@pytest.mark.timeout(300)
 @pytest.mark.parametrize("rank", [1, 7])
 def test_cfg4_rank_shard(env, rank):
     """cfg4 (B = 128 over 8 GPUs, 16 per rank): the shard a rank owns (global cloud ids from

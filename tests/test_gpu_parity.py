@@ -758,7 +758,9 @@ def test_sample_and_group_knn(env):
 @pytest.mark.parametrize("kind,B,N,npoints", [
     ("scannet", 3, 8192, [1024, 256, 64, 16]), ("uniform", 2, 3000, [700, 128, 32]),
     ("grid", 2, 4096, [512, 100]), ("dup", 1, 700, [40, 20, 5, 3]), ("uniform", 2, 64, [16]),
-    ("scannet", 1, 8192, [1024, 1000, 900, 50])])
+    ("scannet", 1, 8192, [1024, 1000, 900, 50]), ("uniform", 2, 1024, [100, 300]),
+    ("grid", 2, 1000, [1000, 700, 64]), ("dup", 3, 1024, [256, 64, 16]),
+    ("fewuniq", 2, 1024, [512, 400])])
 def test_fps_chain(env, kind, B, N, npoints):
     """pn2_fps_chain (every SSG sampler of a cloud in one workgroup) gives exactly the
     per-stage farthest_point_sample_and_gather results, and the oracle's indices."""
