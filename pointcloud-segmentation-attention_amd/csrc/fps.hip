@@ -599,7 +599,7 @@ __global__ __launch_bounds__(kChainBlock) void fps_chain_kernel(const float* __r
     const float* cxyz = i == 0 ? sxyz : snew[(i - 1) & 1];
     float* next = i + 1 < c.stages ? snew[i & 1] : nullptr;
     chain_stage(cxyz, c.n[i], c.m[i], cxyz, c.idx[i] + (size_t)b * c.m[i],
-                c.nx[i] + (size_t)b * c.m[i] * 3, next, red, hot);
+                c.nx[i] ? c.nx[i] + (size_t)b * c.m[i] * 3 : nullptr, next, red, hot);
     __syncthreads();  // stage i's LDS output complete before stage i+1 reads it
   }
 }
@@ -630,7 +630,20 @@ int fps_impl(const float* xyz, int B, int N, int M, int32_t* idx, float* nx, voi
   else if (N <= 128) launch_v9<64, 2, 2>(xyz, B, N, M, idx, nx, s);
   else if (N <= 256) launch_v9<64, 4, 4, true>(xyz, B, N, M, idx, nx, s);
   else if (N <= 512) launch_v9<64, 8, 4, true>(xyz, B, N, M, idx, nx, s);
-  else if (N <= 1024) launch_v9<256, 4, 2, true>(xyz, B, N, M, idx, nx, s);
+  else if (N <= 1024) {
+    // the hot-set schedule of the fused chain (one stage): cfg1's 1,024 -> 256 sampler
+    if (M <= kChainNext) {
+      FpsChain c{};
+      c.stages = 1;
+      c.n[0] = N;
+      c.m[0] = M;
+      c.idx[0] = idx;
+      c.nx[0] = nx;
+      hipLaunchKernelGGL(fps_chain_kernel, dim3(B), dim3(kChainBlock), 0, s, xyz, c);
+    } else {
+      launch_v9<256, 4, 2, true>(xyz, B, N, M, idx, nx, s);
+    }
+  }
   else if (N <= 2048) launch_v9<256, 8, 2, true>(xyz, B, N, M, idx, nx, s);
   else if (N <= 4096) launch_v9<256, 16, 4, true>(xyz, B, N, M, idx, nx, s);
   else if (N <= 8192) {
