@@ -201,8 +201,7 @@ def pmc_traffic(config, B):
     (profiles/<round>/pmc_traffic_<config>_B<B>.json, written by tools/pmc_summary.py from
     separate FETCH_SIZE and WRITE_SIZE passes of this bench). Counters cannot be read inside
     this (unprofiled) process, so the figure is the profiled run's, for the same workload."""
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", f"pmc_traffic_{config}_B{B}.json")))
+    files = _profile_files(f"pmc_traffic_{config}_B{B}.json")
     if not files:
         return None, None
     with open(files[-1]) as f:
@@ -221,9 +220,23 @@ def pmc_traffic(config, B):
 MAX_CLOCK_GHZ = 2.4  # MI355X_MICROARCH.md, chip-level parameters
 
 
-def _latest_profile(name):
+def _profile_files(name):
+    """Committed profile files of this name, oldest first: profiles/r<N>/ and profiles/r<N>/*/,
+    by round, a round's end-of-round evidence (final/) last."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*", name)))
+    import re
+    files = (glob.glob(os.path.join(ROOT, "profiles", "*", name)) +
+             glob.glob(os.path.join(ROOT, "profiles", "*", "*", name)))
+
+    def key(p):
+        rel = os.path.relpath(p, os.path.join(ROOT, "profiles"))
+        m = re.match(r"r(\d+)", rel)
+        return (int(m.group(1)) if m else -1, "/final/" in "/" + rel, rel)
+    return sorted(files, key=key)
+
+
+def _latest_profile(name):
+    files = _profile_files(name)
     if not files:
         return None, None
     with open(files[-1]) as f:

@@ -188,7 +188,8 @@ def test_pipeline_rotations_equal_eager(env):
     before every other rotation; every set's outputs and index intermediates after every
     rotation equal the same clouds' eager step bit for bit. (A race inside the sampler chain's
     publishing -- a 16-byte centre write -- showed here once in ~40 rotations:
-    profiles/r5/chain_hot/pipe_stress_b128_publish.json; tools/pipe_stress.py runs longer.)"""
+    profiles/r5/chain_hot/tools.jsonl, pipe_stress_b128_publish.json; tools/pipe_stress.py
+    runs longer.)"""
     pkg, O, torch, dev = env
     S = pkg.stack
     B = 16
