@@ -173,25 +173,28 @@ struct FpsChain {
 // split by wave. Waves 1-3 (the cold waves) hold the cloud's points, PPT per thread, in the
 // reference's tie order (k mod 512, k div 512) (tf_sampling_g.cu:146-163); wave 0 (the hot
 // wave, alone on its SIMD) holds no points. A round:
-//   1. the cold waves' running mins are exact; the block max Mx and tau = Mx * frac (the
-//      smallest fraction whose count of points above it fits K = 64; the last round's
-//      fraction first) choose the hot set, which the cold waves stage, in tie order;
+//   1. the cold waves' running mins are exact; tau = ref * frac chooses the hot set (ref: the
+//      last round's tau, an upper bound of every value, else the block max; counted and
+//      staged for two fractions at once, the lower one taken when at most K = 64 points lie
+//      above it), which the cold waves stage, in tie order;
 //   2. wave 0 takes one hot point per lane and picks from them alone while its best value is
 //      > tau: every other point is <= tau and running mins only decrease, so that best IS the
-//      reference's next centre. Per pick: a wave max, one ballot, four readlanes and one LDS
-//      write of the centre -- no barrier, no LDS read;
+//      reference's next centre. Per pick: a wave max, one ballot, the winning lane's four
+//      4-byte LDS writes of the centre and the count, three readlanes -- no barrier, no LDS
+//      read;
 //   3. meanwhile the cold waves apply every published centre to their points (they poll the
-//      pick list), so their mins are exact again when the round ends.
+//      count), so their mins are exact again when the round ends.
+// The first picks of a stage are exact block argmaxes (the first rounds certify few picks).
 // A cloud of at most 64 points is all hot (wave 0 alone, tau = -1). If no fraction fits (ties
 // crowd the top) or the max is negative, one exact block argmax (fps_v9's rule: the lowest
 // position holding the max, position 0 when every value is below 0) picks the centre. The
 // outputs (idx, new_xyz, the next stage's LDS copy) are written from the pick list after the
-// stage. Same picks as fps_v9_body bit for bit: the same fp32 distance, the same int-bit
+// stage (bulk, coalesced). Same picks as fps_v9_body bit for bit: the same fp32 distance, the same int-bit
 // running mins and tie order.
 constexpr int kHotFracs = 12;  // kCullFrac (fps_cull.h): the thresholds
 constexpr int kHotK = kWave;  // hot points: one per lane of wave 0
 constexpr int kHotCold = kChainBlock / kWave - 1;  // cold waves
-constexpr int kHotPollLimit = 1 << 22;
+constexpr int kHotPollLimit = 1 << 22;  // a cold wave's polls per round (never reached: bound)
 #ifndef PN2_HOT_EXACT
 #define PN2_HOT_EXACT 16
 #endif
@@ -199,9 +202,9 @@ constexpr int kHotPollLimit = 1 << 22;
 #define PN2_HOT_EXACT2 6
 #endif
 constexpr int kHotExact = PN2_HOT_EXACT;  // picks of the 1,024-point stage made one at a time
-constexpr int kHotExact2 = PN2_HOT_EXACT2;  // ... of the smaller ones  // a cold wave's polls per round (never reached: bound)
+constexpr int kHotExact2 = PN2_HOT_EXACT2;  // ... of the smaller ones
 struct HotLds {
-  float4 pc[kChainNext];          // picks by number: x, y, z, bits(index); w = -1 until written
+  float4 pc[kChainNext];          // picks by number: x, y, z, bits(index)
   float4 hk[2][kHotCold][kHotK];  // hot staging for two thresholds, per cold wave: x, y, z, bits(index)
   int hv[2][kHotCold][kHotK];     // hot staging: running min (int bits)
   int wmax[2][kHotCold];          // per cold wave: its max (double-buffered by try)
@@ -229,18 +232,14 @@ __device__ unsigned long long g_hot_ev[3 * 64 * 8];
 // tie position p -> point index: p = k below 512 points, else p = 2 (k mod 512) + k div 512
 PN2_DEV int hot_point(int p, bool wide) { return wide ? (p >> 1) + ((p & 1) << 9) : p; }
 
-// wave 0's picks from its hot points (value hv, point hk, coordinates hx/hy/hz; empty lanes
-// hold INT_MIN) while the best is > tau and j < M; each pick is published at once: the
-// winning lane writes its centre to pc[j], then the count to *pub (fps_cull.h hot_publish;
-// DS operations of one wave execute in order, so a cold wave that reads the count reads the
-// centre). Returns the picks made so far.
 using hf4 = float __attribute__((ext_vector_type(4)));
 
 // wave 0's picks from its hot entries (e = x, y, z, bits(point index), value hv; empty lanes
 // hold INT_MIN) while the best is > tau and j < M; each pick is published at once (the count
-// after the centre; a cold wave reads the count, waits for it, then the centres). At most lim picks (a picked entry drops to 0 <= tau, so a round
-// cannot outrun its hot set -- except through NaN distances, which the bound covers; the all-hot
-// path, tau = -1, needs it to stop at M). Returns the picks made so far.
+// after the centre; a cold wave reads the count, waits for it, then the centres). At most lim
+// picks (a picked entry drops to 0 <= tau, so a round cannot outrun its hot set -- except
+// through NaN distances, which the bound covers; the all-hot path, tau = -1, needs it to stop
+// at M). Returns the picks made so far.
 PN2_DEV int hot_picks(hf4 e, int hv, int tau, int j, int lim, int* pub, HotLds& S) {
   j = __builtin_amdgcn_readfirstlane(j);  // (a scalar loop count: no exec-mask bookkeeping)
   // publishing addresses and the count in VGPRs, advanced by one VALU add per pick
