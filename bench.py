@@ -21,7 +21,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 # HIP hardware queues per process (GPU_MAX_HW_QUEUES, set from --hw-queues before HIP starts;
 # the GPU box exports 4). Streams map onto them round-robin. Measured on one box
-# (scripts/ab_queues.sh): with 4 queues the geometric step runs 21.7k
+# (scripts/archive/r5/ab_queues.sh): with 4 queues the geometric step runs 21.7k
 # clouds/s, with 8 or 16 the side lanes run fully beside the SA1 sampler and slow it from
 # 0.72 to 0.81 ms (18.7k clouds/s) -- while the whole-model step gains (11.2k -> 14.5k).
 DEFAULT_HW_QUEUES = 4
@@ -537,7 +537,7 @@ def main():
 
     # Lane 0 (the SA1 sampler chain) runs on the current stream. "high" makes it a
     # high-priority stream (HIP keeps a separate queue pool per priority, so the sampler never
-    # waits behind side-lane work in a shared queue). Measured (scripts/ab_prio.sh,
+    # waits behind side-lane work in a shared queue). Measured (scripts/archive/r5/ab_prio.sh,
     # DESIGN.md §3.6): the geometric step is faster with the default priority (21.8k vs 18.9k
     # clouds/s: with its side lanes fully concurrent the latency-bound sampler slows 0.715 ->
     # 0.80 ms), the whole model with high (its side lanes carry most of the work). "auto" =

@@ -163,6 +163,7 @@ constexpr int kChainNext = 1024;  // points per fused stage (LDS: input copy + 2
 
 struct FpsChain {
   int stages;
+  int* fault;  // the device fault word (fault_word_dev)
   int n[kChainMax], m[kChainMax];
   int32_t* idx[kChainMax];
   float* nx[kChainMax];
@@ -194,7 +195,11 @@ struct FpsChain {
 constexpr int kHotFracs = 12;  // kCullFrac (fps_cull.h): the thresholds
 constexpr int kHotK = kWave;  // hot points: one per lane of wave 0
 constexpr int kHotCold = kChainBlock / kWave - 1;  // cold waves
-constexpr int kHotPollLimit = 1 << 22;  // a cold wave's polls per round (never reached: bound)
+// a cold wave's polls per round: at PN2_FPS_POLL_LIMIT (fps_cull.h) it stores
+// PN2_FAULT_FPS_POLL and goes on waiting (the picks stay exact: the polltest build's 4 polls
+// report the fault without breaking the stage); at kHotPollHard (~2 s, a hung hot wave) it gives
+// up, and the stage's picks are wrong -- reported by the same fault
+constexpr int kHotPollHard = 1 << 24;
 #ifndef PN2_HOT_EXACT
 #define PN2_HOT_EXACT 16
 #endif
@@ -235,48 +240,49 @@ PN2_DEV int hot_point(int p, bool wide) { return wide ? (p >> 1) + ((p & 1) << 9
 using hf4 = float __attribute__((ext_vector_type(4)));
 
 // wave 0's picks from its hot entries (e = x, y, z, bits(point index), value hv; empty lanes
-// hold INT_MIN) while the best is > tau and j < M; each pick is published at once (the count
-// after the centre; a cold wave reads the count, waits for it, then the centres). At most lim
+// hold INT_MIN) while the best is > tau and j < M; each pick is published as it is made (its
+// slot with tag pick_tag(tag0 + pick), then -- released -- the count of the picks before it;
+// fps_cull.h hot_publish; a cold wave acquires the count, then reads the slots). At most lim
 // picks (a picked entry drops to 0 <= tau, so a round cannot outrun its hot set -- except
 // through NaN distances, which the bound covers; the all-hot path, tau = -1, needs it to stop
 // at M). Returns the picks made so far.
-PN2_DEV int hot_picks(hf4 e, int hv, int tau, int j, int lim, int* pub, HotLds& S) {
+PN2_DEV int hot_picks(hf4 e, int hv, int tau, int j, int lim, int* pub, HotLds& S, int tag0) {
   j = __builtin_amdgcn_readfirstlane(j);  // (a scalar loop count: no exec-mask bookkeeping)
-  // publishing addresses and the count in VGPRs, advanced by one VALU add per pick
-  int va_c, va_n, vcnt;
+  // publishing addresses, the count and the tag in VGPRs, advanced by one VALU add per pick
+  int va_c, va_n, vcnt, vtag;
   asm volatile("v_mov_b32 %0, %1" : "=v"(va_c)
                : "s"((uint32_t)(uintptr_t)(__attribute__((address_space(3))) float4*)&S.pc[j]));
   asm volatile("v_mov_b32 %0, %1" : "=v"(va_n)
                : "s"((uint32_t)(uintptr_t)(__attribute__((address_space(3))) int*)pub));
-  asm volatile("v_mov_b32 %0, %1" : "=v"(vcnt) : "s"(j + 1));
+  asm volatile("v_mov_b32 %0, %1" : "=v"(vcnt) : "s"(j));
+  asm volatile("v_mov_b32 %0, %1" : "=v"(vtag) : "s"(pick_tag(tag0 + j)));
   int n = 0;
   // (one exit, at the bottom: the loop carries no break flags)
   int km = __builtin_amdgcn_readlane(wave_max_i32_l63(hv), kWave - 1);
   while (km > tau) {  // else the certificate fails: the round ends
     const int L = (int)__builtin_ctzll(__builtin_amdgcn_ballot_w64(hv == km));
     float cx, cy, cz;
-    // (the centre as four 4-byte writes, fps_cull.h hot_publish: measured, a 16-byte write
-    // followed by the count's 4-byte write let a poller read the count with the centre not yet
-    // all there -- tools/pipe_stress.py, 9 mismatching tensors in 40 rotations)
-    hot_publish(L, va_c, va_n, vcnt, e.x, e.y, e.z, __float_as_int(e.w), cx, cy, cz);
+    hot_publish(L, va_c, va_n, vcnt, vtag, e.x, e.y, e.z, __float_as_int(e.w), cx, cy, cz);
     __builtin_amdgcn_sched_barrier(0);
     ++n;
     hv = min(hv, __float_as_int(sqdist(e.x, e.y, e.z, cx, cy, cz)));
     va_c += 16;
     vcnt += 1;
+    vtag += 1 << 16;
     km = __builtin_amdgcn_readlane(wave_max_i32_l63(hv), kWave - 1);
     km = n >= lim ? tau : km;
   }
   return j + n;
 }
 
+// tag0: the picks of the launch's earlier stages (the slots' tags are pick_tag(tag0 + pick))
 template <int PPT>
 PN2_DEV void fps_hot_body(const float* CXYZ, int N, int M, int32_t* I, float* NX, float* SNEXT,
-                          HotLds& S) {
+                          HotLds& S, int tag0, int* fault) {
   const int t = threadIdx.x, lane = t & (kWave - 1), w = t / kWave;
   const bool wide = N > 512;
   const float c0x = CXYZ[0], c0y = CXYZ[1], c0z = CXYZ[2];
-  if (t == 0) S.pc[0] = make_float4(c0x, c0y, c0z, __int_as_float(0));
+  if (t == 0) S.pc[0] = make_float4(c0x, c0y, c0z, __uint_as_float(pick_tag(tag0)));
   int j = 1;  // picks made (uniform)
   PN2_HOTEV(63, 0, __builtin_amdgcn_s_memtime())
   if (N <= kHotK) {
@@ -288,12 +294,12 @@ PN2_DEV void fps_hot_body(const float* CXYZ, int N, int M, int32_t* I, float* NX
       int hv = in ? min(__float_as_int(kInitTemp), __float_as_int(sqdist(hx, hy, hz, c0x, c0y, c0z)))
                   : (-2147483647 - 1);
       while (j < M) {
-        j = hot_picks(hf4{hx, hy, hz, __int_as_float(lane)}, hv, -1, j, M - j, &S.pub[0], S);
+        j = hot_picks(hf4{hx, hy, hz, __int_as_float(lane)}, hv, -1, j, M - j, &S.pub[0], S, tag0);
         if (j >= M) break;
         // every value < 0 (padding / negative NaN bits): fps_v9 picks point 0; refresh the
         // lanes' values from the centres published since (cheap: this path is degenerate)
         hv = in ? __float_as_int(kInitTemp) : (-2147483647 - 1);
-        if (lane == 0) S.pc[j] = make_float4(c0x, c0y, c0z, __int_as_float(0));
+        if (lane == 0) S.pc[j] = make_float4(c0x, c0y, c0z, __uint_as_float(pick_tag(tag0 + j)));
         ++j;
         for (int p = 0; p < j && in; ++p) {
           const float4 c = S.pc[p];
@@ -372,7 +378,7 @@ PN2_DEV void fps_hot_body(const float* CXYZ, int N, int M, int32_t* I, float* NX
       }
       const int old = __builtin_amdgcn_readfirstlane((int)best.y);
       const float cx = CXYZ[3 * old + 0], cy = CXYZ[3 * old + 1], cz = CXYZ[3 * old + 2];
-      if (t == 0) S.pc[j] = make_float4(cx, cy, cz, __int_as_float(old));
+      if (t == 0) S.pc[j] = make_float4(cx, cy, cz, __uint_as_float((uint32_t)old | pick_tag(tag0 + j)));
       if (w > 0) apply(cx, cy, cz);
       ++j;
       r = j;
@@ -511,22 +517,28 @@ PN2_DEV void fps_hot_body(const float* CXYZ, int N, int M, int32_t* I, float* NX
         const bool in = lane < c[0] + c[1] + c[2];
         const hf4 e = *reinterpret_cast<const hf4*>(&S.hk[sel][src][in ? off : 0]);
         const int hv = in ? S.hv[sel][src][off] : (-2147483647 - 1);
-        j = hot_picks(e, hv, tau, j, min(M - j, kHotK), pub, S);
+        j = hot_picks(e, hv, tau, j, min(M - j, kHotK), pub, S, tag0);
         PN2_HOTEV(round - 1, 2, __builtin_amdgcn_s_memtime())
         PN2_HOTEV(round - 1, 3, j)
-        if (lane == 0) {
-          asm volatile("" ::: "memory");
-          __hip_atomic_store(pub, j | kHotEnd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
+        if (lane == 0) publish_end(pub, j | kHotEnd);
       } else {
         // 3. the cold waves apply the centres as wave 0 publishes them, up to 64 per LDS read
-        for (int it = 0; it < kHotPollLimit; ++it) {
+        for (int it = 0; it < kHotPollHard; ++it) {
+          if (it == PN2_FPS_POLL_LIMIT && fault && lane == 0)
+            __hip_atomic_store(fault, PN2_FAULT_FPS_POLL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           const int sv = __builtin_amdgcn_readfirstlane(
               __hip_atomic_load(pub, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
           const int av = sv & (kHotEnd - 1);
           if (av > r) {
             const int n = min(av - r, kWave);
-            const float4 cv = S.pc[r + min(lane, n - 1)];
+            const int p = r + min(lane, n - 1);
+            const float4 cv = S.pc[p];
+            // every slot below the acquired count carries its pick's tag (fps_cull.h hot_publish)
+            if (__builtin_amdgcn_ballot_w64((__float_as_uint(cv.w) & ~kPickIdxMask) !=
+                                            pick_tag(tag0 + p))) {
+              PN2_TORN_SEEN();
+              continue;
+            }
             for (int i = 0; i < n; ++i) {
               const float cx = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__float_as_int(cv.x), i));
               const float cy = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__float_as_int(cv.y), i));
@@ -548,7 +560,7 @@ PN2_DEV void fps_hot_body(const float* CXYZ, int N, int M, int32_t* I, float* NX
   // the outputs from the pick list
   for (int i = t; i < M; i += kChainBlock) {
     const float4 c = S.pc[i];
-    I[i] = __float_as_int(c.w);
+    I[i] = (int)(__float_as_uint(c.w) & kPickIdxMask);
     if (NX) { NX[3 * i + 0] = c.x; NX[3 * i + 1] = c.y; NX[3 * i + 2] = c.z; }
     if (SNEXT) { SNEXT[3 * i + 0] = c.x; SNEXT[3 * i + 1] = c.y; SNEXT[3 * i + 2] = c.z; }
   }
@@ -564,17 +576,19 @@ PN2_DEV void fps_hot_body(const float* CXYZ, int N, int M, int32_t* I, float* NX
 #define PN2_CHAIN_HOT 1
 #endif
 PN2_DEV void chain_stage(const float* P, int N, int M, const float* CXYZ, int32_t* I, float* NX,
-                         float* SNEXT, uint2 (*red)[8], HotLds& hot) {
+                         float* SNEXT, uint2 (*red)[8], HotLds& hot, int tag0, int* fault) {
 #if PN2_CHAIN_HOT
   // (the pick list holds kChainNext: a larger last stage takes the v9 bodies below)
   if (M <= kChainNext) {
-    if (N <= 384) fps_hot_body<2>(CXYZ, N, M, I, NX, SNEXT, hot);
-    else if (N <= 512) fps_hot_body<3>(CXYZ, N, M, I, NX, SNEXT, hot);
-    else fps_hot_body<6>(CXYZ, N, M, I, NX, SNEXT, hot);
+    if (N <= 384) fps_hot_body<2>(CXYZ, N, M, I, NX, SNEXT, hot, tag0, fault);
+    else if (N <= 512) fps_hot_body<3>(CXYZ, N, M, I, NX, SNEXT, hot, tag0, fault);
+    else fps_hot_body<6>(CXYZ, N, M, I, NX, SNEXT, hot, tag0, fault);
     return;
   }
 #else
   (void)hot;
+  (void)tag0;
+  (void)fault;
 #endif
   const bool w0 = threadIdx.x < kWave;
   if (N <= 64) { if (w0) fps_v9_body<64, 1, 1>(P, N, M, CXYZ, I, NX, SNEXT, red); }
@@ -593,12 +607,18 @@ __global__ __launch_bounds__(kChainBlock) void fps_chain_kernel(const float* __r
   const int b = blockIdx.x;
   const float* __restrict__ P = xyz + (size_t)b * c.n[0] * 3;
   for (int e = threadIdx.x; e < 3 * c.n[0]; e += kChainBlock) sxyz[e] = P[e];
+  // the pick slots start untagged (an earlier workgroup on this CU left its own tags there)
+  for (int e = threadIdx.x; e < kChainNext; e += kChainBlock)
+    hot.pc[e] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   __syncthreads();
+  int tag0 = 0;  // the picks of the earlier stages: every slot tag of the launch is distinct
   for (int i = 0; i < c.stages; ++i) {
     const float* cxyz = i == 0 ? sxyz : snew[(i - 1) & 1];
     float* next = i + 1 < c.stages ? snew[i & 1] : nullptr;
     chain_stage(cxyz, c.n[i], c.m[i], cxyz, c.idx[i] + (size_t)b * c.m[i],
-                c.nx[i] ? c.nx[i] + (size_t)b * c.m[i] * 3 : nullptr, next, red, hot);
+                c.nx[i] ? c.nx[i] + (size_t)b * c.m[i] * 3 : nullptr, next, red, hot, tag0,
+                c.fault);
+    tag0 += c.m[i];
     __syncthreads();  // stage i's LDS output complete before stage i+1 reads it
   }
 }
@@ -634,6 +654,7 @@ int fps_impl(const float* xyz, int B, int N, int M, int32_t* idx, float* nx, voi
     if (M <= kChainNext) {
       FpsChain c{};
       c.stages = 1;
+      c.fault = fault_word_dev();
       c.n[0] = N;
       c.m[0] = M;
       c.idx[0] = idx;
@@ -720,6 +741,7 @@ int fps_chain_launch(const float* xyz, int B, int N, int nstages, const int* npo
   }
   FpsChain c;
   c.stages = nstages - first;
+  c.fault = fault_word_dev();
   int n = N;
   for (int i = 0; i < kChainMax; ++i) {
     const bool on = i < c.stages;
@@ -748,6 +770,20 @@ int pn2_hot_stamps(unsigned long long* host_out) {  // 3 x 64 x 8 u64 (DIAGNOSTI
   return (int)hipMemcpyFromSymbol(host_out, HIP_SYMBOL(pn2::g_hot_ev),
                                   sizeof(unsigned long long) * 3 * 64 * 8, 0,
                                   hipMemcpyDeviceToHost);
+}
+#endif
+
+#if PN2_PUBLISH_BROKEN
+// DIAGNOSTIC (torntest builds only): the slot reads whose tag check failed since the last call
+unsigned int pn2_torn_reads(void) {
+  unsigned int v = 0;
+  if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(pn2::g_torn_reads), sizeof(v), 0,
+                          hipMemcpyDeviceToHost) != hipSuccess)
+    return 0xFFFFFFFFu;
+  const unsigned int zero = 0;
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(pn2::g_torn_reads), &zero, sizeof(zero), 0,
+                          hipMemcpyHostToDevice);
+  return v;
 }
 #endif
 

@@ -191,30 +191,80 @@ PN2_DEV void hot_best4(const int (&hv)[4], const hf2 (&hx)[2], const hf2 (&hy)[2
         [k0] "v"(hk[0]), [k1] "v"(hk[1]), [k2] "v"(hk[2]), [k3] "v"(hk[3]));
 }
 
-// publish pick L from the winning lane itself (exec = lane L only): its lx, ly, lz, lk are the
-// centre, written to the batch slot at LDS address va_c, then the count vcnt to va_n (DS
-// operations of one wave execute in order, so a reader of the count reads the centre). The
-// centre's coordinates come back to SGPRs inside the same block (v_readlane ignores exec), so
-// no wait states follow the exec restore; L comes from SALU (no lane-select wait).
-PN2_DEV void hot_publish(int L, int va_c, int va_n, int vcnt, float lx, float ly, float lz,
-                         int lk, float& cx, float& cy, float& cz) {
+// ---- publishing picks to the cold waves (the SA1 sampler here, the chain in fps.hip) -------
+// A pick's slot is (x, y, z, w) with w = point index | pick_tag(p), p the pick's number in the
+// launch (the chain adds the earlier stages' picks). The protocol is the LLVM AMDGPU memory
+// model's own mapping of a workgroup-scope release / acquire on LDS, not the in-order execution
+// of a wave's DS operations (which no document promises across waves, and which a 16-byte centre
+// write followed by the count did break: profiles/r5/chain_hot/pipe_stress_b128_publish.json):
+//  * release: the count store that makes slot p visible is issued only after an
+//    s_waitcnt lgkmcnt has seen slot p's writes complete (hipcc emits exactly that wait before a
+//    __ATOMIC_RELEASE workgroup store to LDS). So the wait never stalls the hot wave, each pick
+//    publishes the count of the picks BEFORE it: slot p is written, then lgkmcnt(4) (everything
+//    but those 4 writes is complete -- slot p - 1 was written ~500 cycles earlier), then count p.
+//    The batch's last pick goes out with the end flag, after lgkmcnt(0);
+//  * acquire: a cold wave reads the count with __ATOMIC_ACQUIRE (ds_read, s_waitcnt lgkmcnt(0)
+//    before any later LDS read), then the slots below it.
+// On top, the consumer checks every slot's tag and re-polls on a mismatch (a stale slot from an
+// earlier batch or launch cannot carry p's tag: tags grow within a launch and the slots are
+// cleared at its start). The check is what a build that publishes the count BEFORE the centre
+// (-DPN2_PUBLISH_BROKEN=1, csrc/Makefile target torntest) leans on: it stays index-exact and
+// counts the torn reads it caught (pn2_torn_reads, tests/test_gpu_a_fullsize.py).
+#ifndef PN2_PUBLISH_BROKEN
+#define PN2_PUBLISH_BROKEN 0
+#endif
+PN2_DEV uint32_t pick_tag(int p) { return ((uint32_t)(p + 1) & 0xFFFFu) << 16; }
+constexpr uint32_t kPickIdxMask = 0xFFFFu;  // point indices < 65536 (N <= 16384 here)
+constexpr int kPickTagMax = 0xFFFF;         // picks per launch below this: tags never repeat
+#if PN2_PUBLISH_BROKEN
+__device__ unsigned int g_torn_reads;
+#define PN2_TORN_SEEN() if (lane == 0) atomicAdd(&g_torn_reads, 1u)
+#else
+#define PN2_TORN_SEEN()
+#endif
+
+// publish pick L from the winning lane itself (exec = lane L only): its lx, ly, lz and
+// lk | vtag are the slot at LDS address va_c; then, once the writes before them are complete,
+// the count vcnt (the picks of this batch before this one) to va_n. The centre's coordinates
+// come back to SGPRs inside the same block (v_readlane ignores exec), so no wait states follow
+// the exec restore; L comes from SALU (no lane-select wait).
+PN2_DEV void hot_publish(int L, int va_c, int va_n, int vcnt, int vtag, float lx, float ly,
+                         float lz, int lk, float& cx, float& cy, float& cz) {
   uint64_t sv;
+  int kt;
   asm volatile(
       "s_mov_b64 %[sv], exec\n\t"
       "s_lshl_b64 exec, 1, %[L]\n\t"
+#if PN2_PUBLISH_BROKEN
+      // DIAGNOSTIC: the count (including this pick) first, the slot ~800 cycles later (longer
+      // than a cold wave takes from reading the count to reading the slots)
+      "v_add_u32 %[kt], 1, %[n]\n\t"
+      "ds_write_b32 %[c], %[kt]\n\t"
+      "s_sleep 12\n\t"
+#endif
       "ds_write_b32 %[a], %[x]\n\t"
+      "v_or_b32 %[kt], %[k], %[tg]\n\t"
       "ds_write_b32 %[a], %[y] offset:4\n\t"
       "ds_write_b32 %[a], %[z] offset:8\n\t"
-      "ds_write_b32 %[a], %[k] offset:12\n\t"
+      "ds_write_b32 %[a], %[kt] offset:12\n\t"
+#if !PN2_PUBLISH_BROKEN
+      "s_waitcnt lgkmcnt(4)\n\t"
       "ds_write_b32 %[c], %[n]\n\t"
+#endif
       "v_readlane_b32 %[cx], %[x], %[L]\n\t"
       "v_readlane_b32 %[cy], %[y], %[L]\n\t"
       "v_readlane_b32 %[cz], %[z], %[L]\n\t"
       "s_mov_b64 exec, %[sv]"
-      : [sv] "=&s"(sv), [cx] "=&s"(cx), [cy] "=&s"(cy), [cz] "=&s"(cz)
+      : [sv] "=&s"(sv), [cx] "=&s"(cx), [cy] "=&s"(cy), [cz] "=&s"(cz), [kt] "=&v"(kt)
       : [L] "s"(L), [a] "v"(va_c), [c] "v"(va_n), [x] "v"(lx), [y] "v"(ly), [z] "v"(lz),
-        [k] "v"(lk), [n] "v"(vcnt)
+        [k] "v"(lk), [tg] "v"(vtag), [n] "v"(vcnt)
       : "memory", "scc");
+}
+
+// the end of a batch: every slot write complete (release), then the final count | end flag
+PN2_DEV void publish_end(int* word, int value) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __hip_atomic_store(word, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
 // the hot values after the pick (cx, cy, cz): running min with the fp32 distance
@@ -329,6 +379,10 @@ __device__ __attribute__((always_inline)) inline void hotcull_body(
   }
   const float* __restrict__ X = XYZ_LDS ? (const float*)sxyz : P;  // coordinates
   for (int e = t; e < NBK; e += BLOCK) shist[e] = 0u;
+  // the batch slots start untagged (LEAN: they alias shist, whose counts / offsets < 65536
+  // carry tag 0 too)
+  if constexpr (!LEAN)
+    for (int e = t; e < K + 1; e += BLOCK) scl_[e] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   if (t < NW * 4) swcnt[t / 4][t % 4] = 0u;
   // KG: the grid's address waits in LDS until the epilogue (a pointer kept in registers
   // through the pick loop made the allocator spill inside it)
@@ -453,7 +507,7 @@ __device__ __attribute__((always_inline)) inline void hotcull_body(
     }
   }
   if (t == 0) {  // the first batch: centre 0 (tf_sampling_g.cu:121-125), already complete
-    scl[0] = make_float4(X[0], X[1], X[2], __int_as_float(0));
+    scl[0] = make_float4(X[0], X[1], X[2], __uint_as_float(pick_tag(0)));
     sj[0] = 1 | kEnd;
     sj[1] = 0;
     for (int v = 0; v < NW; ++v) swmax[v] = -1;  // waves without cells keep -1
@@ -662,9 +716,9 @@ __device__ __attribute__((always_inline)) inline void hotcull_body(
         return true;
       }
       if (t == 0) {
-        scl[0] = make_float4(X[3 * k], X[3 * k + 1], X[3 * k + 2], __int_as_float(k));
-        asm volatile("" ::: "memory");
-        __hip_atomic_store(&sj[rp ^ 1], 1 | kEnd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        scl[0] = make_float4(X[3 * k], X[3 * k + 1], X[3 * k + 2],
+                             __uint_as_float((uint32_t)k | pick_tag(j)));
+        publish_end(&sj[rp ^ 1], 1 | kEnd);
       }
     }
     hot_turn = !stall;
@@ -676,8 +730,8 @@ __device__ __attribute__((always_inline)) inline void hotcull_body(
     for (int round = 0; round <= M; ++round) {
       if (hot_turn) {
         // ---- hot phase: certified picks while the best hot value is above T, each one
-        // published to the cold waves at once (scl[jj], then the count sj; DS operations of
-        // one wave execute in order, so a cold wave that reads the count reads the centre)
+        // published to the cold waves as it is made (scl[jj] with its tag, then -- released --
+        // the count sj of the picks before it; hot_publish)
         static_assert(HQ == 2 || HQ == 4, "hot entries per lane");
         int hv[HQ], hk[HQ];
         uint32_t hkey[HQ];
@@ -735,12 +789,15 @@ __device__ __attribute__((always_inline)) inline void hotcull_body(
         __builtin_amdgcn_s_waitcnt(0xC07F);
         // publishing addresses and the published count in VGPRs, advanced by one VALU add per
         // pick (as SGPRs they cost an SALU add and a v_mov each for the DS stores)
-        int va_c, va_n, vcnt;
+        // (vcnt: the picks of this batch so far, published after each pick's slot; vtag: the
+        // next pick's tag, pick_tag(j + vcnt))
+        int va_c, va_n, vcnt, vtag;
         asm volatile("v_mov_b32 %0, %1" : "=v"(va_c)
                      : "s"((uint32_t)(uintptr_t)(__attribute__((address_space(3))) float4*)&scl[0]));
         asm volatile("v_mov_b32 %0, %1" : "=v"(va_n)
                      : "s"((uint32_t)(uintptr_t)(__attribute__((address_space(3))) int*)&sj[rp]));
-        asm volatile("v_mov_b32 %0, 1" : "=v"(vcnt));
+        asm volatile("v_mov_b32 %0, 0" : "=v"(vcnt));
+        asm volatile("v_mov_b32 %0, %1" : "=v"(vtag) : "s"(pick_tag(j)));
         // the pick loop ends when the best hot value is no longer above T; it cannot run past
         // the nh <= K hot entries (a picked entry drops to 0 <= T), so only the last batch of
         // the cloud (fewer than K picks left) needs a count test per pick
@@ -784,23 +841,21 @@ __device__ __attribute__((always_inline)) inline void hotcull_body(
               L = (int)__builtin_ctzll(__builtin_amdgcn_ballot_w64(cv == wm && ck == km));
             }
             float cx, cy, cz;
-            hot_publish(L, va_c, va_n, vcnt, lx, ly, lz, lk, cx, cy, cz);
+            hot_publish(L, va_c, va_n, vcnt, vtag, lx, ly, lz, lk, cx, cy, cz);
             __builtin_amdgcn_sched_barrier(0);
             hot_update<HP>(hv, hx, hy, hz, cx, cy, cz);  // the next pick depends on it
             va_c += 16;
             vcnt += 1;
+            vtag += 1 << 16;
             if constexpr (CHECKED)
-              if (__builtin_amdgcn_readfirstlane(vcnt) > lim) break;
+              if (__builtin_amdgcn_readfirstlane(vcnt) >= lim) break;
           }
         };
         if (lim >= K) pick_loop(std::false_type{});
         else if (lim > 0) pick_loop(std::true_type{});
-        jj = __builtin_amdgcn_readfirstlane(vcnt) - 1;
+        jj = __builtin_amdgcn_readfirstlane(vcnt);
         if constexpr (PRIO > 0) __builtin_amdgcn_s_setprio(0);
-        if (lane == 0) {
-          asm volatile("" ::: "memory");
-          __hip_atomic_store(&sj[rp], jj | kEnd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
+        if (lane == 0) publish_end(&sj[rp], jj | kEnd);
         if constexpr (STAMP) {
           n_hot += jj;
         }
@@ -827,13 +882,19 @@ __device__ __attribute__((always_inline)) inline void hotcull_body(
         stop = (sv & kEnd) != 0;  // set in the same word as the final count
         if (av - applied >= GRP || (stop && av > applied)) {
           const int a1 = min(av, applied + GRP);
-          if constexpr (PRIO > 0) __builtin_amdgcn_s_setprio(PRIO - 1);
-          if constexpr (STAMP) tcnt0 = __builtin_amdgcn_s_memtime();
           const int ci = applied + lane / PPT;
           const bool valid = lane < GRP * PPT && ci < a1;
           const float4 cv = scl[valid ? ci : 0];
+          // every slot below the acquired count carries its pick's tag (see hot_publish)
+          if (__builtin_amdgcn_ballot_w64(
+                  valid && (__float_as_uint(cv.w) & ~kPickIdxMask) != pick_tag(j + ci))) {
+            PN2_TORN_SEEN();
+            continue;
+          }
+          if constexpr (PRIO > 0) __builtin_amdgcn_s_setprio(PRIO - 1);
+          if constexpr (STAMP) tcnt0 = __builtin_amdgcn_s_memtime();
           if (cw == 0 && valid && lane % PPT == 0) {  // wave 1 stores the batch's outputs
-            I[j + ci] = __float_as_int(cv.w);
+            I[j + ci] = (int)(__float_as_uint(cv.w) & kPickIdxMask);
             if (NX) {
               NX[3 * (j + ci)] = cv.x;
               NX[3 * (j + ci) + 1] = cv.y;

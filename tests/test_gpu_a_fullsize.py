@@ -366,6 +366,91 @@ def test_fps_poll_bound_reports_fault(env):
     assert pkg._lib.lib().pn2_fault_status(0) == 0
 
 
+def _chain_call(h, x, npoints, dev, torch):
+    """pn2_fps_chain through library handle h: [(idx, new_xyz)] per stage, and the return code."""
+    import ctypes
+    B, N = x.shape[0], x.shape[1]
+    outs = [(torch.empty((B, m), dtype=torch.int32, device=dev),
+             torch.empty((B, m, 3), dtype=torch.float32, device=dev)) for m in npoints]
+    npt = (ctypes.c_int * len(npoints))(*npoints)
+    ib = (ctypes.c_void_p * len(npoints))(*[o[0].data_ptr() for o in outs])
+    nb = (ctypes.c_void_p * len(npoints))(*[o[1].data_ptr() for o in outs])
+    rc = h.pn2_fps_chain(x.data_ptr(), B, N, len(npoints), ctypes.addressof(npt),
+                         ctypes.addressof(ib), ctypes.addressof(nb),
+                         torch.cuda.current_stream().cuda_stream)
+    return rc, outs
+
+
+def test_fps_chain_poll_bound_reports_fault(env):
+    """The sampler chain's hot-set stages report a cold wave's wait past its poll bound too
+    (PN2_FAULT_FPS_POLL; the polltest build's bound is 4 polls). The cold waves go on waiting
+    after reporting, so the stage's picks stay exact (they give up only at a hard bound that
+    only a hung hot wave reaches)."""
+    import ctypes
+    pkg, O, torch, dev = env
+    h = ctypes.CDLL(POLLTEST_LIB)
+    for name in ("pn2_fps_chain", "pn2_fault_status"):
+        fn = getattr(h, name)
+        fn.restype, fn.argtypes = pkg._lib.SIGNATURES[name]
+    x = _cloud(pkg, "scannet", 2, 1024)
+    rc, outs = _chain_call(h, torch.from_numpy(x).to(dev), [256, 64], dev, torch)
+    assert rc == 0
+    torch.cuda.synchronize()
+    assert h.pn2_fault_status(1) == pkg._lib.PN2_FAULT_FPS_POLL
+    ref = O.fps(x, 256)
+    _exact("chain stage 0 idx", outs[0][0].cpu().numpy(), ref)
+    _exact("chain stage 1 idx", outs[1][0].cpu().numpy(), O.fps(O.gather_point(x, ref), 64))
+    assert pkg._lib.lib().pn2_fault_status(0) == 0
+
+
+TORNTEST_LIB = os.path.join(os.path.dirname(HERE), PKG_NAME, "csrc", "build",
+                            "libpn2hip_torntest.so")
+
+
+def test_publish_tag_check_catches_torn_reads(env):
+    """The samplers' pick publishing (fps_cull.h hot_publish): a build that writes the count
+    BEFORE the centre, ~800 cycles ahead of it (-DPN2_PUBLISH_BROKEN=1, csrc/Makefile target
+    torntest), lets the cold waves read slots that are not yet written. Their tag check must
+    catch every such read (pn2_torn_reads counts them: > 0 here) and wait, so both users of the
+    publish -- the SA1 culled sampler and the SA2-4 chain -- stay index-exact."""
+    import ctypes
+    pkg, O, torch, dev = env
+    assert os.path.exists(TORNTEST_LIB), "build it: make -C <pkg>/csrc torntest"
+    h = ctypes.CDLL(TORNTEST_LIB)
+    for name in ("pn2_fps_gather", "pn2_fps_chain", "pn2_fault_status"):
+        fn = getattr(h, name)
+        fn.restype, fn.argtypes = pkg._lib.SIGNATURES[name]
+    h.pn2_torn_reads.restype, h.pn2_torn_reads.argtypes = ctypes.c_uint, []
+    st = torch.cuda.current_stream().cuda_stream
+    h.pn2_torn_reads()  # (clear)
+    # the SA1 sampler
+    x = _cloud(pkg, "scannet", 8, 8192, seed=5)
+    xt = torch.from_numpy(x).to(dev)
+    idx = torch.empty((8, 1024), dtype=torch.int32, device=dev)
+    nx = torch.empty((8, 1024, 3), dtype=torch.float32, device=dev)
+    assert h.pn2_fps_gather(xt.data_ptr(), 8, 8192, 1024, idx.data_ptr(), nx.data_ptr(), st) == 0
+    torch.cuda.synchronize()
+    torn_sa1 = h.pn2_torn_reads()
+    ref = O.fps(x, 1024)
+    _exact("torn-build SA1 idx", idx.cpu().numpy(), ref)
+    _exact("torn-build SA1 new_xyz", nx.cpu().numpy(), O.gather_point(x, ref))
+    # the chain (1,024 -> 256 -> 64 -> 16, from the SA1 picks)
+    nx1 = O.gather_point(x, ref)
+    rc, outs = _chain_call(h, torch.from_numpy(nx1).to(dev), [256, 64, 16], dev, torch)
+    assert rc == 0
+    torch.cuda.synchronize()
+    torn_chain = h.pn2_torn_reads()
+    cur = nx1
+    for k, ((i, n), m) in enumerate(zip(outs, [256, 64, 16])):
+        r = O.fps(cur, m)
+        _exact(f"torn-build chain stage {k} idx", i.cpu().numpy(), r)
+        cur = O.gather_point(cur, r)
+        _exact(f"torn-build chain stage {k} new_xyz", n.cpu().numpy(), cur)
+    assert h.pn2_fault_status(1) == 0
+    print(f"torn reads caught: SA1 {torn_sa1}, chain {torn_chain}")
+    assert torn_sa1 > 0 and torn_chain > 0, (torn_sa1, torn_chain)
+
+
 FPS_GOLDEN = sorted(glob.glob(os.path.join(HERE, "golden", "fps*.npz")))
 
 

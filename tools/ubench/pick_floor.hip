@@ -56,7 +56,7 @@ __global__ __launch_bounds__(64) void pick_floor_kernel(const float* __restrict_
       const int L = (int)__builtin_ctzll(__builtin_amdgcn_ballot_w64(cv == wm));
       float cx, cy, cz;
       if constexpr (VAR == 1) {
-        hot_publish(L, va_c, va_n, vcnt, lx, ly, lz, lk, cx, cy, cz);
+        hot_publish(L, va_c, va_n, vcnt, vcnt << 16, lx, ly, lz, lk, cx, cy, cz);
         va_c += 16;
         vcnt += 1;
       } else {
