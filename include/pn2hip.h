@@ -72,6 +72,7 @@ typedef void* pn2_stream_t; /* hipStream_t */
 #define PN2_OK 0
 #define PN2_EINVAL (-22)
 #define PN2_EFAULT (-14) /* an earlier launch stored a device fault code (pn2_fault_status)   */
+#define PN2_ENOTSUP (-95) /* valid arguments this device / path does not take (see each call)  */
 
 /* device fault codes (pn2_fault_status) */
 #define PN2_FAULT_FPS_POLL 1 /* culled sampler: a cold wave waited past its poll bound for
@@ -350,7 +351,8 @@ int pn2_fp_apply(const float* dist, const int32_t* idx, const void* unknown_grid
  * every workgroup sorts the cloud's m known points into a grid in its own LDS (the automatic
  * edge of pn2_grid_build) and searches it, then writes its rows -- the output of
  * pn2_grid_build + pn2_three_nn_grid + pn2_fp_apply, bit for bit. 1 <= m <= 4096 (else
- * PN2_EINVAL: use those three). `unknown_grid` (optional, a grid over the n unknown points)
+ * PN2_EINVAL); PN2_ENOTSUP when the known grid does not fit this device's LDS per workgroup
+ * (use those three). `unknown_grid` (optional, a grid over the n unknown points)
  * orders the rows as in pn2_fp_apply; with it xyz1 may be NULL. dist / idx (B,n,3): the
  * three_nn result as well, or both NULL. C1 + C2 >= 1. */
 int pn2_fp_grid_fused(const float* xyz1, const float* xyz2, const void* unknown_grid,
@@ -377,7 +379,8 @@ int pn2_attn_reduce(const float* Q, const float* K, const float* V, int B, int M
                     int C, float* out, pn2_stream_t stream);
 /* Several attention reductions of one nsample in ONE launch (the SSG stack's four SA layers,
  * attention_layer.py:35-42 per layer): per layer exactly pn2_attn_reduce(Q, K, V, B, M, ns,
- * C, out). nsample in {8, 16, 32, 64, 128}, the same for every layer, else PN2_EINVAL. */
+ * C, out); one nsample for every layer, else PN2_EINVAL (an nsample outside {8, 16, 32, 64, 128},
+ * or a layer too large for the one-launch task arithmetic, runs as pn2_attn_reduce does). */
 #define PN2_ATTN_MAX_LAYERS 4
 typedef struct pn2_attn_layer {
   const float* Q;

@@ -71,7 +71,7 @@ int pn2_plan_launch_timed(pn2_plan* plan, void* ev_start, void* ev_end);
  * unchanged while the plan is launched. */
 int pn2_plan_graph_direct(pn2_plan* plan, void* graph, pn2_stream_t stream);
 
-#define PN2_ENOTSUP (-95) /* pn2_plan_graph_direct: not a plain chain of kernel / memset nodes */
+/* PN2_ENOTSUP (pn2hip.h), from pn2_plan_graph_direct: not a plain chain of kernel / memset nodes */
 
 #ifdef __cplusplus
 }

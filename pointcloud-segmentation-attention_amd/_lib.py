@@ -19,7 +19,7 @@ PN2_EINVAL = -22
 PN2_BQ_MAX_RADII = 3  # include/pn2hip.h
 PN2_EFAULT = -14
 PN2_FAULT_FPS_POLL = 1
-PN2_ENOTSUP = -95  # include/pn2plan.h
+PN2_ENOTSUP = -95  # include/pn2hip.h
 PN2_FPS_AUTO, PN2_FPS_BLOCKSCAN = 0, 1
 PN2_USE_XYZ = 1
 PN2_XYZ_LAST = 2

@@ -39,7 +39,9 @@ def attention_reduce(Q, K, V):
 def attention_reduce_layers(qkvs):
     """attention_reduce of several layers that share nsample (the SSG stack's four SA layers)
     in ONE launch (pn2_attn_reduce_layers): qkvs = [(Q, K, V)], returns [out] per layer,
-    each exactly attention_reduce(Q, K, V). Inference only (no autograd)."""
+    each exactly attention_reduce(Q, K, V) (an nsample outside {8, 16, 32, 64, 128}, or a layer
+    too large for the one-launch task arithmetic, runs as attention_reduce runs it). All layers
+    share one nsample. Inference only (no autograd)."""
     if not 1 <= len(qkvs) <= PN2_ATTN_MAX_LAYERS:
         raise InvalidArgumentError(f"attention_reduce_layers: 1..{PN2_ATTN_MAX_LAYERS} layers")
     arr = (AttnLayer * len(qkvs))()

@@ -381,7 +381,7 @@ int pn2_attn_reduce_layers(const pn2_attn_layer* layers, int nlayers, int B,
                            pn2_stream_t stream) {
   if (!layers || nlayers < 1 || nlayers > PN2_ATTN_MAX_LAYERS || B < 0) return PN2_EINVAL;
   hipStream_t s = (hipStream_t)stream;
-  pn2::AttnLayers a{};
+  pn2::AttnLayers a{}, big{};
   int ns = 0;
   for (int i = 0; i < nlayers; ++i) {
     const pn2_attn_layer& l = layers[i];
@@ -393,12 +393,21 @@ int pn2_attn_reduce_layers(const pn2_attn_layer* layers, int nlayers, int B,
     if (!l.Q || !l.K || !l.V || !l.out || G > INT32_MAX) return PN2_EINVAL;
     if ((((uintptr_t)l.Q | (uintptr_t)l.K | (uintptr_t)l.V | (uintptr_t)l.out) & 15) != 0)
       return PN2_EINVAL;
-    if (!pn2::attn_small_tasks(G, l.C)) return PN2_EINVAL;
-    a.l[a.nlayers++] = pn2::AttnLayer{l.Q, l.K, l.V, l.out, (int)G, l.C, 0, {}};
+    // a layer too large for the FastDiv task arithmetic: its own generic launch, as
+    // pn2_attn_reduce runs it (the same results)
+    pn2::AttnLayers& dst = pn2::attn_small_tasks(G, l.C) ? a : big;
+    dst.l[dst.nlayers++] = pn2::AttnLayer{l.Q, l.K, l.V, l.out, (int)G, l.C, 0, {}};
   }
-  if (a.nlayers == 0) return PN2_OK;
-  const int rc = pn2::attn_launch(a, ns, s);
-  if (rc != PN2_OK) return rc;  // (an nsample the layers kernel has no instance for)
+  // an nsample the layers kernel has no instance for: every layer generic, as pn2_attn_reduce
+  if (a.nlayers > 0 && pn2::attn_launch(a, ns, s) != PN2_OK)
+    for (int i = 0; i < a.nlayers; ++i) big.l[big.nlayers++] = a.l[i];
+  for (int i = 0; i < big.nlayers; ++i) {
+    const pn2::AttnLayer& l = big.l[i];
+    hipLaunchKernelGGL(pn2::attn_reduce_generic_kernel,
+                       dim3(pn2::grid_for((long long)l.G * (l.C / 4))), dim3(pn2::kBlock), 0, s,
+                       l.Q, l.K, l.V, l.G, ns, l.C, l.out);
+  }
+  if (a.nlayers == 0 && big.nlayers == 0) return PN2_OK;
   PN2_RETURN_LAUNCH();
 }
 

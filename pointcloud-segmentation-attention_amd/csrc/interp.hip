@@ -938,10 +938,10 @@ int fp_grid_launch(const float* xyz1, const float* xyz2, const void* ugrid, cons
       blk(kFpgBlock);
   const size_t lds = fp_grid_lds(m);
   // the known grid must fit this device's LDS per workgroup (160 KB on gfx950; m = 4096 needs
-  // ~74 KB): a smaller part reports PN2_EINVAL, and fp_interpolate then takes the three-launch
-  // path (grid build + three_nn_grid + fp_apply)
+  // ~74 KB): a smaller part reports PN2_ENOTSUP, and fp_interpolate then takes the
+  // three-launch path (grid build + three_nn_grid + fp_apply)
   constexpr int FR = kFpgBlock / kNNGroup;
-  if (lds + 28 * FR + 64 > device_lds_per_block()) return PN2_EINVAL;  // (+ s_idx, s_wv, hdr)
+  if (lds + 28 * FR + 64 > device_lds_per_block()) return PN2_ENOTSUP;  // (+ s_idx, s_wv, hdr)
   if ((long long)FR * f.p.cw * f.p.cw >= (1LL << 32)) return PN2_EINVAL;
   const char* kg = (const char*)kgrid;
 #define PN2_FPG_K(V2, V1, U)                                                                   \

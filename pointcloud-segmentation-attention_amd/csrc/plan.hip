@@ -229,6 +229,15 @@ int pn2_plan_graph_direct(pn2_plan* plan, void* graph, pn2_stream_t stream) {
       if (hipGraphKernelNodeGetParams(nodes[i], &o.kp) != hipSuccess || o.kp.extra ||
           !o.kp.func)
         return PN2_ENOTSUP;
+      // hipLaunchKernel takes a registered host stub only; a node captured from
+      // hipModuleLaunchKernel holds a hipFunction_t instead, and node attributes (cooperative
+      // launch, ...) would be dropped: such nodes keep the graph launch
+      hipFuncAttributes fa;
+      if (hipFuncGetAttributes(&fa, o.kp.func) != hipSuccess) return PN2_ENOTSUP;
+      hipKernelNodeAttrValue av{};
+      if (hipGraphKernelNodeGetAttribute(nodes[i], hipKernelNodeAttributeCooperative, &av) ==
+              hipSuccess && av.cooperative)
+        return PN2_ENOTSUP;
     } else if (t == hipGraphNodeTypeMemset) {
       o.kind = kMemset;
       if (hipGraphMemsetNodeGetParams(nodes[i], &o.mp) != hipSuccess || o.mp.height > 1 ||

@@ -27,7 +27,7 @@ import ctypes
 import torch
 
 from . import tf_grouping, tf_interpolate, tf_sampling, tf_util
-from ._lib import (POOL_MODES, PN2_BQ_MAX_RADII, PN2_EINVAL, PN2_FP_MAX_LAYERS, PN2_POOL_NONE,
+from ._lib import (POOL_MODES, PN2_BQ_MAX_RADII, PN2_ENOTSUP, PN2_FP_MAX_LAYERS, PN2_POOL_NONE,
                    PN2_SA_MAX_LAYERS, PN2_USE_XYZ, PN2_XYZ_LAST, FpLayer, InvalidArgumentError,
                    SaLayer, check, device_tensor, lib, ptr, stream_of)
 
@@ -136,8 +136,9 @@ def ball_group_xyz_radii(radii, nsamples, xyz, new_xyz, grid):
     B, N, M = int(xyz.shape[0]), int(xyz.shape[1]), int(new_xyz.shape[1])
     if int(new_xyz.shape[0]) != B:
         raise InvalidArgumentError("ball_group_xyz_radii: xyz and new_xyz need the same batch")
-    if nr * ((N + 31) // 32 + max(int(n) for n in nsamples)) > 4096:
-        # the bitmasks' and hit lists' LDS bound: one launch per radius
+    if nr * ((N + 31) // 32) > 4096:
+        # the bitmasks' LDS bound (grid.hip ball_query_grid: 4 waves x nr x words x 4 B <= 64 KB;
+        # the xyz-only path keeps no hit lists): one launch per radius
         return [ball_group_xyz(r, ns, xyz, new_xyz, grid) for r, ns in zip(radii, nsamples)]
     outs = []
     for ns in nsamples:
@@ -326,8 +327,9 @@ def fp_interpolate(xyz1, xyz2, points1, points2, known_grid=None, unknown_grid=N
             None if unknown_grid is None else ptr(unknown_grid.buf),
             ptr(points1), C1, ptr(points2), C2, B, n, m, ptr(out),
             ptr(nn[0]) if nn else None, ptr(nn[1]) if nn else None, stream_of(xyz1))
-        if rc == PN2_EINVAL and B > 0 and n > 0:
-            # (the arguments are valid: the known grid does not fit this device's LDS)
+        if rc == PN2_ENOTSUP:
+            # (the known grid does not fit this device's LDS per workgroup; any other code,
+            # PN2_EINVAL included, is an argument error and raises below)
             nn = tf_interpolate.three_nn(xyz1, xyz2, known_grid, unknown_grid)
             out = fp_apply(nn, points1, points2, unknown_grid)
         else:
@@ -346,8 +348,9 @@ def fp_interpolate(xyz1, xyz2, points1, points2, known_grid=None, unknown_grid=N
                                      ptr(points1), C1, ptr(points2), C2, B, n, m, ptr(out),
                                      ptr(nn[0]) if nn else None, ptr(nn[1]) if nn else None,
                                      stream_of(xyz1))
-        if rc == PN2_EINVAL and B > 0 and n > 0:
-            # (the arguments are valid: the known grid does not fit this device's LDS)
+        if rc == PN2_ENOTSUP:
+            # (the known grid does not fit this device's LDS per workgroup; any other code,
+            # PN2_EINVAL included, is an argument error and raises below)
             nn = tf_interpolate.three_nn(xyz1, xyz2, None, unknown_grid)
             out = fp_apply(nn, points1, points2, unknown_grid)
         else:

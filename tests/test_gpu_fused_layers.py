@@ -245,6 +245,7 @@ def test_ball_group_rejects(env):
     [(1024, 32, 64), (256, 32, 128), (64, 32, 256), (16, 32, 512)],
     [(100, 8, 4), (7, 8, 12)],          # few heads, odd group counts
     [(33, 128, 32)],                    # one layer, ns 128
+    [(50, 20, 16), (9, 20, 8)],         # an nsample without a layers-kernel instance: per layer
 ])
 def test_attention_reduce_layers(env, shapes):
     """attention_layer.attention_reduce_layers (pn2_attn_reduce_layers: several layers' attention
