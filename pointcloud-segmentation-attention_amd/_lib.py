@@ -82,6 +82,7 @@ PN2_ATTN_MAX_LAYERS = 4
 SIGNATURES = {
     "pn2_version": (ctypes.c_char_p, []),
     "pn2_strerror": (ctypes.c_char_p, [_I]),
+    "pn2_copy_f4": (_I, [_P, _P, _S, _I, _P]),
     "pn2_fps": (_I, [_P, _I, _I, _I, _P, _P]),
     "pn2_fps_gather": (_I, [_P, _I, _I, _I, _P, _P, _P]),
     "pn2_fps_max_points": (_I, []),

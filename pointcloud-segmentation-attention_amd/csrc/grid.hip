@@ -40,14 +40,26 @@ constexpr int kMaxBitWords = 4096;  // bitmask words per wave (N <= 131072)
 // iteration (~35 us for a 16,384-point cloud); PPT = 0 keeps that loop for clouds beyond
 // kBuildBlock * kBuildMaxPpt points.
 constexpr int kBuildMaxPpt = 16;
+constexpr int kBuildSmallN = 2048;     // clouds up to this many points: 256-thread workgroups
+// LDS count words of an explicit-edge build: the full cap (an 8192-word array, 32 KB, sent the
+// SA1 crops' 0.1-edge grids to the global-count path: their build 24 -> 65 us, profiles/r6/gb)
+constexpr int kBuildCapEdge = kGridCap;
 
-template <int PPT>
-__global__ __launch_bounds__(kBuildBlock) void grid_build_kernel(const float* __restrict__ xyz,
-                                                                 int N, float edge,
-                                                                 char* __restrict__ grid) {
-  constexpr int NW = kBuildBlock / kWave;
+// One workgroup of BLOCK threads per cloud. The count array lives in dynamic LDS of `cap`
+// words, which the host sizes to the cells the grid can have: max(N, 64) for the automatic
+// edge (grid_dims' bound), kBuildCapEdge for an explicit edge, the full kGridCap for the
+// point-loop build (PPT = 0). A workgroup with ~128 KB of LDS -- the array sized kGridCap for
+// every grid, as rounds 1-5 had it -- waits in a busy pipeline for a CU to drain completely
+// (cfg3's 1,024-point known grid: 78.7 us per build in the pipeline against ~14 alone). A
+// grid with more cells than `cap` (an explicit edge over a big extent; PPT > 0 then) counts
+// in its own offset array in global memory instead.
+template <int PPT, int BLOCK>
+__global__ __launch_bounds__(BLOCK) void grid_build_kernel(const float* __restrict__ xyz, int N,
+                                                           float edge, char* __restrict__ grid,
+                                                           int cap) {
+  constexpr int NW = BLOCK / kWave;
   constexpr int R = PPT > 0 ? PPT : 1;  // register slots
-  __shared__ uint32_t cnt[kGridCap];
+  extern __shared__ uint32_t s_cnt[];   // cap words
   __shared__ float red[6][NW];
   __shared__ int wsum[NW];
   __shared__ GridHdr sh;
@@ -57,12 +69,12 @@ __global__ __launch_bounds__(kBuildBlock) void grid_build_kernel(const float* __
   int* __restrict__ off = (int*)(G + sizeof(GridHdr));
   float4* __restrict__ pts = (float4*)(G + kGridOffBytes);
 
-  // 0. the thread's points (k = t + i * kBuildBlock), all loads in flight at once
+  // 0. the thread's points (k = t + i * BLOCK), all loads in flight at once
   float rx[R], ry[R], rz[R];
   if constexpr (PPT > 0) {
 #pragma unroll
     for (int i = 0; i < PPT; ++i) {
-      const int k = min(t + i * kBuildBlock, N - 1);  // clamped: loads stay in bounds (N > 0)
+      const int k = min(t + i * BLOCK, N - 1);  // clamped: loads stay in bounds (N > 0)
       rx[i] = P[3 * k + 0];
       ry[i] = P[3 * k + 1];
       rz[i] = P[3 * k + 2];
@@ -74,14 +86,14 @@ __global__ __launch_bounds__(kBuildBlock) void grid_build_kernel(const float* __
   if constexpr (PPT > 0) {
 #pragma unroll
     for (int i = 0; i < PPT; ++i) {
-      if (t + i * kBuildBlock < N) {
+      if (t + i * BLOCK < N) {
         mn[0] = fminf(mn[0], rx[i]); mx[0] = fmaxf(mx[0], rx[i]);
         mn[1] = fminf(mn[1], ry[i]); mx[1] = fmaxf(mx[1], ry[i]);
         mn[2] = fminf(mn[2], rz[i]); mx[2] = fmaxf(mx[2], rz[i]);
       }
     }
   } else {
-    for (int k = t; k < N; k += kBuildBlock) {
+    for (int k = t; k < N; k += BLOCK) {
 #pragma unroll
       for (int a = 0; a < 3; ++a) {
         const float v = P[3 * k + a];
@@ -113,16 +125,61 @@ __global__ __launch_bounds__(kBuildBlock) void grid_build_kernel(const float* __
   }
   __syncthreads();
   const GridHdr h = sh;
-  for (int i = t; i < h.ncell; i += kBuildBlock) cnt[i] = 0;
-  __syncthreads();
-
-  // 2. count points per cell
   auto cell_at = [&](float x, float y, float z) {
     const int ix = cell_coord(x, h.ox, h.inv, h.nx);
     const int iy = cell_coord(y, h.oy, h.inv, h.ny);
     const int iz = cell_coord(z, h.oz, h.inv, h.nz);
     return (iz * h.ny + iy) * h.nx + ix;
   };
+
+  if (PPT > 0 && h.ncell > cap) {
+    // ---- more cells than the LDS array: counts, offsets and ranks in the grid's offset array
+    // (global atomics; the loads that read other threads' results bypass L1, and an agent-scope
+    // fence orders each phase's writes before the barrier)
+    auto fence_barrier = [] {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      __syncthreads();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    };
+    auto ld = [&](int i) { return __hip_atomic_load(&off[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+    for (int i = t; i < h.ncell; i += BLOCK) off[i] = 0;
+    fence_barrier();
+    int rc[R], rk[R];
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      rc[i] = cell_at(rx[i], ry[i], rz[i]);
+      rk[i] = t + i * BLOCK < N ? atomicAdd(&off[rc[i]], 1) : 0;
+    }
+    fence_barrier();
+    const int per = (h.ncell + BLOCK - 1) / BLOCK;
+    const int s0 = min(t * per, h.ncell), s1 = min(s0 + per, h.ncell);
+    int sum = 0;
+    for (int i = s0; i < s1; ++i) sum += ld(i);
+    const int incl = wave_incl_scan(sum, lane);
+    if (lane == kWave - 1) wsum[w] = incl;
+    __syncthreads();
+    int base = incl - sum;
+    for (int i = 0; i < w; ++i) base += wsum[i];
+    for (int i = s0; i < s1; ++i) {
+      const int c = ld(i);
+      off[i] = base;
+      base += c;
+    }
+    if (t == 0) off[h.ncell] = N;
+    fence_barrier();
+#pragma unroll
+    for (int i = 0; i < R; ++i) {
+      const int k = t + i * BLOCK;
+      if (k < N) pts[ld(rc[i]) + rk[i]] = make_float4(rx[i], ry[i], rz[i], __int_as_float(k));
+    }
+    return;
+  }
+
+  uint32_t* cnt = s_cnt;
+  for (int i = t; i < h.ncell; i += BLOCK) cnt[i] = 0;
+  __syncthreads();
+
+  // 2. count points per cell
   // (with the points in registers the count's atomic returns each point's rank in its cell,
   // kept beside its cell: the scatter then needs no second atomic pass)
   int rc[R], rk[R];
@@ -130,17 +187,17 @@ __global__ __launch_bounds__(kBuildBlock) void grid_build_kernel(const float* __
 #pragma unroll
     for (int i = 0; i < PPT; ++i) {
       rc[i] = cell_at(rx[i], ry[i], rz[i]);
-      rk[i] = t + i * kBuildBlock < N ? (int)atomicAdd(&cnt[rc[i]], 1u) : 0;
+      rk[i] = t + i * BLOCK < N ? (int)atomicAdd(&cnt[rc[i]], 1u) : 0;
     }
   } else {
-    for (int k = t; k < N; k += kBuildBlock)
+    for (int k = t; k < N; k += BLOCK)
       atomicAdd(&cnt[cell_at(P[3 * k + 0], P[3 * k + 1], P[3 * k + 2])], 1u);
   }
   __syncthreads();
 
   // 3. exclusive scan of the counts (contiguous chunk per thread) -> offsets and cursors
-  const int per = (h.ncell + kBuildBlock - 1) / kBuildBlock;
-  const int s0 = t * per, s1 = min(s0 + per, h.ncell);
+  const int per = (h.ncell + BLOCK - 1) / BLOCK;
+  const int s0 = min(t * per, h.ncell), s1 = min(s0 + per, h.ncell);
   int sum = 0;
   for (int i = s0; i < s1; ++i) sum += (int)cnt[i];
   const int incl = wave_incl_scan(sum, lane);
@@ -161,11 +218,11 @@ __global__ __launch_bounds__(kBuildBlock) void grid_build_kernel(const float* __
   if constexpr (PPT > 0) {
 #pragma unroll
     for (int i = 0; i < PPT; ++i) {
-      const int k = t + i * kBuildBlock;
+      const int k = t + i * BLOCK;
       if (k < N) pts[(int)cnt[rc[i]] + rk[i]] = make_float4(rx[i], ry[i], rz[i], __int_as_float(k));
     }
   } else {
-    for (int k = t; k < N; k += kBuildBlock) {
+    for (int k = t; k < N; k += BLOCK) {
       const float x = P[3 * k + 0], y = P[3 * k + 1], z = P[3 * k + 2];
       const int pos = (int)atomicAdd(&cnt[cell_at(x, y, z)], 1u);
       pts[pos] = make_float4(x, y, z, __int_as_float(k));
@@ -396,17 +453,51 @@ int pn2_grid_build(const float* xyz, int B, int N, float cell_edge, void* grid,
   if (B == 0) return PN2_OK;
   if (!grid || grid_bytes < pn2_grid_size(B, N) || (N > 0 && !xyz)) return PN2_EINVAL;
   if ((uintptr_t)grid % 16 || B > 65535) return PN2_EINVAL;
-  const int ppt = (N + pn2::kBuildBlock - 1) / pn2::kBuildBlock;
-  const dim3 grd(B), blk(pn2::kBuildBlock);
   hipStream_t s = (hipStream_t)stream;
   char* g = (char*)grid;
-  if (N == 0) hipLaunchKernelGGL(pn2::grid_build_kernel<0>, grd, blk, 0, s, xyz, N, cell_edge, g);
-  else if (ppt <= 2) hipLaunchKernelGGL(pn2::grid_build_kernel<2>, grd, blk, 0, s, xyz, N, cell_edge, g);
-  else if (ppt <= 4) hipLaunchKernelGGL(pn2::grid_build_kernel<4>, grd, blk, 0, s, xyz, N, cell_edge, g);
-  else if (ppt <= 8) hipLaunchKernelGGL(pn2::grid_build_kernel<8>, grd, blk, 0, s, xyz, N, cell_edge, g);
-  else if (ppt <= pn2::kBuildMaxPpt)
-    hipLaunchKernelGGL(pn2::grid_build_kernel<pn2::kBuildMaxPpt>, grd, blk, 0, s, xyz, N, cell_edge, g);
-  else hipLaunchKernelGGL(pn2::grid_build_kernel<0>, grd, blk, 0, s, xyz, N, cell_edge, g);
+  const dim3 grd(B);
+  // (dynamic LDS up to the full kGridCap array, 128 KB: opted into once per instantiation)
+  static const hipError_t attr = [] {
+    hipError_t e = hipSuccess;
+    auto opt = [&](const void* f) {
+      const hipError_t r = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               (int)(pn2::kGridCap * 4));
+      if (r != hipSuccess) e = r;
+    };
+    opt(reinterpret_cast<const void*>(&pn2::grid_build_kernel<0, 256>));
+    opt(reinterpret_cast<const void*>(&pn2::grid_build_kernel<2, 256>));
+    opt(reinterpret_cast<const void*>(&pn2::grid_build_kernel<4, 256>));
+    opt(reinterpret_cast<const void*>(&pn2::grid_build_kernel<8, 256>));
+    opt(reinterpret_cast<const void*>(&pn2::grid_build_kernel<2, pn2::kBuildBlock>));
+    opt(reinterpret_cast<const void*>(&pn2::grid_build_kernel<4, pn2::kBuildBlock>));
+    opt(reinterpret_cast<const void*>(&pn2::grid_build_kernel<8, pn2::kBuildBlock>));
+    opt(reinterpret_cast<const void*>(&pn2::grid_build_kernel<pn2::kBuildMaxPpt, pn2::kBuildBlock>));
+    opt(reinterpret_cast<const void*>(&pn2::grid_build_kernel<0, pn2::kBuildBlock>));
+    return e;
+  }();
+  if (attr != hipSuccess) return (int)attr;
+  // the count array's words (grid_build_kernel): what the grid's cells can number
+  const bool loop = N > pn2::kBuildBlock * pn2::kBuildMaxPpt;
+  const int cap = loop ? pn2::kGridCap
+                       : (cell_edge > 0.0f ? pn2::kBuildCapEdge : std::max(N, pn2::kAutoMinCells));
+  const size_t lds = (size_t)cap * 4;
+#define PN2_GB(PPT, BLK) \
+  hipLaunchKernelGGL((pn2::grid_build_kernel<PPT, BLK>), grd, dim3(BLK), lds, s, xyz, N, cell_edge, g, cap)
+  if (N <= pn2::kBuildSmallN) {  // 256 threads: PPT <= 8
+    const int ppt = (N + 255) / 256;
+    if (N == 0) PN2_GB(0, 256);
+    else if (ppt <= 2) PN2_GB(2, 256);
+    else if (ppt <= 4) PN2_GB(4, 256);
+    else PN2_GB(8, 256);
+  } else {
+    const int ppt = (N + pn2::kBuildBlock - 1) / pn2::kBuildBlock;
+    if (ppt <= 2) PN2_GB(2, pn2::kBuildBlock);
+    else if (ppt <= 4) PN2_GB(4, pn2::kBuildBlock);
+    else if (ppt <= 8) PN2_GB(8, pn2::kBuildBlock);
+    else if (ppt <= pn2::kBuildMaxPpt) PN2_GB(pn2::kBuildMaxPpt, pn2::kBuildBlock);
+    else PN2_GB(0, pn2::kBuildBlock);
+  }
+#undef PN2_GB
   PN2_RETURN_LAUNCH();
 }
 

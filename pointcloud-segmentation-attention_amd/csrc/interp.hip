@@ -174,6 +174,21 @@ PN2_DEV bool box_certifies(const GridHdr& h, float px, float py, float pz, int x
   return gap > 0.0f && d3 < gap * gap * 0.9999f;
 }
 
+// a cell's gap along one axis from p (p's own cell: 0), less the certificate's slack (0 at
+// least): every point the grid assigns to cell c of that axis is at least this far from p
+// along it. Cells below p's are bounded by their upper face, cells above by their lower one
+// (never a clamped grid boundary: c < cp <= n - 1 and c > cp >= 0).
+PN2_DEV float axis_gap(float p, float o, float edge, int c, int cp) {
+  if (c == cp) return 0.0f;
+  const int f = c > cp ? c : c + 1;  // the face between p and cell c
+  const float fc = o + (float)f * edge;
+  const float d = c > cp ? fc - p : p - fc;
+  return fmaxf(d - 1e-5f * (fabsf(p) + fabsf(o) + fabsf(fc) + (float)f * edge) - 1e-30f, 0.0f);
+}
+// cells whose squared gap exceeds d3 (the certificate's 0.9999 slack for the distance's fp32
+// rounding) hold only points strictly farther than the third best: they cannot enter the top 3
+PN2_DEV bool gap_excludes(float g2, float d3) { return d3 < g2 * 0.9999f; }
+
 constexpr int kNNFirst = 1;  // the walk's first pass: the cube of shells 0..kNNFirst
 // (Measured and not kept, profiles/r5/round2: the cube's rows a z slab at a time with the
 // slab's offsets and first points loaded together -- FP4 42.5 -> 44.3 us; the walk is not
@@ -213,14 +228,60 @@ PN2_DEV Best3 grid_nn3(const GridHdr& h, const float4* __restrict__ pts,
         best3_insert_lex(best, sqdist(p.x, p.y, p.z, px, py, pz), __float_as_int(p.w));
       }
     };
-    for (int z = max(zl, 0); z <= min(zh, h.nz - 1); ++z) {
-      for (int y = max(yl, 0); y <= min(yh, h.ny - 1); ++y) {
-        const int row = (z * h.ny + y) * h.nx;
-        if (block || z == zl || z == zh || y == yl || y == yh) {
-          visit(off[row + x0], off[row + x1 + 1]);  // a face row: all of x0..x1
-        } else {
-          if (xl >= 0) visit(off[row + xl], off[row + xl + 1]);
-          if (xh < h.nx) visit(off[row + xh], off[row + xh + 1]);
+    if (block) {
+      for (int z = max(zl, 0); z <= min(zh, h.nz - 1); ++z) {
+        for (int y = max(yl, 0); y <= min(yh, h.ny - 1); ++y) {
+          const int row = (z * h.ny + y) * h.nx;
+          if (block || z == zl || z == zh || y == yl || y == yh) {
+            visit(off[row + x0], off[row + x1 + 1]);  // a face row: all of x0..x1
+          } else {
+            if (xl >= 0) visit(off[row + xl], off[row + xl + 1]);
+            if (xh < h.nx) visit(off[row + xh], off[row + xh + 1]);
+          }
+        }
+      }
+    } else {
+      // shells past the first: only the cells that can still hold a point within the merged
+      // third-best distance of the shells before (most of a shell is farther: skipped whole
+      // z slabs and rows, face rows narrowed to their x cells within reach). The quad's lanes
+      // hold the same merged list, so they take the same cells. A skipped cell is farther
+      // than the final third best too (it only shrinks), so the certificate below is unchanged.
+      // (Measured, tools/bench_nn.py, profiles/r6/nn: neutral at FP4's automatic edge -- 42.4
+      // vs 42.6 us fused, the 27-cell first pass nearly always certifies -- and 42.5 -> 39 us
+      // for the grid search over a 0.15 edge, where later shells are common.)
+      const float d3 = res.d3, edge = 1.0f / h.inv;
+#pragma nounroll
+      for (int z = max(zl, 0); z <= min(zh, h.nz - 1); ++z) {
+        const float gz = axis_gap(pz, h.oz, edge, z, cz), gz2 = gz * gz;
+        if (gap_excludes(gz2, d3)) continue;
+#pragma nounroll
+        for (int y = max(yl, 0); y <= min(yh, h.ny - 1); ++y) {
+          const float gy = axis_gap(py, h.oy, edge, y, cy), gyz = gz2 + gy * gy;
+          if (gap_excludes(gyz, d3)) continue;
+          const int row = (z * h.ny + y) * h.nx;
+          // the row's cells in reach: a face row's x0..x1 narrowed from both ends, an inner
+          // row's two shell cells xl and xh (each tested on its own)
+          const bool face = z == zl || z == zh || y == yl || y == yh;
+          int xa = face ? x0 : xl, xb = face ? x1 : xh;
+#pragma nounroll
+          while (xa <= xb) {
+            const float g = axis_gap(px, h.ox, edge, xa, cx);
+            if (xa >= 0 && xa < h.nx && !gap_excludes(gyz + g * g, d3)) break;
+            xa = face || xa != xl ? xa + 1 : xh;
+          }
+#pragma nounroll
+          while (xb > xa) {
+            const float g = axis_gap(px, h.ox, edge, xb, cx);
+            if (xb >= 0 && xb < h.nx && !gap_excludes(gyz + g * g, d3)) break;
+            xb = face || xb != xh ? xb - 1 : xl;
+          }
+          if (xa > xb) continue;
+          if (face || xa == xb) {
+            visit(off[row + xa], off[row + xb + 1]);
+          } else {  // both shell cells of an inner row
+            visit(off[row + xa], off[row + xa + 1]);
+            visit(off[row + xb], off[row + xb + 1]);
+          }
         }
       }
     }

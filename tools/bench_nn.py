@@ -68,6 +68,12 @@ def main():
         None, k.data_ptr(), ug.buf.data_ptr(), None, 0, p2.data_ptr(), 128, B, n, m,
         out2.data_ptr(), dist.data_ptr(), idx.data_ptr(), st))
     assert torch.equal(out, out2) and torch.equal(idx, ref[1])
+    kg0 = pkg.grid.PointGrid(k, 0.0)
+    out3 = torch.empty((B, n, 128), device=dev)
+    res["fp4 grid fused known"] = timeit(lambda: L.pn2_fp_grid_fused_known(
+        kg0.buf.data_ptr(), None, k.data_ptr(), ug.buf.data_ptr(), None, 0, p2.data_ptr(), 128,
+        B, n, m, out3.data_ptr(), None, None, st))
+    assert torch.equal(out, out3)
     # cfg3's FP4: points1 = rgb + normals (C1 = 9, rows of 137 floats: not 16-B aligned)
     p1 = torch.rand((B, n, 9), device=dev)
     o3 = torch.empty((B, n, 137), device=dev)
@@ -81,6 +87,17 @@ def main():
     assert torch.equal(o3, o3b)
     res["build known grid"] = timeit(lambda: pkg.grid.PointGrid(k, 0.0))
     res["build cloud grid"] = timeit(lambda: pkg.grid.PointGrid(t1, 0.1))
+    # the build launches alone, into fixed buffers (no allocation between the events)
+    gk = pkg.grid.PointGrid(k, 0.0)
+    gc = pkg.grid.PointGrid(t1, 0.1)
+    res["build known grid launch"] = timeit(lambda: L.pn2_grid_build(
+        k.data_ptr(), B, m, 0.0, gk.buf.data_ptr(), gk.nbytes, st))
+    res["build cloud grid launch"] = timeit(lambda: L.pn2_grid_build(
+        t1.data_ptr(), B, n, 0.1, gc.buf.data_ptr(), gc.nbytes, st))
+    x5 = torch.from_numpy(pkg.synth.batch(range(8), 16384, "scannet")[0]).to(dev)
+    g5 = pkg.grid.PointGrid(x5, 0.1)
+    res["build msg grid launch"] = timeit(lambda: L.pn2_grid_build(
+        x5.data_ptr(), 8, 16384, 0.1, g5.buf.data_ptr(), g5.nbytes, st))
     print(json.dumps({k_: round(v, 1) for k_, v in res.items()}))
 
 
