@@ -175,7 +175,7 @@ def cfg1_leg(dev, seconds=2.0):
 
 def copy_peak(dev, mib=1024, reps=5):
     """A measured HBM figure beside the 8 TB/s nominal (BASELINE.md:75): a float4 copy kernel
-    (pn2_copy_f4: four 16-byte loads in flight per thread, 8 workgroups per CU, the form
+    (pn2_copy_f4: four 16-byte loads in flight per thread, 16 workgroups per CU, the form
     MI355X_MICROARCH.md measures 6.29 TB/s with) of `mib` MiB, read + write bytes per second,
     best of `reps`; torch's copy_ (hipMemcpyAsync) beside it for reference."""
     import torch
@@ -210,7 +210,7 @@ def copy_peak(dev, mib=1024, reps=5):
     del a, b
     return {"GBps": 2 * n * 4 / (ms * 1e-3) / 1e9, "bytes": 2 * n * 4,
             "torch_copy_GBps": round(2 * n * 4 / (ms_torch * 1e-3) / 1e9, 1),
-            "method": f"float4 copy kernel (pn2_copy_f4, {cus} CUs x 8 workgroups) of {mib} "
+            "method": f"float4 copy kernel (pn2_copy_f4, {cus} CUs x 16 workgroups) of {mib} "
                       f"MiB, read + write bytes, best of {reps}"}
 
 

@@ -109,7 +109,7 @@ const char* pn2_version(void);
 const char* pn2_strerror(int status);
 
 /* Measurement utility (bench.py's copy peak; no operator uses it): copy `bytes` (a multiple
- * of 16, both pointers 16-byte aligned) with float4 loads and stores over 8 workgroups per
+ * of 16, both pointers 16-byte aligned) with float4 loads and stores over 16 workgroups per
  * CU of `cus` CUs. */
 int pn2_copy_f4(const void* src, void* dst, size_t bytes, int cus, pn2_stream_t stream);
 

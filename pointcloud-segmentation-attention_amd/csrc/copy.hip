@@ -1,7 +1,8 @@
 // The HBM copy peak that bench.py quotes the roofline fractions against beside the 8 TB/s
 // nominal (MI355X_MICROARCH.md: 6.29 TB/s for a float4 copy): every thread
 // moves four 16-byte elements per trip, all four loads issued before the first store, over a
-// grid of 8 workgroups per CU. A measurement utility only: no operator uses it.
+// grid of 16 workgroups per CU (tools/ubench/copy_peak.hip: 6.03 TB/s, the best of unroll
+// 1-8, plain or non-temporal, 4-16 workgroups per CU). A measurement utility only: no operator uses it.
 #include "common.h"
 
 namespace pn2 {
@@ -37,7 +38,7 @@ extern "C" int pn2_copy_f4(const void* src, void* dst, size_t bytes, int cus,
   const size_t n4 = bytes / 16;
   const size_t tiles = (n4 + pn2::kCopyBlock * pn2::kCopyUnroll - 1) /
                        (pn2::kCopyBlock * pn2::kCopyUnroll);
-  const unsigned grid = (unsigned)std::min<size_t>(tiles, (size_t)cus * 8);
+  const unsigned grid = (unsigned)std::min<size_t>(tiles, (size_t)cus * 16);
   hipLaunchKernelGGL(pn2::copy_f4_kernel, dim3(grid), dim3(pn2::kCopyBlock), 0,
                      (hipStream_t)stream, (const pn2::v4f*)src, (pn2::v4f*)dst, n4);
   PN2_RETURN_LAUNCH();
