@@ -47,9 +47,13 @@ MSG_GRID_EDGE = 0.2  # 105 us for the three radii vs 110 at 0.1, 122 at 0.4 (pro
 # "off" = each FP4 workgroup sorts them in LDS (pn2_fp_grid_fused). None = per config
 # (FP4_KNOWN_GRID_BY_CONFIG, else "off"): the 500-step A/B (profiles/r5/kgrid2) gave cfg3
 # 60.6-60.8k with "lane" against 57.6-57.7k "off" (58.8k "sampler"), cfg2 87.2-87.4k "lane",
-# 87.9-88.4k "sampler", 88.5k "off". bench.py --fp4-known-grid overrides it.
+# 87.9-88.4k "sampler", 88.5k "off". Round 6 (FP4 fused 42.4 us alone, 35.5 over a known grid;
+# profiles/r6/kg, kg20): cfg2 at 500 steps "sampler" 89.3 / 88.7k against "off" 87.5 / 87.2k,
+# the driver's 20-step window 77.5 / 72.0 / 82.4k against 74.4 / 72.7 / 71.1k; cfg3 "lane"
+# 58.4 / 57.9 / 58.5k, "sampler" 57.2 / 56.7 / 58.5k, "off" 56.3-56.5k. bench.py
+# --fp4-known-grid overrides it.
 FP4_KNOWN_GRID = None
-FP4_KNOWN_GRID_BY_CONFIG = {"cfg3": "lane"}
+FP4_KNOWN_GRID_BY_CONFIG = {"cfg2": "sampler", "cfg3": "lane"}
 
 NSIDE = 4  # side streams of the whole-model step (the geometric steps use 3)
 MAX_LANES = 8  # lanes of any step layout (0 = the sampler stream)
