@@ -79,6 +79,51 @@ PN2_DEV void best3_merge_xor(Best3& b, int mask) {
   best3_insert_lex(b, d3, i3);
 }
 
+// The (d, k)-lexicographic top 3 as three 64-bit keys (bits(d) << 32 | k): for d >= +0 (a
+// sum of squares; NaN keys sort above +inf, so a NaN distance never enters, as with the float
+// compares) the unsigned key order IS the lexicographic order, so an insert is three
+// v_cmp_lt_u64 and the selects, where the float form took three compares and two mask
+// operations per test (the grid walk's inner loop, round 6).
+struct Best3K {
+  uint64_t k1, k2, k3;
+};
+PN2_DEV uint64_t nn_key(float d, int k) {
+  return ((uint64_t)__float_as_uint(d) << 32) | (uint32_t)k;
+}
+PN2_DEV void best3k_init(Best3K& b) { b.k1 = b.k2 = b.k3 = nn_key(__builtin_inff(), 0); }
+PN2_DEV void best3k_insert(Best3K& b, uint64_t key) {
+  const bool c1 = key < b.k1, c2 = key < b.k2, c3 = key < b.k3;
+  b.k3 = c2 ? b.k2 : (c3 ? key : b.k3);
+  b.k2 = c1 ? b.k1 : (c2 ? key : b.k2);
+  b.k1 = c1 ? key : b.k1;
+}
+// the quad partner's key (lane ^ 1 or lane ^ 2): DPP quad permutes, no LDS crossbar trip (a
+// quad's lanes are active together, so the partner's registers are always there)
+template <int CTRL>
+PN2_DEV uint64_t quad_xor_u64(uint64_t v) {
+  const uint32_t lo = dpp_u32<CTRL>((uint32_t)v);
+  const uint32_t hi = dpp_u32<CTRL>((uint32_t)(v >> 32));
+  return ((uint64_t)hi << 32) | lo;
+}
+template <int CTRL>
+PN2_DEV void best3k_merge_quad(Best3K& b) {
+  const uint64_t o1 = quad_xor_u64<CTRL>(b.k1), o2 = quad_xor_u64<CTRL>(b.k2),
+                 o3 = quad_xor_u64<CTRL>(b.k3);
+  best3k_insert(b, o1);
+  best3k_insert(b, o2);
+  best3k_insert(b, o3);
+}
+PN2_DEV Best3 best3_of(const Best3K& b) {
+  Best3 r;
+  r.d1 = __uint_as_float((uint32_t)(b.k1 >> 32));
+  r.d2 = __uint_as_float((uint32_t)(b.k2 >> 32));
+  r.d3 = __uint_as_float((uint32_t)(b.k3 >> 32));
+  r.i1 = (int)(uint32_t)b.k1;
+  r.i2 = (int)(uint32_t)b.k2;
+  r.i3 = (int)(uint32_t)b.k3;
+  return r;
+}
+
 // Top-3 search of one unknown point (x1,y1,z1) by the 4 lanes of a quad over the m known
 // points of one cloud. Every thread of the block must call it (tiles are staged with
 // barriers). On return every lane of the quad holds the quad's result.
@@ -202,15 +247,15 @@ constexpr int kNNFirst = 1;  // the walk's first pass: the cube of shells 0..kNN
 template <int G, typename Off>
 PN2_DEV Best3 grid_nn3(const GridHdr& h, const float4* __restrict__ pts,
                        const Off* __restrict__ off, float px, float py, float pz, int q) {
-  Best3 best;
-  best3_init(best);
+  Best3K best;
+  best3k_init(best);
   auto merged = [&]() {  // the lanes' top 3 (every lane of the G gets the same)
-    Best3 mb = best;
+    Best3K mb = best;
     if constexpr (G == 4) {
-      best3_merge_xor(mb, 1);
-      best3_merge_xor(mb, 2);
+      best3k_merge_quad<kDppXor1>(mb);
+      best3k_merge_quad<kDppXor2>(mb);
     }
-    return mb;
+    return best3_of(mb);
   };
   const int cx = cell_coord(px, h.ox, h.inv, h.nx);
   const int cy = cell_coord(py, h.oy, h.inv, h.ny);
@@ -225,21 +270,17 @@ PN2_DEV Best3 grid_nn3(const GridHdr& h, const float4* __restrict__ pts,
     auto visit = [&](int lo, int hi) {  // sorted points [lo, hi), this lane's share
       for (int e = lo + q; e < hi; e += G) {
         const float4 p = pts[e];
-        best3_insert_lex(best, sqdist(p.x, p.y, p.z, px, py, pz), __float_as_int(p.w));
+        best3k_insert(best, nn_key(sqdist(p.x, p.y, p.z, px, py, pz), __float_as_int(p.w)));
       }
     };
     if (block) {
-      for (int z = max(zl, 0); z <= min(zh, h.nz - 1); ++z) {
+      // (Measured and not kept, profiles/r6/nn: every row's offsets read before any point and
+      // two points a lane per trip -- 21.4 -> 24.2 us for the search, 70 VGPRs.)
+      for (int z = max(zl, 0); z <= min(zh, h.nz - 1); ++z)
         for (int y = max(yl, 0); y <= min(yh, h.ny - 1); ++y) {
           const int row = (z * h.ny + y) * h.nx;
-          if (block || z == zl || z == zh || y == yl || y == yh) {
-            visit(off[row + x0], off[row + x1 + 1]);  // a face row: all of x0..x1
-          } else {
-            if (xl >= 0) visit(off[row + xl], off[row + xl + 1]);
-            if (xh < h.nx) visit(off[row + xh], off[row + xh + 1]);
-          }
+          visit(off[row + x0], off[row + x1 + 1]);  // a row of the block: all of x0..x1
         }
-      }
     } else {
       // shells past the first: only the cells that can still hold a point within the merged
       // third-best distance of the shells before (most of a shell is farther: skipped whole
