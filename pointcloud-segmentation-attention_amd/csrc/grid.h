@@ -73,12 +73,18 @@ PN2_DEV float wave_minmax_f(float v) {
 }
 PN2_DEV float wave_min_f(float v) { return wave_minmax_f<false>(v); }
 PN2_DEV float wave_max_f(float v) { return wave_minmax_f<true>(v); }
+// inclusive prefix sum over the wave: DPP row shifts (1, 2, 4, 8 within each 16-lane row; a
+// lane without a source adds 0), then row_bcast:15 / :31 carry each row's total into the rows
+// above -- six VALU steps, where the __shfl_up form was six dependent LDS-crossbar round trips
+// (every lane of the wave active; SA1's grid query 22.0 -> 21.0 us, tools/bench_side.py)
 PN2_DEV int wave_incl_scan(int v, int lane) {
-#pragma unroll
-  for (int o = 1; o < kWave; o <<= 1) {
-    const int u = __shfl_up(v, o, kWave);
-    if (lane >= o) v += u;
-  }
+  (void)lane;
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);  // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);  // row_shr:2
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, false);  // row_shr:4
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, false);  // row_shr:8
+  v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);  // row_bcast:15, rows 1, 3
+  v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);  // row_bcast:31, rows 2, 3
   return v;
 }
 

@@ -34,6 +34,7 @@ constexpr int kBuildBlock = 1024;
 // the flattened walk won on short rows, lost at r = 0.4 on r-sized cells)
 constexpr int kGqLongRows = 24;
 constexpr int kMaxBitWords = 4096;  // bitmask words per wave (N <= 131072)
+
 // The cloud's points are read ONCE into registers (PPT per thread, every load issued before
 // the first is used): the bounding box, the count and the scatter all work from them. The
 // first version looped over the cloud three times from memory with one dependent load trip per
@@ -435,6 +436,163 @@ __global__ __launch_bounds__(BLOCK) void ball_query_grid_kernel(
   }
 }
 
+
+// NR = 1 without features (cfg2's SA1: the query and its grouped xyz) with TWO queries per
+// wave at once. One query per wave left each wave a chain of dependent memory trips per query
+// (its centre, its rows' offsets, their points, the hits' coordinates), and with every wave of
+// the launch resident at once the launch time was two such chains. Here the two queries' rows
+// sit side by side in one 64-lane row list (query a's first), the walk takes the
+// concatenation of all their points 64 at a time, each lane testing its point against its
+// row's query into that query's bitmask, and the ranking runs lanes 0-31 over query a's
+// bitmask and 32-63 over b's: one chain per pair. Same tests, same bitmasks, same ranks and
+// rows as ball_query_grid_kernel. (cfg2's SA1: 21.0 -> 20.1 us standalone, tools/bench_side.py,
+// profiles/r6/side: the chains were a smaller part of the launch than their count suggests.)
+template <int BLOCK, bool GROUP>
+__global__ __launch_bounds__(BLOCK) void ball_query_grid_pair_kernel(
+    const char* __restrict__ grid, const float* __restrict__ xyz2, int N, int M, float radius,
+    int qpb, int words, int gx, int nblk, const BqRadii rd, const float* __restrict__ xyz1) {
+  constexpr int NW = BLOCK / kWave;
+  constexpr int HALF = kWave / 2;
+  extern __shared__ uint32_t bits[];  // NW x 2 x words: query a's bitmask, then b's
+  const int lb = xcd_block((int)blockIdx.x, nblk);
+  if (lb >= nblk) return;
+  const int b = lb / gx, bx = lb - b * gx;
+  const int t = threadIdx.x, lane = t & (kWave - 1), w = t / kWave;
+  const GridView g = grid_view(grid, b, N);
+  const GridHdr& h = g.h;
+  const int* __restrict__ off = g.off;
+  const float4* __restrict__ pts = g.pts;
+  uint32_t* const mine = bits + (size_t)w * 2 * words;
+  const int hb = lane >= HALF ? 1 : 0, hl = lane - hb * HALF;  // ranking: half and its lane
+  const int wph = (words + HALF - 1) / HALF;                    // bitmask words per lane of a half
+  const float thresh = rd.thresh[0];
+  const int ns = rd.ns[0];
+  const int q_end = min(M, (bx + 1) * qpb);
+  for (int qa = bx * qpb + 2 * w; qa < q_end; qa += 2 * NW) {
+    const bool two = qa + 1 < q_end;
+    for (int i = lane; i < 2 * words; i += kWave) mine[i] = 0u;
+    const float* Qa = xyz2 + ((size_t)b * M + qa) * 3;
+    const float* Qb = two ? Qa + 3 : Qa;
+    const float ax = Qa[0], ay = Qa[1], az = Qa[2], bxq = Qb[0], byq = Qb[1], bzq = Qb[2];
+    // each query's cell block (ball_query_grid_kernel's ranges)
+    int x0[2], x1[2], y0[2], z0[2], nyr[2], nrows[2];
+    {
+      const float qc[2][3] = {{ax, ay, az}, {bxq, byq, bzq}};
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const float qx = qc[s][0], qy = qc[s][1], qz = qc[s][2];
+        const float big = fmaxf(fmaxf(fmaxf(fabsf(qx), fabsf(qy)), fmaxf(fabsf(qz), radius)), 1.0f);
+        const float rr = radius + big * 1e-5f;
+        x0[s] = cell_coord(qx - rr, h.ox, h.inv, h.nx);
+        x1[s] = cell_coord(qx + rr, h.ox, h.inv, h.nx);
+        y0[s] = cell_coord(qy - rr, h.oy, h.inv, h.ny);
+        const int y1 = cell_coord(qy + rr, h.oy, h.inv, h.ny);
+        z0[s] = cell_coord(qz - rr, h.oz, h.inv, h.nz);
+        const int z1 = cell_coord(qz + rr, h.oz, h.inv, h.nz);
+        nyr[s] = y1 - y0[s] + 1;
+        nrows[s] = s == 1 && !two ? 0 : (z1 - z0[s] + 1) * nyr[s];
+      }
+    }
+    const int R = nrows[0] + nrows[1];
+    for (int r0 = 0; r0 < R; r0 += kWave) {
+      // lane j: row r0 + j of the pair's list (query a's rows, then b's)
+      int beg = 0, len = 0;
+      const int r = r0 + lane;
+      const bool rb = r >= nrows[0];
+      if (r < R) {
+        const int s = rb ? 1 : 0, rq = rb ? r - nrows[0] : r;
+        const int zr = rq / nyr[s];
+        const int row = ((z0[s] + zr) * h.ny + y0[s] + (rq - zr * nyr[s])) * h.nx;
+        beg = off[row + x0[s]];
+        len = off[row + x1[s] + 1] - beg;
+      }
+      const uint64_t rowb = __ballot(rb);  // rows of query b (by lane)
+      const int incl = wave_incl_scan(len, lane);
+      const int total = __builtin_amdgcn_readlane(incl, kWave - 1);
+      const int excl = incl - len;
+      for (int i0 = 0; i0 < total; i0 += kWave) {
+        // the rows overlapping [i0, i0 + 64): each lane takes the last one starting at or
+        // before its position, and that row's query
+        const int i = i0 + lane;
+        uint64_t span = __ballot(len > 0 && incl > i0 && excl < i0 + kWave);
+        int base = 0;
+        bool qb = false;
+        while (span) {
+          const int j = (int)__builtin_ctzll(span);
+          span &= span - 1;
+          const int ej = __builtin_amdgcn_readlane(excl, j);
+          const int bj = __builtin_amdgcn_readlane(beg, j);
+          const bool sel = ej <= i;
+          base = sel ? bj - ej : base;
+          qb = sel ? ((rowb >> j) & 1ull) != 0 : qb;
+        }
+        if (i < total) {  // tf_grouping_g.cu:24-25
+          const float4 p = pts[base + i];
+          const float d = qb ? sqdist(bxq, byq, bzq, p.x, p.y, p.z) : sqdist(ax, ay, az, p.x, p.y, p.z);
+          const int k = __float_as_int(p.w);
+          if (d < thresh) atomicOr(&mine[(qb ? words : 0) + (k >> 5)], 1u << (k & 31));
+        }
+      }
+    }
+    // ranking: lanes 0-31 own query a's bitmask words [hl*wph, (hl+1)*wph), lanes 32-63 b's
+    const uint32_t* mr = mine + hb * words;
+    int pop = 0, myfirst = -1;
+    for (int j = 0; j < wph; ++j) {
+      const int wi = hl * wph + j;
+      if (wi < words) {
+        const uint32_t v = mr[wi];
+        if (myfirst < 0 && v) myfirst = 32 * wi + __builtin_ctz(v);
+        pop += __popc(v);
+      }
+    }
+    const int incl = wave_incl_scan(pop, lane);
+    const int tot_a = __builtin_amdgcn_readlane(incl, HALF - 1);
+    const int tot_b = __builtin_amdgcn_readlane(incl, kWave - 1) - tot_a;
+    const int total = hb ? tot_b : tot_a;
+    const int cnt = min(total, ns);
+    const int q = qa + hb;
+    const bool mineq = hb == 0 || two;
+    const float qx = hb ? bxq : ax, qy = hb ? byq : ay, qz = hb ? bzq : az;
+    int32_t* __restrict__ row = rd.idx[0] + ((size_t)b * M + q) * ns;
+    float* __restrict__ grow = GROUP ? rd.gout[0] + ((size_t)b * M + q) * ns * 3 : nullptr;
+    const float* __restrict__ X1 = GROUP ? xyz1 + (size_t)b * N * 3 : nullptr;
+    int rank = incl - pop - (hb ? tot_a : 0);
+    if (mineq) {
+      for (int j = 0; j < wph && rank < ns; ++j) {
+        const int wi = hl * wph + j;
+        uint32_t v = wi < words ? mr[wi] : 0u;
+        while (v && rank < ns) {
+          const int k = 32 * wi + __builtin_ctz(v);
+          if constexpr (GROUP) {
+            grow[3 * rank + 0] = X1[3 * k + 0] - qx;  // pointnet_util.py:40
+            grow[3 * rank + 1] = X1[3 * k + 1] - qy;
+            grow[3 * rank + 2] = X1[3 * k + 2] - qz;
+          }
+          row[rank++] = k;
+          v &= v - 1u;
+        }
+      }
+    }
+    const uint64_t has = __ballot(pop > 0);
+    const uint64_t hma = has & 0xFFFFFFFFull, hmb = has >> HALF;
+    const int fa = hma ? __builtin_amdgcn_readlane(myfirst, (int)__builtin_ctzll(hma)) : 0;
+    const int fbl = hmb ? (int)__builtin_ctzll(hmb) + HALF : 0;
+    const int fb = hmb ? __builtin_amdgcn_readlane(myfirst, fbl) : 0;
+    const int first = hb ? fb : fa;
+    if (mineq) {
+      for (int p = cnt + hl; p < ns; p += HALF) {
+        row[p] = first;  // :26-29 (0 when no hit)
+        if constexpr (GROUP) {
+          grow[3 * p + 0] = X1[3 * first + 0] - qx;
+          grow[3 * p + 1] = X1[3 * first + 1] - qy;
+          grow[3 * p + 2] = X1[3 * first + 2] - qz;
+        }
+      }
+      if (hl == 0) rd.cnt[0][(size_t)b * M + q] = cnt;
+    }
+  }
+}
+
 }  // namespace
 }  // namespace pn2
 
@@ -561,6 +719,21 @@ int ball_query_grid(const void* grid, const float* xyz2, int B, int N, int M, in
     if (nr != 1) return PN2_EINVAL;
     hipLaunchKernelGGL((pn2::ball_query_grid_kernel<BLOCK, true, 1, true>), grd, blk, lds, stream,
                        g, xyz2, N, M, rmax, (int)qpb, words, (int)gx, (int)nblk, rd, xyz1);
+  } else if (nr == 1 && 2 * lds <= 64 * 1024) {
+    // two queries per wave (ball_query_grid_pair_kernel): a workgroup's queries a whole number
+    // of pairs per wave
+    const long long qpb2 = ((qpb + 2 * NW - 1) / (2 * NW)) * (2 * NW);
+    const unsigned gx2 = (unsigned)((M + qpb2 - 1) / qpb2);
+    const long long nblk2 = (long long)gx2 * B;
+    const dim3 grd2(pn2::xcd_grid(nblk2));
+    if (group)
+      hipLaunchKernelGGL((pn2::ball_query_grid_pair_kernel<BLOCK, true>), grd2, blk, 2 * lds,
+                         stream, g, xyz2, N, M, rmax, (int)qpb2, words, (int)gx2, (int)nblk2, rd,
+                         xyz1);
+    else
+      hipLaunchKernelGGL((pn2::ball_query_grid_pair_kernel<BLOCK, false>), grd2, blk, 2 * lds,
+                         stream, g, xyz2, N, M, rmax, (int)qpb2, words, (int)gx2, (int)nblk2, rd,
+                         nullptr);
   } else if (group) {
     if (nr == 1) PN2_BQG(true, 1);
     else if (nr == 2) PN2_BQG(true, 2);

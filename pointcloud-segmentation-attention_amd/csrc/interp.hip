@@ -952,7 +952,7 @@ int batch_chunk(int B, int n, int C, int rows) {
 // Channel split of an FP layer over grid.z (tools/bench_layers.py): split until kFpMinBlocks
 // workgroups, keeping >= kFpMinCols vector columns per workgroup and (search variant, which
 // scans the m known points again per slice) m * slices <= the budget
-constexpr int kFpMinBlocks = 512;
+constexpr int kFpMinBlocks = 512;  // (round 6, tools/bench_side.py: 128 / 256 / 1024 / 2048 slower)
 constexpr int kFpMinCols = 16;
 constexpr int kFpScanBudget = 4096;
 
