@@ -111,6 +111,7 @@ __global__ void gather_point_grad_kernel(const float* __restrict__ out_g,
 }
 
 constexpr int kMaxRegPoints = 1024 * 16;
+
 constexpr int kCullGridMax = 4096;  // picks whose grid the culled sampler builds itself
 
 // ---- device fault word ------------------------------------------------------------------
@@ -676,6 +677,8 @@ int fps_impl(const float* xyz, int B, int N, int M, int32_t* idx, float* nx, voi
         launch_hotcull_grid<16, 9, 3, 4>(xyz, B, N, M, idx, nx, fault_word_dev(), s, kgrid);
         kgrid = nullptr;  // (built)
       } else {
+        // (the LEAN form -- 53 KB of LDS, so a CU holding a sampler can take side workgroups
+        // too -- measured again in round 6: the same rate, profiles/r6/lanes20, lanes500)
         launch_hotcull<16, 9, 3, 4>(xyz, B, N, M, idx, nx, fault_word_dev(), s);
       }
     }

@@ -1035,10 +1035,11 @@ __global__ __launch_bounds__(64 * NW) void fps_hotcull_grid_kernel(const float* 
                                                                kgrid);
 }
 
-template <int NW, int PPT, int PRIO = 0, int HQ = 2, int NPTS = 8192, int PPC = 1>
+template <int NW, int PPT, int PRIO = 0, int HQ = 2, int NPTS = 8192, int PPC = 1,
+          bool LEAN = false>
 void launch_hotcull(const float* xyz, int B, int N, int M, int32_t* idx, float* nx, int* fault,
                     hipStream_t s) {
-  hipLaunchKernelGGL((fps_hotcull_kernel<NW, PPT, NPTS, false, PRIO, HQ, PPC>), dim3(B),
+  hipLaunchKernelGGL((fps_hotcull_kernel<NW, PPT, NPTS, false, PRIO, HQ, PPC, LEAN>), dim3(B),
                      dim3(64 * NW), 0, s, xyz, N, M, idx, nx, fault);
 }
 
