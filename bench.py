@@ -31,8 +31,11 @@ DEFAULT_HW_QUEUES = 4
 # stream: samplers + side lanes) and buffer sets (how far the host may run ahead).
 # chain: the later samplers (SA2.. chain) behind SA1 on its sampler stream, or on a stream of
 # their own (profiles/r3/chainown: cfg2 65.6k -> 69.8k, cfg3 50.7k -> 54.3k clouds/s; cfg5 no
-# gain).
-LAYOUTS = {"cfg2": {"lanes": 3, "side": "b", "queues": 7, "sets": 9, "chain": "own"},
+# gain). cfg2's sets: 5 (round 6, the driver's command, ten interleaved runs each, profiles/r6/
+# sets20, sets20b: median 78.4k, min 76.8k against 75.0k / 70.1k with 9; 4 / 6 / 7 sets 75.6 /
+# 75.3 / 76.5k; 500 steps 92.1 / 90.9k against 90.5 / 90.4k): the side lanes bound the step, and
+# fewer sets hold the samplers' run-ahead -- and the CUs it takes from the side work -- shorter.
+LAYOUTS = {"cfg2": {"lanes": 3, "side": "b", "queues": 7, "sets": 5, "chain": "own"},
            "cfg3": {"lanes": 2, "side": "a", "queues": 6, "sets": 6, "chain": "own"},
            "cfg5": {"lanes": 5, "side": "a", "queues": 8, "sets": 10, "chain": "behind"}}
 
@@ -233,6 +236,15 @@ def pmc_traffic(config, B):
     # kernel it lands within 6 % of the algorithmic read bytes, and WRITE_SIZE equals the
     # idx + new_xyz bytes exactly.
     return e["fetch_bytes_x2"] + e["write_bytes"], os.path.relpath(files[-1], ROOT) + f" [{k}]"
+
+
+def sa1_algorithmic_bytes(B, N, M1, known_grid):
+    """Algorithmic bytes of one SA1 sampler launch: the cloud read once (N x 12), idx + new_xyz
+    written (M1 x 16), per cloud; with known_grid (the sampler's workgroups grid their picks for
+    FP4, pn2_fps_chain_grid) also that grid: header, max(M1, 64) + 1 offsets, M1 sorted points
+    (csrc/grid.h)."""
+    grid = 32 + (max(M1, 64) + 1) * 4 + M1 * 16 if known_grid else 0
+    return B * (N * 12 + M1 * 16 + grid)
 
 
 MAX_CLOCK_GHZ = 2.4  # MI355X_MICROARCH.md, chip-level parameters
@@ -710,8 +722,11 @@ def main():
         N, _, _, _ = pkg.stack.CONFIGS[args.config]
         M1 = (pkg.stack.MSG_SA if args.config == "cfg5" else pkg.stack.SSG_SA)[0][0]
         # algorithmic bytes of the timed SA1 sampler launch (FPS + fused gather): read the
-        # cloud once (N x 12), write idx + new_xyz (M1 x (4 + 12)), per cloud
-        fps_bytes = B * (N * 12 + M1 * 16)
+        # cloud once (N x 12), write idx + new_xyz (M1 x (4 + 12)), per cloud; plus FP4's known
+        # grid when the sampler's workgroups build it (cfg2)
+        kg_mode = (None if args.model or args.config == "cfg5" else
+                   pkg.stack.FP4_KNOWN_GRID or pkg.stack.FP4_KNOWN_GRID_BY_CONFIG.get(args.config))
+        fps_bytes = sa1_algorithmic_bytes(B, N, M1, kg_mode == "sampler")
         achieved = fps_bytes / (fps_ms * 1e-3) / 1e9
         traffic, traffic_src = pmc_traffic(args.config, B)
         lat = sa1_latency(args.config, fps_ms, M1, N)
