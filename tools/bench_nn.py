@@ -61,6 +61,14 @@ def main():
     res["fp4 apply only"] = timeit(lambda: L.pn2_fp_apply(
         dist.data_ptr(), idx.data_ptr(), ug.buf.data_ptr(), None, 0, p2.data_ptr(), 128, B, n, m,
         out.data_ptr(), st))
+    # the same rows in index order (sequential writes, scattered neighbour gathers)
+    res["fp4 apply only (index order)"] = timeit(lambda: L.pn2_fp_apply(
+        dist.data_ptr(), idx.data_ptr(), None, None, 0, p2.data_ptr(), 128, B, n, m,
+        out.data_ptr(), st))
+    # a copy of the FP4 output size (67 MB read + 67 MB written): the write-rate reference
+    big = torch.empty((B, n, 128), device=dev)
+    res["fp4-size copy (read+write 67 MB each)"] = timeit(lambda: L.pn2_copy_f4(
+        out.data_ptr(), big.data_ptr(), B * n * 128 * 4, 256, st))
     res["fp4 grid fused"] = timeit(lambda: L.pn2_fp_grid_fused(
         None, k.data_ptr(), ug.buf.data_ptr(), None, 0, p2.data_ptr(), 128, B, n, m,
         out2.data_ptr(), None, None, st))
