@@ -242,34 +242,33 @@ using hf4 = float __attribute__((ext_vector_type(4)));
 
 // wave 0's picks from its hot entries (e = x, y, z, bits(point index), value hv; empty lanes
 // hold INT_MIN) while the best is > tau and j < M; each pick is published as it is made (its
-// slot with tag pick_tag(tag0 + pick), then -- released -- the count of the picks before it;
+// slot with the batch's tag pick_tag(tag0 + j), then -- released -- the count of the picks before it;
 // fps_cull.h hot_publish; a cold wave acquires the count, then reads the slots). At most lim
 // picks (a picked entry drops to 0 <= tau, so a round cannot outrun its hot set -- except
 // through NaN distances, which the bound covers; the all-hot path, tau = -1, needs it to stop
 // at M). Returns the picks made so far.
 PN2_DEV int hot_picks(hf4 e, int hv, int tau, int j, int lim, int* pub, HotLds& S, int tag0) {
   j = __builtin_amdgcn_readfirstlane(j);  // (a scalar loop count: no exec-mask bookkeeping)
-  // publishing addresses, the count and the tag in VGPRs, advanced by one VALU add per pick
-  int va_c, va_n, vcnt, vtag;
+  // publishing addresses and the count in VGPRs, advanced by one VALU add per pick
+  int va_c, va_n, vcnt;
   asm volatile("v_mov_b32 %0, %1" : "=v"(va_c)
                : "s"((uint32_t)(uintptr_t)(__attribute__((address_space(3))) float4*)&S.pc[j]));
   asm volatile("v_mov_b32 %0, %1" : "=v"(va_n)
                : "s"((uint32_t)(uintptr_t)(__attribute__((address_space(3))) int*)pub));
   asm volatile("v_mov_b32 %0, %1" : "=v"(vcnt) : "s"(j));
-  asm volatile("v_mov_b32 %0, %1" : "=v"(vtag) : "s"(pick_tag(tag0 + j)));
+  const int lw = __float_as_int(e.w) | (int)pick_tag(tag0 + j);  // the slots' w
   int n = 0;
   // (one exit, at the bottom: the loop carries no break flags)
   int km = __builtin_amdgcn_readlane(wave_max_i32_l63(hv), kWave - 1);
   while (km > tau) {  // else the certificate fails: the round ends
     const int L = (int)__builtin_ctzll(__builtin_amdgcn_ballot_w64(hv == km));
     float cx, cy, cz;
-    hot_publish(L, va_c, va_n, vcnt, vtag, e.x, e.y, e.z, __float_as_int(e.w), cx, cy, cz);
+    hot_publish(L, va_c, va_n, vcnt, e.x, e.y, e.z, lw, cx, cy, cz);
     __builtin_amdgcn_sched_barrier(0);
     ++n;
     hv = min(hv, __float_as_int(sqdist(e.x, e.y, e.z, cx, cy, cz)));
     va_c += 16;
     vcnt += 1;
-    vtag += 1 << 16;
     km = __builtin_amdgcn_readlane(wave_max_i32_l63(hv), kWave - 1);
     km = n >= lim ? tau : km;
   }
@@ -534,9 +533,10 @@ PN2_DEV void fps_hot_body(const float* CXYZ, int N, int M, int32_t* I, float* NX
             const int n = min(av - r, kWave);
             const int p = r + min(lane, n - 1);
             const float4 cv = S.pc[p];
-            // every slot below the acquired count carries its pick's tag (fps_cull.h hot_publish)
+            // every slot below the acquired count carries the batch's tag (fps_cull.h
+            // hot_publish; j: this round's first pick)
             if (__builtin_amdgcn_ballot_w64((__float_as_uint(cv.w) & ~kPickIdxMask) !=
-                                            pick_tag(tag0 + p))) {
+                                            pick_tag(tag0 + j))) {
               PN2_TORN_SEEN();
               continue;
             }

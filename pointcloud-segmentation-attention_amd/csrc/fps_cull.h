@@ -192,11 +192,12 @@ PN2_DEV void hot_best4(const int (&hv)[4], const hf2 (&hx)[2], const hf2 (&hy)[2
 }
 
 // ---- publishing picks to the cold waves (the SA1 sampler here, the chain in fps.hip) -------
-// A pick's slot is (x, y, z, w) with w = point index | pick_tag(p), p the pick's number in the
-// launch (the chain adds the earlier stages' picks). The protocol is the LLVM AMDGPU memory
-// model's own mapping of a workgroup-scope release / acquire on LDS, not the in-order execution
-// of a wave's DS operations (which no document promises across waves, and which a 16-byte centre
-// write followed by the count did break: profiles/r5/chain_hot/pipe_stress_b128_publish.json):
+// A pick's slot is (x, y, z, w) with w = point index | pick_tag(j), j the number of the first
+// pick of the slot's batch in the launch (the chain adds the earlier stages' picks). The protocol
+// is the LLVM AMDGPU memory model's own mapping of a workgroup-scope release / acquire on LDS,
+// not the in-order execution of a wave's DS operations (which no document promises across waves,
+// and which a 16-byte centre write followed by the count did break:
+// profiles/r5/chain_hot/pipe_stress_b128_publish.json):
 //  * release: the count store that makes slot p visible is issued only after an
 //    s_waitcnt lgkmcnt has seen slot p's writes complete (hipcc emits exactly that wait before a
 //    __ATOMIC_RELEASE workgroup store to LDS). So the wait never stalls the hot wave, each pick
@@ -205,11 +206,14 @@ PN2_DEV void hot_best4(const int (&hv)[4], const hf2 (&hx)[2], const hf2 (&hy)[2
 //    The batch's last pick goes out with the end flag, after lgkmcnt(0);
 //  * acquire: a cold wave reads the count with __ATOMIC_ACQUIRE (ds_read, s_waitcnt lgkmcnt(0)
 //    before any later LDS read), then the slots below it.
-// On top, the consumer checks every slot's tag and re-polls on a mismatch (a stale slot from an
-// earlier batch or launch cannot carry p's tag: tags grow within a launch and the slots are
-// cleared at its start). The check is what a build that publishes the count BEFORE the centre
-// (-DPN2_PUBLISH_BROKEN=1, csrc/Makefile target torntest) leans on: it stays index-exact and
-// counts the torn reads it caught (pn2_torn_reads, tests/test_gpu_a_fullsize.py).
+// On top, the consumer checks every slot's tag and re-polls on a mismatch. A stale slot cannot
+// carry the batch's tag: a slot is written once per batch, batches start at increasing pick
+// numbers (a batch that wrote a slot made a pick), and the slots are cleared (tag 0) at the
+// launch's start. The tag is per batch, not per pick, so the hot entries carry it from before
+// the pick loop and a pick costs no tag arithmetic (a per-pick tag OR cost the SA1 sampler ~30
+// cycles a pick, 6 %: profiles/r6/pubab). The check is what a build that publishes the count
+// BEFORE the centre (-DPN2_PUBLISH_BROKEN=1, csrc/Makefile target torntest) leans on: it stays
+// index-exact and counts the torn reads it caught (pn2_torn_reads, tests/test_gpu_a_fullsize.py).
 #ifndef PN2_PUBLISH_BROKEN
 #define PN2_PUBLISH_BROKEN 0
 #endif
@@ -223,30 +227,28 @@ __device__ unsigned int g_torn_reads;
 #define PN2_TORN_SEEN()
 #endif
 
-// publish pick L from the winning lane itself (exec = lane L only): its lx, ly, lz and
-// lk | vtag are the slot at LDS address va_c; then, once the writes before them are complete,
-// the count vcnt (the picks of this batch before this one) to va_n. The centre's coordinates
-// come back to SGPRs inside the same block (v_readlane ignores exec), so no wait states follow
-// the exec restore; L comes from SALU (no lane-select wait).
-PN2_DEV void hot_publish(int L, int va_c, int va_n, int vcnt, int vtag, float lx, float ly,
-                         float lz, int lk, float& cx, float& cy, float& cz) {
-  uint64_t sv;
+// publish pick L from the winning lane itself (exec = lane L only): its lx, ly, lz and lw (the
+// point index with the batch's tag) are the slot at LDS address va_c; then, once the writes
+// before them are complete, the count vcnt (the picks of this batch before this one) to va_n.
+// The centre's coordinates come back to SGPRs inside the same block (v_readlane ignores exec),
+// so no wait states follow the exec restore; L comes from SALU (no lane-select wait).
+PN2_DEV void hot_publish(int L, int va_c, int va_n, int vcnt, float lx, float ly, float lz,
+                         int lw, float& cx, float& cy, float& cz) {
+#if PN2_PUBLISH_BROKEN
+  // DIAGNOSTIC: the count (including this pick) first, the slot ~800 cycles later (longer than
+  // a cold wave takes from reading the count to reading the slots)
   int kt;
+  asm volatile("v_add_u32 %0, 1, %1\n\tds_write_b32 %2, %0\n\ts_sleep 12"
+               : "=&v"(kt) : "v"(vcnt), "v"(va_n) : "memory");
+#endif
+  uint64_t sv;
   asm volatile(
       "s_mov_b64 %[sv], exec\n\t"
       "s_lshl_b64 exec, 1, %[L]\n\t"
-#if PN2_PUBLISH_BROKEN
-      // DIAGNOSTIC: the count (including this pick) first, the slot ~800 cycles later (longer
-      // than a cold wave takes from reading the count to reading the slots)
-      "v_add_u32 %[kt], 1, %[n]\n\t"
-      "ds_write_b32 %[c], %[kt]\n\t"
-      "s_sleep 12\n\t"
-#endif
       "ds_write_b32 %[a], %[x]\n\t"
-      "v_or_b32 %[kt], %[k], %[tg]\n\t"
       "ds_write_b32 %[a], %[y] offset:4\n\t"
       "ds_write_b32 %[a], %[z] offset:8\n\t"
-      "ds_write_b32 %[a], %[kt] offset:12\n\t"
+      "ds_write_b32 %[a], %[k] offset:12\n\t"
 #if !PN2_PUBLISH_BROKEN
       "s_waitcnt lgkmcnt(4)\n\t"
       "ds_write_b32 %[c], %[n]\n\t"
@@ -255,9 +257,9 @@ PN2_DEV void hot_publish(int L, int va_c, int va_n, int vcnt, int vtag, float lx
       "v_readlane_b32 %[cy], %[y], %[L]\n\t"
       "v_readlane_b32 %[cz], %[z], %[L]\n\t"
       "s_mov_b64 exec, %[sv]"
-      : [sv] "=&s"(sv), [cx] "=&s"(cx), [cy] "=&s"(cy), [cz] "=&s"(cz), [kt] "=&v"(kt)
+      : [sv] "=&s"(sv), [cx] "=&s"(cx), [cy] "=&s"(cy), [cz] "=&s"(cz)
       : [L] "s"(L), [a] "v"(va_c), [c] "v"(va_n), [x] "v"(lx), [y] "v"(ly), [z] "v"(lz),
-        [k] "v"(lk), [tg] "v"(vtag), [n] "v"(vcnt)
+        [k] "v"(lw), [n] "v"(vcnt)
       : "memory", "scc");
 }
 
@@ -779,6 +781,7 @@ __device__ __attribute__((always_inline)) inline void hotcull_body(
           hx[q / 2][q % 2] = LEAN ? qx[q] : X[3 * hk[q]];
           hy[q / 2][q % 2] = LEAN ? qy[q] : X[3 * hk[q] + 1];
           hz[q / 2][q % 2] = LEAN ? qz[q] : X[3 * hk[q] + 2];
+          hk[q] |= (int)pick_tag(j);  // the slots' w: the point index with the batch's tag
         }
         const int lim = min(K, M - j);
         int jj = 0;
@@ -789,15 +792,13 @@ __device__ __attribute__((always_inline)) inline void hotcull_body(
         __builtin_amdgcn_s_waitcnt(0xC07F);
         // publishing addresses and the published count in VGPRs, advanced by one VALU add per
         // pick (as SGPRs they cost an SALU add and a v_mov each for the DS stores)
-        // (vcnt: the picks of this batch so far, published after each pick's slot; vtag: the
-        // next pick's tag, pick_tag(j + vcnt))
-        int va_c, va_n, vcnt, vtag;
+        // (vcnt: the picks of this batch so far, published after each pick's slot)
+        int va_c, va_n, vcnt;
         asm volatile("v_mov_b32 %0, %1" : "=v"(va_c)
                      : "s"((uint32_t)(uintptr_t)(__attribute__((address_space(3))) float4*)&scl[0]));
         asm volatile("v_mov_b32 %0, %1" : "=v"(va_n)
                      : "s"((uint32_t)(uintptr_t)(__attribute__((address_space(3))) int*)&sj[rp]));
         asm volatile("v_mov_b32 %0, 0" : "=v"(vcnt));
-        asm volatile("v_mov_b32 %0, %1" : "=v"(vtag) : "s"(pick_tag(j)));
         // the pick loop ends when the best hot value is no longer above T; it cannot run past
         // the nh <= K hot entries (a picked entry drops to 0 <= T), so only the last batch of
         // the cloud (fewer than K picks left) needs a count test per pick
@@ -841,12 +842,11 @@ __device__ __attribute__((always_inline)) inline void hotcull_body(
               L = (int)__builtin_ctzll(__builtin_amdgcn_ballot_w64(cv == wm && ck == km));
             }
             float cx, cy, cz;
-            hot_publish(L, va_c, va_n, vcnt, vtag, lx, ly, lz, lk, cx, cy, cz);
+            hot_publish(L, va_c, va_n, vcnt, lx, ly, lz, lk, cx, cy, cz);
             __builtin_amdgcn_sched_barrier(0);
             hot_update<HP>(hv, hx, hy, hz, cx, cy, cz);  // the next pick depends on it
             va_c += 16;
             vcnt += 1;
-            vtag += 1 << 16;
             if constexpr (CHECKED)
               if (__builtin_amdgcn_readfirstlane(vcnt) >= lim) break;
           }
@@ -885,9 +885,9 @@ __device__ __attribute__((always_inline)) inline void hotcull_body(
           const int ci = applied + lane / PPT;
           const bool valid = lane < GRP * PPT && ci < a1;
           const float4 cv = scl[valid ? ci : 0];
-          // every slot below the acquired count carries its pick's tag (see hot_publish)
+          // every slot below the acquired count carries the batch's tag (see hot_publish)
           if (__builtin_amdgcn_ballot_w64(
-                  valid && (__float_as_uint(cv.w) & ~kPickIdxMask) != pick_tag(j + ci))) {
+                  valid && (__float_as_uint(cv.w) & ~kPickIdxMask) != pick_tag(j))) {
             PN2_TORN_SEEN();
             continue;
           }
