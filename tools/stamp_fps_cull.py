@@ -83,6 +83,15 @@ for kind in ("scannet", "uniform"):
                      "B2_to_B3": int(E[r_, 0, 6] - E[r_, 0, 4]),
                      "append_max": int((E[r_, 1:, 5] - E[r_, 1:, 4]).max()),
                      "B3_to_next_hot_end": int(E[r_ + 1, 0, 0] - E[r_, 0, 6]) if E[r_ + 1, 0, 0] else None})
+    # per cold wave: median cycles from the hot phase's end to its loop end / tail end, and how
+    # often it is the last to finish (which waves the round's end waits for)
+    rr = [r_ for r_ in range(2, 40) if E[r_, 0, 0] and E[r_, 0, 2]]
+    print(json.dumps({"kind": kind, "per_wave_loop_end_after_hot": [
+        int(np.median([E[r_, w_, 0] - E[r_, 0, 0] for r_ in rr])) for w_ in range(1, 16)],
+        "per_wave_tail_end_after_hot": [
+        int(np.median([E[r_, w_, 1] - E[r_, 0, 0] for r_ in rr])) for w_ in range(1, 16)],
+        "last_wave_counts": np.bincount([int(np.argmax(E[r_, 1:, 1])) + 1 for r_ in rr],
+                                        minlength=16).tolist()}), flush=True)
     keys = rows[0].keys()
     med = {k: float(np.median([r[k] for r in rows if r[k] is not None])) for k in keys}
     print(json.dumps({"kind": kind, "median_per_round": med, "rounds": len(rows)}), flush=True)
