@@ -599,6 +599,80 @@ PN2_DEV void chain_stage(const float* P, int N, int M, const float* CXYZ, int32_
   else fps_v9_body<256, 4, 2, false, true>(P, N, M, CXYZ, I, NX, SNEXT, red);
 }
 
+// ---- a chain over an earlier sampler's output: its stages are prefixes ---------------------
+// If P[0..n) is itself a farthest-point sampling in pick order (the fused tail's input is the
+// SA1 sampler's new_xyz), FPS(P, m) picks 0, 1, ..., m - 1: pick j of P's own sampling was the
+// farthest point of a superset of P from picks 0 .. j - 1, and it lies in P, so it is also the
+// farthest point of P -- unless another point ties with it, where the sampler's tie order
+// (tf_sampling_g.cu:131-165: strided scan, left-biased tree) decides. So the check demands a
+// unique maximum at every step: with the running mins of the reference's sampler,
+// temp_j(s) = min(1e38, min_{i<j} d(P_s, P_i)) (sqdist: the samplers' uncontracted fp32
+// distance) and M_j = temp_j(j), the value pick j is chosen with, every s != j has
+// temp_j(s) < M_j, for j = 1 .. m - 1. Then FPS(P, m) = [0, m), and every later stage of the
+// chain (m' <= m picks of that prefix) is a prefix as well, by the same argument on the subset.
+// Non-finite coordinates, M_j <= 0 (duplicates) and every tie fail the check; the stages then
+// run as samplers. A quick test of pick 1 first (the unique farthest point from pick 0), so an
+// arbitrary input (a chain whose first stage samples a raw cloud) is rejected in one pass.
+// The whole workgroup calls it; sm: >= m floats of LDS.
+PN2_DEV bool fps_prefix_holds(const float* __restrict__ P, int n, int m, float* sm, int* sbad) {
+  const int t = threadIdx.x;
+  if (m > n) return false;
+  if (m <= 1) return true;  // FPS(P, 1) = [0]
+  if (t == 0) *sbad = 0;
+  __syncthreads();
+  bool bad = false;
+  {
+    const float m1 = fminf(1e38f, sqdist(P[3], P[4], P[5], P[0], P[1], P[2]));
+    bad = !(m1 > 0.0f);
+    for (int s = t; s < n; s += kChainBlock) {
+      const float x = P[3 * s], y = P[3 * s + 1], z = P[3 * s + 2];
+      bad = bad || !(__builtin_isfinite(x) && __builtin_isfinite(y) && __builtin_isfinite(z));
+      bad = bad || (s != 1 && !(fminf(1e38f, sqdist(x, y, z, P[0], P[1], P[2])) < m1));
+    }
+  }
+  if (bad) *sbad = 1;
+  __syncthreads();
+  if (*sbad) return false;
+  for (int j = t; j < m; j += kChainBlock) {  // M_j
+    const float x = P[3 * j], y = P[3 * j + 1], z = P[3 * j + 2];
+    float v = 1e38f;
+    for (int i = 0; i < j; ++i) v = fminf(v, sqdist(x, y, z, P[3 * i], P[3 * i + 1], P[3 * i + 2]));
+    sm[j] = v;
+    if (j > 0 && !(v > 0.0f)) *sbad = 1;
+  }
+  __syncthreads();
+  if (*sbad) return false;
+  // every point's running min against each M_j: the one hit allowed is s's own step (j = s,
+  // where temp_s(s) is M_s bit for bit: the same distances, and min is exact)
+  constexpr int PT = kChainNext / kChainBlock;
+  float qx[PT], qy[PT], qz[PT], v[PT];
+  int hits[PT];
+#pragma unroll
+  for (int k = 0; k < PT; ++k) {
+    const int s = t + k * kChainBlock;
+    const bool in = s < n;
+    qx[k] = in ? P[3 * s] : 0.0f;
+    qy[k] = in ? P[3 * s + 1] : 0.0f;
+    qz[k] = in ? P[3 * s + 2] : 0.0f;
+    v[k] = 1e38f;
+    hits[k] = in ? (s >= 1 && s < m ? -1 : 0) : 0;
+  }
+  for (int j = 1; j < m; ++j) {
+    const float cx = P[3 * (j - 1)], cy = P[3 * (j - 1) + 1], cz = P[3 * (j - 1) + 2];
+    const float mj = sm[j];
+#pragma unroll
+    for (int k = 0; k < PT; ++k) {
+      v[k] = fminf(v[k], sqdist(qx[k], qy[k], qz[k], cx, cy, cz));
+      hits[k] += (t + k * kChainBlock < n && v[k] >= mj) ? 1 : 0;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < PT; ++k) bad = bad || hits[k] != 0;
+  if (bad) *sbad = 1;
+  __syncthreads();
+  return *sbad == 0;
+}
+
 __global__ __launch_bounds__(kChainBlock) void fps_chain_kernel(const float* __restrict__ xyz,
                                                                 FpsChain c) {
   __shared__ uint2 red[2][8];
@@ -612,6 +686,20 @@ __global__ __launch_bounds__(kChainBlock) void fps_chain_kernel(const float* __r
   for (int e = threadIdx.x; e < kChainNext; e += kChainBlock)
     hot.pc[e] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   __syncthreads();
+  // every stage a prefix of the input (fps_prefix_holds): the outputs are copies
+  bool nested = c.m[0] <= c.n[0];
+  for (int i = 1; i < c.stages; ++i) nested = nested && c.m[i] <= c.m[i - 1];
+  __shared__ int sbad;
+  if (nested && fps_prefix_holds(sxyz, c.n[0], c.m[0], snew[1], &sbad)) {
+    for (int i = 0; i < c.stages; ++i) {
+      int32_t* I = c.idx[i] + (size_t)b * c.m[i];
+      float* NX = c.nx[i] ? c.nx[i] + (size_t)b * c.m[i] * 3 : nullptr;
+      for (int e = threadIdx.x; e < c.m[i]; e += kChainBlock) I[e] = e;
+      if (NX)
+        for (int e = threadIdx.x; e < 3 * c.m[i]; e += kChainBlock) NX[e] = sxyz[e];
+    }
+    return;
+  }
   int tag0 = 0;  // the picks of the earlier stages: every slot tag of the launch is distinct
   for (int i = 0; i < c.stages; ++i) {
     const float* cxyz = i == 0 ? sxyz : snew[(i - 1) & 1];

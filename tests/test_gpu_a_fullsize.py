@@ -434,8 +434,9 @@ def test_publish_tag_check_catches_torn_reads(env):
     ref = O.fps(x, 1024)
     _exact("torn-build SA1 idx", idx.cpu().numpy(), ref)
     _exact("torn-build SA1 new_xyz", nx.cpu().numpy(), O.gather_point(x, ref))
-    # the chain (1,024 -> 256 -> 64 -> 16, from the SA1 picks)
-    nx1 = O.gather_point(x, ref)
+    # the chain (1,024 -> 256 -> 64 -> 16) over a raw cloud: over the SA1 picks its stages
+    # would be prefixes (fps_prefix_holds) and no stage would sample
+    nx1 = _cloud(pkg, "scannet", 8, 1024, seed=6)
     rc, outs = _chain_call(h, torch.from_numpy(nx1).to(dev), [256, 64, 16], dev, torch)
     assert rc == 0
     torch.cuda.synchronize()
@@ -449,6 +450,60 @@ def test_publish_tag_check_catches_torn_reads(env):
     assert h.pn2_fault_status(1) == 0
     print(f"torn reads caught: SA1 {torn_sa1}, chain {torn_chain}")
     assert torn_sa1 > 0 and torn_chain > 0, (torn_sa1, torn_chain)
+
+
+def _chain_vs_oracle(pkg, O, torch, dev, p, npoints, what):
+    """pn2_fps_chain over p (B, n, 3) against the oracle's samplers stage by stage."""
+    rc, outs = _chain_call(pkg._lib.lib(), torch.from_numpy(np.ascontiguousarray(p)).to(dev),
+                           npoints, dev, torch)
+    assert rc == 0
+    torch.cuda.synchronize()
+    cur, refs = p, []
+    for k, ((i, n), m) in enumerate(zip(outs, npoints)):
+        r = O.fps(cur, m)
+        _exact(f"{what} stage {k} idx", i.cpu().numpy(), r)
+        cur = O.gather_point(cur, r)
+        _exact(f"{what} stage {k} new_xyz", n.cpu().numpy(), cur)
+        refs.append(r)
+    return refs
+
+
+def test_chain_over_sampler_output_is_prefix(env):
+    """A chain over an earlier sampler's picks (SA2-4 over the SA1 sampler's new_xyz): every
+    stage is the prefix of its input (pick j of the SA1 sampling was the farthest point of the
+    whole cloud, hence of its picks), which fps_prefix_holds verifies -- unique maxima at every
+    step -- before the chain kernel writes the outputs as copies. Exact against the oracle's
+    samplers stage by stage, on ScanNet and uniform clouds (and the property itself holds)."""
+    pkg, O, torch, dev = env
+    for kind in ("scannet", "uniform"):
+        x = _cloud(pkg, kind, 4, 8192, seed=11)
+        nx1 = O.gather_point(x, O.fps(x, 1024))
+        refs = _chain_vs_oracle(pkg, O, torch, dev, nx1, [256, 64, 16], f"{kind} prefix chain")
+        for r, m in zip(refs, [256, 64, 16]):
+            assert (r == np.arange(m)[None]).all(), kind
+        # MSG (cfg5): 512 picks -> 128
+        nx1 = O.gather_point(x, O.fps(x, 512))
+        _chain_vs_oracle(pkg, O, torch, dev, nx1, [128], f"{kind} msg prefix chain")
+
+
+def test_chain_prefix_check_rejects(env):
+    """Inputs that look like sampler output but are not prefixes -- two picks swapped; a later
+    point on an early pick (a tie at that pick's maximum, which the reference's tie order gives
+    to the other point); a tie in the stage's last step; duplicates of pick 0 -- must fail the
+    check and run the stages as samplers: exact against the oracle."""
+    pkg, O, torch, dev = env
+    x = _cloud(pkg, "scannet", 4, 8192, seed=12)
+    nx1 = O.gather_point(x, O.fps(x, 1024))
+    cases = {}
+    p = nx1.copy(); p[:, [100, 101]] = p[:, [101, 100]]; cases["swap 100/101"] = p
+    p = nx1.copy(); p[:, 700] = p[:, 200]; cases["tie at pick 200"] = p
+    p = nx1.copy(); p[:, 900] = p[:, 255]; cases["tie at pick 255"] = p
+    p = nx1.copy(); p[:, 513] = p[:, 1]; cases["tie at pick 1"] = p
+    p = nx1.copy(); p[:, 1:] = p[:, :1]; cases["all equal"] = p
+    for what, p in cases.items():
+        refs = _chain_vs_oracle(pkg, O, torch, dev, p, [256, 64, 16], what)
+        if what.startswith("swap") or what == "tie at pick 200":
+            assert not (refs[0] == np.arange(256)[None]).all(), what  # really not a prefix
 
 
 FPS_GOLDEN = sorted(glob.glob(os.path.join(HERE, "golden", "fps*.npz")))
