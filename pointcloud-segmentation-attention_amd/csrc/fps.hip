@@ -164,6 +164,7 @@ constexpr int kChainNext = 1024;  // points per fused stage (LDS: input copy + 2
 
 struct FpsChain {
   int stages;
+  int verdicts;  // > 0: fps_prefix_check_kernel's verdict words at the head of each idx[0] row
   int* fault;  // the device fault word (fault_word_dev)
   int n[kChainMax], m[kChainMax];
   int32_t* idx[kChainMax];
@@ -606,71 +607,103 @@ PN2_DEV void chain_stage(const float* P, int N, int M, const float* CXYZ, int32_
 // farthest point of P -- unless another point ties with it, where the sampler's tie order
 // (tf_sampling_g.cu:131-165: strided scan, left-biased tree) decides. So the check demands a
 // unique maximum at every step: with the running mins of the reference's sampler,
-// temp_j(s) = min(1e38, min_{i<j} d(P_s, P_i)) (sqdist: the samplers' uncontracted fp32
-// distance) and M_j = temp_j(j), the value pick j is chosen with, every s != j has
-// temp_j(s) < M_j, for j = 1 .. m - 1. Then FPS(P, m) = [0, m), and every later stage of the
-// chain (m' <= m picks of that prefix) is a prefix as well, by the same argument on the subset.
-// Non-finite coordinates, M_j <= 0 (duplicates) and every tie fail the check; the stages then
-// run as samplers. A quick test of pick 1 first (the unique farthest point from pick 0), so an
+// temp_j(s) = min(1e38, min_{i<j} d(P_s, P_i)) (the samplers' uncontracted fp32 distance) and
+// M_j = temp_j(j), the value pick j is chosen with, every s != j has temp_j(s) < M_j, for
+// j = 1 .. m - 1. Then FPS(P, m) = [0, m), and every later stage of the chain (m' <= m picks of
+// that prefix) is a prefix as well, by the same argument on the subset. Non-finite
+// coordinates, M_j <= 0 (duplicates) and every tie fail the check; the stages then run as
+// samplers. A quick test of pick 1 first (the unique farthest point from pick 0), so an
 // arbitrary input (a chain whose first stage samples a raw cloud) is rejected in one pass.
-// The whole workgroup calls it; sm: >= m floats of LDS.
-PN2_DEV bool fps_prefix_holds(const float* __restrict__ P, int n, int m, float* sm, int* sbad) {
-  const int t = threadIdx.x;
-  if (m > n) return false;
-  if (m <= 1) return true;  // FPS(P, 1) = [0]
-  if (t == 0) *sbad = 0;
+//
+// fps_prefix_check_kernel: one workgroup per (slice of kPrefixPts points, cloud); each checks
+// its points against every M_j (computed by every workgroup: no exchange) and stores its
+// verdict, 0 (holds) or -1, in word `slice` of the cloud's stage-0 idx row, which the chain
+// kernel reads before it writes that row. The work is ~n x m independent distance updates per
+// cloud, spread over the chip instead of the chain's one workgroup per cloud.
+constexpr int kPrefixPts = 256;
+using pf2 = float __attribute__((ext_vector_type(2)));
+
+__global__ __launch_bounds__(kPrefixPts) void fps_prefix_check_kernel(
+    const float* __restrict__ xyz, int n, int m, int32_t* __restrict__ verdict) {
+  // picks 0 .. m - 1 as x, y, z arrays (a pair of consecutive picks from an even index is one
+  // 8-byte read); smm[j + 1] = M_j (a pair M_j, M_j+1 from an odd j likewise)
+  __shared__ __attribute__((aligned(16))) float sx[kChainNext + 2], sy[kChainNext + 2],
+      sz[kChainNext + 2], smm[kChainNext + 4];
+  const int b = blockIdx.y, slice = blockIdx.x, t = threadIdx.x;
+  const float* __restrict__ P = xyz + (size_t)b * n * 3;
+  for (int e = t; e < m; e += kPrefixPts) {
+    sx[e] = P[3 * e];
+    sy[e] = P[3 * e + 1];
+    sz[e] = P[3 * e + 2];
+  }
+  if (t < 2) sx[m + t] = sy[m + t] = sz[m + t] = 0.0f;  // (pair tails)
   __syncthreads();
-  bool bad = false;
+  const int s = slice * kPrefixPts + t;
+  const bool in = s < n;
+  // a point past n stands in as a copy of pick 0: its running min is 0 from step 1 on
+  const float px = in ? P[3 * s] : sx[0], py = in ? P[3 * s + 1] : sy[0],
+              pz = in ? P[3 * s + 2] : sz[0];
+  bool bad = !(__builtin_isfinite(px) && __builtin_isfinite(py) && __builtin_isfinite(pz));
   {
-    const float m1 = fminf(1e38f, sqdist(P[3], P[4], P[5], P[0], P[1], P[2]));
-    bad = !(m1 > 0.0f);
-    for (int s = t; s < n; s += kChainBlock) {
-      const float x = P[3 * s], y = P[3 * s + 1], z = P[3 * s + 2];
-      bad = bad || !(__builtin_isfinite(x) && __builtin_isfinite(y) && __builtin_isfinite(z));
-      bad = bad || (s != 1 && !(fminf(1e38f, sqdist(x, y, z, P[0], P[1], P[2])) < m1));
-    }
+    const float m1 = fminf(1e38f, sqdist(sx[1], sy[1], sz[1], sx[0], sy[0], sz[0]));
+    bad = bad || !(m1 > 0.0f) ||
+          (s != 1 && !(fminf(1e38f, sqdist(px, py, pz, sx[0], sy[0], sz[0])) < m1));
   }
-  if (bad) *sbad = 1;
-  __syncthreads();
-  if (*sbad) return false;
-  for (int j = t; j < m; j += kChainBlock) {  // M_j
-    const float x = P[3 * j], y = P[3 * j + 1], z = P[3 * j + 2];
+  if (__syncthreads_or(bad)) {
+    if (t == 0) verdict[(size_t)b * m + slice] = -1;
+    return;
+  }
+  // M_j = temp_j(j), two picks' distances per packed step
+  for (int j = t; j < m; j += kPrefixPts) {
+    const pf2 qx = {sx[j], sx[j]}, qy = {sy[j], sy[j]}, qz = {sz[j], sz[j]};
     float v = 1e38f;
-    for (int i = 0; i < j; ++i) v = fminf(v, sqdist(x, y, z, P[3 * i], P[3 * i + 1], P[3 * i + 2]));
-    sm[j] = v;
-    if (j > 0 && !(v > 0.0f)) *sbad = 1;
-  }
-  __syncthreads();
-  if (*sbad) return false;
-  // every point's running min against each M_j: the one hit allowed is s's own step (j = s,
-  // where temp_s(s) is M_s bit for bit: the same distances, and min is exact)
-  constexpr int PT = kChainNext / kChainBlock;
-  float qx[PT], qy[PT], qz[PT], v[PT];
-  int hits[PT];
-#pragma unroll
-  for (int k = 0; k < PT; ++k) {
-    const int s = t + k * kChainBlock;
-    const bool in = s < n;
-    qx[k] = in ? P[3 * s] : 0.0f;
-    qy[k] = in ? P[3 * s + 1] : 0.0f;
-    qz[k] = in ? P[3 * s + 2] : 0.0f;
-    v[k] = 1e38f;
-    hits[k] = in ? (s >= 1 && s < m ? -1 : 0) : 0;
-  }
-  for (int j = 1; j < m; ++j) {
-    const float cx = P[3 * (j - 1)], cy = P[3 * (j - 1) + 1], cz = P[3 * (j - 1) + 2];
-    const float mj = sm[j];
-#pragma unroll
-    for (int k = 0; k < PT; ++k) {
-      v[k] = fminf(v[k], sqdist(qx[k], qy[k], qz[k], cx, cy, cz));
-      hits[k] += (t + k * kChainBlock < n && v[k] >= mj) ? 1 : 0;
+    int i = 0;
+#pragma unroll 4
+    for (; i + 1 < j; i += 2) {
+      const pf2 cx = *reinterpret_cast<const pf2*>(&sx[i]),
+                cy = *reinterpret_cast<const pf2*>(&sy[i]),
+                cz = *reinterpret_cast<const pf2*>(&sz[i]);
+      const pf2 dx = qx - cx, dy = qy - cy, dz = qz - cz;
+      const pf2 d = (dx * dx + dy * dy) + dz * dz;
+      v = fminf(fminf(v, d.x), d.y);
     }
+    if (i < j) v = fminf(v, sqdist(qx.x, qy.x, qz.x, sx[i], sy[i], sz[i]));
+    smm[j + 1] = v;
+    bad = bad || (j > 0 && !(v > 0.0f));
   }
-#pragma unroll
-  for (int k = 0; k < PT; ++k) bad = bad || hits[k] != 0;
-  if (bad) *sbad = 1;
-  __syncthreads();
-  return *sbad == 0;
+  if (t == 0) smm[m + 1] = 0.0f;  // (pair tail)
+  if (__syncthreads_or(bad)) {
+    if (t == 0) verdict[(size_t)b * m + slice] = -1;
+    return;
+  }
+  // every point's running min against each M_j; the one hit allowed is s's own step (j = s,
+  // where temp_s(s) is M_s bit for bit: the same distances, and min is exact)
+  {
+    const pf2 qx = {px, px}, qy = {py, py}, qz = {pz, pz};
+    float v = 1e38f;
+    int hits = in && s >= 1 && s < m ? -1 : 0;
+    int j = 1;
+#pragma unroll 4
+    for (; j + 1 < m; j += 2) {  // steps j and j + 1: picks j - 1 and j
+      const pf2 cx = *reinterpret_cast<const pf2*>(&sx[j - 1]),
+                cy = *reinterpret_cast<const pf2*>(&sy[j - 1]),
+                cz = *reinterpret_cast<const pf2*>(&sz[j - 1]),
+                mm = *reinterpret_cast<const pf2*>(&smm[j + 1]);
+      const pf2 dx = qx - cx, dy = qy - cy, dz = qz - cz;
+      const pf2 d = (dx * dx + dy * dy) + dz * dz;
+      v = fminf(v, d.x);
+      hits += v >= mm.x ? 1 : 0;
+      v = fminf(v, d.y);
+      hits += v >= mm.y ? 1 : 0;
+    }
+    if (j < m) {
+      v = fminf(v, sqdist(px, py, pz, sx[j - 1], sy[j - 1], sz[j - 1]));
+      hits += v >= smm[j + 1] ? 1 : 0;
+    }
+    bad = hits != 0;
+  }
+  bad = __syncthreads_or(bad);
+  if (t == 0) verdict[(size_t)b * m + slice] = bad ? -1 : 0;
 }
 
 __global__ __launch_bounds__(kChainBlock) void fps_chain_kernel(const float* __restrict__ xyz,
@@ -681,25 +714,27 @@ __global__ __launch_bounds__(kChainBlock) void fps_chain_kernel(const float* __r
   __shared__ HotLds hot;
   const int b = blockIdx.x;
   const float* __restrict__ P = xyz + (size_t)b * c.n[0] * 3;
+  if (c.verdicts > 0) {  // fps_prefix_check_kernel ran before: every stage a prefix?
+    const int32_t* vw = c.idx[0] + (size_t)b * c.m[0];
+    bool prefix = true;
+    for (int k = 0; k < c.verdicts; ++k) prefix = prefix && vw[k] == 0;
+    __syncthreads();  // (every thread has read the words before any writes the row)
+    if (prefix) {
+      for (int i = 0; i < c.stages; ++i) {
+        int32_t* I = c.idx[i] + (size_t)b * c.m[i];
+        float* NX = c.nx[i] ? c.nx[i] + (size_t)b * c.m[i] * 3 : nullptr;
+        for (int e = threadIdx.x; e < c.m[i]; e += kChainBlock) I[e] = e;
+        if (NX)
+          for (int e = threadIdx.x; e < 3 * c.m[i]; e += kChainBlock) NX[e] = P[e];
+      }
+      return;
+    }
+  }
   for (int e = threadIdx.x; e < 3 * c.n[0]; e += kChainBlock) sxyz[e] = P[e];
   // the pick slots start untagged (an earlier workgroup on this CU left its own tags there)
   for (int e = threadIdx.x; e < kChainNext; e += kChainBlock)
     hot.pc[e] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
   __syncthreads();
-  // every stage a prefix of the input (fps_prefix_holds): the outputs are copies
-  bool nested = c.m[0] <= c.n[0];
-  for (int i = 1; i < c.stages; ++i) nested = nested && c.m[i] <= c.m[i - 1];
-  __shared__ int sbad;
-  if (nested && fps_prefix_holds(sxyz, c.n[0], c.m[0], snew[1], &sbad)) {
-    for (int i = 0; i < c.stages; ++i) {
-      int32_t* I = c.idx[i] + (size_t)b * c.m[i];
-      float* NX = c.nx[i] ? c.nx[i] + (size_t)b * c.m[i] * 3 : nullptr;
-      for (int e = threadIdx.x; e < c.m[i]; e += kChainBlock) I[e] = e;
-      if (NX)
-        for (int e = threadIdx.x; e < 3 * c.m[i]; e += kChainBlock) NX[e] = sxyz[e];
-    }
-    return;
-  }
   int tag0 = 0;  // the picks of the earlier stages: every slot tag of the launch is distinct
   for (int i = 0; i < c.stages; ++i) {
     const float* cxyz = i == 0 ? sxyz : snew[(i - 1) & 1];
@@ -834,14 +869,24 @@ int fps_chain_launch(const float* xyz, int B, int N, int nstages, const int* npo
   c.stages = nstages - first;
   c.fault = fault_word_dev();
   int n = N;
+  bool nested = true;  // every stage samples no more points than its input holds
   for (int i = 0; i < kChainMax; ++i) {
     const bool on = i < c.stages;
     c.n[i] = on ? n : 0;
     c.m[i] = on ? npoint[first + i] : 0;
     c.idx[i] = on ? idx[first + i] : nullptr;
     c.nx[i] = on ? new_xyz[first + i] : nullptr;
-    if (on) n = c.m[i];
+    if (on) {
+      nested = nested && c.m[i] <= n;
+      n = c.m[i];
+    }
   }
+  // the prefix check (fps_prefix_check_kernel) when the verdict words fit the stage-0 row
+  const int slices = (c.n[0] + kPrefixPts - 1) / kPrefixPts;
+  c.verdicts = nested && c.m[0] >= 2 && c.m[0] >= slices ? slices : 0;
+  if (c.verdicts)
+    hipLaunchKernelGGL(fps_prefix_check_kernel, dim3(slices, B), dim3(kPrefixPts), 0, s, xyz,
+                       c.n[0], c.m[0], c.idx[0]);
   hipLaunchKernelGGL(fps_chain_kernel, dim3(B), dim3(kChainBlock), 0, s, xyz, c);
   if (grid0) {  // stage 0 ran inside the chain kernel: its picks' grid as a launch after it
     const hipError_t e = hipGetLastError();
