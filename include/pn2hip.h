@@ -145,9 +145,13 @@ int pn2_fps_ws(const float* xyz, int B, int N, int npoint, int32_t* idx, float* 
  * 8192 -> 1024 -> 256 -> 64 -> 16). idx[i] (B,npoint[i]) and new_xyz[i] (B,npoint[i],3) are
  * exactly what pn2_fps_gather returns for that stage's input. N <= pn2_fps_max_points(),
  * npoint[i] <= 1024 for every stage that feeds another, 1 <= nstages <= 4. Host arrays of
- * device pointers. At most two launches on `stream`: a first stage over N > 1024 points as
- * the ordinary sampler, then every remaining stage fused in one launch (one workgroup per
- * cloud; a stage of up to 1024 picks on the hot-set schedule, the same picks). */
+ * device pointers. At most three launches on `stream`: a first stage over N > 1024 points as
+ * the ordinary sampler; a check whether the remaining stages are prefixes of their input
+ * (they are when that input is itself a sampler's output -- SA2 sampling SA1's picks -- and
+ * no two points tie: csrc/fps.hip fps_prefix_holds; it leaves its verdict in the head of each
+ * cloud's idx row of the first fused stage, which the next launch overwrites); then every
+ * remaining stage fused in one launch (one workgroup per cloud: copies of the prefix, or a
+ * stage of up to 1024 picks on the hot-set schedule, the same picks either way). */
 int pn2_fps_chain(const float* xyz, int B, int N, int nstages, const int* npoint,
                   int32_t* const* idx, float* const* new_xyz, pn2_stream_t stream);
 /* pn2_fps_chain plus the automatic-edge grid of stage 0's picks (the known points of the last
