@@ -416,8 +416,8 @@ class Step:
         v["pts"] = [inp["feats"], None, None, None, None]
         v["nn"], v["fp"] = [None] * 4, [None] * 4
         tasks = []
-        if big:
-            tasks.append(Task("grid1", 1, (), lambda: v.__setitem__(
+        if big:  # on a search lane (lane 1 carries the MLPs only)
+            tasks.append(Task("grid1", 2, (), lambda: v.__setitem__(
                 "grid1", tf_grouping.BallGrid(xyz0, SSG_SA[0][1]))))
         tasks.append(Task("fps1", 0, (), lambda: tf_sampling.farthest_point_sample_chain(
             npoints[:1], xyz0, out=v["chain"][:1]), direct=True,
@@ -435,12 +435,19 @@ class Step:
                     unknown_grid=v.get("grid1") if lvl == 0 else None)
             return f
 
-        def sa(i):
+        v["bq"] = [None] * 4
+
+        def bq(i):  # layer i's ball query: needs only the sampled coordinates
             def f():
                 _, radius, nsample, _ = SSG_SA[i]
-                xyz, new_xyz = v["xyz"][i], v["xyz"][i + 1]
-                idx, _ = tf_grouping.query_ball_point(radius, nsample, xyz, new_xyz,
-                                                      grid=v.get("grid1") if i == 0 else None)
+                v["bq"][i] = tf_grouping.query_ball_point(
+                    radius, nsample, v["xyz"][i], v["xyz"][i + 1],
+                    grid=v.get("grid1") if i == 0 else None)[0]
+            return f
+
+        def sa(i):
+            def f():
+                xyz, new_xyz, idx = v["xyz"][i], v["xyz"][i + 1], v["bq"][i]
                 if mdl.attention:  # attention + batch norm (attention_layer.py:229-276)
                     v["pts"][i + 1] = attention_layer.group_mlp_attention(
                         xyz, v["pts"][i], new_xyz, idx, mdl.sa[i], mdl.store, f"layer{i + 1}")
@@ -458,14 +465,19 @@ class Step:
             return f
 
         grid_dep = ("grid1",) if big else ()
-        # task "nn<k+1>" = FP layer k+1's search (fa_layer<k+1>)
+        # the searches (ball queries "bq<i>", FP layer k+1's three_nn "nn<k+1>") need only
+        # the sampled coordinates: they run on lanes 2-3, so lane 1 carries the MLP kernels
+        # alone (with the queries on it they were ~60 us of its ~810 us per step,
+        # profiles/r5/model/lanes_model_cfg2.txt)
+        tasks.append(Task("bq1", 2, (sampled[0],) + grid_dep, bq(0)))
         tasks.append(Task("nn4", 2, (sampled[0],) + grid_dep, nn(3)))
+        for i in (1, 2, 3):
+            tasks.append(Task(f"bq{i + 1}", 3, (sampled[i],), bq(i)))
         tasks.append(Task("nn3", 2, (sampled[1],), nn(2)))
         tasks.append(Task("nn2", 3, (sampled[2],), nn(1)))
         tasks.append(Task("nn1", 3, (sampled[3],), nn(0)))
-        tasks.append(Task("sa1", 1, (sampled[0],), sa(0)))
-        for i in (1, 2, 3):
-            tasks.append(Task(f"sa{i + 1}", 1, (sampled[i],), sa(i)))
+        for i in range(4):
+            tasks.append(Task(f"sa{i + 1}", 1, (f"bq{i + 1}",), sa(i)))
         for k in range(4):
             tasks.append(Task(f"fp{k + 1}", 1, (f"nn{k + 1}",), fp(k)))
         return tasks
