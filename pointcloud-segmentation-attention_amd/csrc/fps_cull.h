@@ -523,7 +523,42 @@ __device__ __attribute__((always_inline)) inline void hotcull_body(
   // contiguous cells the wave holding the region being sampled lagged the others)
   float px[PPT * PPC], py[PPT * PPC], pz[PPT * PPC];
   int tb[PPT * PPC];
-  auto spos = [&](int s, int h) { return (s * NCW + cw) * CP + h * kWave + lane; };
+  // The hot wave's SIMD (SIMD 0: waves 0, 4, 8, 12) holds the cold waves 4, 8 and 12 too; they
+  // take issue slots from the pick chain. Those three hold kLD cells fewer than the others
+  // (7 instead of 9 at NW = 16, PPT = 9: 21 cold cells on SIMD 0 against 35-36 on SIMDs 1-3),
+  // out of the spare slots (135 for 128 cells). Slots are ranked s-major over the valid ones
+  // (valid = not a dropped slot of a light wave), the dropped ones after them (cells past N:
+  // empty), so every cell is held once and the picks do not depend on it. The SA1 sampler over
+  // the known grid alone: 380.8 -> 370.0 us at B = 16 (profiles/r6/light: cold waves 3 / 6
+  // cells lighter or the youngest waves lighter were slower or the same).
+  // (-DPN2_SA1_LIGHT_MASK / _D: other layouts for A/B builds; mask 0 = slot s of cold wave cw
+  // is cell s * NCW + cw)
+#ifdef PN2_SA1_LIGHT_MASK
+  constexpr uint32_t kLight = PN2_SA1_LIGHT_MASK;
+  constexpr int kLD = PN2_SA1_LIGHT_D;
+#else
+  constexpr uint32_t kLight = [] {
+    uint32_t m = 0;
+    for (int c = 0; c < NCW; ++c)
+      if ((c + 1) % 4 == 0) m |= 1u << c;
+    return m;
+  }();
+  constexpr int kSpare = NCELL - (NPTS + CP - 1) / CP;
+  constexpr int kNLW = __builtin_popcount(kLight);
+  constexpr int kLD = kNLW == 0 ? 0 : (kSpare / kNLW < 2 ? kSpare / kNLW : 2);
+#endif
+  constexpr int kNL = kLD > 0 ? __builtin_popcount(kLight) : 0;
+  static_assert(kLight < (1u << NCW), "light waves are cold waves");
+  static_assert((NCELL - kNL * kLD) * CP >= NPTS, "light layout capacity");
+  const int lbefore = cw >= 0 ? __builtin_popcount(kLight & ((1u << cw) - 1u)) : 0;
+  const bool light = cw >= 0 && ((kLight >> cw) & 1u);
+  auto cellof = [&](int s) {
+    if (kNL == 0 || s < PPT - kLD) return s * NCW + cw;
+    const int q = s - (PPT - kLD);
+    if (!light) return s * NCW - kNL * q + cw - lbefore;
+    return NCELL - kNL * kLD + q * kNL + lbefore;
+  };
+  auto spos = [&](int s, int h) { return cellof(s) * CP + h * kWave + lane; };
   // a cell's maximum running min (every lane gets it)
 #define PN2_CELLMAX(s) wave_max_i32(PPC == 1 ? tb[(s) * PPC] : max(tb[(s) * PPC], tb[(s) * PPC + PPC - 1]))
   int Tm[PPT];  // exact max running min of each cell (wave-uniform), -1 = empty cell
@@ -549,8 +584,8 @@ __device__ __attribute__((always_inline)) inline void hotcull_body(
       Tm[s] = any ? __float_as_int(kInitTemp) : -1;
     }
     if (lane < GRP * PPT) {
-      glo = scell[2 * ((lane % PPT) * NCW + cw)];
-      ghi = scell[2 * ((lane % PPT) * NCW + cw) + 1];
+      glo = scell[2 * cellof(lane % PPT)];
+      ghi = scell[2 * cellof(lane % PPT) + 1];
     }
 #pragma unroll
     for (int s = 0; s < PPT; ++s) tmv = lane % PPT == s ? Tm[s] : tmv;
