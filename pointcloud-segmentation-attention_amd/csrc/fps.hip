@@ -14,6 +14,9 @@
 #include <mutex>
 
 #include "fps_kernels.h"
+#ifndef PN2_SA1_PPT
+#define PN2_SA1_PPT 9  // cell slots per cold wave of the SA1 sampler (A/B builds: -DPN2_SA1_PPT)
+#endif
 #include "fps_cull.h"
 
 // Code placement of the SA1 (256 x 32) sampler's iteration loop. The loop runs ~6 % slower
@@ -797,12 +800,12 @@ int fps_impl(const float* xyz, int B, int N, int M, int32_t* idx, float* nx, voi
       launch_v9<256, 32, 4, true, PN2_SA1_PAD>(xyz, B, N, M, idx, nx, s);
     } else {
       if (kgrid && M <= kCullGridMax) {
-        launch_hotcull_grid<16, 9, 3, 4>(xyz, B, N, M, idx, nx, fault_word_dev(), s, kgrid);
+        launch_hotcull_grid<16, PN2_SA1_PPT, 3, 4>(xyz, B, N, M, idx, nx, fault_word_dev(), s, kgrid);
         kgrid = nullptr;  // (built)
       } else {
         // (the LEAN form -- 53 KB of LDS, so a CU holding a sampler can take side workgroups
         // too -- measured again in round 6: the same rate, profiles/r6/lanes20, lanes500)
-        launch_hotcull<16, 9, 3, 4>(xyz, B, N, M, idx, nx, fault_word_dev(), s);
+        launch_hotcull<16, PN2_SA1_PPT, 3, 4>(xyz, B, N, M, idx, nx, fault_word_dev(), s);
       }
     }
   }

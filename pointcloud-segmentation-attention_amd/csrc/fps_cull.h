@@ -535,7 +535,7 @@ __device__ __attribute__((always_inline)) inline void hotcull_body(
   // is cell s * NCW + cw)
 #ifdef PN2_SA1_LIGHT_MASK
   constexpr uint32_t kLight = PN2_SA1_LIGHT_MASK;
-  constexpr int kLD = PN2_SA1_LIGHT_D;
+  constexpr int kWantD = PN2_SA1_LIGHT_D;
 #else
   constexpr uint32_t kLight = [] {
     uint32_t m = 0;
@@ -543,10 +543,11 @@ __device__ __attribute__((always_inline)) inline void hotcull_body(
       if ((c + 1) % 4 == 0) m |= 1u << c;
     return m;
   }();
-  constexpr int kSpare = NCELL - (NPTS + CP - 1) / CP;
-  constexpr int kNLW = __builtin_popcount(kLight);
-  constexpr int kLD = kNLW == 0 ? 0 : (kSpare / kNLW < 2 ? kSpare / kNLW : 2);
+  constexpr int kWantD = 2;
 #endif
+  constexpr int kSpare = NCELL - (NPTS + CP - 1) / CP;  // slots beyond the cells a cloud fills
+  constexpr int kNLW = __builtin_popcount(kLight);
+  constexpr int kLD = kNLW == 0 ? 0 : (kSpare / kNLW < kWantD ? kSpare / kNLW : kWantD);
   constexpr int kNL = kLD > 0 ? __builtin_popcount(kLight) : 0;
   static_assert(kLight < (1u << NCW), "light waves are cold waves");
   static_assert((NCELL - kNL * kLD) * CP >= NPTS, "light layout capacity");
