@@ -547,7 +547,8 @@ __device__ __attribute__((always_inline)) inline void hotcull_body(
 #endif
   constexpr int kSpare = NCELL - (NPTS + CP - 1) / CP;  // slots beyond the cells a cloud fills
   constexpr int kNLW = __builtin_popcount(kLight);
-  constexpr int kLD = kNLW == 0 ? 0 : (kSpare / kNLW < kWantD ? kSpare / kNLW : kWantD);
+  constexpr int kPerW = kSpare / (kNLW > 0 ? kNLW : 1);  // dropped slots each light wave can take
+  constexpr int kLD = kNLW == 0 ? 0 : (kPerW < kWantD ? kPerW : kWantD);
   constexpr int kNL = kLD > 0 ? __builtin_popcount(kLight) : 0;
   static_assert(kLight < (1u << NCW), "light waves are cold waves");
   static_assert((NCELL - kNL * kLD) * CP >= NPTS, "light layout capacity");
