@@ -525,7 +525,8 @@ __device__ __attribute__((always_inline)) inline void hotcull_body(
   int tb[PPT * PPC];
   // The hot wave's SIMD (SIMD 0: waves 0, 4, 8, 12) holds the cold waves 4, 8 and 12 too; they
   // take issue slots from the pick chain. Those three hold kLD cells fewer than the others
-  // (7 instead of 9 at NW = 16, PPT = 9: 21 cold cells on SIMD 0 against 35-36 on SIMDs 1-3),
+  // (SA1: 7 instead of 9 at NW = 16, PPT = 9: 21 cold cells on SIMD 0 against 35-36 on SIMDs
+  // 1-3; MSG: 8),
   // out of the spare slots (135 for 128 cells). Slots are ranked s-major over the valid ones
   // (valid = not a dropped slot of a light wave), the dropped ones after them (cells past N:
   // empty), so every cell is held once and the picks do not depend on it. The SA1 sampler over
@@ -543,7 +544,10 @@ __device__ __attribute__((always_inline)) inline void hotcull_body(
       if ((c + 1) % 4 == 0) m |= 1u << c;
     return m;
   }();
-  constexpr int kWantD = 2;
+  // 2 slots each with one point per lane per cell (SA1); 1 with two (MSG SA1, 16,384 points:
+  // its cells hold twice the work, and 2 dropped slots made the cold SIMDs the bound, 0.341 ms
+  // against 0.331 with 1 and 0.333 with none at B = 8, profiles/r6/light/msg)
+  constexpr int kWantD = PPC == 1 ? 2 : 1;
 #endif
   constexpr int kSpare = NCELL - (NPTS + CP - 1) / CP;  // slots beyond the cells a cloud fills
   constexpr int kNLW = __builtin_popcount(kLight);
