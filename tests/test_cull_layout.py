@@ -15,7 +15,8 @@ def layout(NW, PPT, NPTS, PPC, mask=None, D=None):
         mask = sum(1 << c for c in range(NCW) if (c + 1) % 4 == 0)
         spare = NCELL - (NPTS + CP - 1) // CP
         nlw = bin(mask).count("1")
-        D = 0 if nlw == 0 else min(2, spare // nlw)
+        want = 2 if PPC == 1 else 1  # the MSG size (two points per lane per cell) drops one
+        D = 0 if nlw == 0 else min(want, spare // nlw)
     nL = bin(mask).count("1") if D > 0 else 0
     cells = {}
     for cw in range(NCW):
@@ -31,10 +32,12 @@ def layout(NW, PPT, NPTS, PPC, mask=None, D=None):
     return NCELL, CP, nL * D, cells
 
 
-@pytest.mark.parametrize("NW,PPT,NPTS,PPC", [(16, 9, 8192, 1), (16, 9, 16384, 2)])
-def test_default_layout_is_a_bijection(NW, PPT, NPTS, PPC):
+@pytest.mark.parametrize("NW,PPT,NPTS,PPC,dropped_want,simd_want",
+                         [(16, 9, 8192, 1, 6, [21, 36, 36, 35]),
+                          (16, 9, 16384, 2, 3, [24, 35, 35, 34])])
+def test_default_layout_is_a_bijection(NW, PPT, NPTS, PPC, dropped_want, simd_want):
     NCELL, CP, dropped, cells = layout(NW, PPT, NPTS, PPC)
-    assert dropped == 6  # waves 4, 8, 12 hold 7 cells each instead of 9
+    # SA1: waves 4, 8, 12 hold 7 cells each instead of 9; MSG: 8
     assert sorted(c for c, _ in cells.values()) == list(range(NCELL))
     valid = sorted(c for c, v in cells.values() if v)
     assert valid == list(range(NCELL - dropped))
@@ -43,7 +46,8 @@ def test_default_layout_is_a_bijection(NW, PPT, NPTS, PPC):
     for (s, cw), (c, v) in cells.items():
         if v and c * CP < NPTS:
             per_simd[(cw + 1) % 4] += 1
-    assert per_simd == [21, 36, 36, 35]
+    assert dropped == dropped_want
+    assert per_simd == simd_want
 
 
 @pytest.mark.parametrize("mask,D", [(0, 0), (0x088, 3), (0x7000, 2), (0x888, 1)])
